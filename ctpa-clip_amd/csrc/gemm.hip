@@ -1,0 +1,373 @@
+// bf16 MFMA GEMM for gfx950 with fused epilogues.
+//
+// Tile 128x128x64, 256 threads = 4 waves (2x2), each wave a 64x64 block of 4x4
+// v_mfma_f32_16x16x32_bf16.  Operands are register-staged into a double-buffered LDS
+// image (one barrier per K-step, next tile's global loads in flight under the MFMAs).
+//   K-contiguous operand tile: [128 rows][64 k] bf16, row stride 144 B (padding kills
+//     the ds_read_b128 row-group conflicts), fragments by ds_read_b128.
+//   MN-contiguous operand tile: [64 k][128] bf16, 256-B rows, 32-B chunks XOR-swizzled by
+//     (k&3)|((k>>3)&1)<<2 so ds_read_b64_tr_b16 (hardware transpose) is conflict-free;
+//     this lets dX = dY.W and dW = dY^T.X run without materialising transposes.
+// Epilogue stages the f32 accumulator tile through LDS and writes 16-B row chunks with
+// bias / residual / GELU / GEGLU / argmax fused.  blockIdx is remapped XCD-aware (T1).
+#include <algorithm>
+#include "common.h"
+#include "../../include/ctclip_hip.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BKT = 64, NTH = 256;
+constexpr int KROW = BKT * 2 + 16;           // 144-byte rows for K-contiguous tiles
+constexpr int TILE_BYTES = 128 * KROW;       // 18432 >= 64*256 for MN tiles
+constexpr int SMEM_BYTES = 4 * TILE_BYTES;   // 2 buffers x (A, B) = 73728
+constexpr int CS_LD = 132;                   // f32 epilogue staging row stride
+
+struct P {
+  int64_t M, N, K;
+  const u16* A; int64_t lda;
+  const u16* B; int64_t ldb;
+  void* C; int64_t ldc; int c_f32;
+  u16* C2; int64_t ldc2;
+  const float* bias;
+  const void* R; int64_t ldr; int r_f32;
+  float alpha; int act; int accumulate; int split_k;
+  int64_t sA, sB, sC, sC2, sR;
+  int64_t kper;
+};
+
+__device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+
+template <bool KC>
+__device__ __forceinline__ void gload(u32x4 (&r)[4], const u16* __restrict__ base, int64_t ld,
+                                      int64_t rows, int64_t kend, int64_t row0, int64_t k0) {
+  const int t = threadIdx.x;
+  if constexpr (KC) {
+    const int kc = t & 7;
+    const int64_t gk = k0 + kc * 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t gr = row0 + (t >> 3) + 32 * i;
+      if (gr < rows && gk < kend) r[i] = *(const u32x4*)(base + gr * ld + gk);
+      else r[i] = make_uint4(0, 0, 0, 0);
+    }
+  } else {
+    const int mc = t & 15;
+    const int64_t gm = row0 + mc * 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t gk = k0 + (t >> 4) + 16 * i;
+      if (gk < kend && gm < rows) r[i] = *(const u32x4*)(base + gk * ld + gm);
+      else r[i] = make_uint4(0, 0, 0, 0);
+    }
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ void swrite(char* tile, const u32x4 (&r)[4]) {
+  const int t = threadIdx.x;
+  if constexpr (KC) {
+    const int kc = t & 7;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *(u32x4*)(tile + ((t >> 3) + 32 * i) * KROW + kc * 16) = r[i];
+  } else {
+    const int mc = t & 15, c32 = mc >> 1, half = mc & 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int kk = (t >> 4) + 16 * i;
+      *(u32x4*)(tile + kk * 256 + ((((c32 ^ mn_swz(kk)) << 1) | half) << 4)) = r[i];
+    }
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ bf16x8 frag(const char* tile, int r0, int s, int lane) {
+  if constexpr (KC) {
+    const int row = r0 + (lane & 15);
+    return *(const bf16x8*)(tile + row * KROW + ((s * 4 + (lane >> 4)) << 4));
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int m = r0 + 4 * p;
+    const int k1 = s * 32 + 8 * g + q, k2 = k1 + 4;
+    const int c32 = m >> 4, within = (m & 15) * 2;
+    const int o1 = k1 * 256 + ((c32 ^ mn_swz(k1)) << 5) + within;
+    const int o2 = k2 * 256 + ((c32 ^ mn_swz(k2)) << 5) + within;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, tile + o1));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, tile + o2));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+__device__ __forceinline__ void xcd_remap(int& tx, int& ty) {
+  const int gx = gridDim.x, nwg = gridDim.x * gridDim.y;
+  const int orig = blockIdx.y * gx + blockIdx.x;
+  int id = orig;
+  if (nwg >= 16) {
+    const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+    id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  }
+  ty = id / gx;
+  tx = id - ty * gx;
+}
+
+template <bool AK, bool BK>
+__global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
+  int tx, ty;
+  xcd_remap(tx, ty);
+  const int split = blockIdx.z % p.split_k, bidx = blockIdx.z / p.split_k;
+  const int64_t m0 = (int64_t)ty * BM, n0 = (int64_t)tx * BN;
+  const int64_t kbeg = split * p.kper;
+  const int64_t kend = min(p.K, kbeg + p.kper);
+  const u16* A = p.A + bidx * p.sA;
+  const u16* B = p.B + bidx * p.sB;
+#define AS(i) (smem + (i) * TILE_BYTES)
+#define BS(i) (smem + (2 + (i)) * TILE_BYTES)
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ra[4], rb[4];
+  const int nk = kend > kbeg ? (int)((kend - kbeg + BKT - 1) / BKT) : 0;
+  if (nk > 0) {
+    gload<AK>(ra, A, p.lda, p.M, kend, m0, kbeg);
+    gload<BK>(rb, B, p.ldb, p.N, kend, n0, kbeg);
+    swrite<AK>(AS(0), ra);
+    swrite<BK>(BS(0), rb);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      gload<AK>(ra, A, p.lda, p.M, kend, m0, kbeg + (int64_t)(kt + 1) * BKT);
+      gload<BK>(rb, B, p.ldb, p.N, kend, n0, kbeg + (int64_t)(kt + 1) * BKT);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag<AK>(AS(cur), wr * 64 + i * 16, s, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = frag<BK>(BS(cur), wc * 64 + j * 16, s, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) {
+      swrite<AK>(AS(cur ^ 1), ra);
+      swrite<BK>(BS(cur ^ 1), rb);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: stage f32 tile in LDS
+  float* cs = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        cs[(wr * 64 + i * 16 + (lane >> 4) * 4 + r) * CS_LD + wc * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+
+  const int t = threadIdx.x;
+  if (p.act == 3) {
+    // argmax over this tile's columns per row: write (value, index) pairs per (row, tile)
+    // C = float2 [M][ntiles]; columns >= N excluded.
+    // two threads per row, 64 columns each, first-max tie-break (torch.argmax semantics)
+    const int row = t >> 1, half = t & 1;
+    const int ncol = (int)min((int64_t)BN, p.N - n0);
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int c = half * 64; c < half * 64 + 64; ++c) {
+      const float v = cs[row * CS_LD + c];
+      if (c < ncol && v > best) { best = v; bi = c; }
+    }
+    const float ob = __shfl_xor(best, 1, 64);
+    const int oi = __shfl_xor(bi, 1, 64);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    const int64_t gm = m0 + row;
+    if (half == 0 && gm < p.M) {
+      float2* out = (float2*)p.C + bidx * p.sC;
+      out[gm * p.ldc + tx] = make_float2(best, __int_as_float((int)(n0 + bi)));
+    }
+    return;
+  }
+  const bool slab = p.split_k > 1;
+  for (int it = 0; it < (BM * BN / 8) / NTH; ++it) {
+    const int c = t + NTH * it;
+    const int row = c >> 4, cc = (c & 15) * 8;
+    const int64_t gm = m0 + row, gn = n0 + cc;
+    if (gm >= p.M || gn >= p.N) continue;
+    float v[8];
+    const f32x4 lo = *(const f32x4*)(cs + row * CS_LD + cc);
+    const f32x4 hi = *(const f32x4*)(cs + row * CS_LD + cc + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = lo[j] * p.alpha; v[4 + j] = hi[j] * p.alpha; }
+    if (slab) {
+      float* Cf = (float*)p.C + (int64_t)split * p.M * p.ldc + bidx * p.sC + gm * p.ldc + gn;
+      *(f32x4*)Cf = f32x4{v[0], v[1], v[2], v[3]};
+      *(f32x4*)(Cf + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      continue;
+    }
+    if (p.bias) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += p.bias[gn + j];
+    }
+    if (p.R) {
+      if (p.r_f32) {
+        const float* Rp = (const float*)p.R + bidx * p.sR + gm * p.ldr + gn;
+        const f32x4 a = *(const f32x4*)Rp, b = *(const f32x4*)(Rp + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[j] += a[j]; v[4 + j] += b[j]; }
+      } else {
+        float rr[8];
+        unpack8(*(const u32x4*)((const u16*)p.R + bidx * p.sR + gm * p.ldr + gn), rr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += rr[j];
+      }
+    }
+    if (p.act == 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
+    }
+    if (p.c_f32) {
+      float* Cf = (float*)p.C + bidx * p.sC + gm * p.ldc + gn;
+      if (p.accumulate) {
+        const f32x4 a = *(const f32x4*)Cf, b = *(const f32x4*)(Cf + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[j] += a[j]; v[4 + j] += b[j]; }
+      }
+      *(f32x4*)Cf = f32x4{v[0], v[1], v[2], v[3]};
+      *(f32x4*)(Cf + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    } else {
+      u16* Cb = (u16*)p.C + bidx * p.sC + gm * p.ldc + gn;
+      if (p.accumulate) {
+        float rr[8];
+        unpack8(*(const u32x4*)Cb, rr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += rr[j];
+      }
+      *(u32x4*)Cb = pack8(v);
+    }
+    if (p.C2 && p.act != 2) *(u32x4*)(p.C2 + bidx * p.sC2 + gm * p.ldc2 + gn) = pack8(v);
+  }
+  if (p.act == 2 && p.C2) {
+    // GEGLU: tile columns [0,64) are x, [64,128) the matching gates -> 64 output columns
+    for (int it = 0; it < (BM * 64 / 8) / NTH; ++it) {
+      const int c = t + NTH * it;
+      const int row = c >> 3, cc = (c & 7) * 8;
+      const int64_t gm = m0 + row, gn = n0 / 2 + cc;
+      if (gm >= p.M || n0 + cc >= p.N) continue;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = cs[row * CS_LD + cc + j] * p.alpha;
+        const float gt = cs[row * CS_LD + 64 + cc + j] * p.alpha;
+        // round h to bf16 first so forward g == geglu(stored h) bit-for-bit in backward
+        const float xb = bf2f(f2bf(x)), gb = bf2f(f2bf(gt));
+        v[j] = gelu_erf(gb) * xb;
+      }
+      *(u32x4*)(p.C2 + bidx * p.sC2 + gm * p.ldc2 + gn) = pack8(v);
+    }
+  }
+}
+
+template <bool AK, bool BK>
+int launch(const P& p, int batch, hipStream_t st) {
+  dim3 grid(cdiv(p.N, BN), cdiv(p.M, BM), batch * p.split_k);
+  hipLaunchKernelGGL((gemm_kernel<AK, BK>), grid, dim3(NTH), SMEM_BYTES, st, p);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void reduce_slabs_kernel(const float* __restrict__ s, int64_t nslab, int64_t rows, int64_t cols,
+                                    int64_t ld, void* out, int64_t ldo, int out_f32, int accumulate) {
+  const int64_t n4 = cols / 4;
+  const int64_t total = rows * n4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / n4, c = (i - r * n4) * 4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t z = 0; z < nslab; ++z) acc += *(const f32x4*)(s + (z * rows + r) * ld + c);
+    if (out_f32) {
+      float* o = (float*)out + r * ldo + c;
+      if (accumulate) acc += *(const f32x4*)o;
+      *(f32x4*)o = acc;
+    } else {
+      u16* o = (u16*)out + r * ldo + c;
+      if (accumulate) {
+        acc[0] += bf2f(o[0]); acc[1] += bf2f(o[1]); acc[2] += bf2f(o[2]); acc[3] += bf2f(o[3]);
+      }
+      o[0] = f2bf(acc[0]); o[1] = f2bf(acc[1]); o[2] = f2bf(acc[2]); o[3] = f2bf(acc[3]);
+    }
+  }
+}
+
+static bool s_smem_set = false;
+
+}  // namespace
+
+extern "C" int ctclip_gemm(const ctclip_gemm_args* a, void* stream) {
+  if (!a) return CT_EINVAL;
+  if (a->M <= 0 || a->N <= 0 || a->K <= 0) return a->M == 0 || a->N == 0 ? 0 : CT_ESHAPE;
+  const int split = a->split_k > 0 ? a->split_k : 1;
+  if (split > 1 && !a->c_f32) return CT_EINVAL;
+  if (a->act == 2 && !a->C2) return CT_EINVAL;
+  // 16-byte alignment of every operand row / chunk
+  CT_REQUIRE(aligned16(a->A) && aligned16(a->B) && aligned16(a->C), CT_EALIGN);
+  CT_REQUIRE(a->lda % 8 == 0 && a->ldb % 8 == 0, CT_EALIGN);
+  CT_REQUIRE(a->a_kcontig ? (a->K % 8 == 0) : (a->M % 8 == 0), CT_EALIGN);
+  CT_REQUIRE(a->b_kcontig ? (a->K % 8 == 0) : (a->N % 8 == 0), CT_EALIGN);
+  if (a->act != 3) {
+    CT_REQUIRE(a->N % 8 == 0 && a->ldc % 8 == 0, CT_EALIGN);
+    if (a->C2) CT_REQUIRE(aligned16(a->C2) && a->ldc2 % 8 == 0, CT_EALIGN);
+    if (a->R) CT_REQUIRE(aligned16(a->R) && a->ldr % 8 == 0, CT_EALIGN);
+  }
+  if (a->act == 2) CT_REQUIRE(a->N % BN == 0, CT_ESHAPE);
+  if (!s_smem_set) {
+    (void)hipFuncSetAttribute((const void*)gemm_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
+    s_smem_set = true;
+  }
+  P p;
+  p.M = a->M; p.N = a->N; p.K = a->K;
+  p.A = (const u16*)a->A; p.lda = a->lda;
+  p.B = (const u16*)a->B; p.ldb = a->ldb;
+  p.C = a->C; p.ldc = a->ldc; p.c_f32 = a->c_f32;
+  p.C2 = (u16*)a->C2; p.ldc2 = a->ldc2;
+  p.bias = a->bias;
+  p.R = a->R; p.ldr = a->ldr; p.r_f32 = a->r_f32;
+  p.alpha = a->alpha; p.act = a->act; p.accumulate = a->accumulate; p.split_k = split;
+  p.sA = a->sA; p.sB = a->sB; p.sC = a->sC; p.sC2 = a->sC2; p.sR = a->sR;
+  int64_t kper = (a->K + split - 1) / split;
+  kper = (kper + BKT - 1) / BKT * BKT;
+  p.kper = kper;
+  const int batch = a->batch > 0 ? a->batch : 1;
+  hipStream_t st = (hipStream_t)stream;
+  if (a->a_kcontig && a->b_kcontig) return launch<true, true>(p, batch, st);
+  if (a->a_kcontig && !a->b_kcontig) return launch<true, false>(p, batch, st);
+  if (!a->a_kcontig && a->b_kcontig) return launch<false, true>(p, batch, st);
+  return launch<false, false>(p, batch, st);
+}
+
+extern "C" int ctclip_reduce_slabs(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,
+                                   void* out, int64_t ldo, int32_t out_f32, int32_t accumulate, void* stream) {
+  if (rows == 0 || cols == 0) return 0;
+  CT_REQUIRE(cols % 4 == 0 && ld % 4 == 0 && ldo % 4 == 0, CT_EALIGN);
+  const int64_t total = rows * (cols / 4);
+  const int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slabs, nslab, rows, cols,
+                     ld, out, ldo, out_f32, accumulate);
+  CT_CHECK_LAUNCH();
+  return 0;
+}

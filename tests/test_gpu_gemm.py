@@ -1,0 +1,96 @@
+"""MFMA GEMM kernel vs a plain torch fp32 reference (GPU)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def K():
+    from ctclip_mi355x import kernels
+    return kernels
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize('M,N,K_', [(128, 128, 64), (256, 384, 512), (300, 136, 200), (1000, 2816, 512),
+                                    (64, 512, 1408), (8, 512, 4096)])
+def test_linear_nt(K, M, N, K_):
+    torch.manual_seed(0)
+    x = torch.randn(M, K_, device='cuda').bfloat16()
+    w = torch.randn(N, K_, device='cuda').bfloat16()
+    b = torch.randn(N, device='cuda')
+    r = torch.randn(M, N, device='cuda')
+    y = K.linear(x, w, bias=b, residual=r, out_dtype=torch.float32)
+    ref = x.float() @ w.float().t() + b + r
+    assert _rel(y, ref) < 1e-5
+
+
+def test_layout_asymmetric_exact(K):
+    # integer-valued operands -> exact f32 results; catches row/col swaps
+    M, N, K_ = 256, 256, 128
+    x = (torch.arange(M * K_, device='cuda').reshape(M, K_) % 7 - 3).bfloat16()
+    w = (torch.arange(N * K_, device='cuda').reshape(N, K_) % 5 - 2).bfloat16()
+    y = K.linear(x, w, out_dtype=torch.float32)
+    assert torch.equal(y, x.float() @ w.float().t())
+    dy = (torch.arange(M * N, device='cuda').reshape(M, N) % 3 - 1).bfloat16()
+    dx = K.matmul_nn(dy, w, out_dtype=torch.float32)
+    assert torch.equal(dx, dy.float() @ w.float())
+    dw = K.matmul_tn(dy, x, split_k=1)
+    assert torch.equal(dw, dy.float().t() @ x.float())
+    dw2 = K.matmul_tn(dy, x, split_k=3)
+    assert torch.equal(dw2, dy.float().t() @ x.float())
+
+
+@pytest.mark.parametrize('M,N,K_', [(512, 512, 256), (1000, 1408, 512), (4096, 512, 2816)])
+def test_matmul_nn(K, M, N, K_):
+    torch.manual_seed(1)
+    dy = torch.randn(M, N, device='cuda').bfloat16()
+    w = torch.randn(N, K_, device='cuda').bfloat16()
+    dx = K.matmul_nn(dy, w, out_dtype=torch.float32)
+    assert _rel(dx, dy.float() @ w.float()) < 1e-5
+
+
+@pytest.mark.parametrize('M,N,K_', [(4096, 512, 512), (20000, 256, 512), (1024, 2816, 512), (8, 512, 1024)])
+def test_matmul_tn(K, M, N, K_):
+    torch.manual_seed(2)
+    dy = torch.randn(M, N, device='cuda').bfloat16()
+    x = torch.randn(M, K_, device='cuda').bfloat16()
+    dw = K.matmul_tn(dy, x)
+    assert _rel(dw, dy.float().t() @ x.float()) < 1e-5
+
+
+def test_gelu_and_geglu_epilogue(K):
+    torch.manual_seed(3)
+    M, Kd = 384, 512
+    x = torch.randn(M, Kd, device='cuda').bfloat16()
+    w = (torch.randn(256, Kd, device='cuda') / 20).bfloat16()
+    y = K.linear(x, w, act=K.ACT_GELU, out_dtype=torch.float32)
+    ref = torch.nn.functional.gelu(x.float() @ w.float().t())
+    assert _rel(y, ref) < 1e-5
+    g = torch.empty(M, 128, device='cuda', dtype=torch.bfloat16)
+    h = K.linear(x, w, act=K.ACT_GEGLU, out2=g)
+    hf = h.float()
+    ref_g = torch.cat([torch.nn.functional.gelu(hf[:, 64:128]) * hf[:, :64],
+                       torch.nn.functional.gelu(hf[:, 192:256]) * hf[:, 128:192]], 1)
+    assert _rel(g, ref_g) < 4e-3
+    assert _rel(h, x.float() @ w.float().t()) < 4e-3
+
+
+def test_argmax_epilogue(K):
+    torch.manual_seed(4)
+    M, Nc, Kd = 1000, 1024, 512
+    x = torch.randn(M, Kd, device='cuda').bfloat16()
+    w = torch.randn(Nc, Kd, device='cuda').bfloat16()
+    nt = Nc // 128
+    out = torch.empty(M, nt, 2, device='cuda', dtype=torch.float32)
+    K.gemm_raw(M, Nc, Kd, x, Kd, True, w, Kd, True, out, nt, act=K.ACT_ARGMAX)
+    vals = out[..., 0]
+    idx = out[..., 1].contiguous().view(torch.int32)
+    s = x.float() @ w.float().t()
+    best = vals.argmax(1)
+    got = idx.gather(1, best[:, None])[:, 0].long()
+    ref = s.argmax(1)
+    assert (got == ref).float().mean().item() > 0.999

@@ -1,0 +1,106 @@
+"""Pin the CPU oracle (oracle/ctclip_oracle.py) against fixtures produced by the reference's
+own ct_clip modules (tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ctclip_oracle as O
+from oracle import weights as W
+
+
+def _close(a, b, tol):
+    a, b = a.double(), b.double()
+    err = (a - b).abs().max().item()
+    scale = max(1.0, b.abs().max().item())
+    assert err <= tol * scale, f'max err {err} (scale {scale})'
+
+
+def test_hu_division_bit_exact():
+    """f32 x/1000.f == f64 divide-then-cast for every int16."""
+    x = np.arange(-32768, 32768, dtype=np.int64)
+    c = np.clip(x, -1000, 1000)
+    ref = (c.astype(np.float64) / 1000).astype(np.float32)
+    ours = O.normalize_hu(torch.from_numpy(x.astype(np.int16))).numpy()
+    assert np.array_equal(ref.view(np.uint32), ours.view(np.uint32))
+
+
+def test_recipe_is_deterministic():
+    a = W.make_state_dict(O.TINY)
+    b = W.make_state_dict(O.TINY)
+    assert all(torch.equal(a[k], b[k]) for k in a)
+
+
+def _run_tiny(golden, training=True, grads=False):
+    cfg = O.TINY
+    sd = W.make_state_dict(cfg)
+    if grads:
+        for k, v in sd.items():
+            if k.startswith(O.trainable_prefixes()) and v.is_floating_point() and 'vq._codebook' not in k \
+                    and not k.endswith('norm.beta') and not k.endswith('norm_out.beta') \
+                    and not k.endswith('context_norm.beta'):
+                v.requires_grad_(True)
+    video = O.normalize_hu(golden['in.hu'])
+    trace = {}
+    out = O.ctclip_forward(sd, golden['in.ids'], golden['in.mask'], video, cfg, training, trace)
+    return sd, out, trace
+
+
+def test_tiny_forward_matches_reference(golden_tiny):
+    g = golden_tiny
+    assert torch.equal(g['in.hu'], W.make_hu(4, O.TINY.vit))
+    sd, out, trace = _run_tiny(g)
+    _close(trace['patch_emb'], g['out.patch_emb'], 1e-5)
+    _close(trace['cpb'], g['out.cpb'], 1e-5)
+    _close(trace['spatial_out'], g['out.spatial_out'].reshape(trace['spatial_out'].shape), 1e-4)
+    _close(trace['temporal_out'],
+           g['out.temporal_out'].reshape(4, 4, 4, 8, 64).permute(0, 3, 1, 2, 4), 1e-4)
+    assert torch.equal(out['indices'], g['out.vq_indices'])
+    _close(out['enc_text'], g['out.enc_text'], 1e-4)
+    _close(out['loss'].reshape(1), g['out.loss'], 1e-5)
+    _close(out['new_embed'], g['out.new_embed'], 1e-5)
+    _close(out['new_cluster_size'], g['out.new_cluster_size'], 1e-6)
+
+
+def test_tiny_grads_match_reference(golden_tiny):
+    g = golden_tiny
+    sd, out, _ = _run_tiny(g, grads=True)
+    out['loss'].backward()
+    n = 0
+    for k in g:
+        if not k.startswith('grad.'):
+            continue
+        name = k[5:]
+        if g[k].numel() == 0:
+            continue
+        assert sd[name].grad is not None, name
+        _close(sd[name].grad, g[k], 2e-4)
+        n += 1
+    assert n > 50
+
+
+def test_tiny_eval_scores(golden_tiny):
+    g = golden_tiny
+    sd = W.make_state_dict(O.TINY)
+    s = O.eval_scores(sd, g['in.ids'], g['in.mask'], O.normalize_hu(g['in.hu']), O.TINY)
+    _close(s, g['out.eval_scores'], 1e-5)
+
+
+@pytest.mark.slow
+def test_base_b2_matches_reference(golden_base):
+    g = golden_base
+    cfg = O.BASE
+    torch.set_num_threads(max(1, torch.get_num_threads()))
+    sd = W.make_state_dict(cfg)
+    ids, mask = W.make_text(2, 128, cfg.bert.vocab_size)
+    video = O.normalize_hu(W.make_hu(2, cfg.vit))
+    trace = {}
+    with torch.no_grad():
+        out = O.ctclip_forward(sd, ids, mask, video, cfg, True, trace)
+    _close(trace['patch_emb'].reshape(-1, 512)[:256], g['out.patch_emb_head'], 1e-4)
+    _close(trace['cpb'][:, :4, :], g['out.cpb_rows'], 1e-5)
+    _close(trace['spatial_out'].reshape(-1, 512)[:256], g['out.spatial_out_head'], 1e-3)
+    tout = trace['temporal_out'].permute(0, 2, 3, 1, 4).reshape(-1, 512)[:256]
+    _close(tout, g['out.temporal_out_head'], 1e-3)
+    mism = (out['indices'].to(torch.int32) != g['out.vq_indices']).float().mean().item()
+    assert mism < 1e-3, mism
+    _close(out['loss'].reshape(1), g['out.loss'], 1e-4)
