@@ -1,0 +1,524 @@
+// Fused multi-head attention (forward + backward) for gfx950, head dim 32 or 64.
+//
+// Replaces the core of Attention.forward (ct_clip/attention.py:156-180): sim = scale * q.k^T
+// (+ continuous position bias, attention.py:160-162) -> softmax -> attn @ v; and BERT's
+// self-attention (scale 1/sqrt(64), additive key mask).  q and k arrive already
+// l2-normalised and multiplied by q_scale / k_scale (norm.hip), so `scale` = 8 for CTViT.
+//
+// Sequences are gathered straight from the canonical token layout:
+//   row(s, i) = (s / n_inner) * s_outer + (s % n_inner) * s_inner + i * s_pos
+// (spatial: s = b*T + t, 576 rows per frame; temporal: s = b*H*W + hw, stride H*W; BERT: s = b).
+//
+// Layout trick: scores are computed transposed, S^T = K.Q^T with v_mfma_f32_16x16x32_bf16,
+// so each lane owns ONE query column and its probabilities feed the P.V MFMA as the B operand
+// with a permuted key order; V (and K in the backward) are read from their row-major LDS
+// image with ds_read_b64_tr_b16 in that same permuted order.  Online softmax keeps the
+// running max/sum per lane.  The CPB bias is read from the deduplicated table u[h][bin],
+// bin = (dh + Hg-1)*(2Wg-1) + (dw + Wg-1) (2,209 entries at 24x24), and its gradient is
+// binned the same way in LDS (one global atomic per bin per workgroup).
+#include "common.h"
+#include "../../include/ctclip_hip.h"
+
+namespace {
+
+struct AP {
+  const u16* q; int64_t ldq;
+  const u16* k; int64_t ldk;
+  const u16* v; int64_t ldv;
+  const u16* o; int64_t ldo;      // forward output (read in backward for delta)
+  u16* out; int64_t ldout;        // forward: O
+  const u16* dout; int64_t lddo;  // backward: dO
+  u16* dq; int64_t lddq;
+  u16* dk; int64_t lddk;
+  u16* dv; int64_t lddv;
+  float* lse;                     // [H][M]
+  float* delta;                   // [H][M]
+  const float* bias_u;            // [H][nbins] or null
+  float* dbias_u;                 // [H][nbins] (accumulated with atomics) or null
+  const int32_t* kmask;           // [nseq][L] 1 = keep, or null
+  float scale;
+  int L, H, nseq;
+  int64_t M;
+  int Hg, Wg, nbins;
+  float inv_wg;
+  int n_inner;
+  int64_t s_outer, s_inner, s_pos;
+  int pp;                         // (seq, head) pairs per workgroup
+};
+
+constexpr int NW = 8;             // waves per workgroup
+constexpr int NT = NW * 64;
+
+__device__ __forceinline__ int64_t seq_row(const AP& p, int s, int i) {
+  return (int64_t)(s / p.n_inner) * p.s_outer + (int64_t)(s % p.n_inner) * p.s_inner + (int64_t)i * p.s_pos;
+}
+
+__device__ __forceinline__ int bin_of(const AP& p, int hq, int wq, int key) {
+  const int hk = (int)(((float)key + 0.5f) * p.inv_wg);
+  const int wk = key - hk * p.Wg;
+  return (hq - hk + p.Hg - 1) * (2 * p.Wg - 1) + (wq - wk + p.Wg - 1);
+}
+
+template <int D>
+struct Img {
+  static constexpr int RS = D * 2 + 16;  // padded row stride (bytes)
+};
+
+// stage rows [0, Lp) of one head's [L][D] slice into a padded LDS image (zero rows >= L)
+template <int D>
+__device__ __forceinline__ void stage(char* img, const u16* base, int64_t ld, const AP& p, int s, int h, int Lp,
+                                      int tid, int nth) {
+  constexpr int CH = D / 8;
+  for (int idx = tid; idx < Lp * CH; idx += nth) {
+    const int r = idx / CH, c = idx - r * CH;
+    u32x4 v = make_uint4(0, 0, 0, 0);
+    if (r < p.L) v = *(const u32x4*)(base + seq_row(p, s, r) * ld + h * D + c * 8);
+    *(u32x4*)(img + r * Img<D>::RS + c * 16) = v;
+  }
+}
+
+// A/B fragment from a row-major image: lane gets [r0 + (lane&15)][kk*32 + 8*(lane>>4) + 0..7]
+template <int D>
+__device__ __forceinline__ bf16x8 rowfrag(const char* img, int r0, int kk, int lane) {
+  return *(const bf16x8*)(img + (r0 + (lane & 15)) * Img<D>::RS + ((kk * 4 + (lane >> 4)) << 4));
+}
+
+// transposed fragment: lane gets column c0 + (lane&15) of rows
+//   r0 + 4g + 0..3 (elements 0..3) and r0 + 16 + 4g + 0..3 (elements 4..7),  g = lane>>4
+template <int D>
+__device__ __forceinline__ bf16x8 trfrag(const char* img, int r0, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  const char* a1 = img + (r0 + 4 * g + q) * Img<D>::RS + (c0 + 4 * pp) * 2;
+  const char* a2 = a1 + 16 * Img<D>::RS;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a1));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a2));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ bf16x8 pack_perm(const f32x4& a, const f32x4& b) {
+  bf16x8 r;
+  r[0] = (bf16)a[0]; r[1] = (bf16)a[1]; r[2] = (bf16)a[2]; r[3] = (bf16)a[3];
+  r[4] = (bf16)b[0]; r[5] = (bf16)b[1]; r[6] = (bf16)b[2]; r[7] = (bf16)b[3];
+  return r;
+}
+
+__device__ __forceinline__ bf16x8 gload8(const u16* p) { return __builtin_bit_cast(bf16x8, *(const u32x4*)p); }
+__device__ __forceinline__ bf16x8 zero8() { return __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0)); }
+
+// ------------------------------------------------------------------------------------ forward
+template <int D>
+__global__ __launch_bounds__(NT) void attn_fwd_kernel(AP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KK = D / 32, DB = D / 16, RS = Img<D>::RS;
+  const int L = p.L, Lp = (L + 31) & ~31;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wpp = NW / p.pp;                         // waves per pair
+  const int pair_local = w / wpp, wi = w - pair_local * wpp;
+  const int pair_bytes = 2 * Lp * RS;
+  float* ub = (float*)(smem + p.pp * pair_bytes);
+  for (int pl = 0; pl < p.pp; ++pl) {
+    const int pair = blockIdx.x * p.pp + pl;
+    if (pair >= p.nseq * p.H) break;
+    const int s = pair / p.H, h = pair - s * p.H;
+    stage<D>(smem + pl * pair_bytes, p.k, p.ldk, p, s, h, Lp, tid, NT);
+    stage<D>(smem + pl * pair_bytes + Lp * RS, p.v, p.ldv, p, s, h, Lp, tid, NT);
+  }
+  if (p.bias_u) {
+    const int h = blockIdx.x % p.H;  // pp == 1 when a bias is present
+    for (int i = tid; i < p.nbins; i += NT) ub[i] = p.bias_u[(int64_t)h * p.nbins + i];
+  }
+  __syncthreads();
+  const int pair = blockIdx.x * p.pp + pair_local;
+  if (pair >= p.nseq * p.H) return;
+  const int s = pair / p.H, h = pair - s * p.H;
+  const char* Kimg = smem + pair_local * pair_bytes;
+  const char* Vimg = Kimg + Lp * RS;
+  const int g = lane >> 4, li = lane & 15;
+  const int nqb = (L + 15) >> 4;
+  for (int qb = wi; qb < nqb; qb += wpp) {
+    const int q = qb * 16 + li;
+    const bool qv = q < L;
+    const int64_t qrow = qv ? seq_row(p, s, q) : 0;
+    bf16x8 qf[KK];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) qf[kk] = qv ? gload8(p.q + qrow * p.ldq + h * D + kk * 32 + 8 * g) : zero8();
+    int hq = 0, wq = 0;
+    if (p.bias_u) { hq = (int)(((float)q + 0.5f) * p.inv_wg); wq = q - hq * p.Wg; }
+    float m = -INFINITY, lsum = 0.f;
+    f32x4 o[DB];
+#pragma unroll
+    for (int d = 0; d < DB; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kc = 0; kc < Lp; kc += 32) {
+      f32x4 sa[2];
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi) {
+        sa[bi] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk)
+          sa[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag<D>(Kimg, kc + 16 * bi, kk, lane), qf[kk], sa[bi], 0, 0, 0);
+      }
+      float cmax = -INFINITY;
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kc + 16 * bi + 4 * g + r;
+          float x = sa[bi][r] * p.scale;
+          bool valid = key < L;
+          if (valid && p.kmask) valid = p.kmask[(int64_t)s * L + key] != 0;
+          if (valid && p.bias_u) x += ub[bin_of(p, hq, wq, key)];
+          x = valid ? x : -INFINITY;
+          sa[bi][r] = x;
+          cmax = fmaxf(cmax, x);
+        }
+      cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+      cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+      const float mnew = fmaxf(m, cmax);
+      const float msafe = mnew == -INFINITY ? 0.f : mnew;
+      const float alpha = __expf(m - msafe);
+      float psum = 0.f;
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __expf(sa[bi][r] - msafe);
+          sa[bi][r] = e;
+          psum += e;
+        }
+      lsum = lsum * alpha + psum;
+      m = mnew;
+      const bf16x8 pb = pack_perm(sa[0], sa[1]);
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        o[d] *= alpha;
+        o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag<D>(Vimg, kc, d * 16, lane), pb, o[d], 0, 0, 0);
+      }
+    }
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    if (qv) {
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        uint2 pk;
+        pk.x = pack2(o[d][0] * inv, o[d][1] * inv);
+        pk.y = pack2(o[d][2] * inv, o[d][3] * inv);
+        *(uint2*)(p.out + qrow * p.ldout + h * D + d * 16 + 4 * g) = pk;
+      }
+      if (g == 0 && p.lse) p.lse[(int64_t)h * p.M + qrow] = lsum > 0.f ? m + __logf(lsum) : INFINITY;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------- backward dQ
+// also writes delta = rowsum(dO * O) and bins the bias gradient
+template <int D>
+__global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(AP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KK = D / 32, DB = D / 16, RS = Img<D>::RS;
+  const int L = p.L, Lp = (L + 31) & ~31;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wpp = NW / p.pp;
+  const int pair_local = w / wpp, wi = w - pair_local * wpp;
+  const int pair_bytes = 2 * Lp * RS;
+  float* ub = (float*)(smem + p.pp * pair_bytes);
+  float* bins = ub + p.nbins;
+  for (int pl = 0; pl < p.pp; ++pl) {
+    const int pair = blockIdx.x * p.pp + pl;
+    if (pair >= p.nseq * p.H) break;
+    const int s = pair / p.H, h = pair - s * p.H;
+    stage<D>(smem + pl * pair_bytes, p.k, p.ldk, p, s, h, Lp, tid, NT);
+    stage<D>(smem + pl * pair_bytes + Lp * RS, p.v, p.ldv, p, s, h, Lp, tid, NT);
+  }
+  if (p.bias_u) {
+    const int h = blockIdx.x % p.H;
+    for (int i = tid; i < p.nbins; i += NT) { ub[i] = p.bias_u[(int64_t)h * p.nbins + i]; bins[i] = 0.f; }
+  }
+  __syncthreads();
+  const int pair = blockIdx.x * p.pp + pair_local;
+  const bool active = pair < p.nseq * p.H;
+  const int s = active ? pair / p.H : 0, h = active ? pair - s * p.H : 0;
+  const char* Kimg = smem + pair_local * pair_bytes;
+  const char* Vimg = Kimg + Lp * RS;
+  const int g = lane >> 4, li = lane & 15;
+  const int nqb = active ? (L + 15) >> 4 : 0;
+  for (int qb = wi; qb < nqb; qb += wpp) {
+    const int q = qb * 16 + li;
+    const bool qv = q < L;
+    const int64_t qrow = qv ? seq_row(p, s, q) : 0;
+    bf16x8 qf[KK], df[KK];
+    float dl = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      if (qv) {
+        qf[kk] = gload8(p.q + qrow * p.ldq + h * D + kk * 32 + 8 * g);
+        df[kk] = gload8(p.dout + qrow * p.lddo + h * D + kk * 32 + 8 * g);
+        const bf16x8 of = gload8(p.o + qrow * p.ldo + h * D + kk * 32 + 8 * g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dl += (float)df[kk][j] * (float)of[j];
+      } else {
+        qf[kk] = zero8();
+        df[kk] = zero8();
+      }
+    }
+    dl += __shfl_xor(dl, 16, 64);
+    dl += __shfl_xor(dl, 32, 64);
+    const float lse = qv ? p.lse[(int64_t)h * p.M + qrow] : INFINITY;
+    if (qv && g == 0) p.delta[(int64_t)h * p.M + qrow] = dl;
+    int hq = 0, wq = 0;
+    if (p.bias_u) { hq = (int)(((float)q + 0.5f) * p.inv_wg); wq = q - hq * p.Wg; }
+    f32x4 dq[DB];
+#pragma unroll
+    for (int d = 0; d < DB; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kc = 0; kc < Lp; kc += 32) {
+      f32x4 sa[2], da[2];
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi) {
+        sa[bi] = f32x4{0.f, 0.f, 0.f, 0.f};
+        da[bi] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          sa[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag<D>(Kimg, kc + 16 * bi, kk, lane), qf[kk], sa[bi], 0, 0, 0);
+          da[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag<D>(Vimg, kc + 16 * bi, kk, lane), df[kk], da[bi], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kc + 16 * bi + 4 * g + r;
+          bool valid = qv && key < L;
+          if (valid && p.kmask) valid = p.kmask[(int64_t)s * L + key] != 0;
+          float ds = 0.f;
+          if (valid) {
+            int bn = 0;
+            float x = sa[bi][r] * p.scale;
+            if (p.bias_u) { bn = bin_of(p, hq, wq, key); x += ub[bn]; }
+            const float pr = __expf(x - lse);
+            ds = pr * (da[bi][r] - dl);
+            if (p.dbias_u) atomicAdd(&bins[bn], ds);
+          }
+          sa[bi][r] = ds * p.scale;
+        }
+      const bf16x8 dsb = pack_perm(sa[0], sa[1]);
+#pragma unroll
+      for (int d = 0; d < DB; ++d)
+        dq[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag<D>(Kimg, kc, d * 16, lane), dsb, dq[d], 0, 0, 0);
+    }
+    if (qv) {
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        uint2 pk;
+        pk.x = pack2(dq[d][0], dq[d][1]);
+        pk.y = pack2(dq[d][2], dq[d][3]);
+        *(uint2*)(p.dq + qrow * p.lddq + h * D + d * 16 + 4 * g) = pk;
+      }
+    }
+  }
+  if (p.dbias_u) {
+    __syncthreads();
+    const int hh = blockIdx.x % p.H;
+    for (int i = tid; i < p.nbins; i += NT) {
+      const float v = bins[i];
+      if (v != 0.f) atomicAdd(&p.dbias_u[(int64_t)hh * p.nbins + i], v);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- backward dK dV
+template <int D>
+__global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(AP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KK = D / 32, DB = D / 16, RS = Img<D>::RS;
+  const int L = p.L, Lp = (L + 31) & ~31;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wpp = NW / p.pp;
+  const int pair_local = w / wpp, wi = w - pair_local * wpp;
+  const int pair_bytes = 2 * Lp * RS + 2 * Lp * 4;
+  float* ub = (float*)(smem + p.pp * pair_bytes);
+  for (int pl = 0; pl < p.pp; ++pl) {
+    const int pair = blockIdx.x * p.pp + pl;
+    if (pair >= p.nseq * p.H) break;
+    const int s = pair / p.H, h = pair - s * p.H;
+    char* base = smem + pl * pair_bytes;
+    stage<D>(base, p.q, p.ldq, p, s, h, Lp, tid, NT);
+    stage<D>(base + Lp * RS, p.dout, p.lddo, p, s, h, Lp, tid, NT);
+    float* ls = (float*)(base + 2 * Lp * RS);
+    float* dls = ls + Lp;
+    for (int i = tid; i < Lp; i += NT) {
+      const bool v = i < L;
+      const int64_t r = v ? seq_row(p, s, i) : 0;
+      ls[i] = v ? p.lse[(int64_t)h * p.M + r] : INFINITY;
+      dls[i] = v ? p.delta[(int64_t)h * p.M + r] : 0.f;
+    }
+  }
+  if (p.bias_u) {
+    const int h = blockIdx.x % p.H;
+    for (int i = tid; i < p.nbins; i += NT) ub[i] = p.bias_u[(int64_t)h * p.nbins + i];
+  }
+  __syncthreads();
+  const int pair = blockIdx.x * p.pp + pair_local;
+  if (pair >= p.nseq * p.H) return;
+  const int s = pair / p.H, h = pair - s * p.H;
+  const char* Qimg = smem + pair_local * pair_bytes;
+  const char* Dimg = Qimg + Lp * RS;
+  const float* ls = (const float*)(Qimg + 2 * Lp * RS);
+  const float* dls = ls + Lp;
+  const int g = lane >> 4, li = lane & 15;
+  const int nkb = (L + 15) >> 4;
+  for (int kb = wi; kb < nkb; kb += wpp) {
+    const int key = kb * 16 + li;
+    bool kv = key < L;
+    if (kv && p.kmask) kv = p.kmask[(int64_t)s * L + key] != 0;
+    const int64_t krow = key < L ? seq_row(p, s, key) : 0;
+    bf16x8 kf[KK], vf[KK];
+#pragma unroll
+    for (int kk = 0; kk < KK; ++kk) {
+      kf[kk] = key < L ? gload8(p.k + krow * p.ldk + h * D + kk * 32 + 8 * g) : zero8();
+      vf[kk] = key < L ? gload8(p.v + krow * p.ldv + h * D + kk * 32 + 8 * g) : zero8();
+    }
+    int hk = 0, wk = 0;
+    if (p.bias_u) { hk = (int)(((float)key + 0.5f) * p.inv_wg); wk = key - hk * p.Wg; }
+    f32x4 dk[DB], dv[DB];
+#pragma unroll
+    for (int d = 0; d < DB; ++d) { dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[d] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+    for (int qc = 0; qc < Lp; qc += 32) {
+      f32x4 sa[2], da[2];
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi) {
+        sa[bi] = f32x4{0.f, 0.f, 0.f, 0.f};
+        da[bi] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) {
+          sa[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag<D>(Qimg, qc + 16 * bi, kk, lane), kf[kk], sa[bi], 0, 0, 0);
+          da[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag<D>(Dimg, qc + 16 * bi, kk, lane), vf[kk], da[bi], 0, 0, 0);
+        }
+      }
+      // element (bi, r): query = qc + 16bi + 4g + r, key = this lane's key
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qi = qc + 16 * bi + 4 * g + r;
+          float pr = 0.f, ds = 0.f;
+          if (kv && qi < L) {
+            float x = sa[bi][r] * p.scale;
+            if (p.bias_u) {
+              const int hq = (int)(((float)qi + 0.5f) * p.inv_wg);
+              const int wq = qi - hq * p.Wg;
+              x += ub[(hq - hk + p.Hg - 1) * (2 * p.Wg - 1) + (wq - wk + p.Wg - 1)];
+            }
+            pr = __expf(x - ls[qi]);
+            ds = pr * (da[bi][r] - dls[qi]);
+          }
+          sa[bi][r] = pr;
+          da[bi][r] = ds * p.scale;
+        }
+      const bf16x8 pa = pack_perm(sa[0], sa[1]);
+      const bf16x8 dsa = pack_perm(da[0], da[1]);
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, trfrag<D>(Dimg, qc, d * 16, lane), dv[d], 0, 0, 0);
+        dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsa, trfrag<D>(Qimg, qc, d * 16, lane), dk[d], 0, 0, 0);
+      }
+    }
+    // C[key][d]: rows = keys kb*16 + 4g + r, col = d*16 + li
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int kr = kb * 16 + 4 * g + r;
+      if (kr >= L) continue;
+      const int64_t row = seq_row(p, s, kr);
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        p.dk[row * p.lddk + h * D + d * 16 + li] = f2bf(dk[d][r]);
+        p.dv[row * p.lddv + h * D + d * 16 + li] = f2bf(dv[d][r]);
+      }
+    }
+  }
+}
+
+bool s_attr = false;
+
+template <int D>
+void set_attrs() {
+  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+int fill(AP& p, const ctclip_attn_args* a) {
+  if (a->D != 32 && a->D != 64) return CT_ESHAPE;
+  if (a->L <= 0 || a->L > 1024) return CT_ESHAPE;
+  p.q = (const u16*)a->q; p.ldq = a->ldq;
+  p.k = (const u16*)a->k; p.ldk = a->ldk;
+  p.v = (const u16*)a->v; p.ldv = a->ldv;
+  p.o = (const u16*)a->o; p.ldo = a->ldo;
+  p.out = (u16*)a->o; p.ldout = a->ldo;
+  p.dout = (const u16*)a->dout; p.lddo = a->lddo;
+  p.dq = (u16*)a->dq; p.lddq = a->lddq;
+  p.dk = (u16*)a->dk; p.lddk = a->lddk;
+  p.dv = (u16*)a->dv; p.lddv = a->lddv;
+  p.lse = a->lse; p.delta = a->delta;
+  p.bias_u = a->bias_u; p.dbias_u = a->dbias_u;
+  p.kmask = a->kmask;
+  p.scale = a->scale;
+  p.L = a->L; p.H = a->H; p.nseq = a->nseq; p.M = a->M;
+  p.Hg = a->grid_h; p.Wg = a->grid_w;
+  p.nbins = (2 * a->grid_h - 1) * (2 * a->grid_w - 1);
+  p.inv_wg = a->grid_w > 0 ? 1.f / (float)a->grid_w : 0.f;
+  p.n_inner = a->n_inner > 0 ? a->n_inner : 1;
+  p.s_outer = a->s_outer; p.s_inner = a->s_inner; p.s_pos = a->s_pos;
+  if (p.bias_u && a->grid_h * a->grid_w != a->L) return CT_ESHAPE;
+  // pairs per workgroup: enough (seq, head) pairs that every wave has query blocks
+  const int nqb = (a->L + 15) / 16;
+  int pp = NW / std::max(1, std::min(NW, nqb));
+  while (NW % pp) --pp;
+  if (p.bias_u) pp = 1;
+  p.pp = pp;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int ctclip_attn_fwd(const ctclip_attn_args* a, void* stream) {
+  AP p;
+  int rc = fill(p, a);
+  if (rc) return rc;
+  if (!s_attr) { set_attrs<32>(); set_attrs<64>(); s_attr = true; }
+  const int Lp = (p.L + 31) & ~31;
+  const int pairs = p.nseq * p.H;
+  const size_t RSb = a->D * 2 + 16;
+  const size_t lds = (size_t)p.pp * 2 * Lp * RSb + (p.bias_u ? p.nbins * 4 : 0);
+  if (lds > 160 * 1024) return CT_ESHAPE;
+  dim3 grid(cdiv(pairs, p.pp));
+  if (a->D == 32) hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(NT), lds, (hipStream_t)stream, p);
+  else hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(NT), lds, (hipStream_t)stream, p);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream) {
+  AP p;
+  int rc = fill(p, a);
+  if (rc) return rc;
+  if (!s_attr) { set_attrs<32>(); set_attrs<64>(); s_attr = true; }
+  const int Lp = (p.L + 31) & ~31;
+  const int pairs = p.nseq * p.H;
+  const size_t RSb = a->D * 2 + 16;
+  const size_t lds1 = (size_t)p.pp * 2 * Lp * RSb + (p.bias_u ? 2 * p.nbins * 4 : 0);
+  const size_t lds2 = (size_t)p.pp * (2 * Lp * RSb + 2 * Lp * 4) + (p.bias_u ? p.nbins * 4 : 0);
+  if (lds1 > 160 * 1024 || lds2 > 160 * 1024) return CT_ESHAPE;
+  dim3 grid(cdiv(pairs, p.pp));
+  hipStream_t st = (hipStream_t)stream;
+  if (a->D == 32) {
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<32>, grid, dim3(NT), lds1, st, p);
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<32>, grid, dim3(NT), lds2, st, p);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<64>, grid, dim3(NT), lds1, st, p);
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<64>, grid, dim3(NT), lds2, st, p);
+  }
+  CT_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,152 @@
+// Bandwidth-bound helpers: GEGLU / GELU backward, weight packing (f32 master -> bf16
+// working layout), gradient unpacking, casts, HU normalisation.
+#include "common.h"
+#include "../../include/ctclip_hip.h"
+
+namespace {
+
+// GEGLU backward on the tile-interleaved pre-activation h (see gemm.hip act=2):
+// tile t: h[:, 128t + c] = x part, h[:, 128t + 64 + c] = gate part, g[:, 64t + c] = gelu(gate)*x.
+// (ct_clip/attention.py:39-42)
+__global__ __launch_bounds__(256) void geglu_bwd_kernel(const u16* __restrict__ dg, int64_t lddg,
+                                                        const u16* __restrict__ h, int64_t ldh, int64_t rows,
+                                                        int gcols, u16* __restrict__ dh, int64_t lddh) {
+  const int nch = gcols / 8;
+  const int64_t total = rows * nch;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / nch;
+    const int gc = (int)(i - r * nch) * 8;
+    const int t = gc >> 6, c = gc & 63;
+    float d[8], x[8], gt[8], ox[8], og[8];
+    unpack8(*(const u32x4*)(dg + r * lddg + gc), d);
+    unpack8(*(const u32x4*)(h + r * ldh + t * 128 + c), x);
+    unpack8(*(const u32x4*)(h + r * ldh + t * 128 + 64 + c), gt);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ox[j] = d[j] * gelu_erf(gt[j]);
+      og[j] = d[j] * x[j] * gelu_erf_grad(gt[j]);
+    }
+    *(u32x4*)(dh + r * lddh + t * 128 + c) = pack8(ox);
+    *(u32x4*)(dh + r * lddh + t * 128 + 64 + c) = pack8(og);
+  }
+}
+
+// dpre = dy * gelu'(pre)    (BERT intermediate GELU)
+__global__ __launch_bounds__(256) void gelu_bwd_kernel(const u16* __restrict__ dy, const u16* __restrict__ pre,
+                                                       u16* __restrict__ dx, int64_t n8) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    float d[8], x[8], o[8];
+    unpack8(((const u32x4*)dy)[i], d);
+    unpack8(((const u32x4*)pre)[i], x);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = d[j] * gelu_erf_grad(x[j]);
+    ((u32x4*)dx)[i] = pack8(o);
+  }
+}
+
+// dst[r][c] (bf16, ld_dst) = src[map[r]][c] * (colscale ? colscale[c] : 1), zero if map[r] < 0 or c >= cols
+__global__ __launch_bounds__(256) void pack_rows_kernel(const float* __restrict__ src, int64_t ld_src,
+                                                        const int32_t* __restrict__ map, int64_t rows_dst,
+                                                        int cols, int cols_dst, const float* __restrict__ colscale,
+                                                        u16* __restrict__ dst, int64_t ld_dst) {
+  const int64_t total = rows_dst * cols_dst;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / cols_dst;
+    const int c = (int)(i - r * cols_dst);
+    const int64_t sr = map ? (int64_t)map[r] : r;
+    float v = 0.f;
+    if (sr >= 0 && c < cols) {
+      v = src[sr * ld_src + c];
+      if (colscale) v *= colscale[c];
+    }
+    dst[r * ld_dst + c] = f2bf(v);
+  }
+}
+
+// dst[map[r]][c] (f32) (+)= src[r][c] for r with map[r] >= 0, c < cols
+__global__ __launch_bounds__(256) void unpack_rows_kernel(const float* __restrict__ src, int64_t ld_src,
+                                                          const int32_t* __restrict__ map, int64_t rows_src, int cols,
+                                                          float* __restrict__ dst, int64_t ld_dst, int accumulate) {
+  const int64_t total = rows_src * cols;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / cols;
+    const int c = (int)(i - r * cols);
+    const int64_t dr = map ? (int64_t)map[r] : r;
+    if (dr < 0) continue;
+    const float v = src[r * ld_src + c];
+    float* d = dst + dr * ld_dst + c;
+    *d = accumulate ? *d + v : v;
+  }
+}
+
+__global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restrict__ x, u16* __restrict__ y, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = f2bf(x[i]);
+}
+
+// y = a + b (f32) with optional bf16 shadow; n % 4 == 0
+__global__ __launch_bounds__(256) void add_f32_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                      float* __restrict__ y, u16* __restrict__ yb, int64_t n4) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 v = ((const f32x4*)a)[i];
+    if (b) v += ((const f32x4*)b)[i];
+    if (y) ((f32x4*)y)[i] = v;
+    if (yb) {
+      uint2 o;
+      o.x = pack2(v[0], v[1]);
+      o.y = pack2(v[2], v[3]);
+      ((uint2*)yb)[i] = o;
+    }
+  }
+}
+
+inline int grid_for(int64_t n) { return (int)std::min<int64_t>(8192, std::max<int64_t>(1, (n + 255) / 256)); }
+
+}  // namespace
+
+extern "C" int ctclip_geglu_bwd(const void* dg, int64_t lddg, const void* h, int64_t ldh, int64_t rows, int32_t gcols,
+                                void* dh, int64_t lddh, void* stream) {
+  CT_REQUIRE(gcols % 64 == 0, CT_ESHAPE);
+  hipLaunchKernelGGL(geglu_bwd_kernel, dim3(grid_for(rows * gcols / 8)), dim3(256), 0, (hipStream_t)stream,
+                     (const u16*)dg, lddg, (const u16*)h, ldh, rows, gcols, (u16*)dh, lddh);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_gelu_bwd(const void* dy, const void* pre, void* dx, int64_t n, void* stream) {
+  CT_REQUIRE(n % 8 == 0 && aligned16(dy) && aligned16(pre) && aligned16(dx), CT_EALIGN);
+  hipLaunchKernelGGL(gelu_bwd_kernel, dim3(grid_for(n / 8)), dim3(256), 0, (hipStream_t)stream, (const u16*)dy,
+                     (const u16*)pre, (u16*)dx, n / 8);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_pack_rows(const float* src, int64_t ld_src, const int32_t* map, int64_t rows_dst, int32_t cols,
+                                int32_t cols_dst, const float* colscale, void* dst, int64_t ld_dst, void* stream) {
+  hipLaunchKernelGGL(pack_rows_kernel, dim3(grid_for(rows_dst * cols_dst)), dim3(256), 0, (hipStream_t)stream, src,
+                     ld_src, map, rows_dst, cols, cols_dst, colscale, (u16*)dst, ld_dst);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_unpack_rows(const float* src, int64_t ld_src, const int32_t* map, int64_t rows_src,
+                                  int32_t cols, float* dst, int64_t ld_dst, int32_t accumulate, void* stream) {
+  hipLaunchKernelGGL(unpack_rows_kernel, dim3(grid_for(rows_src * cols)), dim3(256), 0, (hipStream_t)stream, src,
+                     ld_src, map, rows_src, cols, dst, ld_dst, accumulate);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream) {
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, (u16*)y, n);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_add_f32(const float* a, const float* b, float* y, void* yb, int64_t n, void* stream) {
+  CT_REQUIRE(n % 4 == 0, CT_EALIGN);
+  hipLaunchKernelGGL(add_f32_kernel, dim3(grid_for(n / 4)), dim3(256), 0, (hipStream_t)stream, a, b, y, (u16*)yb,
+                     n / 4);
+  CT_CHECK_LAUNCH();
+  return 0;
+}

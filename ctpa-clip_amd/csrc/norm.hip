@@ -1,0 +1,358 @@
+// LayerNorm (affine / bias-less), per-head l2norm+scale, and column sums.
+//
+// LayerNorm replaces: ct_clip/attention.py:28-35 (bias-less LayerNorm, gamma only, eps 1e-5),
+// nn.LayerNorm in FeedForward (attention.py:47) and to_patch_emb (ctvit.py:171,173), BERT's
+// LayerNorms (eps 1e-12).  One wave per row, the row held in registers (CPL chunks of 8 per
+// lane), 16-B vector loads, f32 statistics.
+#include "common.h"
+#include "../../include/ctclip_hip.h"
+
+namespace {
+
+template <int CPL>
+__device__ __forceinline__ void load_row(const void* x, int x_f32, int64_t row, int64_t ld, int D, int lane,
+                                         float (&v)[CPL][8]) {
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < D) {
+      if (x_f32) {
+        const float* p = (const float*)x + row * ld + col;
+        const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { v[c][j] = a[j]; v[c][4 + j] = b[j]; }
+      } else {
+        unpack8(*(const u32x4*)((const u16*)x + row * ld + col), v[c]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = 0.f;
+    }
+  }
+}
+
+template <int CPL>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x, int x_f32, int64_t ldx, int64_t rows,
+                                                     int D, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps, u16* __restrict__ yb,
+                                                     int64_t ldyb, float* __restrict__ yf, int64_t ldyf,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float v[CPL][8];
+  load_row<CPL>(x, x_f32, row, ldx, D, lane, v);
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[c][j];
+  const float mean = warp_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col < D)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { const float d = v[c][j] - mean; q += d * d; }
+  }
+  const float var = warp_sum(q) / D;
+  const float rstd = rsqrtf(var + eps);
+  if (lane == 0) {
+    if (mean_out) mean_out[row] = mean;
+    if (rstd_out) rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (col >= D) continue;
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float t = (v[c][j] - mean) * rstd;
+      if (gamma) t *= gamma[col + j];
+      if (beta) t += beta[col + j];
+      o[j] = t;
+    }
+    if (yb) *(u32x4*)(yb + row * ldyb + col) = pack8(o);
+    if (yf) {
+      float* p = yf + row * ldyf + col;
+      *(f32x4*)p = f32x4{o[0], o[1], o[2], o[3]};
+      *(f32x4*)(p + 4) = f32x4{o[4], o[5], o[6], o[7]};
+    }
+  }
+}
+
+// dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)) [+ dres];  dgamma/dbeta partials.
+template <int CPL>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy, int dy_f32, int64_t lddy,
+                                                     const void* __restrict__ x, int x_f32, int64_t ldx,
+                                                     const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, const float* __restrict__ gamma,
+                                                     int64_t rows, int D, const float* __restrict__ dres,
+                                                     int64_t lddres, float* __restrict__ dxf, int64_t lddxf,
+                                                     u16* __restrict__ dxb, int64_t lddxb,
+                                                     float* __restrict__ part_g, float* __restrict__ part_b) {
+  __shared__ float red[4][2][CPL * 512];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float ag[CPL][8], ab[CPL][8];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { ag[c][j] = 0.f; ab[c][j] = 0.f; }
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < rows; row += nw) {
+    float g[CPL][8], xv[CPL][8];
+    load_row<CPL>(dy, dy_f32, row, lddy, D, lane, g);
+    load_row<CPL>(x, x_f32, row, ldx, D, lane, xv);
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      if (col >= D) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xh = (xv[c][j] - mean) * rstd;
+        xv[c][j] = xh;
+        ag[c][j] += g[c][j] * xh;
+        ab[c][j] += g[c][j];
+        const float gg = gamma ? g[c][j] * gamma[col + j] : g[c][j];
+        g[c][j] = gg;
+        s1 += gg;
+        s2 += gg * xh;
+      }
+    }
+    s1 = warp_sum(s1) / D;
+    s2 = warp_sum(s2) / D;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      if (col >= D) continue;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = rstd * (g[c][j] - s1 - xv[c][j] * s2);
+      if (dres) {
+        const float* p = dres + row * lddres + col;
+        const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { o[j] += a[j]; o[4 + j] += b[j]; }
+      }
+      if (dxf) {
+        float* p = dxf + row * lddxf + col;
+        *(f32x4*)p = f32x4{o[0], o[1], o[2], o[3]};
+        *(f32x4*)(p + 4) = f32x4{o[4], o[5], o[6], o[7]};
+      }
+      if (dxb) *(u32x4*)(dxb + row * lddxb + col) = pack8(o);
+    }
+  }
+  if (!part_g) return;
+#pragma unroll
+  for (int c = 0; c < CPL; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[w][0][(c * 64 + lane) * 8 + j] = ag[c][j];
+      red[w][1][(c * 64 + lane) * 8 + j] = ab[c][j];
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < D; i += 256) {
+    part_g[(int64_t)blockIdx.x * D + i] = red[0][0][i] + red[1][0][i] + red[2][0][i] + red[3][0][i];
+    if (part_b) part_b[(int64_t)blockIdx.x * D + i] = red[0][1][i] + red[1][1][i] + red[2][1][i] + red[3][1][i];
+  }
+}
+
+// per-head l2norm + per-dim scale:  y = x / max(||x||, 1e-12) * scale[d]     (attention.py:152-154)
+// one lane handles 8 of a head's D elements; D in {16, 32, 64}; x row stride ldx, heads at h*D.
+__global__ __launch_bounds__(256) void l2n_fwd_kernel(const u16* __restrict__ x, int64_t ldx, int64_t rows, int H,
+                                                      int D, const float* __restrict__ scale, u16* __restrict__ y,
+                                                      int64_t ldy) {
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int lpr = H * D / 8;  // lanes per row
+  const int64_t row = gid / lpr;
+  const int c = (int)(gid - row * lpr);
+  if (row >= rows) return;
+  const int col = c * 8, d0 = col % D;
+  float v[8];
+  unpack8(*(const u32x4*)(x + row * ldx + col), v);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += v[j] * v[j];
+  for (int o = 1; o < D / 8; o <<= 1) s += __shfl_xor(s, o, 64);
+  const float inv = 1.f / fmaxf(sqrtf(s), 1e-12f);
+  float o8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o8[j] = v[j] * inv * scale[d0 + j];
+  *(u32x4*)(y + row * ldy + col) = pack8(o8);
+}
+
+// backward of the above: dx = (du - u (u.du)) / max(||x||,eps) (only if ||x|| > eps), du = dy*scale;
+// dscale partial[d] += dy * u
+__global__ __launch_bounds__(256) void l2n_bwd_kernel(const u16* __restrict__ x, int64_t ldx, const u16* __restrict__ dy,
+                                                      int64_t lddy, int64_t rows, int H, int D,
+                                                      const float* __restrict__ scale, u16* __restrict__ dx,
+                                                      int64_t lddx, float* __restrict__ part) {
+  __shared__ float red[256][8];
+  const int lpr = H * D / 8;
+  const int64_t nthreads = (int64_t)gridDim.x * 256;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // grid-stride over (row, chunk) keeping chunk fixed per thread: requires nthreads % lpr == 0
+  const int64_t gid0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c = (int)(gid0 % lpr);
+  const int col = c * 8, d0 = col % D;
+  for (int64_t row = gid0 / lpr; row < rows; row += nthreads / lpr) {
+    float v[8], g[8];
+    unpack8(*(const u32x4*)(x + row * ldx + col), v);
+    unpack8(*(const u32x4*)(dy + row * lddy + col), g);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[j] * v[j];
+    for (int o = 1; o < D / 8; o <<= 1) s += __shfl_xor(s, o, 64);
+    const float n = sqrtf(s);
+    const float inv = 1.f / fmaxf(n, 1e-12f);
+    float du[8], ud = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float u = v[j] * inv;
+      acc[j] += g[j] * u;
+      du[j] = g[j] * scale[d0 + j];
+      ud += du[j] * u;
+    }
+    for (int o = 1; o < D / 8; o <<= 1) ud += __shfl_xor(ud, o, 64);
+    float o8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float u = v[j] * inv;
+      o8[j] = n > 1e-12f ? (du[j] - u * ud) * inv : du[j] * inv;
+    }
+    *(u32x4*)(dx + row * lddx + col) = pack8(o8);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = acc[j];
+  __syncthreads();
+  // fold threads with the same d0 (d0 = (c*8) % D, c = gid % lpr)
+  if (threadIdx.x < D) {
+    const int d = threadIdx.x;
+    float s = 0.f;
+    for (int t = 0; t < 256; ++t) {
+      const int cc = (int)(((int64_t)blockIdx.x * 256 + t) % lpr);
+      const int dd = (cc * 8) % D;
+      if (d >= dd && d < dd + 8) s += red[t][d - dd];
+    }
+    part[(int64_t)blockIdx.x * D + d] = s;
+  }
+}
+
+// column sums of a [rows][cols] matrix (bf16 or f32) -> per-block partials [nblk][cols]
+__global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ x, int x_f32, int64_t ld, int64_t rows,
+                                                     int cols, float* __restrict__ part) {
+  const int nch = cols / 8;
+  // thread -> (chunk, row-lane)
+  const int per_row = min(nch, 256);
+  const int rl = 256 / per_row;
+  const int ch0 = threadIdx.x % per_row, r0 = threadIdx.x / per_row;
+  __shared__ float red[256][8];
+  for (int ch = ch0; ch < nch; ch += per_row) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (r0 < rl) {
+      for (int64_t r = (int64_t)blockIdx.x * rl + r0; r < rows; r += (int64_t)gridDim.x * rl) {
+        float v[8];
+        if (x_f32) {
+          const float* p = (const float*)x + r * ld + ch * 8;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = p[j];
+        } else {
+          unpack8(*(const u32x4*)((const u16*)x + r * ld + ch * 8), v);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += v[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = acc[j];
+    __syncthreads();
+    if (r0 == 0) {
+      float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int k = 0; k < rl; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += red[ch0 + k * per_row][j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part[(int64_t)blockIdx.x * cols + ch * 8 + j] = s[j];
+    }
+    __syncthreads();
+  }
+}
+
+int ln_cpl(int D) { return (D + 511) / 512; }
+
+}  // namespace
+
+extern "C" int ctclip_layernorm_fwd(const void* x, int32_t x_f32, int64_t ldx, int64_t rows, int32_t D,
+                                    const float* gamma, const float* beta, float eps, void* y_bf16, int64_t ldyb,
+                                    float* y_f32, int64_t ldyf, float* mean, float* rstd, void* stream) {
+  if (rows == 0) return 0;
+  CT_REQUIRE(D % 8 == 0 && ldx % 8 == 0, CT_EALIGN);
+  const int cpl = ln_cpl(D);
+  dim3 grid(cdiv(rows, 4));
+  hipStream_t st = (hipStream_t)stream;
+#define LNF(C) hipLaunchKernelGGL(ln_fwd_kernel<C>, grid, dim3(256), 0, st, x, x_f32, ldx, rows, D, gamma, beta, eps, \
+                                  (u16*)y_bf16, ldyb, y_f32, ldyf, mean, rstd)
+  if (cpl == 1) LNF(1);
+  else if (cpl == 2) LNF(2);
+  else if (cpl <= 8) LNF(8);
+  else return CT_ESHAPE;
+#undef LNF
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_layernorm_bwd(const void* dy, int32_t dy_f32, int64_t lddy, const void* x, int32_t x_f32,
+                                    int64_t ldx, const float* mean, const float* rstd, const float* gamma,
+                                    int64_t rows, int32_t D, const float* dres, int64_t lddres, float* dx_f32,
+                                    int64_t lddxf, void* dx_bf16, int64_t lddxb, float* part_gamma,
+                                    float* part_beta, int32_t nblocks, void* stream) {
+  if (rows == 0) return 0;
+  CT_REQUIRE(D % 8 == 0, CT_EALIGN);
+  const int cpl = ln_cpl(D);
+  dim3 grid(nblocks);
+  hipStream_t st = (hipStream_t)stream;
+#define LNB(C) hipLaunchKernelGGL(ln_bwd_kernel<C>, grid, dim3(256), 0, st, dy, dy_f32, lddy, x, x_f32, ldx, mean, rstd, \
+                                  gamma, rows, D, dres, lddres, dx_f32, lddxf, (u16*)dx_bf16, lddxb, part_gamma, part_beta)
+  if (cpl == 1) LNB(1);
+  else if (cpl == 2) LNB(2);
+  else return CT_ESHAPE;  // D > 1024 not needed on the backward path (patch LN uses the folded-weight trick)
+#undef LNB
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_l2norm_scale_fwd(const void* x, int64_t ldx, int64_t rows, int32_t H, int32_t D,
+                                       const float* scale, void* y, int64_t ldy, void* stream) {
+  if (rows == 0) return 0;
+  CT_REQUIRE(D % 8 == 0 && D <= 512 && ldx % 8 == 0 && ldy % 8 == 0, CT_EALIGN);
+  const int64_t total = rows * (H * D / 8);
+  hipLaunchKernelGGL(l2n_fwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream, (const u16*)x, ldx,
+                     rows, H, D, scale, (u16*)y, ldy);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_l2norm_scale_bwd(const void* x, int64_t ldx, const void* dy, int64_t lddy, int64_t rows,
+                                       int32_t H, int32_t D, const float* scale, void* dx, int64_t lddx,
+                                       float* part_scale, int32_t nblocks, void* stream) {
+  if (rows == 0) return 0;
+  const int lpr = H * D / 8;
+  CT_REQUIRE((256 % lpr == 0) || (lpr % 256 == 0), CT_ESHAPE);
+  CT_REQUIRE(((int64_t)nblocks * 256) % lpr == 0, CT_ESHAPE);
+  hipLaunchKernelGGL(l2n_bwd_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, (const u16*)x, ldx,
+                     (const u16*)dy, lddy, rows, H, D, scale, (u16*)dx, lddx, part_scale);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_colsum(const void* x, int32_t x_f32, int64_t ld, int64_t rows, int32_t cols, float* part,
+                             int32_t nblocks, void* stream) {
+  CT_REQUIRE(cols % 8 == 0, CT_EALIGN);
+  hipLaunchKernelGGL(colsum_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, x, x_f32, ld, rows, cols, part);
+  CT_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,113 @@
+// Fused input normalisation + patchify + LayerNorm(patch_dim) for CTViT.to_patch_emb.
+//   int16 HU -> clamp(-1000, 1000) / 1000.f      (ct_clip/data.py:150-152; f32 division is
+//                                                 bit-identical to the reference's f64 path)
+//   Rearrange 'b c (t pt) (h p1) (w p2) -> b t h w (c pt p1 p2)'   (ct_clip/ctvit.py:170)
+//   LayerNorm(patch_dim) statistics (ctvit.py:171); the kernel writes xhat = (x-mean)*rstd in
+//   bf16.  The LN affine (gamma, beta) is folded into the following Linear on the host:
+//   W' = W*diag(gamma), b' = b + W.beta, so the same xhat also serves the weight gradient.
+// One wave per token (patch), the patch held in registers, element -> voxel offsets from a
+// small per-call table (no integer division in the loop).
+#include "common.h"
+#include "../../include/ctclip_hip.h"
+
+namespace {
+
+constexpr int MAXC = 64;  // patch_dim <= 64*64 = 4096
+
+__global__ __launch_bounds__(256) void patch_ln_kernel(const void* __restrict__ video, int is_f32, int is_hu,
+                                                       int64_t ntok, int T, int Hg, int Wg, int64_t vol_stride,
+                                                       int64_t frame_elems, int W, int PT, int P,
+                                                       const int32_t* __restrict__ offs, int pd, float eps,
+                                                       u16* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tok >= ntok) return;
+  int64_t r = tok;
+  const int wg = (int)(r % Wg); r /= Wg;
+  const int hg = (int)(r % Hg); r /= Hg;
+  const int t = (int)(r % T);
+  const int64_t b = r / T;
+  const int64_t base = b * vol_stride + (int64_t)t * PT * frame_elems + (int64_t)hg * P * W + (int64_t)wg * P;
+  float v[MAXC];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int e = lane + 64 * i;
+    float x = 0.f;
+    if (e < pd) {
+      const int64_t a = base + offs[e];
+      if (is_f32) {
+        x = ((const float*)video)[a];
+      } else {
+        x = (float)((const short*)video)[a];
+      }
+      if (is_hu) x = fminf(fmaxf(x, -1000.f), 1000.f) / 1000.f;
+    }
+    v[i] = x;
+    s += x;
+  }
+  const float mean = warp_sum(s) / pd;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int e = lane + 64 * i;
+    if (e < pd) { const float d = v[i] - mean; q += d * d; }
+  }
+  const float rstd = rsqrtf(warp_sum(q) / pd + eps);
+  u16* o = out + tok * pd;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int e = lane + 64 * i;
+    if (e < pd) o[e] = f2bf((v[i] - mean) * rstd);
+  }
+}
+
+// Given G = dy^T . xhat  [N][K] (f32) and colsum(dy) cs[N], produce the grads of the folded
+// LayerNorm+Linear pair: dW = G*g + cs (x) b, dgamma[k] = sum_n W[n,k] G[n,k], dbeta[k] = sum_n W[n,k] cs[n].
+__global__ __launch_bounds__(256) void patch_wgrad_kernel(const float* __restrict__ G, const float* __restrict__ cs,
+                                                          const float* __restrict__ Wt, const float* __restrict__ g,
+                                                          const float* __restrict__ bt, int N, int K,
+                                                          float* __restrict__ dW, float* __restrict__ dg,
+                                                          float* __restrict__ db, int accumulate) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  float sg = 0.f, sb = 0.f;
+  const float gk = g[k], bk = bt[k];
+  for (int n = 0; n < N; ++n) {
+    const float Gv = G[(int64_t)n * K + k], w = Wt[(int64_t)n * K + k];
+    sg += w * Gv;
+    sb += w * cs[n];
+    const float d = Gv * gk + cs[n] * bk;
+    float* p = dW + (int64_t)n * K + k;
+    *p = accumulate ? *p + d : d;
+  }
+  dg[k] = accumulate ? dg[k] + sg : sg;
+  db[k] = accumulate ? db[k] + sb : sb;
+}
+
+}  // namespace
+
+extern "C" int ctclip_patch_ln(const void* video, int32_t is_f32, int32_t is_hu, int64_t B, int32_t C, int32_t F,
+                               int32_t H, int32_t W, int32_t PT, int32_t P, const int32_t* offs, float eps,
+                               void* out, void* stream) {
+  const int pd = C * PT * P * P;
+  CT_REQUIRE(pd <= 64 * MAXC, CT_ESHAPE);
+  CT_REQUIRE(F % PT == 0 && H % P == 0 && W % P == 0, CT_ESHAPE);
+  const int T = F / PT, Hg = H / P, Wg = W / P;
+  const int64_t ntok = B * T * Hg * Wg;
+  const int64_t frame = (int64_t)H * W;
+  const int64_t vol = (int64_t)C * F * frame;
+  hipLaunchKernelGGL(patch_ln_kernel, dim3(cdiv(ntok, 4)), dim3(256), 0, (hipStream_t)stream, video, is_f32, is_hu,
+                     ntok, T, Hg, Wg, vol, frame, W, PT, P, offs, pd, eps, (u16*)out);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_patch_wgrad(const float* G, const float* cs, const float* Wt, const float* g, const float* b,
+                                  int32_t N, int32_t K, float* dW, float* dg, float* db, int32_t accumulate,
+                                  void* stream) {
+  hipLaunchKernelGGL(patch_wgrad_kernel, dim3(cdiv(K, 256)), dim3(256), 0, (hipStream_t)stream, G, cs, Wt, g, b, N,
+                     K, dW, dg, db, accumulate);
+  CT_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,183 @@
+// Cosine-similarity vector quantiser (vector_quantize_pytorch==1.1.2, used at
+// ct_clip/ctvit.py:187,421-427) and the image pooling of CTCLIP.forward (ct_clip.py:724,740).
+//
+// The distance matmul l2norm(x) . codebook^T runs as a bf16 MFMA GEMM whose epilogue keeps
+// the per-(row, 128-code tile) argmax (gemm.hip act=3).  vq_select then re-scores, in f32
+// against the f32 codebook, every tile winner within `margin` of the best bf16 score, so the
+// chosen index is the exact f32 argmax whenever the true winner's bf16 score is within the
+// margin (bf16 operand rounding moves a unit-vector cosine by ~1e-4; margin default 2e-2).
+#include "common.h"
+#include "../../include/ctclip_hip.h"
+
+namespace {
+
+// one wave per row; D % 8 == 0, D <= 512 handled as 8 floats per lane (+ loop for larger)
+__global__ __launch_bounds__(256) void vq_select_kernel(const float2* __restrict__ cand, int ntiles,
+                                                        const float* __restrict__ x, int64_t rows, int D,
+                                                        const float* __restrict__ cb, float margin,
+                                                        int32_t* __restrict__ idx_out, float* __restrict__ xn_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + row * D;
+  // f32 l2norm of x (F.normalize, eps 1e-12)
+  float ss = 0.f;
+  for (int c = lane; c < D; c += 64) ss += xr[c] * xr[c];
+  ss = warp_sum(ss);
+  const float inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
+  // best bf16 score over tiles
+  float best = -INFINITY;
+  for (int t = lane; t < ntiles; t += 64) best = fmaxf(best, cand[row * ntiles + t].x);
+  best = warp_max(best);
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int t0 = 0; t0 < ntiles; t0 += 64) {
+    const int t = t0 + lane;
+    bool take = false;
+    float2 c = make_float2(-INFINITY, 0.f);
+    if (t < ntiles) { c = cand[row * ntiles + t]; take = c.x >= best - margin; }
+    unsigned long long mask = __ballot(take);
+    while (mask) {
+      const int src = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      const int ci = __float_as_int(__shfl(c.y, src, 64));
+      const float* cr = cb + (int64_t)ci * D;
+      float d = 0.f;
+      for (int k = lane; k < D; k += 64) d += xr[k] * inv * cr[k];
+      d = warp_sum(d);
+      if (d > bv || (d == bv && ci < bi)) { bv = d; bi = ci; }
+    }
+  }
+  if (lane == 0) idx_out[row] = bi;
+  if (xn_out)
+    for (int c = lane; c < D; c += 64) xn_out[row * D + c] = xr[c] * inv;
+}
+
+// pooled[b][hw][d] = (1/T) sum_t cb[idx[b][t*HW + hw]][d]
+__global__ __launch_bounds__(256) void vq_pool_kernel(const int32_t* __restrict__ idx, const float* __restrict__ cb,
+                                                      int64_t B, int T, int HW, int D, float* __restrict__ out,
+                                                      u16* __restrict__ outb) {
+  const int nch = D / 4;
+  const int64_t total = B * HW * nch;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % nch);
+    const int64_t bh = i / nch;
+    const int hw = (int)(bh % HW);
+    const int64_t b = bh / HW;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < T; ++t) {
+      const int ci = idx[b * (int64_t)T * HW + (int64_t)t * HW + hw];
+      acc += *(const f32x4*)(cb + (int64_t)ci * D + c * 4);
+    }
+    acc *= (1.f / (float)T);
+    if (out) *(f32x4*)(out + bh * D + c * 4) = acc;
+    if (outb) {
+      uint2 pk;
+      pk.x = pack2(acc[0], acc[1]);
+      pk.y = pack2(acc[2], acc[3]);
+      *(uint2*)(outb + bh * D + c * 4) = pk;
+    }
+  }
+}
+
+// out[r][:] = cb[idx[r]][:]
+__global__ __launch_bounds__(256) void vq_gather_kernel(const int32_t* __restrict__ idx, const float* __restrict__ cb,
+                                                        int64_t rows, int D, float* __restrict__ out) {
+  const int nch = D / 4;
+  const int64_t total = rows * nch;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / nch;
+    const int c = (int)(i - r * nch);
+    *(f32x4*)(out + r * D + c * 4) = *(const f32x4*)(cb + (int64_t)idx[r] * D + c * 4);
+  }
+}
+
+// EMA statistics: bins[c] += count, esum[c][:] += xn rows (f32 atomics)
+__global__ __launch_bounds__(256) void vq_ema_accum_kernel(const int32_t* __restrict__ idx,
+                                                           const float* __restrict__ xn, int64_t rows, int D,
+                                                           float* __restrict__ bins, float* __restrict__ esum) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += nw) {
+    const int ci = idx[row];
+    if (lane == 0) atomicAdd(&bins[ci], 1.f);
+    for (int c = lane; c < D; c += 64) atomicAdd(&esum[(int64_t)ci * D + c], xn[row * D + c]);
+  }
+}
+
+// cluster_size = cs*decay + bins*(1-decay);  en = l2norm(esum / max(bins,1)); zero bins keep the
+// old code;  embed = embed*decay + en*(1-decay);  also refresh the bf16 working codebook.
+__global__ __launch_bounds__(64) void vq_ema_finalize_kernel(const float* __restrict__ bins,
+                                                             const float* __restrict__ esum, int C, int D,
+                                                             float decay, float* __restrict__ embed,
+                                                             float* __restrict__ cluster, u16* __restrict__ embed_bf16) {
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x;
+  const float nb = bins[c];
+  if (lane == 0) cluster[c] = cluster[c] * decay + nb * (1.f - decay);
+  float* e = embed + (int64_t)c * D;
+  if (nb == 0.f) {
+    if (embed_bf16)
+      for (int k = lane; k < D; k += 64) embed_bf16[(int64_t)c * D + k] = f2bf(e[k]);
+    return;
+  }
+  const float* s = esum + (int64_t)c * D;
+  float ss = 0.f;
+  for (int k = lane; k < D; k += 64) { const float v = s[k] / nb; ss += v * v; }
+  ss = warp_sum(ss);
+  const float inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
+  for (int k = lane; k < D; k += 64) {
+    const float en = s[k] / nb * inv;
+    const float v = e[k] * decay + en * (1.f - decay);
+    e[k] = v;
+    if (embed_bf16) embed_bf16[(int64_t)c * D + k] = f2bf(v);
+  }
+}
+
+inline int gridn(int64_t n) { return (int)std::min<int64_t>(8192, std::max<int64_t>(1, (n + 255) / 256)); }
+
+}  // namespace
+
+extern "C" int ctclip_vq_select(const float* cand, int32_t ntiles, const float* x, int64_t rows, int32_t D,
+                                const float* codebook, float margin, int32_t* idx, float* xn_out, void* stream) {
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(vq_select_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, (hipStream_t)stream, (const float2*)cand,
+                     ntiles, x, rows, D, codebook, margin, idx, xn_out);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_vq_pool(const int32_t* idx, const float* codebook, int64_t B, int32_t T, int32_t HW, int32_t D,
+                              float* out, void* out_bf16, void* stream) {
+  CT_REQUIRE(D % 4 == 0, CT_EALIGN);
+  hipLaunchKernelGGL(vq_pool_kernel, dim3(gridn(B * HW * D / 4)), dim3(256), 0, (hipStream_t)stream, idx, codebook, B,
+                     T, HW, D, out, (u16*)out_bf16);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_vq_gather(const int32_t* idx, const float* codebook, int64_t rows, int32_t D, float* out,
+                                void* stream) {
+  CT_REQUIRE(D % 4 == 0, CT_EALIGN);
+  hipLaunchKernelGGL(vq_gather_kernel, dim3(gridn(rows * D / 4)), dim3(256), 0, (hipStream_t)stream, idx, codebook,
+                     rows, D, out);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_vq_ema_accum(const int32_t* idx, const float* xn, int64_t rows, int32_t D, float* bins,
+                                   float* esum, void* stream) {
+  const int blocks = (int)std::min<int64_t>(4096, std::max<int64_t>(1, rows / 16));
+  hipLaunchKernelGGL(vq_ema_accum_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, idx, xn, rows, D, bins,
+                     esum);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_vq_ema_finalize(const float* bins, const float* esum, int32_t C, int32_t D, float decay,
+                                      float* embed, float* cluster_size, void* embed_bf16, void* stream) {
+  hipLaunchKernelGGL(vq_ema_finalize_kernel, dim3(C), dim3(64), 0, (hipStream_t)stream, bins, esum, C, D, decay,
+                     embed, cluster_size, (u16*)embed_bf16);
+  CT_CHECK_LAUNCH();
+  return 0;
+}

@@ -39,12 +39,57 @@ class GemmArgs(ctypes.Structure):
     ]
 
 
+class AttnArgs(ctypes.Structure):
+    _fields_ = [
+        ('q', c_vp), ('ldq', c_i64), ('k', c_vp), ('ldk', c_i64), ('v', c_vp), ('ldv', c_i64),
+        ('o', c_vp), ('ldo', c_i64), ('dout', c_vp), ('lddo', c_i64),
+        ('dq', c_vp), ('lddq', c_i64), ('dk', c_vp), ('lddk', c_i64), ('dv', c_vp), ('lddv', c_i64),
+        ('lse', c_vp), ('delta', c_vp), ('bias_u', c_vp), ('dbias_u', c_vp), ('kmask', c_vp),
+        ('scale', c_f32), ('L', c_i32), ('H', c_i32), ('D', c_i32), ('nseq', c_i32), ('M', c_i64),
+        ('grid_h', c_i32), ('grid_w', c_i32), ('n_inner', c_i32),
+        ('s_outer', c_i64), ('s_inner', c_i64), ('s_pos', c_i64),
+    ]
+
+
 # name -> argtypes (restype is always int32)
 _SIGS = {
     'ctclip_version': [],
     'ctclip_device_arch': [ctypes.c_char_p, c_i32],
     'ctclip_gemm': [ctypes.POINTER(GemmArgs), c_vp],
     'ctclip_reduce_slabs': [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp],
+    'ctclip_layernorm_fwd': [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_f32, c_vp, c_i64, c_vp, c_i64,
+                             c_vp, c_vp, c_vp],
+    'ctclip_layernorm_bwd': [c_vp, c_i32, c_i64, c_vp, c_i32, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_i64,
+                             c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp],
+    'ctclip_l2norm_scale_fwd': [c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp],
+    'ctclip_l2norm_scale_bwd': [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],
+    'ctclip_colsum': [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_i32, c_vp],
+    'ctclip_geglu_bwd': [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
+    'ctclip_gelu_bwd': [c_vp, c_vp, c_vp, c_i64, c_vp],
+    'ctclip_pack_rows': [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp],
+    'ctclip_unpack_rows': [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp],
+    'ctclip_cast_f32_bf16': [c_vp, c_vp, c_i64, c_vp],
+    'ctclip_add_f32': [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
+    'ctclip_patch_ln': [c_vp, c_i32, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp, c_vp],
+    'ctclip_patch_wgrad': [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp],
+    'ctclip_peg_fwd': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp],
+    'ctclip_peg_bwd_data': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp],
+    'ctclip_peg_bwd_weight': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp],
+    'ctclip_attn_fwd': [ctypes.POINTER(AttnArgs), c_vp],
+    'ctclip_attn_bwd': [ctypes.POINTER(AttnArgs), c_vp],
+    'ctclip_vq_select': [c_vp, c_i32, c_vp, c_i64, c_i32, c_vp, c_f32, c_vp, c_vp, c_vp],
+    'ctclip_vq_pool': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
+    'ctclip_vq_gather': [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp],
+    'ctclip_vq_ema_accum': [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp],
+    'ctclip_vq_ema_finalize': [c_vp, c_vp, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp],
+    'ctclip_clip_loss': [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
+    'ctclip_clip_scores': [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp],
+    'ctclip_sgemm': [c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_f32,
+                     c_i32, c_f32, c_vp, c_i64, c_i64, c_i32, c_vp],
+    'ctclip_embed_fwd': [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
+    'ctclip_embed_bwd': [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
+    'ctclip_grad_norm': [c_vp, c_i64, c_f32, c_vp, c_i32, c_vp, c_vp],
+    'ctclip_adam': [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_i32, c_vp, c_vp, c_vp],
 }
 
 

@@ -94,3 +94,317 @@ def reduce_slabs(slabs, out, accumulate=False):
     call('ctclip_reduce_slabs', ptr(slabs), s, rows, cols, cols, ptr(out), out.stride(0),
          int(out.dtype == F32), int(accumulate), stream_ptr())
     return out
+
+
+# ----------------------------------------------------------------------------- reductions
+def nblocks_for(rows, cap=1024):
+    return int(max(1, min(cap, (rows + 63) // 64)))
+
+
+def colsum(x, out=None, accumulate=False):
+    """Column sums of x[rows, cols] (bf16 or f32) -> f32 [cols]."""
+    rows, cols = x.shape
+    nb = nblocks_for(rows, 512)
+    part = torch.empty(nb, cols, device=x.device, dtype=F32)
+    call('ctclip_colsum', ptr(x), int(x.dtype == F32), x.stride(0), rows, cols, ptr(part), nb, stream_ptr())
+    if out is None:
+        out = torch.zeros(cols, device=x.device, dtype=F32) if accumulate else torch.empty(cols, device=x.device,
+                                                                                           dtype=F32)
+    reduce_slabs(part.view(nb, 1, cols), out.view(1, cols), accumulate=accumulate)
+    return out
+
+
+# ----------------------------------------------------------------------------- LayerNorm
+def layernorm_fwd(x, gamma, beta, eps, *, out_bf16=True, out_f32=False):
+    rows, D = x.shape
+    yb = torch.empty(rows, D, device=x.device, dtype=BF16) if out_bf16 else None
+    yf = torch.empty(rows, D, device=x.device, dtype=F32) if out_f32 else None
+    mean = torch.empty(rows, device=x.device, dtype=F32)
+    rstd = torch.empty(rows, device=x.device, dtype=F32)
+    call('ctclip_layernorm_fwd', ptr(x), int(x.dtype == F32), x.stride(0), rows, D, ptr(gamma), ptr(beta), eps,
+         ptr(yb), D, ptr(yf), D, ptr(mean), ptr(rstd), stream_ptr())
+    return yb, yf, mean, rstd
+
+
+def layernorm_bwd(dy, x, mean, rstd, gamma, *, dres=None, want_beta=True, dx_f32=True, dx_bf16=True):
+    """Returns (dx_f32, dx_bf16, dgamma, dbeta)."""
+    rows, D = x.shape
+    nb = nblocks_for(rows, 1024)
+    dxf = torch.empty(rows, D, device=x.device, dtype=F32) if dx_f32 else None
+    dxb = torch.empty(rows, D, device=x.device, dtype=BF16) if dx_bf16 else None
+    pg = torch.empty(nb, D, device=x.device, dtype=F32)
+    pb = torch.empty(nb, D, device=x.device, dtype=F32) if want_beta else None
+    call('ctclip_layernorm_bwd', ptr(dy), int(dy.dtype == F32), dy.stride(0), ptr(x), int(x.dtype == F32),
+         x.stride(0), ptr(mean), ptr(rstd), ptr(gamma), rows, D, ptr(dres),
+         dres.stride(0) if dres is not None else 0, ptr(dxf), D, ptr(dxb), D, ptr(pg), ptr(pb), nb, stream_ptr())
+    dg = torch.empty(D, device=x.device, dtype=F32)
+    reduce_slabs(pg.view(nb, 1, D), dg.view(1, D))
+    db = None
+    if want_beta:
+        db = torch.empty(D, device=x.device, dtype=F32)
+        reduce_slabs(pb.view(nb, 1, D), db.view(1, D))
+    return dxf, dxb, dg, db
+
+
+def l2norm_scale_fwd(x, H, D, scale, out=None):
+    rows = x.shape[0]
+    if out is None:
+        out = torch.empty(rows, H * D, device=x.device, dtype=BF16)
+    call('ctclip_l2norm_scale_fwd', ptr(x), x.stride(0), rows, H, D, ptr(scale), ptr(out), out.stride(0),
+         stream_ptr())
+    return out
+
+
+def l2norm_scale_bwd(x, dy, H, D, scale, out):
+    rows = x.shape[0]
+    lpr = H * D // 8
+    nb = 512
+    while (nb * 256) % lpr:
+        nb += 1
+    part = torch.empty(nb, D, device=x.device, dtype=F32)
+    call('ctclip_l2norm_scale_bwd', ptr(x), x.stride(0), ptr(dy), dy.stride(0), rows, H, D, ptr(scale), ptr(out),
+         out.stride(0), ptr(part), nb, stream_ptr())
+    ds = torch.empty(D, device=x.device, dtype=F32)
+    reduce_slabs(part.view(nb, 1, D), ds.view(1, D))
+    return ds
+
+
+# ----------------------------------------------------------------------------- elementwise
+def geglu_bwd(dg, h, out=None):
+    rows, gcols = dg.shape
+    if out is None:
+        out = torch.empty(rows, 2 * gcols, device=dg.device, dtype=BF16)
+    call('ctclip_geglu_bwd', ptr(dg), dg.stride(0), ptr(h), h.stride(0), rows, gcols, ptr(out), out.stride(0),
+         stream_ptr())
+    return out
+
+
+def gelu_bwd(dy, pre):
+    out = torch.empty_like(pre)
+    call('ctclip_gelu_bwd', ptr(dy), ptr(pre), ptr(out), pre.numel(), stream_ptr())
+    return out
+
+
+def pack_rows(src, rows_dst, cols_dst, rowmap=None, colscale=None, out=None):
+    rows, cols = src.shape
+    if out is None:
+        out = torch.empty(rows_dst, cols_dst, device=src.device, dtype=BF16)
+    call('ctclip_pack_rows', ptr(src), src.stride(0), ptr(rowmap), rows_dst, cols, cols_dst, ptr(colscale), ptr(out),
+         out.stride(0), stream_ptr())
+    return out
+
+
+def unpack_rows(src, dst, rowmap=None, cols=None, accumulate=True):
+    rows_src = src.shape[0]
+    cols = dst.shape[1] if cols is None else cols
+    call('ctclip_unpack_rows', ptr(src), src.stride(0), ptr(rowmap), rows_src, cols, ptr(dst), dst.stride(0),
+         int(accumulate), stream_ptr())
+    return dst
+
+
+def cast_bf16(x, out=None):
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=BF16)
+    call('ctclip_cast_f32_bf16', ptr(x), ptr(out), x.numel(), stream_ptr())
+    return out
+
+
+def add_f32(a, b, out=None, out_bf16=None):
+    call('ctclip_add_f32', ptr(a), ptr(b), ptr(out), ptr(out_bf16), a.numel(), stream_ptr())
+
+
+# ----------------------------------------------------------------------------- patch embed
+def patch_ln(video, is_hu, PT, P, offs, eps=1e-5):
+    B, C, Fr, H, W = video.shape
+    T, Hg, Wg = Fr // PT, H // P, W // P
+    pd = C * PT * P * P
+    out = torch.empty(B * T * Hg * Wg, pd, device=video.device, dtype=BF16)
+    call('ctclip_patch_ln', ptr(video), int(video.dtype == F32), int(is_hu), B, C, Fr, H, W, PT, P, ptr(offs), eps,
+         ptr(out), stream_ptr())
+    return out
+
+
+def patch_wgrad(G, cs, W, g, b, dW, dg, db, accumulate=True):
+    N, K = G.shape
+    call('ctclip_patch_wgrad', ptr(G), ptr(cs), ptr(W), ptr(g), ptr(b), N, K, ptr(dW), ptr(dg), ptr(db),
+         int(accumulate), stream_ptr())
+
+
+# ----------------------------------------------------------------------------- PEG
+def peg_fwd(xb, xf, B, T, H, W, weight, bias, mode):
+    D = xb.shape[1]
+    outf = torch.empty_like(xf)
+    outb = torch.empty_like(xb)
+    call('ctclip_peg_fwd', ptr(xb), ptr(xf), B, T, H, W, D, ptr(weight), ptr(bias), mode, ptr(outf), ptr(outb),
+         stream_ptr())
+    return outf, outb
+
+
+def peg_bwd(doutb, doutf, xb, B, T, H, W, weight, mode):
+    """Returns (dx_f32, dx_bf16, dweight [D,27], dbias [D])."""
+    D = xb.shape[1]
+    dxf = torch.empty_like(doutf)
+    dxb = torch.empty_like(doutb)
+    call('ctclip_peg_bwd_data', ptr(doutb), ptr(doutf), B, T, H, W, D, ptr(weight), mode, ptr(dxf), ptr(dxb),
+         stream_ptr())
+    nblk = 256
+    part = torch.empty(nblk, D * 28, device=xb.device, dtype=F32)
+    call('ctclip_peg_bwd_weight', ptr(doutb), ptr(xb), B, T, H, W, D, mode, ptr(part), nblk, stream_ptr())
+    red = torch.empty(D * 28, device=xb.device, dtype=F32)
+    reduce_slabs(part.view(nblk, 1, D * 28), red.view(1, D * 28))
+    red = red.view(D, 28)
+    return dxf, dxb, red[:, :27], red[:, 27]
+
+
+# ----------------------------------------------------------------------------- attention
+def _attn_args(q, k, v, o, *, L, H, D, nseq, M, scale, seq, bias_u=None, grid=(0, 0), kmask=None, lse=None,
+               dout=None, dq=None, dk=None, dv=None, delta=None, dbias_u=None):
+    a = _lib.AttnArgs()
+    a.q, a.ldq = ptr(q), q.stride(0)
+    a.k, a.ldk = ptr(k), k.stride(0)
+    a.v, a.ldv = ptr(v), v.stride(0)
+    a.o, a.ldo = ptr(o), o.stride(0)
+    a.dout, a.lddo = ptr(dout), dout.stride(0) if dout is not None else 0
+    a.dq, a.lddq = ptr(dq), dq.stride(0) if dq is not None else 0
+    a.dk, a.lddk = ptr(dk), dk.stride(0) if dk is not None else 0
+    a.dv, a.lddv = ptr(dv), dv.stride(0) if dv is not None else 0
+    a.lse, a.delta = ptr(lse), ptr(delta)
+    a.bias_u, a.dbias_u, a.kmask = ptr(bias_u), ptr(dbias_u), ptr(kmask)
+    a.scale, a.L, a.H, a.D, a.nseq, a.M = scale, L, H, D, nseq, M
+    a.grid_h, a.grid_w = grid
+    a.n_inner, a.s_outer, a.s_inner, a.s_pos = seq
+    return a
+
+
+def attn_fwd(q, k, v, *, L, H, D, nseq, scale, seq, bias_u=None, grid=(0, 0), kmask=None):
+    """q/k/v: 2D views [M, ...] whose head h occupies columns h*D:(h+1)*D.  Returns (o [M, H*D], lse [H, M])."""
+    M = q.shape[0]
+    o = torch.empty(M, H * D, device=q.device, dtype=BF16)
+    lse = torch.empty(H, M, device=q.device, dtype=F32)
+    a = _attn_args(q, k, v, o, L=L, H=H, D=D, nseq=nseq, M=M, scale=scale, seq=seq, bias_u=bias_u, grid=grid,
+                   kmask=kmask, lse=lse)
+    call('ctclip_attn_fwd', _lib.ctypes.byref(a), stream_ptr())
+    return o, lse
+
+
+def attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, *, L, H, D, nseq, scale, seq, bias_u=None, dbias_u=None,
+             grid=(0, 0), kmask=None):
+    M = q.shape[0]
+    delta = torch.empty(H, M, device=q.device, dtype=F32)
+    a = _attn_args(q, k, v, o, L=L, H=H, D=D, nseq=nseq, M=M, scale=scale, seq=seq, bias_u=bias_u, grid=grid,
+                   kmask=kmask, lse=lse, dout=dout, dq=dq, dk=dk, dv=dv, delta=delta, dbias_u=dbias_u)
+    call('ctclip_attn_bwd', _lib.ctypes.byref(a), stream_ptr())
+
+
+# ----------------------------------------------------------------------------- VQ
+def vq_select(cand, x, codebook_f32, margin=2e-2, want_xn=True):
+    rows, D = x.shape
+    idx = torch.empty(rows, device=x.device, dtype=torch.int32)
+    xn = torch.empty(rows, D, device=x.device, dtype=F32) if want_xn else None
+    call('ctclip_vq_select', ptr(cand), cand.shape[1], ptr(x), rows, D, ptr(codebook_f32), margin, ptr(idx), ptr(xn),
+         stream_ptr())
+    return idx, xn
+
+
+def vq_pool(idx, codebook_f32, B, T, HW, want_bf16=True):
+    D = codebook_f32.shape[1]
+    out = torch.empty(B, HW * D, device=idx.device, dtype=F32)
+    outb = torch.empty(B, HW * D, device=idx.device, dtype=BF16) if want_bf16 else None
+    call('ctclip_vq_pool', ptr(idx), ptr(codebook_f32), B, T, HW, D, ptr(out), ptr(outb), stream_ptr())
+    return out, outb
+
+
+def vq_gather(idx, codebook_f32):
+    D = codebook_f32.shape[1]
+    out = torch.empty(idx.numel(), D, device=idx.device, dtype=F32)
+    call('ctclip_vq_gather', ptr(idx), ptr(codebook_f32), idx.numel(), D, ptr(out), stream_ptr())
+    return out
+
+
+def vq_ema_accum(idx, xn, bins, esum):
+    call('ctclip_vq_ema_accum', ptr(idx), ptr(xn), xn.shape[0], xn.shape[1], ptr(bins), ptr(esum), stream_ptr())
+
+
+def vq_ema_finalize(bins, esum, decay, embed, cluster, embed_bf16=None):
+    C, D = esum.shape
+    call('ctclip_vq_ema_finalize', ptr(bins), ptr(esum), C, D, decay, ptr(embed), ptr(cluster), ptr(embed_bf16),
+         stream_ptr())
+
+
+# ----------------------------------------------------------------------------- loss
+def clip_loss(t_raw, i_raw, log_temp):
+    Bg, Dl = t_raw.shape
+    dev = t_raw.device
+    tn = torch.empty_like(t_raw)
+    inn = torch.empty_like(i_raw)
+    loss = torch.empty(1, device=dev, dtype=F32)
+    dt = torch.empty_like(t_raw)
+    di = torch.empty_like(i_raw)
+    dlt = torch.empty(1, device=dev, dtype=F32)
+    sim = torch.empty(Bg, Bg, device=dev, dtype=F32)
+    call('ctclip_clip_loss', ptr(t_raw), ptr(i_raw), Bg, Dl, ptr(log_temp), ptr(tn), ptr(inn), ptr(loss), ptr(dt),
+         ptr(di), ptr(dlt), ptr(sim), stream_ptr())
+    return loss, dt, di, dlt, tn, inn, sim
+
+
+def clip_scores(t_raw, i_raw, log_temp):
+    B, Dl = t_raw.shape
+    out = torch.empty(B, device=t_raw.device, dtype=F32)
+    call('ctclip_clip_scores', ptr(t_raw), ptr(i_raw), B, Dl, ptr(log_temp), ptr(out), stream_ptr())
+    return out
+
+
+# ----------------------------------------------------------------------------- sgemm
+def sgemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, *, bias=None, alpha=1.0, act=0, slope=0.1, aux=None,
+          sxm=0, sxn=0, accumulate=False):
+    call('ctclip_sgemm', M, N, K, ptr(A), sam, sak, ptr(B), sbk, sbn, ptr(C), scm, scn, ptr(bias), alpha, act, slope,
+         ptr(aux), sxm, sxn, int(accumulate), stream_ptr())
+    return C
+
+
+def slinear(x, w, bias=None, act=0, slope=0.1, out=None, accumulate=False):
+    """f32 y = x @ w^T (+b), x [M,K], w [N,K] (any strides)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=F32)
+    return sgemm(M, N, K, x, x.stride(0), x.stride(1), w, w.stride(1), w.stride(0), out, out.stride(0),
+                 out.stride(1), bias=bias, act=act, slope=slope, accumulate=accumulate)
+
+
+def smm(a, b, out=None, accumulate=False, act=0, slope=0.1, aux=None):
+    """f32 out = a @ b for 2D strided views; act=2 multiplies by LeakyReLU'(aux)."""
+    M, K = a.shape
+    N = b.shape[1]
+    if out is None:
+        out = torch.empty(M, N, device=a.device, dtype=F32)
+    return sgemm(M, N, K, a, a.stride(0), a.stride(1), b, b.stride(0), b.stride(1), out, out.stride(0),
+                 out.stride(1), act=act, slope=slope, aux=aux, sxm=aux.stride(0) if aux is not None else 0,
+                 sxn=aux.stride(1) if aux is not None else 0, accumulate=accumulate)
+
+
+# ----------------------------------------------------------------------------- BERT embeddings
+def embed_fwd(ids, word, pos, type0):
+    B, L = ids.shape
+    Hd = word.shape[1]
+    out = torch.empty(B * L, Hd, device=ids.device, dtype=F32)
+    call('ctclip_embed_fwd', ptr(ids), B, L, Hd, ptr(word), ptr(pos), ptr(type0), ptr(out), stream_ptr())
+    return out
+
+
+def embed_bwd(ids, dx, dword, dpos, dtype0):
+    B, L = ids.shape
+    call('ctclip_embed_bwd', ptr(ids), B, L, dx.shape[1], ptr(dx), ptr(dword), ptr(dpos), ptr(dtype0), stream_ptr())
+
+
+# ----------------------------------------------------------------------------- optimizer
+def grad_norm(g, max_norm, out):
+    nblk = 1024
+    part = torch.empty(nblk, device=g.device, dtype=F32)
+    call('ctclip_grad_norm', ptr(g), g.numel(), max_norm, ptr(part), nblk, ptr(out), stream_ptr())
+    return out
+
+
+def adam(p, g, m, v, *, lr, b1, b2, eps, wd, step, coef=None, p_bf16=None):
+    call('ctclip_adam', ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, b1, b2, eps, wd, step, ptr(coef), ptr(p_bf16),
+         stream_ptr())

@@ -60,6 +60,142 @@ int ctclip_gemm(const ctclip_gemm_args* a, void* stream);
 int ctclip_reduce_slabs(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,
                         void* out, int64_t ldo, int32_t out_f32, int32_t accumulate, void* stream);
 
+
+/* ---------------------------------------------------------------- LayerNorm family
+ * ct_clip/attention.py:28-35 (bias-less LayerNorm: gamma, beta = 0 buffer, eps 1e-5),
+ * nn.LayerNorm in FeedForward / to_patch_emb (attention.py:47, ctvit.py:171,173), BERT LayerNorms.
+ * x, y row-major with leading dims; f32 statistics; y in bf16 and/or f32.  D % 8 == 0. */
+int ctclip_layernorm_fwd(const void* x, int32_t x_f32, int64_t ldx, int64_t rows, int32_t D,
+                         const float* gamma, const float* beta, float eps,
+                         void* y_bf16, int64_t ldyb, float* y_f32, int64_t ldyf,
+                         float* mean, float* rstd, void* stream);
+/* dx = LN'(dy) [+ dres]; per-block partial dgamma/dbeta [nblocks][D] (reduce with
+ * ctclip_reduce_slabs).  D <= 1024. */
+int ctclip_layernorm_bwd(const void* dy, int32_t dy_f32, int64_t lddy, const void* x, int32_t x_f32, int64_t ldx,
+                         const float* mean, const float* rstd, const float* gamma, int64_t rows, int32_t D,
+                         const float* dres, int64_t lddres, float* dx_f32, int64_t lddxf,
+                         void* dx_bf16, int64_t lddxb, float* part_gamma, float* part_beta,
+                         int32_t nblocks, void* stream);
+/* per-head l2norm * scale (attention.py:152-154): y[:, h*D:(h+1)*D] = x / max(|x|,1e-12) * scale */
+int ctclip_l2norm_scale_fwd(const void* x, int64_t ldx, int64_t rows, int32_t H, int32_t D,
+                            const float* scale, void* y, int64_t ldy, void* stream);
+int ctclip_l2norm_scale_bwd(const void* x, int64_t ldx, const void* dy, int64_t lddy, int64_t rows,
+                            int32_t H, int32_t D, const float* scale, void* dx, int64_t lddx,
+                            float* part_scale, int32_t nblocks, void* stream);
+/* per-block column-sum partials [nblocks][cols] (bias gradients) */
+int ctclip_colsum(const void* x, int32_t x_f32, int64_t ld, int64_t rows, int32_t cols, float* part,
+                  int32_t nblocks, void* stream);
+
+/* ---------------------------------------------------------------- elementwise / layout
+ * GEGLU backward on the tile-interleaved pre-activation (FeedForward, attention.py:39-52) */
+int ctclip_geglu_bwd(const void* dg, int64_t lddg, const void* h, int64_t ldh, int64_t rows, int32_t gcols,
+                     void* dh, int64_t lddh, void* stream);
+int ctclip_gelu_bwd(const void* dy, const void* pre, void* dx, int64_t n, void* stream);
+/* bf16 working weights from f32 masters: dst[r][c] = src[map[r]][c] * colscale[c] (zero pads) */
+int ctclip_pack_rows(const float* src, int64_t ld_src, const int32_t* map, int64_t rows_dst, int32_t cols,
+                     int32_t cols_dst, const float* colscale, void* dst, int64_t ld_dst, void* stream);
+int ctclip_unpack_rows(const float* src, int64_t ld_src, const int32_t* map, int64_t rows_src, int32_t cols,
+                       float* dst, int64_t ld_dst, int32_t accumulate, void* stream);
+int ctclip_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
+int ctclip_add_f32(const float* a, const float* b, float* y, void* y_bf16, int64_t n, void* stream);
+
+/* ---------------------------------------------------------------- patch embedding
+ * int16 HU (is_hu: clamp(-1000,1000)/1000.f, ct_clip/data.py:150-152) or f32 video
+ * (B, C, F, H, W) -> xhat (B*T*Hg*Wg, C*PT*P*P) bf16 = LayerNorm statistics applied
+ * (ctvit.py:170-171).  offs[e] = voxel offset of patch element e from the patch origin. */
+int ctclip_patch_ln(const void* video, int32_t is_f32, int32_t is_hu, int64_t B, int32_t C, int32_t F,
+                    int32_t H, int32_t W, int32_t PT, int32_t P, const int32_t* offs, float eps,
+                    void* xhat, void* stream);
+int ctclip_patch_wgrad(const float* G, const float* colsum_dy, const float* W, const float* gamma,
+                       const float* beta, int32_t N, int32_t K, float* dW, float* dgamma, float* dbeta,
+                       int32_t accumulate, void* stream);
+
+/* ---------------------------------------------------------------- PEG (attention.py:56-84)
+ * causal depthwise 3x3x3 conv + residual on canonical (b,t,h,w) token rows; mode 0 = spatial
+ * view, mode 1 = the temporal transformer's raw-reshape view (attention.py:69-70). */
+int ctclip_peg_fwd(const void* x_bf16, const float* x_f32, int64_t B, int32_t T, int32_t H, int32_t W,
+                   int32_t D, const float* weight, const float* bias, int32_t mode, float* out_f32,
+                   void* out_bf16, void* stream);
+int ctclip_peg_bwd_data(const void* dout_bf16, const float* dout_f32, int64_t B, int32_t T, int32_t H,
+                        int32_t W, int32_t D, const float* weight, int32_t mode, float* dx_f32,
+                        void* dx_bf16, void* stream);
+int ctclip_peg_bwd_weight(const void* dout_bf16, const void* x_bf16, int64_t B, int32_t T, int32_t H,
+                          int32_t W, int32_t D, int32_t mode, float* part, int32_t nblk, void* stream);
+
+/* ---------------------------------------------------------------- attention (attention.py:127-181)
+ * softmax(scale * q.k^T + bias + mask) v per (sequence, head); q/k already l2-normalised and
+ * scaled for CTViT.  Sequence rows: row(s,i) = (s/n_inner)*s_outer + (s%n_inner)*s_inner + i*s_pos.
+ * bias_u: deduplicated continuous-position-bias table [H][(2gh-1)(2gw-1)] (attention.py:229-276).
+ * bwd: writes dq, dk, dv (bf16), delta [H][M], accumulates dbias_u with atomics. */
+typedef struct {
+  const void* q; int64_t ldq;
+  const void* k; int64_t ldk;
+  const void* v; int64_t ldv;
+  void* o; int64_t ldo;
+  const void* dout; int64_t lddo;
+  void* dq; int64_t lddq;
+  void* dk; int64_t lddk;
+  void* dv; int64_t lddv;
+  float* lse; float* delta;
+  const float* bias_u; float* dbias_u;
+  const int32_t* kmask;
+  float scale;
+  int32_t L, H, D, nseq;
+  int64_t M;
+  int32_t grid_h, grid_w;
+  int32_t n_inner;
+  int64_t s_outer, s_inner, s_pos;
+} ctclip_attn_args;
+int ctclip_attn_fwd(const ctclip_attn_args* a, void* stream);
+int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream);
+
+/* ---------------------------------------------------------------- vector quantiser
+ * vector_quantize_pytorch==1.1.2 cosine codebook (ct_clip/ctvit.py:187,421-427).
+ * cand = float2[rows][ntiles] (score, index) from ctclip_gemm(act=3) over l2norm(x).codebook_bf16^T;
+ * select re-scores in f32 every candidate within `margin` of the best -> exact f32 argmax. */
+int ctclip_vq_select(const float* cand, int32_t ntiles, const float* x, int64_t rows, int32_t D,
+                     const float* codebook, float margin, int32_t* idx, float* xn_out, void* stream);
+/* pooled[b][hw][:] = mean_t codebook[idx[b][t*HW+hw]]   (ct_clip/ct_clip.py:724,740) */
+int ctclip_vq_pool(const int32_t* idx, const float* codebook, int64_t B, int32_t T, int32_t HW, int32_t D,
+                   float* out, void* out_bf16, void* stream);
+int ctclip_vq_gather(const int32_t* idx, const float* codebook, int64_t rows, int32_t D, float* out, void* stream);
+/* training-mode EMA codebook update (bins / embed_sum accumulate, then finalize) */
+int ctclip_vq_ema_accum(const int32_t* idx, const float* xn, int64_t rows, int32_t D, float* bins, float* esum,
+                        void* stream);
+int ctclip_vq_ema_finalize(const float* bins, const float* esum, int32_t C, int32_t D, float decay, float* embed,
+                           float* cluster_size, void* embed_bf16, void* stream);
+
+/* ---------------------------------------------------------------- contrastive loss
+ * symmetric InfoNCE over the (global) batch, ct_clip/ct_clip.py:771,796,845-901; one workgroup.
+ * Inputs are raw projected latents; returns loss, d loss / d raw latents, d loss / d log-temp. */
+int ctclip_clip_loss(const float* t_raw, const float* i_raw, int32_t Bg, int32_t Dl, const float* log_temp,
+                     float* t_norm, float* i_norm, float* loss, float* dt_raw, float* di_raw, float* dlogtemp,
+                     float* sim, void* stream);
+/* eval branch einsum('b d, b d -> b') * temp (ct_clip.py:805-807) */
+int ctclip_clip_scores(const float* t_raw, const float* i_raw, int32_t B, int32_t Dl, const float* log_temp,
+                       float* out, void* stream);
+
+/* ---------------------------------------------------------------- small exact-f32 GEMM (strided)
+ * CPB MLP (attention.py:247-252,271-274) and its backward; act 1 = LeakyReLU(slope),
+ * act 2 = multiply by LeakyReLU'(aux). */
+int ctclip_sgemm(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam, int64_t sak, const float* B,
+                 int64_t sbk, int64_t sbn, float* C, int64_t scm, int64_t scn, const float* bias, float alpha,
+                 int32_t act, float slope, const float* aux, int64_t sxm, int64_t sxn, int32_t accumulate,
+                 void* stream);
+
+/* ---------------------------------------------------------------- BERT embeddings */
+int ctclip_embed_fwd(const int64_t* ids, int64_t B, int32_t L, int32_t Hd, const float* word, const float* pos,
+                     const float* type0, float* out, void* stream);
+int ctclip_embed_bwd(const int64_t* ids, int64_t B, int32_t L, int32_t Hd, const float* dx, float* dword,
+                     float* dpos, float* dtype0, void* stream);
+
+/* ---------------------------------------------------------------- optimizer (CTCLIPTrainer.py:347-353)
+ * grad norm -> out[0] = norm, out[1] = clip coef (torch clip_grad_norm_ semantics);
+ * Adam over a flat arena (optimizer.py:24), grads scaled by coef[1], bf16 copy refreshed. */
+int ctclip_grad_norm(const float* g, int64_t n, float max_norm, float* part, int32_t nblk, float* out, void* stream);
+int ctclip_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
+                float wd, int32_t step, const float* coef, void* p_bf16, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,305 @@
+"""Each HIP kernel family vs a plain torch fp32 reference of the same op (GPU).
+The references restate the oracle's semantics (oracle/ctclip_oracle.py) on the same inputs."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import ctclip_oracle as O
+
+pytestmark = pytest.mark.gpu
+dev = 'cuda'
+
+
+@pytest.fixture(scope='module')
+def K():
+    from ctclip_mi355x import kernels
+    return kernels
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+# ----------------------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize('D,eps,bias', [(512, 1e-5, False), (512, 1e-5, True), (768, 1e-12, True), (64, 1e-5, True)])
+def test_layernorm(K, D, eps, bias):
+    torch.manual_seed(0)
+    x = torch.randn(1000, D, device=dev) * 3 + 1
+    g = torch.randn(D, device=dev) * 0.1 + 1
+    b = torch.randn(D, device=dev) * 0.1 if bias else None
+    yb, yf, mean, rstd = K.layernorm_fwd(x, g, b, eps, out_f32=True)
+    xr = x.clone().requires_grad_(True)
+    gr = g.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True) if bias else None
+    ref = F.layer_norm(xr, (D,), gr, br, eps)
+    assert rel(yf, ref) < 1e-6
+    assert rel(yb, ref) < 4e-3
+    dy = torch.randn_like(x)
+    res = torch.randn_like(x)
+    ref.backward(dy)
+    dxf, dxb, dg, db = K.layernorm_bwd(dy, x, mean, rstd, g, dres=res, want_beta=bias)
+    assert rel(dxf, xr.grad + res) < 1e-5
+    assert rel(dg, gr.grad) < 1e-5
+    if bias:
+        assert rel(db, br.grad) < 1e-5
+
+
+def test_l2norm_scale(K):
+    torch.manual_seed(1)
+    H, D = 8, 32
+    x = torch.randn(777, 512, device=dev).bfloat16()   # use the k half of a kv-like buffer
+    sc = torch.randn(D, device=dev) * 0.1 + 1
+    y = K.l2norm_scale_fwd(x[:, :256], H, D, sc)
+    xr = x[:, :256].float().reshape(-1, H, D).requires_grad_(True)
+    scr = sc.clone().requires_grad_(True)
+    ref = F.normalize(xr, dim=-1) * scr
+    assert rel(y.reshape(-1, H, D), ref) < 4e-3
+    dy = torch.randn(777, 256, device=dev).bfloat16()
+    ref.backward(dy.float().reshape(-1, H, D))
+    dx = torch.empty(777, 512, device=dev, dtype=torch.bfloat16)
+    ds = K.l2norm_scale_bwd(x[:, :256], dy, H, D, sc, dx[:, :256])
+    assert rel(dx[:, :256].reshape(-1, H, D), xr.grad) < 8e-3
+    assert rel(ds, scr.grad) < 1e-4
+
+
+# ----------------------------------------------------------------------------- PEG
+def _peg_ref(x, w, b, shape, mode):
+    """x canonical (b t h w) rows [M, D] f32; returns out (with residual) via the oracle."""
+    B, T, H, W = shape
+    D = x.shape[1]
+    sd = {'p.dsconv.weight': w, 'p.dsconv.bias': b}
+    if mode == 0:
+        xs = x.reshape(B * T, H * W, D)
+        return (O.peg_forward(sd, 'p.', xs, shape) + xs).reshape(-1, D)
+    xt = x.reshape(B, T, H, W, D).permute(0, 2, 3, 1, 4).reshape(B * H * W, T, D)
+    y = O.peg_forward(sd, 'p.', xt, shape) + xt
+    return y.reshape(B, H, W, T, D).permute(0, 3, 1, 2, 4).reshape(-1, D)
+
+
+@pytest.mark.parametrize('mode', [0, 1])
+def test_peg(K, mode):
+    torch.manual_seed(2)
+    shape = (2, 6, 5, 7)
+    D = 128
+    M = 2 * 6 * 5 * 7
+    xb = torch.randn(M, D, device=dev).bfloat16()
+    xf = xb.float()
+    w = torch.randn(D, 1, 3, 3, 3, device=dev) * 0.2
+    b = torch.randn(D, device=dev) * 0.1
+    outf, outb = K.peg_fwd(xb, xf, *shape, w, b, mode)
+    xr = xf.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    ref = _peg_ref(xr, wr, br, shape, mode)
+    assert rel(outf, ref) < 1e-5
+    dy = torch.randn(M, D, device=dev).bfloat16()
+    ref.backward(dy.float())
+    dxf, dxb, dw, db = K.peg_bwd(dy, dy.float(), xb, *shape, w, mode)
+    assert rel(dxf, xr.grad) < 1e-5
+    assert rel(dw, wr.grad.reshape(D, 27)) < 1e-5
+    assert rel(db, br.grad) < 1e-5
+
+
+# ----------------------------------------------------------------------------- attention
+def _gather_rows(n_inner, s_outer, s_inner, s_pos, nseq, L):
+    s = torch.arange(nseq)[:, None]
+    i = torch.arange(L)[None, :]
+    return ((s // n_inner) * s_outer + (s % n_inner) * s_inner + i * s_pos).to(dev)
+
+
+def _attn_ref(q, k, v, rows, H, D, scale, bias=None, kmask=None):
+    nseq, L = rows.shape
+    def g(t):
+        return t[rows.reshape(-1)].reshape(nseq, L, H, D).permute(0, 2, 1, 3)
+    s = torch.einsum('shid,shjd->shij', g(q), g(k)) * scale
+    if bias is not None:
+        s = s + bias
+    if kmask is not None:
+        s = s.masked_fill(~kmask[:, None, None, :].bool(), float('-inf'))
+    a = s.softmax(-1)
+    o = torch.einsum('shij,shjd->shid', a, g(v))
+    out = torch.zeros(q.shape[0], H * D, device=dev)
+    out = out.index_copy(0, rows.reshape(-1), o.permute(0, 2, 1, 3).reshape(nseq * L, H * D))
+    return out
+
+
+def _cpb_table(H, gh, gw):
+    nb = (2 * gh - 1) * (2 * gw - 1)
+    u = torch.randn(H, nb, device=dev) * 0.5
+    pos = torch.stack(torch.meshgrid(torch.arange(gh), torch.arange(gw), indexing='ij')).reshape(2, -1).t()
+    rel_ = pos[:, None, :] - pos[None, :, :]
+    bins = ((rel_[..., 0] + gh - 1) * (2 * gw - 1) + (rel_[..., 1] + gw - 1)).to(dev)
+    return u, bins
+
+
+@pytest.mark.parametrize('case', ['spatial', 'spatial_small', 'temporal', 'bert'])
+def test_attention(K, case):
+    torch.manual_seed(3)
+    if case.startswith('spatial'):
+        gh = gw = 24 if case == 'spatial' else 6
+        L, H, D, nseq = gh * gw, 8, 32, 3
+        M = nseq * L
+        seq = (1, L, 0, 1)
+        scale = 8.0
+        u, bins = _cpb_table(H, gh, gw)
+        bias = u[:, bins]
+        kmask = None
+        grid = (gh, gw)
+    elif case == 'temporal':
+        B, T, HW = 2, 24, 20
+        L, H, D, nseq = T, 8, 32, B * HW
+        M = B * T * HW
+        seq = (HW, T * HW, 1, HW)
+        scale, u, bias, kmask, grid = 8.0, None, None, None, (0, 0)
+    else:
+        B, L, H, D = 3, 128, 12, 64
+        nseq, M = B, B * 128
+        seq = (1, L, 0, 1)
+        scale, u, bias, grid = 1 / 8, None, None, (0, 0)
+        lens = torch.tensor([128, 77, 5])
+        kmask = (torch.arange(L)[None, :] < lens[:, None]).int().to(dev)
+    rows = _gather_rows(*seq, nseq, L)
+    q = (torch.randn(M, H * D, device=dev) * (0.3 if case == 'bert' else 0.18)).bfloat16()
+    kv = (torch.randn(M, 2 * H * D, device=dev) * 0.18).bfloat16()
+    k, v = kv[:, :H * D], kv[:, H * D:]
+    o, lse = K.attn_fwd(q, k, v, L=L, H=H, D=D, nseq=nseq, scale=scale, seq=seq, bias_u=u, grid=grid, kmask=kmask)
+    qr, kr, vr = q.float().requires_grad_(True), k.float().requires_grad_(True), v.float().requires_grad_(True)
+    ur = u.clone().requires_grad_(True) if u is not None else None
+    ref = _attn_ref(qr, kr, vr, rows, H, D, scale, ur[:, bins] if u is not None else None, kmask)
+    assert rel(o, ref) < 8e-3, rel(o, ref)
+    do = torch.randn(M, H * D, device=dev).bfloat16()
+    ref.backward(do.float())
+    dq = torch.empty(M, H * D, device=dev, dtype=torch.bfloat16)
+    dkv = torch.empty(M, 2 * H * D, device=dev, dtype=torch.bfloat16)
+    du = torch.zeros_like(u) if u is not None else None
+    K.attn_bwd(q, k, v, o, lse, do, dq, dkv[:, :H * D], dkv[:, H * D:], L=L, H=H, D=D, nseq=nseq, scale=scale,
+               seq=seq, bias_u=u, dbias_u=du, grid=grid, kmask=kmask)
+    assert rel(dq, qr.grad) < 2e-2, rel(dq, qr.grad)
+    assert rel(dkv[:, :H * D], kr.grad) < 2e-2, rel(dkv[:, :H * D], kr.grad)
+    assert rel(dkv[:, H * D:], vr.grad) < 2e-2, rel(dkv[:, H * D:], vr.grad)
+    if u is not None:
+        assert rel(du, ur.grad) < 2e-2, rel(du, ur.grad)
+
+
+# ----------------------------------------------------------------------------- VQ
+def test_vq_select_and_pool(K):
+    torch.manual_seed(4)
+    M, D, C = 3000, 512, 8192
+    x = torch.randn(M, D, device=dev)
+    cb = F.normalize(torch.randn(C, D, device=dev), dim=-1)
+    xn = F.normalize(x, dim=-1)
+    nt = C // 128
+    cand = torch.empty(M, nt, 2, device=dev)
+    K.gemm_raw(M, C, D, xn.bfloat16(), D, True, cb.bfloat16(), D, True, cand, nt, act=K.ACT_ARGMAX)
+    idx, xno = K.vq_select(cand, x, cb)
+    ref = (xn @ cb.t()).argmax(1)
+    assert torch.equal(idx.long(), ref)
+    assert rel(xno, xn) < 1e-6
+    B, T, HW = 3, 10, 100
+    pooled, pooled_b = K.vq_pool(idx, cb, B, T, HW)
+    refp = cb[ref].reshape(B, T, HW, D).mean(1).reshape(B, -1)
+    assert rel(pooled, refp) < 1e-6
+    # EMA restatement vs oracle
+    bins = torch.zeros(C, device=dev)
+    esum = torch.zeros(C, D, device=dev)
+    K.vq_ema_accum(idx, xno, bins, esum)
+    emb = cb.clone()
+    cs = torch.zeros(C, device=dev)
+    K.vq_ema_finalize(bins, esum, 0.8, emb, cs)
+    _, _, ne, ncs = O.vq_forward(x.cpu(), cb.cpu()[None], torch.zeros(1, C), True, 0.8)
+    assert rel(emb.cpu(), ne[0]) < 1e-5
+    assert rel(cs.cpu(), ncs[0]) < 1e-6
+
+
+# ----------------------------------------------------------------------------- loss
+@pytest.mark.parametrize('Bg', [2, 8, 64])
+def test_clip_loss(K, Bg):
+    torch.manual_seed(5)
+    t = torch.randn(Bg, 512, device=dev)
+    i = torch.randn(Bg, 512, device=dev)
+    lt = torch.tensor([1.0], device=dev)
+    loss, dt, di, dlt, tn, inn, sim = K.clip_loss(t, i, lt)
+    tr, ir, ltr = t.clone().requires_grad_(True), i.clone().requires_grad_(True), lt.clone().requires_grad_(True)
+    ref = O.infonce(F.normalize(tr, dim=-1), F.normalize(ir, dim=-1), ltr[0])
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-5
+    assert rel(dt, tr.grad) < 1e-4
+    assert rel(di, ir.grad) < 1e-4
+    assert abs(dlt.item() - ltr.grad.item()) < 1e-4 * max(1, abs(ltr.grad.item()))
+    sc = K.clip_scores(t, i, lt)
+    assert rel(sc, (F.normalize(t, dim=-1) * F.normalize(i, dim=-1)).sum(-1) * math.e) < 1e-6
+
+
+# ----------------------------------------------------------------------------- sgemm / CPB
+def test_sgemm_cpb_mlp(K):
+    torch.manual_seed(6)
+    x = O.cpb_rel_pos(24, 24).reshape(-1, 2)
+    rel_u = torch.unique(x, dim=0).to(dev)
+    w0, b0 = torch.randn(512, 2, device=dev), torch.randn(512, device=dev) * 0.1
+    w1, b1 = torch.randn(512, 512, device=dev) / 22, torch.randn(512, device=dev) * 0.1
+    h1 = K.slinear(rel_u, w0, b0, act=1)
+    h2 = K.slinear(h1, w1, b1, act=1)
+    ref = F.leaky_relu(F.linear(F.leaky_relu(F.linear(rel_u, w0, b0), 0.1), w1, b1), 0.1)
+    assert rel(h2, ref) < 1e-5
+    g = torch.randn_like(h2)
+    dz = K.smm(g, w1, act=2, aux=h1)          # dh1 * leaky'(h1)
+    ref2 = (g @ w1) * torch.where(h1 > 0, 1.0, 0.1)
+    assert rel(dz, ref2) < 1e-5
+    dw = K.smm(g.t(), h1)
+    assert rel(dw, g.t() @ h1) < 1e-5
+
+
+# ----------------------------------------------------------------------------- patch embed
+def test_patch_ln(K):
+    torch.manual_seed(7)
+    cfg = O.ViTConfig(dim=64, image_size=40, patch_size=20, temporal_patch_size=10, frames=20)
+    hu = torch.randint(-1200, 1201, (2, 1, 20, 40, 40), dtype=torch.int16, device=dev)
+    from ctclip_mi355x import layers
+    offs = layers.patch_offsets(1, 10, 20, 20, 40, 40).to(dev)
+    xh = K.patch_ln(hu, True, 10, 20, offs)
+    v = O.normalize_hu(hu.cpu())
+    b, c, f, hh, ww = v.shape
+    x = v.reshape(b, c, 2, 10, 2, 20, 2, 20).permute(0, 2, 4, 6, 1, 3, 5, 7).reshape(-1, 4000)
+    ref = F.layer_norm(x, (4000,), eps=1e-5)
+    assert rel(xh.cpu(), ref) < 4e-3
+
+
+def test_embed(K):
+    torch.manual_seed(8)
+    ids = torch.randint(0, 100, (3, 16), device=dev)
+    word = torch.randn(100, 64, device=dev)
+    pos = torch.randn(32, 64, device=dev)
+    typ = torch.randn(2, 64, device=dev)
+    out = K.embed_fwd(ids, word, pos, typ[0])
+    ref = word[ids] + pos[:16][None] + typ[0]
+    assert rel(out.reshape(3, 16, 64), ref) < 1e-6
+    dx = torch.randn(48, 64, device=dev)
+    dw, dp, dt = torch.zeros_like(word), torch.zeros_like(pos), torch.zeros(64, device=dev)
+    K.embed_bwd(ids, dx, dw, dp, dt)
+    refw = torch.zeros_like(word).index_add_(0, ids.reshape(-1), dx)
+    assert rel(dw, refw) < 1e-6
+    assert rel(dp[:16], dx.reshape(3, 16, 64).sum(0)) < 1e-6
+    assert rel(dt, dx.sum(0)) < 1e-6
+
+
+def test_adam_and_norm(K):
+    torch.manual_seed(9)
+    n = 100003
+    p = torch.randn(n, device=dev)
+    g = torch.randn(n, device=dev)
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    out = torch.empty(2, device=dev)
+    K.grad_norm(g, 0.5, out)
+    assert abs(out[0].item() - g.norm().item()) < 1e-3 * g.norm().item()
+    pr = p.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pr], lr=1e-3, betas=(0.9, 0.99), eps=1e-8)
+    pr.grad = g * out[1]
+    opt.step()
+    pb = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    K.adam(p, g, m, v, lr=1e-3, b1=0.9, b2=0.99, eps=1e-8, wd=0.0, step=1, coef=out, p_bf16=pb)
+    assert rel(p, pr.detach()) < 1e-6
+    assert rel(pb, p) < 4e-3
