@@ -150,3 +150,16 @@ extern "C" int ctclip_add_f32(const float* a, const float* b, float* y, void* yb
   CT_CHECK_LAUNCH();
   return 0;
 }
+
+namespace {
+__global__ __launch_bounds__(256) void gelu_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = gelu_erf(x[i]);
+}
+}  // namespace
+
+extern "C" int ctclip_gelu_f32(const float* x, float* y, int64_t n, void* stream) {
+  hipLaunchKernelGGL(gelu_f32_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, y, n);
+  CT_CHECK_LAUNCH();
+  return 0;
+}

@@ -236,6 +236,8 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
       }
     }
     if (p.act == 1) {
+      // C2 (if given) keeps the pre-activation for the GELU backward
+      if (p.C2) *(u32x4*)(p.C2 + bidx * p.sC2 + gm * p.ldc2 + gn) = pack8(v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
     }
@@ -258,7 +260,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
       }
       *(u32x4*)Cb = pack8(v);
     }
-    if (p.C2 && p.act != 2) *(u32x4*)(p.C2 + bidx * p.sC2 + gm * p.ldc2 + gn) = pack8(v);
+    if (p.C2 && p.act == 0) *(u32x4*)(p.C2 + bidx * p.sC2 + gm * p.ldc2 + gn) = pack8(v);
   }
   if (p.act == 2 && p.C2) {
     // GEGLU: tile columns [0,64) are x, [64,128) the matching gates -> 64 output columns

@@ -134,6 +134,28 @@ __global__ __launch_bounds__(64) void vq_ema_finalize_kernel(const float* __rest
   }
 }
 
+// STE + mean-over-t backward: dx[b][t][hw][:] = dpooled[b][hw][:] / T
+__global__ __launch_bounds__(256) void vq_pool_bwd_kernel(const float* __restrict__ dp, int64_t B, int T, int HW,
+                                                          int D, float* __restrict__ dx, u16* __restrict__ dxb) {
+  const int nch = D / 4;
+  const int64_t total = B * (int64_t)T * HW * nch;
+  const float invT = 1.f / (float)T;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % nch);
+    const int64_t row = i / nch;
+    const int hw = (int)(row % HW);
+    const int64_t b = row / ((int64_t)T * HW);
+    const f32x4 v = *(const f32x4*)(dp + (b * HW + hw) * D + c * 4) * invT;
+    if (dx) *(f32x4*)(dx + row * D + c * 4) = v;
+    if (dxb) {
+      uint2 pk;
+      pk.x = pack2(v[0], v[1]);
+      pk.y = pack2(v[2], v[3]);
+      *(uint2*)(dxb + row * D + c * 4) = pk;
+    }
+  }
+}
+
 inline int gridn(int64_t n) { return (int)std::min<int64_t>(8192, std::max<int64_t>(1, (n + 255) / 256)); }
 
 }  // namespace
@@ -178,6 +200,15 @@ extern "C" int ctclip_vq_ema_finalize(const float* bins, const float* esum, int3
                                       float* embed, float* cluster_size, void* embed_bf16, void* stream) {
   hipLaunchKernelGGL(vq_ema_finalize_kernel, dim3(C), dim3(64), 0, (hipStream_t)stream, bins, esum, C, D, decay,
                      embed, cluster_size, (u16*)embed_bf16);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_vq_pool_bwd(const float* dpooled, int64_t B, int32_t T, int32_t HW, int32_t D, float* dx,
+                                  void* dx_bf16, void* stream) {
+  CT_REQUIRE(D % 4 == 0, CT_EALIGN);
+  hipLaunchKernelGGL(vq_pool_bwd_kernel, dim3(gridn(B * T * HW * D / 4)), dim3(256), 0, (hipStream_t)stream, dpooled,
+                     B, T, HW, D, dx, (u16*)dx_bf16);
   CT_CHECK_LAUNCH();
   return 0;
 }

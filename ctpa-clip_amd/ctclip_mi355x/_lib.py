@@ -68,6 +68,7 @@ _SIGS = {
     'ctclip_gelu_bwd': [c_vp, c_vp, c_vp, c_i64, c_vp],
     'ctclip_pack_rows': [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp],
     'ctclip_unpack_rows': [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp],
+    'ctclip_gelu_f32': [c_vp, c_vp, c_i64, c_vp],
     'ctclip_cast_f32_bf16': [c_vp, c_vp, c_i64, c_vp],
     'ctclip_add_f32': [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
     'ctclip_patch_ln': [c_vp, c_i32, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp, c_vp],
@@ -79,6 +80,7 @@ _SIGS = {
     'ctclip_attn_bwd': [ctypes.POINTER(AttnArgs), c_vp],
     'ctclip_vq_select': [c_vp, c_i32, c_vp, c_i64, c_i32, c_vp, c_f32, c_vp, c_vp, c_vp],
     'ctclip_vq_pool': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
+    'ctclip_vq_pool_bwd': [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
     'ctclip_vq_gather': [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp],
     'ctclip_vq_ema_accum': [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp],
     'ctclip_vq_ema_finalize': [c_vp, c_vp, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp],

@@ -1,0 +1,120 @@
+"""BERT-base text encoder on HIP kernels with ``transformers.BertModel``'s state_dict layout
+(the reference's text tower, ct_clip/pretrained_model.py:9, called at ct_clip/ct_clip.py:685-686).
+
+``forward(input_ids, attention_mask)`` returns a tuple whose [0] is last_hidden_state, like
+the HF model output indexed by the reference (``text_embeddings[0]``).  Dropout is not
+applied.  The pooler's parameters are kept for checkpoint
+compatibility; the pooler output is unused by CT-CLIP and is not computed.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+from torch import nn
+
+from . import functional as Fn
+
+
+@dataclass
+class BertConfig:
+    vocab_size: int = 30522
+    hidden_size: int = 768
+    num_hidden_layers: int = 12
+    num_attention_heads: int = 12
+    intermediate_size: int = 3072
+    max_position_embeddings: int = 512
+    type_vocab_size: int = 2
+    layer_norm_eps: float = 1e-12
+    hidden_dropout_prob: float = 0.1
+    attention_probs_dropout_prob: float = 0.1
+
+
+class _Embeddings(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.word_embeddings = nn.Embedding(c.vocab_size, c.hidden_size)
+        self.position_embeddings = nn.Embedding(c.max_position_embeddings, c.hidden_size)
+        self.token_type_embeddings = nn.Embedding(c.type_vocab_size, c.hidden_size)
+        self.LayerNorm = nn.LayerNorm(c.hidden_size, eps=c.layer_norm_eps)
+
+
+class _SelfAttn(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.query = nn.Linear(c.hidden_size, c.hidden_size)
+        self.key = nn.Linear(c.hidden_size, c.hidden_size)
+        self.value = nn.Linear(c.hidden_size, c.hidden_size)
+
+
+class _DenseLN(nn.Module):
+    def __init__(self, din, dout, eps):
+        super().__init__()
+        self.dense = nn.Linear(din, dout)
+        self.LayerNorm = nn.LayerNorm(dout, eps=eps)
+
+
+class _Attention(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.self = _SelfAttn(c)
+        self.output = _DenseLN(c.hidden_size, c.hidden_size, c.layer_norm_eps)
+
+
+class _Dense(nn.Module):
+    def __init__(self, din, dout):
+        super().__init__()
+        self.dense = nn.Linear(din, dout)
+
+
+class BertLayer(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.attention = _Attention(c)
+        self.intermediate = _Dense(c.hidden_size, c.intermediate_size)
+        self.output = _DenseLN(c.intermediate_size, c.hidden_size, c.layer_norm_eps)
+
+
+class _Encoder(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        self.layer = nn.ModuleList([BertLayer(c) for _ in range(c.num_hidden_layers)])
+
+
+class BertModel(nn.Module):
+    def __init__(self, config: BertConfig = None, **kw):
+        super().__init__()
+        self.config = config or BertConfig(**kw)
+        c = self.config
+        if (c.hidden_size // c.num_attention_heads) not in (32, 64):
+            raise NotImplementedError('HIP attention kernels support head dim 32 or 64')
+        self.embeddings = _Embeddings(c)
+        self.encoder = _Encoder(c)
+        self.pooler = _Dense(c.hidden_size, c.hidden_size)
+        for m in self.modules():   # BERT init (std 0.02)
+            if isinstance(m, (nn.Linear, nn.Embedding)):
+                nn.init.normal_(m.weight, std=0.02)
+            if isinstance(m, nn.Linear):
+                nn.init.zeros_(m.bias)
+
+    def forward(self, input_ids, attention_mask=None, **_):
+        c = self.config
+        B, L = input_ids.shape
+        ids = input_ids.to(torch.int64).contiguous()
+        if attention_mask is None:
+            attention_mask = torch.ones_like(ids)
+        kmask = attention_mask.to(torch.int32).contiguous()
+        e = self.embeddings
+        xf, xb = Fn.BertEmbedFn.apply(ids, e.word_embeddings.weight, e.position_embeddings.weight,
+                                      e.token_type_embeddings.weight, e.LayerNorm.weight, e.LayerNorm.bias,
+                                      c.layer_norm_eps)
+        for lyr in self.encoder.layer:
+            a = lyr.attention
+            xf, xb = Fn.BertLayerFn.apply(
+                xf, xb, kmask, B, L, c.num_attention_heads, c.layer_norm_eps,
+                a.self.query.weight, a.self.query.bias, a.self.key.weight, a.self.key.bias,
+                a.self.value.weight, a.self.value.bias, a.output.dense.weight, a.output.dense.bias,
+                a.output.LayerNorm.weight, a.output.LayerNorm.bias, lyr.intermediate.dense.weight,
+                lyr.intermediate.dense.bias, lyr.output.dense.weight, lyr.output.dense.bias,
+                lyr.output.LayerNorm.weight, lyr.output.LayerNorm.bias)
+        return (xf.view(B, L, c.hidden_size), None)

@@ -1,0 +1,117 @@
+"""CTCLIP (ct_clip/ct_clip.py:407-901) — drop-in constructor / forward signature and state_dict
+layout, with the image tower, text tower, projections and InfoNCE running on HIP kernels.
+
+Supported configuration = the one the reference trains (pretrained_model.py:31-42):
+external image / text encoders, use_mlm=False, use_visual_ssl=False, use_all_token_embeds=False,
+downsample_image_embeds=False, no multiview augmentation.  Anything else raises.
+"""
+from __future__ import annotations
+
+import copy
+from pathlib import Path
+
+import torch
+from torch import nn
+
+from . import functional as Fn
+
+
+def l2norm(t):
+    return nn.functional.normalize(t, dim=-1)
+
+
+class CTCLIP(nn.Module):
+    def __init__(self, *, image_encoder=None, text_encoder=None, dim_text=512, dim_image=512, dim_latent=512,
+                 num_text_tokens=28897, text_enc_depth=6, text_seq_len=256, text_heads=8, text_dim_head=64,
+                 text_has_cls_token=False, text_pad_id=0, text_rotary_pos_emb=False, text_causal_mask=False,
+                 text_eos_id=None, text_encode_without_mask=False, visual_enc_depth=6, visual_heads=8,
+                 visual_dim_head=64, visual_image_size=256, visual_patch_size=32, visual_patch_dropout=0.5,
+                 visual_has_cls_token=False, channels=3, use_all_token_embeds=False, downsample_image_embeds=False,
+                 decoupled_contrastive_learning=False, extra_latent_projection=False, use_mlm=False,
+                 text_ssl_loss_weight=0.05, use_visual_ssl=False, visual_ssl=None, visual_ssl_type='simsiam',
+                 visual_ssl_hidden_layer=-1, simclr_temperature=0.1, image_ssl_loss_weight=0.05,
+                 multiview_loss_weight=0.1, checkpoint_during_training=False, **kwargs):
+        super().__init__()
+        unsupported = dict(use_all_token_embeds=use_all_token_embeds, downsample_image_embeds=downsample_image_embeds,
+                           decoupled_contrastive_learning=decoupled_contrastive_learning, use_mlm=use_mlm,
+                           use_visual_ssl=use_visual_ssl or visual_ssl is not None,
+                           text_causal_mask=text_causal_mask)
+        bad = [k for k, v in unsupported.items() if v]
+        if bad:
+            raise NotImplementedError(f'CTCLIP options outside the contrastive hot path: {bad}')
+        if image_encoder is None or text_encoder is None:
+            raise NotImplementedError('the built-in VisionTransformer / TextTransformer are never used by the '
+                                      'reference (pretrained_model.py:31-42); pass image_encoder and text_encoder')
+        self.dim_text = dim_text
+        self.dim_image = dim_image
+        self.dim_latent = dim_latent
+        self.text_transformer = text_encoder
+        self.visual_transformer = image_encoder
+        self.to_text_latent = nn.Linear(dim_text, dim_latent, bias=False)
+        self.to_visual_latent = nn.Linear(dim_image, dim_latent, bias=False)
+        self.temperature = nn.Parameter(torch.tensor(1.))
+        self.extra_latent_projection = extra_latent_projection
+        self.to_text_latent_extra = copy.deepcopy(self.to_text_latent)
+        self.to_visual_latent_extra = copy.deepcopy(self.to_visual_latent)
+        self.multiview_loss_weight = multiview_loss_weight
+        self._wvis = (None, None)
+
+    # ------------------------------------------------------------------ checkpoint
+    def load(self, path):
+        """``CTCLIP.load`` (ct_clip/ct_clip.py:593-597): strict=False; weights-only safe loader."""
+        path = Path(path)
+        assert path.exists()
+        pt = torch.load(str(path), map_location='cpu', weights_only=True)
+        return self.load_state_dict(pt, strict=False)
+
+    # ------------------------------------------------------------------ helpers
+    def _visual_weight_bf16(self, W):
+        key = (W.data_ptr(), W._version)
+        if self._wvis[0] != key:
+            from . import kernels as K
+            self._wvis = (key, K.cast_bf16(W.detach().contiguous()))
+        return self._wvis[1]
+
+    def _project(self, W, Wb, pooled, pooled_b):
+        return Fn.ImageProjFn.apply(pooled, pooled_b, W, Wb)
+
+    def encode(self, text, image):
+        """Text + image towers and raw latents: (enc_text (B,L,768), pooled (B, h*w*d),
+        text_raw (B, dl), image_raw (B, dl))."""
+        enc_text = self.text_transformer(text.input_ids, attention_mask=text.attention_mask)[0]
+        pooled, pooled_b = self.visual_transformer.encode_pooled(image)
+        cls = enc_text[:, 0, :]
+        t_raw = Fn.TextProjFn.apply(cls.contiguous() if not cls.is_contiguous() else cls, self.to_text_latent.weight)
+        W = self.to_visual_latent.weight
+        i_raw = self._project(W, self._visual_weight_bf16(W), pooled, pooled_b)
+        return enc_text, pooled, t_raw, i_raw
+
+    def forward(self, text, image, device=None, return_loss=False, return_encodings=False, return_latents=False,
+                freeze_image_encoder=False, freeze_text_encoder=False, text_to_image=True, aug_text=None,
+                aug_image=None):
+        """``CTCLIP.forward`` (ct_clip/ct_clip.py:614-901)."""
+        if aug_text is not None or aug_image is not None:
+            raise NotImplementedError('multiview augmentation is off in the reference configuration')
+        if self.extra_latent_projection:
+            raise NotImplementedError('extra_latent_projection (CLOOB) is off in the reference configuration')
+        if return_latents:
+            enc_text = self.text_transformer(text.input_ids, attention_mask=text.attention_mask)[0]
+            tokens = self.visual_transformer(image, return_encoded_tokens=True)
+            pooled, pooled_b = self._pool_tokens(tokens)
+            t_raw = Fn.TextProjFn.apply(enc_text[:, 0, :].contiguous(), self.to_text_latent.weight)
+            W = self.to_visual_latent.weight
+            i_raw = self._project(W, self._visual_weight_bf16(W), pooled, pooled_b)
+            return l2norm(t_raw), l2norm(i_raw), tokens
+        enc_text, pooled, t_raw, i_raw = self.encode(text, image)
+        if return_encodings:
+            return enc_text, pooled
+        if not return_loss:
+            from . import kernels as K
+            return K.clip_scores(t_raw.contiguous(), i_raw.contiguous(), self.temperature.detach().reshape(1))
+        return Fn.ClipLossFn.apply(t_raw, i_raw, self.temperature)
+
+    def _pool_tokens(self, tokens):
+        """mean over t + flatten of already-quantised tokens (ct_clip.py:724,740)."""
+        from . import kernels as K
+        pooled = tokens.mean(dim=1).reshape(tokens.shape[0], -1)
+        return pooled, K.cast_bf16(pooled.detach().contiguous())

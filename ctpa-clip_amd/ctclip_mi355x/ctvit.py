@@ -1,0 +1,152 @@
+"""CTViT encoder path (ct_clip/ctvit.py:117-436) on HIP kernels.
+
+Parameter / buffer layout matches the reference's ``CTViT.state_dict()`` (built with
+``use_vgg_and_gan=False``), so ``CT-CLIP_v2.pt``-style checkpoints load unchanged.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from . import functional as Fn
+from .attention import ContinuousPositionBias, Transformer
+from .layers import patch_offsets
+
+
+def pair(v):
+    return (v, v) if not isinstance(v, tuple) else v
+
+
+class _Codebook(nn.Module):
+    def __init__(self, dim, codebook_size):
+        super().__init__()
+        self.register_buffer('initted', torch.ones(1))
+        self.register_buffer('cluster_size', torch.zeros(1, codebook_size))
+        embed = nn.functional.normalize(nn.init.kaiming_uniform_(torch.empty(1, codebook_size, dim)), dim=-1)
+        self.register_buffer('embed', embed)
+
+
+class VectorQuantize(nn.Module):
+    """Cosine-similarity VQ with EMA codebook (vector_quantize_pytorch==1.1.2 semantics as
+    restated in oracle/ctclip_oracle.vq_forward; buffer names ``_codebook.{initted,cluster_size,embed}``)."""
+
+    def __init__(self, dim, codebook_size, use_cosine_sim=True, decay=0.8, commitment_weight=1.):
+        super().__init__()
+        if not use_cosine_sim:
+            raise NotImplementedError('only the cosine-similarity codebook is on the CT-CLIP path')
+        self.dim = dim
+        self.codebook_size = codebook_size
+        self.decay = decay
+        self._codebook = _Codebook(dim, codebook_size)
+        self.state = Fn.VQState()
+
+    @property
+    def codebook(self):
+        return self._codebook.embed[0]
+
+
+class _Slot(nn.Module):
+    """Parameter-free placeholder keeping Sequential indices identical to the reference (Rearrange)."""
+
+
+class CTViT(nn.Module):
+    def __init__(self, *, dim, codebook_size, image_size, patch_size, temporal_patch_size, spatial_depth,
+                 temporal_depth, discr_base_dim=16, dim_head=64, heads=8, channels=1, use_vgg_and_gan=False,
+                 vgg=None, discr_attn_res_layers=(16,), use_hinge_loss=True, attn_dropout=0., ff_dropout=0.):
+        super().__init__()
+        if use_vgg_and_gan:
+            raise NotImplementedError('VGG / GAN reconstruction losses are outside the contrastive hot path '
+                                      '(ct_clip/ctvit.py:199-219); build with use_vgg_and_gan=False')
+        if dim_head not in (32, 64):
+            raise NotImplementedError('HIP attention kernels support dim_head 32 or 64')
+        self.image_size = pair(image_size)
+        self.patch_size = pair(patch_size)
+        ph, pw = self.patch_size
+        if ph != pw:
+            raise NotImplementedError('square patches only')
+        self.temporal_patch_size = temporal_patch_size
+        self.dim = dim
+        self.heads = heads
+        self.dim_head = dim_head
+        self.channels = channels
+        self.spatial_rel_pos_bias = ContinuousPositionBias(dim=dim, heads=heads)
+        pdf = channels * ph * pw
+        pd = pdf * temporal_patch_size
+        self.to_patch_emb_first_frame = nn.Sequential(_Slot(), nn.LayerNorm(pdf), nn.Linear(pdf, dim),
+                                                      nn.LayerNorm(dim))
+        self.to_patch_emb = nn.Sequential(_Slot(), nn.LayerNorm(pd), nn.Linear(pd, dim), nn.LayerNorm(dim))
+        kw = dict(dim_head=dim_head, heads=heads, peg=True, peg_causal=True)
+        self.enc_spatial_transformer = Transformer(dim, depth=spatial_depth, **kw)
+        self.enc_temporal_transformer = Transformer(dim, depth=temporal_depth, **kw)
+        self.vq = VectorQuantize(dim=dim, codebook_size=codebook_size, use_cosine_sim=True)
+        self.to_pixels_first_frame = nn.Sequential(nn.Linear(dim, pdf), _Slot())
+        self.to_pixels = nn.Sequential(nn.Linear(dim, pd), _Slot())
+        self.use_vgg_and_gan = False
+        self._offs = {}
+
+    @property
+    def patch_height_width(self):
+        return self.image_size[0] // self.patch_size[0], self.image_size[1] // self.patch_size[1]
+
+    def _offsets(self, shape, device):
+        key = (tuple(shape), str(device))
+        if key not in self._offs:
+            _, C, F, H, W = shape
+            self._offs[key] = patch_offsets(C, self.temporal_patch_size, self.patch_size[0], F, H, W).to(device)
+        return self._offs[key]
+
+    # ------------------------------------------------------------------ encoder
+    def encode_tokens(self, video):
+        """Patch-embed + spatial + temporal transformers.  video: (B, C, F, H, W) float in [-1, 1]
+        or int16 HU (normalised in-kernel).  Returns (z f32 [M, D], z bf16, geometry)."""
+        if video.ndim == 4:
+            video = video.unsqueeze(2)
+        assert video.ndim == 5
+        B, C, F, H, W = video.shape
+        assert (H, W) == tuple(self.image_size), (H, W)
+        assert F % self.temporal_patch_size == 0
+        is_hu = video.dtype == torch.int16
+        if not is_hu and video.dtype != torch.float32:
+            video = video.float()
+        video = video.contiguous()
+        pe = self.to_patch_emb
+        xf, xb = Fn.PatchEmbedFn.apply(video, pe[1].weight, pe[1].bias, pe[2].weight, pe[2].bias, pe[3].weight,
+                                       pe[3].bias, self.temporal_patch_size, self.patch_size[0], is_hu,
+                                       self._offsets(video.shape, video.device))
+        hg, wg = self.patch_height_width
+        T = F // self.temporal_patch_size
+        g_sp = Fn.Geo(B, T, hg, wg, self.heads, self.dim_head, 0)
+        g_tm = Fn.Geo(B, T, hg, wg, self.heads, self.dim_head, 1)
+        bias_u = self.spatial_rel_pos_bias(hg, wg)                       # ctvit.py:317
+        xf, xb = self.enc_spatial_transformer.run(xf, xb, g_sp, bias_u)   # ctvit.py:319
+        zf, zb = self.enc_temporal_transformer.run(xf, xb, g_tm)         # ctvit.py:327
+        return zf, zb, g_sp
+
+    def encode_pooled(self, video):
+        """Encoder + VQ + mean over t (the CTCLIP image path, ct_clip.py:715,724,740):
+        returns (pooled f32 [B, h*w*d], pooled bf16)."""
+        zf, zb, geo = self.encode_tokens(video)
+        cb = self._codebook_tensors()
+        pooled, pooled_b, _ = Fn.VQPoolFn.apply(zf, zb, cb[0], cb[1], geo, self.training, self.vq.decay,
+                                                self.vq.state, False)
+        return pooled, pooled_b
+
+    def _codebook_tensors(self):
+        c = self.vq._codebook
+        return c.embed, c.cluster_size
+
+    def forward(self, video, mask=None, return_recons=False, return_recons_only=False, return_discr_loss=False,
+                apply_grad_penalty=True, return_only_codebook_ids=False, return_encoded_tokens=False):
+        """``CTViT.forward`` (ct_clip/ctvit.py:377-436): the encoder path
+        (return_encoded_tokens / return_only_codebook_ids)."""
+        if mask is not None:
+            raise NotImplementedError('frame masks are not used on the CT-CLIP path')
+        if not (return_encoded_tokens or return_only_codebook_ids):
+            raise NotImplementedError('reconstruction / GAN losses are outside the contrastive hot path')
+        zf, zb, geo = self.encode_tokens(video)
+        emb, cs = self._codebook_tensors()
+        _, _, toks = Fn.VQPoolFn.apply(zf, zb, emb, cs, geo, self.training, self.vq.decay, self.vq.state,
+                                       return_encoded_tokens)
+        if return_only_codebook_ids:
+            return self.vq.state.last_indices.view(geo.B, -1).long()
+        return toks.view(geo.B, geo.T, geo.Hg, geo.Wg, self.dim)

@@ -1,0 +1,509 @@
+"""Layer-level autograd Functions: each forward runs a fixed chain of HIP kernels and saves
+what its hand-written backward needs.  No torch math on the hot path — torch provides device
+memory, streams, autograd plumbing and RCCL collectives.
+
+Data layout: the CTViT residual stream lives in canonical token order
+(b, t, h, w) as an f32 master [M, D] plus a bf16 shadow for the GEMMs; the spatial and
+temporal transformers address the same rows (attention / PEG kernels gather sequences
+by index arithmetic instead of transposing).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+from . import kernels as K
+
+F32, BF16 = torch.float32, torch.bfloat16
+
+
+# ----------------------------------------------------------------------------- geometry
+@dataclass(frozen=True)
+class Geo:
+    B: int
+    T: int
+    Hg: int
+    Wg: int
+    heads: int
+    dim_head: int
+    mode: int            # 0 spatial transformer, 1 temporal transformer
+
+    @property
+    def M(self):
+        return self.B * self.T * self.Hg * self.Wg
+
+    def seq(self):
+        """(L, nseq, (n_inner, s_outer, s_inner, s_pos)) for the attention row gather."""
+        hw = self.Hg * self.Wg
+        if self.mode == 0:     # '(b t) (h w) d'  (ct_clip/ctvit.py:315)
+            return hw, self.B * self.T, (1, hw, 0, 1)
+        # '(b h w) t d'  (ct_clip/ctvit.py:325): s = b*hw + j, row = b*T*hw + t*hw + j
+        return self.T, self.B * hw, (hw, self.T * hw, 1, hw)
+
+
+# ----------------------------------------------------------------------------- weight packing
+_MAP_CACHE = {}
+
+
+def ff_pad(inner):
+    return (inner + 63) // 64 * 64
+
+
+def ff1_rowmap(inner, device):
+    """Row map of the GEGLU-interleaved W1: packed row t*128 + c  <- x row t*64+c,
+    t*128 + 64 + c <- gate row inner + t*64 + c  (-1 = zero padding)."""
+    key = ('ff1', inner, str(device))
+    if key not in _MAP_CACHE:
+        P = ff_pad(inner)
+        m = torch.full((2 * P,), -1, dtype=torch.int32)
+        for t in range(P // 64):
+            for c in range(64):
+                j = t * 64 + c
+                if j < inner:
+                    m[t * 128 + c] = j
+                    m[t * 128 + 64 + c] = inner + j
+        _MAP_CACHE[key] = m.to(device)
+    return _MAP_CACHE[key]
+
+
+def pack_ff1(W1):
+    inner = W1.shape[0] // 2
+    P = ff_pad(inner)
+    return K.pack_rows(W1, 2 * P, W1.shape[1], rowmap=ff1_rowmap(inner, W1.device))
+
+
+def pack_ff2(W2):
+    return K.pack_rows(W2, W2.shape[0], ff_pad(W2.shape[1]))
+
+
+def bf(W):
+    return K.cast_bf16(W.contiguous())
+
+
+# ----------------------------------------------------------------------------- patch embedding
+class PatchEmbedFn(torch.autograd.Function):
+    """``CTViT.to_patch_emb`` (ct_clip/ctvit.py:169-174) with the input normalisation of
+    ct_clip/data.py:150-152 fused when the volume arrives as int16 HU.
+    LayerNorm(patch) affine is folded into the Linear: W' = W diag(g), b' = b + W beta."""
+
+    @staticmethod
+    def forward(ctx, video, ln1_w, ln1_b, W, b, ln2_w, ln2_b, PT, P, is_hu, offs):
+        xhat = K.patch_ln(video, is_hu, PT, P, offs)                   # [M, pd] bf16
+        Wp = K.pack_rows(W, W.shape[0], W.shape[1], colscale=ln1_w)    # bf16 [D, pd]
+        bp = K.slinear(ln1_b.view(1, -1), W, bias=b).view(-1)          # f32 [D]
+        y1 = K.linear(xhat, Wp, bias=bp, out_dtype=F32)                 # [M, D]
+        yb, yf, mean, rstd = K.layernorm_fwd(y1, ln2_w, ln2_b, 1e-5, out_bf16=True, out_f32=True)
+        ctx.save_for_backward(xhat, y1, mean, rstd, ln1_w, ln1_b, W, ln2_w)
+        ctx.mark_non_differentiable(yb)
+        return yf, yb
+
+    @staticmethod
+    def backward(ctx, dyf, _dyb):
+        xhat, y1, mean, rstd, ln1_w, ln1_b, W, ln2_w = ctx.saved_tensors
+        _, dy1b, dg2, db2 = K.layernorm_bwd(dyf.contiguous(), y1, mean, rstd, ln2_w, dx_f32=False)
+        G = K.matmul_tn(dy1b, xhat)                                     # [D, pd] f32
+        cs = K.colsum(dy1b)                                             # d bias
+        dW = torch.empty_like(W)
+        dg1 = torch.empty_like(ln1_w)
+        db1 = torch.empty_like(ln1_b)
+        K.patch_wgrad(G, cs, W, ln1_w, ln1_b, dW, dg1, db1, accumulate=False)
+        return None, dg1, db1, dW, cs, dg2, db2, None, None, None, None
+
+
+# ----------------------------------------------------------------------------- CPB
+def cpb_table(h, w, device):
+    """Unique relative offsets of an h x w grid, log-spaced (ct_clip/attention.py:261-267):
+    row bin = (dh + h-1)*(2w-1) + (dw + w-1)."""
+    key = ('cpb', h, w, str(device))
+    if key not in _MAP_CACHE:
+        dh = torch.arange(-(h - 1), h).view(-1, 1).expand(2 * h - 1, 2 * w - 1)
+        dw = torch.arange(-(w - 1), w).view(1, -1).expand(2 * h - 1, 2 * w - 1)
+        rel = torch.stack([dh, dw], -1).reshape(-1, 2).to(torch.float32)
+        rel = torch.sign(rel) * torch.log(rel.abs() + 1)
+        _MAP_CACHE[key] = rel.contiguous().to(device)
+    return _MAP_CACHE[key]
+
+
+class CPBFn(torch.autograd.Function):
+    """``ContinuousPositionBias`` (ct_clip/attention.py:229-276) evaluated on the 2,209 distinct
+    offsets only (exact dedup of the 331,776 pairs).  Output u[heads][bin] (f32)."""
+
+    @staticmethod
+    def forward(ctx, rel, w0, b0, w1, b1, w2, b2):
+        nb = rel.shape[0]
+        H = w2.shape[0]
+        h1 = K.slinear(rel, w0, b0, act=1)
+        h2 = K.slinear(h1, w1, b1, act=1)
+        u = torch.empty(H, nb, device=rel.device, dtype=F32)
+        K.sgemm(nb, H, h2.shape[1], h2, h2.stride(0), 1, w2, 1, w2.stride(0), u, 1, nb, bias=b2)
+        ctx.save_for_backward(rel, w0, w1, w2, h1, h2)
+        return u
+
+    @staticmethod
+    def backward(ctx, du):
+        rel, w0, w1, w2, h1, h2 = ctx.saved_tensors
+        du = du.contiguous()
+        H, nb = du.shape
+        dev = du.device
+        dz2 = torch.empty(nb, w2.shape[1], device=dev, dtype=F32)
+        K.sgemm(nb, w2.shape[1], H, du, 1, nb, w2, w2.stride(0), 1, dz2, dz2.stride(0), 1, act=2, aux=h2,
+                sxm=h2.stride(0), sxn=1)
+        dw2 = K.smm(du, h2)
+        ones = torch.ones(nb, device=dev, dtype=F32)
+        db2 = torch.empty(H, device=dev, dtype=F32)
+        K.sgemm(H, 1, nb, du, nb, 1, ones, 1, 0, db2, 1, 1)
+        dw1 = K.smm(dz2.t(), h1)
+        db1 = K.colsum(dz2)
+        dz1 = K.smm(dz2, w1, act=2, aux=h1)
+        dw0 = K.smm(dz1.t(), rel)
+        db0 = K.colsum(dz1)
+        return None, dw0, db0, dw1, db1, dw2, db2
+
+
+# ----------------------------------------------------------------------------- transformer layer
+class ViTLayerFn(torch.autograd.Function):
+    """One CTViT transformer layer (ct_clip/attention.py:322-331):
+    x = PEG(x) + x; x = Attention(x, bias) + x; x = FeedForward(x) + x."""
+
+    @staticmethod
+    def forward(ctx, xf, xb, bias_u, geo, peg_w, peg_b, norm_g, q_scale, k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1,
+                W2):
+        H, dh = geo.heads, geo.dim_head
+        inner = H * dh
+        x1f, x1b = K.peg_fwd(xb, xf, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, peg_b, geo.mode)
+        xn, _, m1, r1 = K.layernorm_fwd(x1f, norm_g, None, 1e-5)
+        Wq_b, Wkv_b, Wo_b = bf(Wq), bf(Wkv), bf(Wo)
+        q = K.linear(xn, Wq_b)
+        kv = K.linear(x1b, Wkv_b)
+        qn = K.l2norm_scale_fwd(q, H, dh, q_scale)
+        kn = K.l2norm_scale_fwd(kv[:, :inner], H, dh, k_scale)
+        L, nseq, seq = geo.seq()
+        use_bias = bias_u is not None
+        o, lse = K.attn_fwd(qn, kn, kv[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
+                            bias_u=bias_u if use_bias else None, grid=(geo.Hg, geo.Wg) if use_bias else (0, 0))
+        x2b = torch.empty_like(xb)
+        x2f = K.linear(o, Wo_b, residual=x1f, out_dtype=F32, out2=x2b)
+        xn2, _, m2, r2 = K.layernorm_fwd(x2f, ff_w, ff_b, 1e-5)
+        W1p, W2p = pack_ff1(W1), pack_ff2(W2)
+        g = torch.empty(xf.shape[0], W2p.shape[1], device=xf.device, dtype=BF16)
+        h = K.linear(xn2, W1p, act=K.ACT_GEGLU, out2=g)
+        x3b = torch.empty_like(xb)
+        x3f = K.linear(g, W2p, residual=x2f, out_dtype=F32, out2=x3b)
+        ctx.geo = geo
+        ctx.use_bias = use_bias
+        ctx.save_for_backward(xb, x1b, m1, r1, xn, q, kv, qn, kn, o, lse, x2b, m2, r2, xn2, h, g,
+                              bias_u if use_bias else torch.empty(0), peg_w, norm_g, q_scale, k_scale,
+                              Wq_b, Wkv_b, Wo_b, ff_w, W1p, W2p, W1, W2)
+        ctx.mark_non_differentiable(x3b)
+        return x3f, x3b
+
+    @staticmethod
+    def backward(ctx, dx3f, _dx3b):
+        (xb, x1b, m1, r1, xn, q, kv, qn, kn, o, lse, x2b, m2, r2, xn2, h, g, bias_u, peg_w, norm_g, q_scale,
+         k_scale, Wq_b, Wkv_b, Wo_b, ff_w, W1p, W2p, W1, W2) = ctx.saved_tensors
+        geo = ctx.geo
+        H, dh = geo.heads, geo.dim_head
+        inner = H * dh
+        dev = dx3f.device
+        dx3f = dx3f.contiguous()
+        dx3b = K.cast_bf16(dx3f)
+        # feed-forward
+        dg = K.matmul_nn(dx3b, W2p)
+        dW2p = K.matmul_tn(dx3b, g)
+        dh_ = K.geglu_bwd(dg, h)
+        dxn2 = K.matmul_nn(dh_, W1p)
+        dW1p = K.matmul_tn(dh_, xn2)
+        dx2f, dx2b, dffw, dffb = K.layernorm_bwd(dxn2, x2b, m2, r2, ff_w, dres=dx3f)
+        dW1 = torch.empty_like(W1)
+        K.unpack_rows(dW1p, dW1, rowmap=ff1_rowmap(W1.shape[0] // 2, dev), accumulate=False)
+        dW2 = torch.empty_like(W2)
+        K.unpack_rows(dW2p, dW2, cols=W2.shape[1], accumulate=False)
+        # attention
+        do = K.matmul_nn(dx2b, Wo_b)
+        dWo = K.matmul_tn(dx2b, o)
+        dqn = torch.empty_like(qn)
+        dkn = torch.empty_like(kn)
+        dkv = torch.empty_like(kv)
+        L, nseq, seq = geo.seq()
+        du = torch.zeros_like(bias_u) if ctx.use_bias else None
+        K.attn_bwd(qn, kn, kv[:, inner:], o, lse, do, dqn, dkn, dkv[:, inner:], L=L, H=H, D=dh, nseq=nseq,
+                   scale=8.0, seq=seq, bias_u=bias_u if ctx.use_bias else None, dbias_u=du,
+                   grid=(geo.Hg, geo.Wg) if ctx.use_bias else (0, 0))
+        dq = torch.empty_like(q)
+        dqs = K.l2norm_scale_bwd(q, dqn, H, dh, q_scale, dq)
+        dks = K.l2norm_scale_bwd(kv[:, :inner], dkn, H, dh, k_scale, dkv[:, :inner])
+        dxn = K.matmul_nn(dq, Wq_b)
+        dWq = K.matmul_tn(dq, xn)
+        dWkv = K.matmul_tn(dkv, x1b)
+        dx1kv = K.matmul_nn(dkv, Wkv_b, residual=dx2f, out_dtype=F32)
+        dx1f, dx1b, dng, _ = K.layernorm_bwd(dxn, x1b, m1, r1, norm_g, dres=dx1kv, want_beta=False)
+        # PEG
+        dxf, _, dpw, dpb = K.peg_bwd(dx1b, dx1f, xb, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, geo.mode)
+        return (dxf, None, du, None, dpw.reshape(peg_w.shape), dpb, dng, dqs, dks, dWq, dWkv, dWo, dffw, dffb,
+                dW1, dW2)
+
+
+class NormFn(torch.autograd.Function):
+    """Bias-less LayerNorm ``norm_out`` (ct_clip/attention.py:309,333) -> (f32, bf16)."""
+
+    @staticmethod
+    def forward(ctx, xf, xb, gamma):
+        yb, yf, mean, rstd = K.layernorm_fwd(xf, gamma, None, 1e-5, out_bf16=True, out_f32=True)
+        ctx.save_for_backward(xb, mean, rstd, gamma)
+        ctx.mark_non_differentiable(yb)
+        return yf, yb
+
+    @staticmethod
+    def backward(ctx, dyf, _):
+        xb, mean, rstd, gamma = ctx.saved_tensors
+        dxf, _, dg, _ = K.layernorm_bwd(dyf.contiguous(), xb, mean, rstd, gamma, want_beta=False, dx_bf16=False)
+        return dxf, None, dg
+
+
+# ----------------------------------------------------------------------------- VQ + pooling
+class VQPoolFn(torch.autograd.Function):
+    """``vq`` (ct_clip/ctvit.py:421-427; vector_quantize_pytorch cosine codebook) followed by the
+    pooling of CTCLIP.forward (ct_clip.py:724,740): mean over t, flatten (h, w, d).
+    Straight-through estimator in training; codebook EMA update in training mode (buffers
+    updated in place AFTER the quantised values are read, as the reference does; all-reduced
+    across ranks so every rank keeps the same codebook).  Optionally also returns the full
+    quantised token tensor codebook[idx] ([M, D] f32)."""
+
+    @staticmethod
+    def forward(ctx, zf, zb, embed, cluster, geo, training, decay, state, want_tokens):
+        ctx.set_materialize_grads(False)
+        D = zf.shape[1]
+        C = embed.shape[-2]
+        cb = embed.view(C, D)
+        cb_b = state.codebook_bf16(cb)
+        ones = state.ones(D, zf.device)
+        xn_b = K.l2norm_scale_fwd(zb, 1, D, ones)
+        nt = (C + 127) // 128
+        cand = torch.empty(zf.shape[0], nt, 2, device=zf.device, dtype=F32)
+        K.gemm_raw(zf.shape[0], C, D, xn_b, D, True, cb_b, D, True, cand, nt, act=K.ACT_ARGMAX)
+        idx, xn = K.vq_select(cand, zf, cb, want_xn=training)
+        HW = geo.Hg * geo.Wg
+        pooled, pooled_b = K.vq_pool(idx, cb, geo.B, geo.T, HW)
+        tokens = K.vq_gather(idx, cb) if want_tokens else torch.empty(0, device=zf.device)
+        if training:
+            bins = torch.zeros(C, device=zf.device, dtype=F32)
+            esum = torch.zeros(C, D, device=zf.device, dtype=F32)
+            K.vq_ema_accum(idx, xn, bins, esum)
+            if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+                dist.all_reduce(bins)
+                dist.all_reduce(esum)
+            K.vq_ema_finalize(bins, esum, decay, cb, cluster.view(-1), cb_b)
+            state.mark_codebook_fresh(cb)
+        ctx.geo = geo
+        ctx.D = D
+        state.last_indices = idx
+        ctx.mark_non_differentiable(pooled_b)
+        return pooled, pooled_b, tokens
+
+    @staticmethod
+    def backward(ctx, dpooled, _, dtokens):
+        geo = ctx.geo
+        dz = None
+        if dpooled is not None:
+            dz, _ = K.vq_pool_bwd(dpooled.contiguous(), geo.B, geo.T, geo.Hg * geo.Wg, ctx.D)
+        if dtokens is not None and dtokens.numel():
+            dz = dtokens.contiguous() if dz is None else dz + dtokens
+        return dz, None, None, None, None, None, None, None, None
+
+
+class VQState:
+    """Caches of the vector quantiser: bf16 codebook mirror and constant vectors."""
+
+    def __init__(self):
+        self._cb = None
+        self._cb_ver = None
+        self._ones = {}
+        self.last_indices = None
+
+    def codebook_bf16(self, cb):
+        key = (cb.data_ptr(), cb._version)
+        if self._cb is None or self._cb_ver != key:
+            self._cb = K.cast_bf16(cb)
+            self._cb_ver = key
+        return self._cb
+
+    def mark_codebook_fresh(self, cb):
+        self._cb_ver = (cb.data_ptr(), cb._version)
+
+    def ones(self, D, device):
+        k = (D, str(device))
+        if k not in self._ones:
+            self._ones[k] = torch.ones(D, device=device, dtype=F32)
+        return self._ones[k]
+
+
+# ----------------------------------------------------------------------------- projections
+class ImageProjFn(torch.autograd.Function):
+    """``to_visual_latent`` Linear(dim_image -> dim_latent, no bias) (ct_clip/ct_clip.py:564,767)
+    as a split-K bf16 MFMA GEMM (the 294,912-wide weight is read once per step)."""
+
+    @staticmethod
+    def forward(ctx, pooled, pooled_b, W, Wb):
+        B, Kd = pooled_b.shape
+        N = Wb.shape[0]
+        split = max(1, min(512, Kd // 1024))
+        slabs = torch.empty(split, B, N, device=pooled.device, dtype=F32)
+        K.gemm_raw(B, N, Kd, pooled_b, Kd, True, Wb, Kd, True, slabs, N, split_k=split)
+        out = torch.empty(B, N, device=pooled.device, dtype=F32)
+        K.reduce_slabs(slabs, out)
+        ctx.save_for_backward(pooled_b, W, Wb)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        pooled_b, W, Wb = ctx.saved_tensors
+        dlb = K.cast_bf16(dout.contiguous())
+        dpooled = K.matmul_nn(dlb, Wb, out_dtype=F32) if ctx.needs_input_grad[0] else None
+        dW = K.matmul_tn(dlb, pooled_b) if ctx.needs_input_grad[2] else None
+        return dpooled, None, dW, None
+
+
+class TextProjFn(torch.autograd.Function):
+    """``to_text_latent`` Linear(768 -> 512, no bias) on the CLS row (ct_clip/ct_clip.py:549,762-765),
+    exact f32."""
+
+    @staticmethod
+    def forward(ctx, cls, W):
+        ctx.save_for_backward(cls, W)
+        return K.slinear(cls, W)
+
+    @staticmethod
+    def backward(ctx, dout):
+        cls, W = ctx.saved_tensors
+        dout = dout.contiguous()
+        dcls = K.smm(dout, W) if ctx.needs_input_grad[0] else None
+        dW = K.smm(dout.t(), cls) if ctx.needs_input_grad[1] else None
+        return dcls, dW
+
+
+# ----------------------------------------------------------------------------- loss
+def _world():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+class ClipLossFn(torch.autograd.Function):
+    """Symmetric InfoNCE (ct_clip/ct_clip.py:845-901).  Under torch.distributed the raw latents
+    are all-gathered (RCCL) so the negatives span the global batch; every rank computes the
+    same global loss and back-propagates its own rows (gradients are then SUM-reduced)."""
+
+    @staticmethod
+    def forward(ctx, t_raw, i_raw, log_temp):
+        world, rank = _world()
+        B = t_raw.shape[0]
+        if world > 1:
+            both = torch.cat([t_raw, i_raw], 0).contiguous()
+            gathered = torch.empty(world * 2 * B, t_raw.shape[1], device=t_raw.device, dtype=F32)
+            dist.all_gather_into_tensor(gathered, both)
+            g = gathered.view(world, 2, B, -1)
+            tg = g[:, 0].reshape(world * B, -1).contiguous()
+            ig = g[:, 1].reshape(world * B, -1).contiguous()
+        else:
+            tg, ig = t_raw.contiguous(), i_raw.contiguous()
+        loss, dt, di, dlt, tn, inn, sim = K.clip_loss(tg, ig, log_temp.reshape(1).contiguous())
+        ctx.save_for_backward(dt[rank * B:(rank + 1) * B], di[rank * B:(rank + 1) * B], dlt)
+        ctx.world = world
+        return loss.reshape(())
+
+    @staticmethod
+    def backward(ctx, dloss):
+        dt, di, dlt = ctx.saved_tensors
+        s = dloss.reshape(1)
+        # log-temperature gradient: every rank holds the full global value -> divide by world so a
+        # SUM all-reduce reproduces it once.
+        return dt * s, di * s, (dlt * s / ctx.world).reshape(())
+
+
+# ----------------------------------------------------------------------------- BERT
+class BertEmbedFn(torch.autograd.Function):
+    """BertEmbeddings: word + position + token_type(0), LayerNorm(eps 1e-12)."""
+
+    @staticmethod
+    def forward(ctx, ids, word, pos, typ, ln_w, ln_b, eps):
+        x = K.embed_fwd(ids, word, pos, typ[0])
+        yb, yf, mean, rstd = K.layernorm_fwd(x, ln_w, ln_b, eps, out_bf16=True, out_f32=True)
+        ctx.save_for_backward(ids, x, mean, rstd, ln_w)
+        ctx.shapes = (word.shape, pos.shape, typ.shape)
+        ctx.mark_non_differentiable(yb)
+        return yf, yb
+
+    @staticmethod
+    def backward(ctx, dyf, _):
+        ids, x, mean, rstd, ln_w = ctx.saved_tensors
+        dx, _, dg, db = K.layernorm_bwd(dyf.contiguous(), x, mean, rstd, ln_w, dx_bf16=False)
+        ws, ps, ts = ctx.shapes
+        dword = torch.zeros(ws, device=dx.device, dtype=F32)
+        dpos = torch.zeros(ps, device=dx.device, dtype=F32)
+        dtyp = torch.zeros(ts, device=dx.device, dtype=F32)
+        K.embed_bwd(ids, dx, dword, dpos, dtyp[0])
+        return None, dword, dpos, dtyp, dg, db, None
+
+
+class BertLayerFn(torch.autograd.Function):
+    """One BertLayer (post-LN): self-attention (fused QKV GEMM + MFMA attention, scale 1/sqrt(d),
+    additive key mask) -> dense + residual -> LN -> GELU MLP -> dense + residual -> LN."""
+
+    @staticmethod
+    def forward(ctx, xf, xb, kmask, B, L, heads, eps, Wq, bq, Wk, bk, Wv, bv, Wo, bo, ln1_w, ln1_b, Wi, bi, Wout,
+                bout, ln2_w, ln2_b):
+        Hd = xf.shape[1]
+        dh = Hd // heads
+        Wqkv = bf(torch.cat([Wq, Wk, Wv], 0))
+        bqkv = torch.cat([bq, bk, bv], 0).contiguous()
+        qkv = K.linear(xb, Wqkv, bias=bqkv)
+        ctxv, lse = K.attn_fwd(qkv[:, :Hd], qkv[:, Hd:2 * Hd], qkv[:, 2 * Hd:], L=L, H=heads, D=dh, nseq=B,
+                               scale=1.0 / math.sqrt(dh), seq=(1, L, 0, 1), kmask=kmask)
+        Wo_b = bf(Wo)
+        a = K.linear(ctxv, Wo_b, bias=bo, residual=xf, out_dtype=F32)
+        x1b, x1f, m1, r1 = K.layernorm_fwd(a, ln1_w, ln1_b, eps, out_bf16=True, out_f32=True)
+        Wi_b = bf(Wi)
+        hpre = torch.empty(xf.shape[0], Wi.shape[0], device=xf.device, dtype=BF16)
+        hact = K.linear(x1b, Wi_b, bias=bi, act=K.ACT_GELU, out2=hpre)
+        Wout_b = bf(Wout)
+        b2 = K.linear(hact, Wout_b, bias=bout, residual=x1f, out_dtype=F32)
+        x2b, x2f, m2, r2 = K.layernorm_fwd(b2, ln2_w, ln2_b, eps, out_bf16=True, out_f32=True)
+        ctx.save_for_backward(xb, kmask, qkv, ctxv, lse, a, m1, r1, x1b, hpre, hact, b2, m2, r2, Wqkv, Wo_b, Wi_b,
+                              Wout_b, ln1_w, ln2_w)
+        ctx.dims = (B, L, heads, dh)
+        ctx.mark_non_differentiable(x2b)
+        return x2f, x2b
+
+    @staticmethod
+    def backward(ctx, dx2f, _):
+        (xb, kmask, qkv, ctxv, lse, a, m1, r1, x1b, hpre, hact, b2, m2, r2, Wqkv, Wo_b, Wi_b, Wout_b, ln1_w,
+         ln2_w) = ctx.saved_tensors
+        B, L, heads, dh = ctx.dims
+        Hd = heads * dh
+        # LN2 + FF out
+        db2f, db2b, dln2w, dln2b = K.layernorm_bwd(dx2f.contiguous(), b2, m2, r2, ln2_w)
+        dhact = K.matmul_nn(db2b, Wout_b)
+        dWout = K.matmul_tn(db2b, hact)
+        dbout = K.colsum(db2b)
+        dhpre = K.gelu_bwd(dhact, hpre)
+        dx1 = K.matmul_nn(dhpre, Wi_b, residual=db2f, out_dtype=F32)
+        dWi = K.matmul_tn(dhpre, x1b)
+        dbi = K.colsum(dhpre)
+        # LN1 + attention out
+        daf, dab, dln1w, dln1b = K.layernorm_bwd(dx1, a, m1, r1, ln1_w)
+        dctx = K.matmul_nn(dab, Wo_b)
+        dWo = K.matmul_tn(dab, ctxv)
+        dbo = K.colsum(dab)
+        dqkv = torch.empty_like(qkv)
+        K.attn_bwd(qkv[:, :Hd], qkv[:, Hd:2 * Hd], qkv[:, 2 * Hd:], ctxv, lse, dctx, dqkv[:, :Hd],
+                   dqkv[:, Hd:2 * Hd], dqkv[:, 2 * Hd:], L=L, H=heads, D=dh, nseq=B, scale=1.0 / math.sqrt(dh),
+                   seq=(1, L, 0, 1), kmask=kmask)
+        dx = K.matmul_nn(dqkv, Wqkv, residual=daf, out_dtype=F32)
+        dWqkv = K.matmul_tn(dqkv, xb)
+        dbqkv = K.colsum(dqkv)
+        return (dx, None, None, None, None, None, None,
+                dWqkv[:Hd], dbqkv[:Hd], dWqkv[Hd:2 * Hd], dbqkv[Hd:2 * Hd], dWqkv[2 * Hd:], dbqkv[2 * Hd:],
+                dWo, dbo, dln1w, dln1b, dWi, dbi, dWout, dbout, dln2w, dln2b)

@@ -314,6 +314,13 @@ def vq_pool(idx, codebook_f32, B, T, HW, want_bf16=True):
     return out, outb
 
 
+def vq_pool_bwd(dpooled, B, T, HW, D):
+    dx = torch.empty(B * T * HW, D, device=dpooled.device, dtype=F32)
+    dxb = torch.empty(B * T * HW, D, device=dpooled.device, dtype=BF16)
+    call('ctclip_vq_pool_bwd', ptr(dpooled), B, T, HW, D, ptr(dx), ptr(dxb), stream_ptr())
+    return dx, dxb
+
+
 def vq_gather(idx, codebook_f32):
     D = codebook_f32.shape[1]
     out = torch.empty(idx.numel(), D, device=idx.device, dtype=F32)
@@ -408,3 +415,21 @@ def grad_norm(g, max_norm, out):
 def adam(p, g, m, v, *, lr, b1, b2, eps, wd, step, coef=None, p_bf16=None):
     call('ctclip_adam', ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, b1, b2, eps, wd, step, ptr(coef), ptr(p_bf16),
          stream_ptr())
+
+
+def gelu_f32(x):
+    y = torch.empty_like(x)
+    call('ctclip_gelu_f32', ptr(x), ptr(y), x.numel(), stream_ptr())
+    return y
+
+
+def colsum_rows_mean(x, B):
+    """x [B*n, D] f32 -> (B, D) mean over each batch's n rows (f32 GEMM against a ones row)."""
+    rows, D = x.shape
+    n = rows // B
+    out = torch.empty(B, D, device=x.device, dtype=F32)
+    ones = torch.ones(n, device=x.device, dtype=F32)
+    for b in range(B):
+        xb = x[b * n:(b + 1) * n]
+        sgemm(1, D, n, ones, 0, 1, xb, xb.stride(0), 1, out[b:b + 1], D, 1, alpha=1.0 / n)
+    return out

@@ -1,0 +1,82 @@
+"""Contrastive train step (ct_clip/CTCLIPTrainer.py:316-354) without the host data loader:
+forward -> backward -> gradient all-reduce (RCCL) -> clip_grad_norm_(max_norm) -> Adam -> zero_grad.
+
+MI355X-native layout: every trainable parameter is a view into ONE flat f32 arena, and every
+.grad a view into ONE flat f32 gradient arena, so the gradient all-reduce is a single large
+RCCL collective, the norm is one reduction kernel and Adam is one fused kernel (which also
+never syncs the host: the clip coefficient stays on the device).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from . import kernels as K
+
+
+class FlatParams:
+    def __init__(self, params, device):
+        self.params = [p for p in params if p.requires_grad]
+        n = sum(p.numel() for p in self.params)
+        self.numel = n
+        self.data = torch.empty(n, device=device, dtype=torch.float32)
+        self.grad = torch.zeros(n, device=device, dtype=torch.float32)
+        self.views = []
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            self.data[off:off + k].copy_(p.detach().reshape(-1))
+            p.data = self.data[off:off + k].view_as(p)
+            g = self.grad[off:off + k].view_as(p)
+            p.grad = g
+            self.views.append((off, k, g))
+            off += k
+
+    def rebind_grads(self):
+        """Make sure every .grad is (still) the arena view; fold stray grads back in."""
+        for p, (off, k, g) in zip(self.params, self.views):
+            if p.grad is None:
+                p.grad = g
+            elif p.grad.data_ptr() != g.data_ptr():
+                g.copy_(p.grad)
+                p.grad = g
+
+
+class CTClipTrainer:
+    """Optimiser + step for a ``ctclip_mi355x.CTCLIP``.  Hyper-parameters default to the
+    reference's (CTCLIPTrainer.py:203-205, optimizer.py:24: Adam lr 1.25e-6, betas (0.9, 0.99),
+    eps 1e-8, wd 0, clip 0.5)."""
+
+    def __init__(self, model, lr=1.25e-6, wd=0.0, max_grad_norm=0.5, betas=(0.9, 0.99), eps=1e-8):
+        self.model = model
+        dev = next(model.parameters()).device
+        self.device = dev
+        self.flat = FlatParams(model.parameters(), dev)
+        self.m = torch.zeros_like(self.flat.data)
+        self.v = torch.zeros_like(self.flat.data)
+        self.lr, self.wd, self.max_grad_norm, self.betas, self.eps = lr, wd, max_grad_norm, betas, eps
+        self.steps = 0
+        self.norm = torch.zeros(2, device=dev, dtype=torch.float32)
+        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+    def forward_backward(self, text, video):
+        loss = self.model(text, video, device=self.device, return_loss=True)
+        loss.backward()
+        self.flat.rebind_grads()
+        return loss
+
+    def optimizer_step(self):
+        if self.world > 1:
+            dist.all_reduce(self.flat.grad)          # SUM: ClipLossFn gives each rank its own rows
+        K.grad_norm(self.flat.grad, self.max_grad_norm if self.max_grad_norm else 0.0, self.norm)
+        self.steps += 1
+        K.adam(self.flat.data, self.flat.grad, self.m, self.v, lr=self.lr, b1=self.betas[0], b2=self.betas[1],
+               eps=self.eps, wd=self.wd, step=self.steps, coef=self.norm)
+        self.flat.grad.zero_()
+
+    def train_step(self, text, video):
+        """One contrastive step; returns the loss tensor (no host sync)."""
+        self.model.train()
+        loss = self.forward_backward(text, video)
+        self.optimizer_step()
+        return loss.detach()

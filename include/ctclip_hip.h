@@ -96,6 +96,7 @@ int ctclip_pack_rows(const float* src, int64_t ld_src, const int32_t* map, int64
                      int32_t cols_dst, const float* colscale, void* dst, int64_t ld_dst, void* stream);
 int ctclip_unpack_rows(const float* src, int64_t ld_src, const int32_t* map, int64_t rows_src, int32_t cols,
                        float* dst, int64_t ld_dst, int32_t accumulate, void* stream);
+int ctclip_gelu_f32(const float* x, float* y, int64_t n, void* stream);
 int ctclip_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
 int ctclip_add_f32(const float* a, const float* b, float* y, void* y_bf16, int64_t n, void* stream);
 
@@ -158,6 +159,9 @@ int ctclip_vq_select(const float* cand, int32_t ntiles, const float* x, int64_t 
 /* pooled[b][hw][:] = mean_t codebook[idx[b][t*HW+hw]]   (ct_clip/ct_clip.py:724,740) */
 int ctclip_vq_pool(const int32_t* idx, const float* codebook, int64_t B, int32_t T, int32_t HW, int32_t D,
                    float* out, void* out_bf16, void* stream);
+/* backward of pool + straight-through estimator: dx[b][t][hw] = dpooled[b][hw] / T */
+int ctclip_vq_pool_bwd(const float* dpooled, int64_t B, int32_t T, int32_t HW, int32_t D, float* dx, void* dx_bf16,
+                       void* stream);
 int ctclip_vq_gather(const int32_t* idx, const float* codebook, int64_t rows, int32_t D, float* out, void* stream);
 /* training-mode EMA codebook update (bins / embed_sum accumulate, then finalize) */
 int ctclip_vq_ema_accum(const int32_t* idx, const float* xn, int64_t rows, int32_t D, float* bins, float* esum,

@@ -230,7 +230,7 @@ def ctvit_encode(sd, p, tokens, cfg: ViTConfig, trace=None):
 
 
 # ----------------------------------------------------------------------------- VQ (unpinned)
-def vq_forward(x, embed, cluster_size, training, decay=0.8):
+def vq_forward(x, embed, cluster_size, training, decay=0.8, force_ind=None):
     """Cosine-similarity VectorQuantize, restated from the published algorithm of
     ``vector_quantize_pytorch==1.1.2`` (third-party; called at ``ct_clip/ctvit.py:187,427``).
 
@@ -243,7 +243,7 @@ def vq_forward(x, embed, cluster_size, training, decay=0.8):
     flat = F.normalize(x.reshape(-1, shape[-1]).float(), dim=-1)
     emb = embed.reshape(-1, shape[-1])
     dist = flat @ emb.t()
-    ind = dist.argmax(dim=-1)
+    ind = dist.argmax(dim=-1) if force_ind is None else force_ind.reshape(-1).to(torch.int64)
     q = emb[ind]
     new_embed, new_cs = embed, cluster_size
     if training:
@@ -261,9 +261,11 @@ def vq_forward(x, embed, cluster_size, training, decay=0.8):
     return q.reshape(shape), ind.reshape(shape[:-1]), new_embed, new_cs
 
 
-def ctvit_forward(sd, p, video, cfg: ViTConfig, training, trace=None):
+def ctvit_forward(sd, p, video, cfg: ViTConfig, training, trace=None, force_ind=None):
     """``CTViT.forward(video, return_encoded_tokens=True)`` (``ct_clip/ctvit.py:377-436``).
-    Returns (tokens (b,t,h,w,d), indices (b, t*h*w), new_embed, new_cluster_size)."""
+    Returns (tokens (b,t,h,w,d), indices (b, t*h*w), new_embed, new_cluster_size).
+    ``force_ind`` (test hook) replaces the argmax so near-tie index flips of a reduced-precision
+    implementation can be separated from everything downstream of the quantiser."""
     tokens = patch_embed(sd, p, video, cfg)
     if trace is not None:
         trace['patch_emb'] = tokens
@@ -271,7 +273,7 @@ def ctvit_forward(sd, p, video, cfg: ViTConfig, training, trace=None):
     x = ctvit_encode(sd, p, tokens, cfg, trace)
     x = x.reshape(b, t * h * w, d)
     q, ind, ne, ncs = vq_forward(x, sd[p + 'vq._codebook.embed'], sd[p + 'vq._codebook.cluster_size'],
-                                 training, cfg.vq_decay)
+                                 training, cfg.vq_decay, force_ind)
     return q.reshape(b, t, h, w, d), ind, ne, ncs
 
 
@@ -332,12 +334,12 @@ def infonce(text_latents, image_latents, temperature):
     return (one(t2i) + one(i2t)) / 2
 
 
-def ctclip_forward(sd, ids, mask, video, cfg: ClipConfig, training=True, trace=None):
+def ctclip_forward(sd, ids, mask, video, cfg: ClipConfig, training=True, trace=None, force_ind=None):
     """``CTCLIP.forward(text, image, return_loss=True)`` (``ct_clip/ct_clip.py:614-901``)
     with MLM / visual-SSL / multiview off (``pretrained_model.py:31-42``).
     Returns dict(loss, text_latents, image_latents, enc_image, indices, new_embed, new_cluster_size)."""
     enc_text = bert_forward(sd, 'text_transformer.', ids, mask, cfg.bert)
-    enc_image, ind, ne, ncs = ctvit_forward(sd, 'visual_transformer.', video, cfg.vit, training, trace)
+    enc_image, ind, ne, ncs = ctvit_forward(sd, 'visual_transformer.', video, cfg.vit, training, trace, force_ind)
     t_lat, i_lat = clip_latents(sd, enc_text, enc_image)
     loss = infonce(t_lat, i_lat, sd['temperature'])
     return dict(loss=loss, text_latents=t_lat, image_latents=i_lat, enc_image=enc_image,
