@@ -1,0 +1,206 @@
+"""Benchmark: CT-CLIP contrastive train step on MI355X (BASELINE.json metric: CT-report pairs/s).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL)
+
+A step = CTCLIP forward (BERT-base text tower on 128-token reports + CTViT base image tower on
+int16-HU 240x480x480 volumes + projections + InfoNCE over the all-gathered global batch) ->
+backward -> RCCL gradient all-reduce -> clip_grad_norm_(0.5) -> Adam, with every weight trained
+that the reference fine-tunes (ct_clip/fine_tuning_ctclip.py:6-14).  Inputs are synthetic and
+generated on the device before the timed region; weights are random-init of the same
+architecture (no network for checkpoints).  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+import types
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'ctpa-clip_amd'))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_HBM_GBS = 8000.0
+VIT_FWD_GFLOP_PER_VOL = 789.33 + 1.18   # 3D-ViT forward + deduplicated CPB
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--batch', type=int, default=8, help='volume/report pairs per GPU (configs[1]: 8)')
+    ap.add_argument('--text-len', type=int, default=128)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-batch', type=int, default=2)
+    return ap.parse_args()
+
+
+def synthetic_inputs(B, L, rank, device, frames=240, size=480, vocab=30522):
+    g = torch.Generator(device=device)
+    g.manual_seed(1234 + rank)
+    hu = torch.randint(-1200, 1201, (B, 1, frames, size, size), generator=g, device=device,
+                       dtype=torch.int32).to(torch.int16)
+    g.manual_seed(4321 + rank)
+    ids = torch.randint(5, vocab, (B, L), generator=g, device=device)
+    ids[:, 0] = 2
+    ids[:, -1] = 3
+    mask = torch.ones(B, L, dtype=torch.long, device=device)
+    return hu, types.SimpleNamespace(input_ids=ids, attention_mask=mask)
+
+
+def cpu_baseline(batch):
+    """The oracle (fp32 eager CPU restatement of the reference, pinned by tests/golden) timed on
+    this host: one full contrastive step (fwd + bwd + Adam) at batch `batch`, base config."""
+    from oracle import ctclip_oracle as O
+    from oracle import weights as W
+    threads = os.cpu_count() or 1
+    threads = min(threads, int(os.environ.get('OMP_NUM_THREADS', threads)))
+    torch.set_num_threads(threads)
+    cfg = O.BASE
+    sd = W.make_state_dict(cfg)
+    params = []
+    for k, v in sd.items():
+        if k.startswith(O.trainable_prefixes()) and v.is_floating_point() and 'vq._codebook' not in k \
+                and not k.endswith('beta') and v.numel():
+            v.requires_grad_(True)
+            params.append(v)
+    opt = torch.optim.Adam(params, lr=1.25e-6, betas=(0.9, 0.99), eps=1e-8)
+    ids, mask = W.make_text(batch, 128, cfg.bert.vocab_size)
+    video = O.normalize_hu(W.make_hu(batch, cfg.vit))
+    t0 = time.perf_counter()
+    out = O.ctclip_forward(sd, ids, mask, video, cfg, training=True)
+    out['loss'].backward()
+    torch.nn.utils.clip_grad_norm_(params, 0.5)
+    opt.step()
+    opt.zero_grad()
+    dt = time.perf_counter() - t0
+    cpu_name = ''
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                cpu_name = line.split(':', 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {'value': batch / dt, 'unit': 'pairs/s', 'cores': threads, 'kind': 'port',
+            'sample': f'1 contrastive step (fwd+bwd+clip+Adam), base config, batch {batch}, 128-token text, '
+                      f'fp32 eager oracle on CPU ({cpu_name}); {dt:.1f} s'}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+
+    from ctclip_mi355x.models import build_ctclip, set_finetune_trainable
+    from ctclip_mi355x.trainer import CTClipTrainer
+    from ctclip_mi355x import kernels as K
+
+    torch.manual_seed(0)   # identical random-init weights on every rank
+    model = set_finetune_trainable(build_ctclip()).to(dev)
+    model.train()
+    trainer = CTClipTrainer(model)
+    hu, text = synthetic_inputs(args.batch, args.text_len, rank, dev)
+
+    # live timing of the dominant kernel + the ViT forward (HIP events on the launch stream)
+    vt = model.visual_transformer
+    orig_encode = vt.encode_pooled
+    vit_events = []
+
+    def timed_encode(video):
+        if K.TIMER.active:
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            out = orig_encode(video)
+            e.record()
+            vit_events.append((s, e))
+            return out
+        return orig_encode(video)
+    vt.encode_pooled = timed_encode
+
+    for _ in range(args.warmup):
+        trainer.train_step(text, hu)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    K.TIMER.start(['ff1'])
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = trainer.train_step(text, hu)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    K.TIMER.stop()
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    ff1 = K.TIMER.summary('ff1')
+    vit_ms = sum(s.elapsed_time(e) for s, e in vit_events) / max(1, len(vit_events))
+    loss_v = float(loss.item())
+
+    pairs = world * args.batch * args.steps
+    value = pairs / elapsed
+    result = {
+        'metric': 'CT-report pairs/sec (contrastive step)',
+        'value': round(value, 3),
+        'unit': 'pairs/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(1000 * elapsed / args.steps, 3),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'bf16',
+        'data': 'synthetic: int16 HU volumes 1x240x480x480 (randint -1200..1200) + 128-token reports; '
+                'random-init CT-CLIP base weights',
+        'config': {'workload': 'CT-CLIP base contrastive train step: BERT-base(128 tok) + CTViT(480^2x240, '
+                               'patch 20x20x10, 4+4 layers, VQ 8192) + InfoNCE + bwd + RCCL grad all-reduce + '
+                               'clip 0.5 + Adam',
+                   'per_gpu_batch': args.batch, 'global_batch': world * args.batch, 'text_len': args.text_len,
+                   'parallelism': f'dp{world}', 'infonce_negatives': 'global batch (RCCL all-gather)'},
+        'loss': round(loss_v, 5),
+    }
+    if ff1:
+        tflops = ff1['flops'] / (ff1['avg_ms'] * 1e-3) / 1e12
+        result['roofline'] = {
+            'kernel': 'gemm_kernel<1,1> FF1 (LN-out x W1^T, GEGLU epilogue)',
+            'bound': 'mfma', 'achieved': round(tflops, 1), 'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
+            'frac': round(tflops / PEAK_BF16_TFLOPS, 4), 'traffic': None,
+            'avg_launch_ms': round(ff1['avg_ms'], 4), 'flops_per_launch': ff1['flops'],
+            'launches': ff1['launches']}
+    if vit_ms > 0:
+        vit_tf = VIT_FWD_GFLOP_PER_VOL * args.batch / (vit_ms * 1e-3) / 1e3
+        result['vit_forward'] = {'ms': round(vit_ms, 3), 'achieved_tflops': round(vit_tf, 1),
+                                 'frac_of_bf16_peak': round(vit_tf / PEAK_BF16_TFLOPS, 4),
+                                 'gflop_per_volume': VIT_FWD_GFLOP_PER_VOL}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        del trainer, model
+        torch.cuda.empty_cache()
+        result['cpu_baseline'] = cpu_baseline(args.cpu_batch)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

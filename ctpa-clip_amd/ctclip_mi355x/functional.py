@@ -189,7 +189,9 @@ class ViTLayerFn(torch.autograd.Function):
         xn2, _, m2, r2 = K.layernorm_fwd(x2f, ff_w, ff_b, 1e-5)
         W1p, W2p = pack_ff1(W1), pack_ff2(W2)
         g = torch.empty(xf.shape[0], W2p.shape[1], device=xf.device, dtype=BF16)
-        h = K.linear(xn2, W1p, act=K.ACT_GEGLU, out2=g)
+        # tagged for bench.py's live roofline: algorithmic flops exclude the zero padding rows
+        h = K.linear(xn2, W1p, act=K.ACT_GEGLU, out2=g, tag='ff1',
+                     flops=2.0 * xf.shape[0] * W1.shape[0] * W1.shape[1])
         x3b = torch.empty_like(xb)
         x3f = K.linear(g, W2p, residual=x2f, out_dtype=F32, out2=x3b)
         ctx.geo = geo

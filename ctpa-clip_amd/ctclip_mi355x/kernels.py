@@ -20,9 +20,55 @@ def _chk(t, name, dtype=None):
         raise ValueError(f'{name}: expected {dtype}, got {t.dtype}')
 
 
+class KernelTimer:
+    """Optional HIP-event bracketing of tagged launches (bench.py's live roofline measurement).
+    Events are recorded on torch's current stream — the stream the kernels launch on."""
+
+    def __init__(self):
+        self.active = False
+        self.tags = set()
+        self.events = []      # (tag, start, end, flops)
+
+    def start(self, tags):
+        self.active, self.tags, self.events = True, set(tags), []
+
+    def stop(self):
+        self.active = False
+
+    def __call__(self, tag, flops):
+        if not (self.active and tag in self.tags):
+            return None
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        self.events.append((tag, s, e, flops))
+        return e
+
+    def summary(self, tag):
+        torch.cuda.synchronize()
+        ev = [(s, e, f) for t, s, e, f in self.events if t == tag]
+        if not ev:
+            return None
+        ms = [s.elapsed_time(e) for s, e, _ in ev]
+        return dict(launches=len(ev), avg_ms=sum(ms) / len(ms), flops=ev[0][2])
+
+
+TIMER = KernelTimer()
+
+
 def gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, *, C2=None, ldc2=0, bias=None,
              R=None, ldr=0, alpha=1.0, act=ACT_NONE, accumulate=False, split_k=1, batch=1,
-             sA=0, sB=0, sC=0, sC2=0, sR=0):
+             sA=0, sB=0, sC=0, sC2=0, sR=0, tag=None, flops=None):
+    end = TIMER(tag, flops if flops is not None else 2.0 * M * N * K * batch) if tag else None
+    _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, C2=C2, ldc2=ldc2, bias=bias, R=R, ldr=ldr,
+              alpha=alpha, act=act, accumulate=accumulate, split_k=split_k, batch=batch, sA=sA, sB=sB, sC=sC,
+              sC2=sC2, sR=sR)
+    if end is not None:
+        end.record()
+
+
+def _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, *, C2=None, ldc2=0, bias=None,
+              R=None, ldr=0, alpha=1.0, act=ACT_NONE, accumulate=False, split_k=1, batch=1,
+              sA=0, sB=0, sC=0, sC2=0, sR=0):
     a = GemmArgs()
     a.M, a.N, a.K = M, N, K
     a.A, a.lda, a.a_kcontig = ptr(A), lda, int(a_kcontig)
@@ -37,7 +83,7 @@ def gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, *, C2=None, 
 
 
 def linear(x, w, *, bias=None, residual=None, out=None, out_dtype=BF16, act=ACT_NONE, out2=None, alpha=1.0,
-           accumulate=False):
+           accumulate=False, tag=None, flops=None):
     """y[M,N] = x[M,K] @ w[N,K]^T (+bias) (+residual); x, w bf16 row-major."""
     M, K = x.shape
     N = w.shape[0]
@@ -46,7 +92,8 @@ def linear(x, w, *, bias=None, residual=None, out=None, out_dtype=BF16, act=ACT_
         out = torch.empty(M, N, device=x.device, dtype=out_dtype)
     gemm_raw(M, N, K, x, x.stride(0), True, w, w.stride(0), True, out, out.stride(0),
              C2=out2, ldc2=out2.stride(0) if out2 is not None else 0, bias=bias, R=residual,
-             ldr=residual.stride(0) if residual is not None else 0, alpha=alpha, act=act, accumulate=accumulate)
+             ldr=residual.stride(0) if residual is not None else 0, alpha=alpha, act=act, accumulate=accumulate,
+             tag=tag, flops=flops)
     return out
 
 
