@@ -439,6 +439,137 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(AP p) {
   }
 }
 
+// ------------------------------------------------------------ backward dQ, biased (spatial) case
+// The continuous-position bias is shared by every frame, so its gradient is a sum over all
+// B*T frames of dS.  This kernel puts the FRAME loop innermost: a workgroup owns (head h,
+// 64 queries, a chunk of frames); its 8 waves = 4 query sub-blocks x 2 key halves keep the
+// frame-summed dS of their (16 queries x L/2 keys) tile in registers, and bin it to the
+// (2gh-1)(2gw-1) offsets once at the end (LDS atomics, then one global atomic per bin).
+// dQ of each frame is complete inside the workgroup (the two key halves meet in LDS).
+template <int MAXCH>   // max 32-key chunks per key half
+__global__ __launch_bounds__(NT) void attn_bwd_dq_bias_kernel(AP p, int nfc) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int D = 32, RS = Img<D>::RS, DB = 2;
+  const int L = p.L, Lp = (L + 31) & ~31, nc = Lp / 32, nc0 = (nc + 1) / 2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h = blockIdx.x, qg = blockIdx.y, fc = blockIdx.z;
+  const int qsub = w & 3, khalf = w >> 2;
+  const int c_begin = khalf ? nc0 : 0, c_end = khalf ? nc : nc0;
+  char* Kimg = smem;
+  char* Vimg = smem + Lp * RS;
+  float* ub = (float*)(smem + 2 * Lp * RS);
+  float* bins = ub + p.nbins;
+  float* xch = bins + p.nbins;   // [4 waves][64 lanes][8] dq exchange
+  for (int i = tid; i < p.nbins; i += NT) { ub[i] = p.bias_u[(int64_t)h * p.nbins + i]; bins[i] = 0.f; }
+  const int g = lane >> 4, li = lane & 15;
+  const int q = qg * 64 + qsub * 16 + li;
+  const bool qv = q < L;
+  const int hq = (int)(((float)q + 0.5f) * p.inv_wg), wq = q - hq * p.Wg;
+  f32x4 acc[MAXCH][2];
+#pragma unroll
+  for (int c = 0; c < MAXCH; ++c) { acc[c][0] = f32x4{0.f, 0.f, 0.f, 0.f}; acc[c][1] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+  const int f0 = (int)((int64_t)p.nseq * fc / nfc), f1 = (int)((int64_t)p.nseq * (fc + 1) / nfc);
+  for (int s = f0; s < f1; ++s) {
+    __syncthreads();   // previous frame's LDS reads done
+    stage<D>(Kimg, p.k, p.ldk, p, s, h, Lp, tid, NT);
+    stage<D>(Vimg, p.v, p.ldv, p, s, h, Lp, tid, NT);
+    __syncthreads();
+    const int64_t qrow = qv ? seq_row(p, s, q) : 0;
+    bf16x8 qf, df;
+    float dl = 0.f;
+    if (qv) {
+      qf = gload8(p.q + qrow * p.ldq + h * D + 8 * g);
+      df = gload8(p.dout + qrow * p.lddo + h * D + 8 * g);
+      const bf16x8 of = gload8(p.o + qrow * p.ldo + h * D + 8 * g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dl += (float)df[j] * (float)of[j];
+    } else {
+      qf = zero8();
+      df = zero8();
+    }
+    dl += __shfl_xor(dl, 16, 64);
+    dl += __shfl_xor(dl, 32, 64);
+    const float lse = qv ? p.lse[(int64_t)h * p.M + qrow] : INFINITY;
+    if (qv && g == 0 && khalf == 0) p.delta[(int64_t)h * p.M + qrow] = dl;
+    f32x4 dq[DB];
+#pragma unroll
+    for (int d = 0; d < DB; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ci = 0; ci < MAXCH; ++ci) {
+      const int c = c_begin + ci;
+      if (c < c_end) {
+        const int kc = c * 32;
+        f32x4 sa[2], da[2];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi) {
+          sa[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag<D>(Kimg, kc + 16 * bi, 0, lane), qf,
+                                                           f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          da[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag<D>(Vimg, kc + 16 * bi, 0, lane), df,
+                                                           f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        }
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = kc + 16 * bi + 4 * g + r;
+            float ds = 0.f;
+            if (qv && key < L) {
+              const float x = sa[bi][r] * p.scale + ub[bin_of(p, hq, wq, key)];
+              ds = __expf(x - lse) * (da[bi][r] - dl);
+            }
+            acc[ci][bi][r] += ds;
+            sa[bi][r] = ds * p.scale;
+          }
+        const bf16x8 dsb = pack_perm(sa[0], sa[1]);
+#pragma unroll
+        for (int d = 0; d < DB; ++d)
+          dq[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag<D>(Kimg, kc, d * 16, lane), dsb, dq[d], 0, 0, 0);
+      }
+    }
+    // combine the two key halves of this frame's dQ
+    if (khalf == 1) {
+#pragma unroll
+      for (int d = 0; d < DB; ++d)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xch[(qsub * 64 + lane) * 8 + d * 4 + r] = dq[d][r];
+    }
+    __syncthreads();
+    if (khalf == 0 && qv) {
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        f32x4 v = dq[d];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += xch[(qsub * 64 + lane) * 8 + d * 4 + r];
+        uint2 pk;
+        pk.x = pack2(v[0], v[1]);
+        pk.y = pack2(v[2], v[3]);
+        *(uint2*)(p.dq + qrow * p.lddq + h * D + d * 16 + 4 * g) = pk;
+      }
+    }
+  }
+  // bin the frame-summed dS once
+  if (qv) {
+#pragma unroll
+    for (int ci = 0; ci < MAXCH; ++ci) {
+      const int c = c_begin + ci;
+      if (c < c_end) {
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = c * 32 + 16 * bi + 4 * g + r;
+            if (key < L) atomicAdd(&bins[bin_of(p, hq, wq, key)], acc[ci][bi][r]);
+          }
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < p.nbins; i += NT) {
+    const float v = bins[i];
+    if (v != 0.f) atomicAdd(&p.dbias_u[(int64_t)h * p.nbins + i], v);
+  }
+}
+
 bool s_attr = false;
 
 template <int D>
@@ -446,6 +577,8 @@ void set_attrs() {
   (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dq_bias_kernel<9>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
 }
 
 int fill(AP& p, const ctclip_attn_args* a) {
@@ -512,6 +645,18 @@ extern "C" int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream) {
   if (lds1 > 160 * 1024 || lds2 > 160 * 1024) return CT_ESHAPE;
   dim3 grid(cdiv(pairs, p.pp));
   hipStream_t st = (hipStream_t)stream;
+  const int nc = Lp / 32;
+  if (a->D == 32 && p.bias_u && p.dbias_u && (nc + 1) / 2 <= 9) {
+    // frame-inner dQ + bias-gradient kernel (see attn_bwd_dq_bias_kernel)
+    const int nqg = cdiv(p.L, 64);
+    int nfc = std::max(1, std::min(p.nseq, (2 * 256 + p.H * nqg - 1) / (p.H * nqg)));
+    const size_t lds = (size_t)2 * Lp * RSb + 2 * (size_t)p.nbins * 4 + 4 * 64 * 8 * 4;
+    if (lds > 160 * 1024) return CT_ESHAPE;
+    hipLaunchKernelGGL(attn_bwd_dq_bias_kernel<9>, dim3(p.H, nqg, nfc), dim3(NT), lds, st, p, nfc);
+    hipLaunchKernelGGL(attn_bwd_dkv_kernel<32>, grid, dim3(NT), lds2, st, p);
+    CT_CHECK_LAUNCH();
+    return 0;
+  }
   if (a->D == 32) {
     hipLaunchKernelGGL(attn_bwd_dq_kernel<32>, grid, dim3(NT), lds1, st, p);
     hipLaunchKernelGGL(attn_bwd_dkv_kernel<32>, grid, dim3(NT), lds2, st, p);

@@ -5,8 +5,8 @@
 
 namespace {
 
-// GEGLU backward on the tile-interleaved pre-activation h (see gemm.hip act=2):
-// tile t: h[:, 128t + c] = x part, h[:, 128t + 64 + c] = gate part, g[:, 64t + c] = gelu(gate)*x.
+// GEGLU backward on the group-interleaved pre-activation h (see gemm.hip act=2):
+// group t: h[:, 64t + c] = x part, h[:, 64t + 32 + c] = gate part, g[:, 32t + c] = gelu(gate)*x.
 // (ct_clip/attention.py:39-42)
 __global__ __launch_bounds__(256) void geglu_bwd_kernel(const u16* __restrict__ dg, int64_t lddg,
                                                         const u16* __restrict__ h, int64_t ldh, int64_t rows,
@@ -16,18 +16,18 @@ __global__ __launch_bounds__(256) void geglu_bwd_kernel(const u16* __restrict__ 
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = i / nch;
     const int gc = (int)(i - r * nch) * 8;
-    const int t = gc >> 6, c = gc & 63;
+    const int t = gc >> 5, c = gc & 31;
     float d[8], x[8], gt[8], ox[8], og[8];
     unpack8(*(const u32x4*)(dg + r * lddg + gc), d);
-    unpack8(*(const u32x4*)(h + r * ldh + t * 128 + c), x);
-    unpack8(*(const u32x4*)(h + r * ldh + t * 128 + 64 + c), gt);
+    unpack8(*(const u32x4*)(h + r * ldh + t * 64 + c), x);
+    unpack8(*(const u32x4*)(h + r * ldh + t * 64 + 32 + c), gt);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       ox[j] = d[j] * gelu_erf(gt[j]);
       og[j] = d[j] * x[j] * gelu_erf_grad(gt[j]);
     }
-    *(u32x4*)(dh + r * lddh + t * 128 + c) = pack8(ox);
-    *(u32x4*)(dh + r * lddh + t * 128 + 64 + c) = pack8(og);
+    *(u32x4*)(dh + r * lddh + t * 64 + c) = pack8(ox);
+    *(u32x4*)(dh + r * lddh + t * 64 + 32 + c) = pack8(og);
   }
 }
 
@@ -106,7 +106,7 @@ inline int grid_for(int64_t n) { return (int)std::min<int64_t>(8192, std::max<in
 
 extern "C" int ctclip_geglu_bwd(const void* dg, int64_t lddg, const void* h, int64_t ldh, int64_t rows, int32_t gcols,
                                 void* dh, int64_t lddh, void* stream) {
-  CT_REQUIRE(gcols % 64 == 0, CT_ESHAPE);
+  CT_REQUIRE(gcols % 32 == 0, CT_ESHAPE);
   hipLaunchKernelGGL(geglu_bwd_kernel, dim3(grid_for(rows * gcols / 8)), dim3(256), 0, (hipStream_t)stream,
                      (const u16*)dg, lddg, (const u16*)h, ldh, rows, gcols, (u16*)dh, lddh);
   CT_CHECK_LAUNCH();

@@ -14,6 +14,8 @@
 #include "common.h"
 #include "../../include/ctclip_hip.h"
 
+int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream);  // gemm256.hip
+
 namespace {
 
 constexpr int BM = 128, BN = 128, BKT = 64, NTH = 256;
@@ -182,7 +184,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
   if (p.act == 3) {
     // argmax over this tile's columns per row: write (value, index) pairs per (row, tile)
     // C = float2 [M][ntiles]; columns >= N excluded.
-    // two threads per row, 64 columns each, first-max tie-break (torch.argmax semantics)
+    // one (value, index) per (row, 64-column group), first-max tie-break (torch.argmax semantics)
     const int row = t >> 1, half = t & 1;
     const int ncol = (int)min((int64_t)BN, p.N - n0);
     float best = -INFINITY;
@@ -191,13 +193,10 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
       const float v = cs[row * CS_LD + c];
       if (c < ncol && v > best) { best = v; bi = c; }
     }
-    const float ob = __shfl_xor(best, 1, 64);
-    const int oi = __shfl_xor(bi, 1, 64);
-    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
     const int64_t gm = m0 + row;
-    if (half == 0 && gm < p.M) {
+    if (gm < p.M && half * 64 < ncol) {
       float2* out = (float2*)p.C + bidx * p.sC;
-      out[gm * p.ldc + tx] = make_float2(best, __int_as_float((int)(n0 + bi)));
+      out[gm * p.ldc + tx * 2 + half] = make_float2(best, __int_as_float((int)(n0 + bi)));
     }
     return;
   }
@@ -263,17 +262,18 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
     if (p.C2 && p.act == 0) *(u32x4*)(p.C2 + bidx * p.sC2 + gm * p.ldc2 + gn) = pack8(v);
   }
   if (p.act == 2 && p.C2) {
-    // GEGLU: tile columns [0,64) are x, [64,128) the matching gates -> 64 output columns
+    // GEGLU: each 64-column group is [32 x | 32 gate] -> 32 output columns
     for (int it = 0; it < (BM * 64 / 8) / NTH; ++it) {
       const int c = t + NTH * it;
-      const int row = c >> 3, cc = (c & 7) * 8;
-      const int64_t gm = m0 + row, gn = n0 / 2 + cc;
-      if (gm >= p.M || n0 + cc >= p.N) continue;
+      const int row = c >> 3, oc = (c & 7) * 8;          // output column within the tile's 64
+      const int grp = oc >> 5, cc = grp * 64 + (oc & 31);  // x column within the tile
+      const int64_t gm = m0 + row, gn = n0 / 2 + oc;
+      if (gm >= p.M || n0 + grp * 64 >= p.N) continue;
       float v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float x = cs[row * CS_LD + cc + j] * p.alpha;
-        const float gt = cs[row * CS_LD + 64 + cc + j] * p.alpha;
+        const float gt = cs[row * CS_LD + 32 + cc + j] * p.alpha;
         // round h to bf16 first so forward g == geglu(stored h) bit-for-bit in backward
         const float xb = bf2f(f2bf(x)), gb = bf2f(f2bf(gt));
         v[j] = gelu_erf(gb) * xb;
@@ -313,6 +313,40 @@ __global__ void reduce_slabs_kernel(const float* __restrict__ s, int64_t nslab, 
   }
 }
 
+// skinny reduction (few output elements, many slabs): block = 64 float4 columns x 16 slab lanes
+__global__ __launch_bounds__(1024) void reduce_slabs_skinny_kernel(const float* __restrict__ s, int64_t nslab,
+                                                                   int64_t rows, int64_t cols, int64_t ld,
+                                                                   void* out, int64_t ldo, int out_f32,
+                                                                   int accumulate) {
+  __shared__ f32x4 red[16][64];
+  const int c4 = threadIdx.x & 63, lane = threadIdx.x >> 6;
+  const int64_t n4 = cols / 4;
+  const int64_t e = (int64_t)blockIdx.x * 64 + c4;   // float4 index over rows*cols/4
+  const bool valid = e < rows * n4;
+  const int64_t r = valid ? e / n4 : 0, c = valid ? (e - r * n4) * 4 : 0;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (valid) {
+#pragma unroll 4
+    for (int64_t z = lane; z < nslab; z += 16) acc += *(const f32x4*)(s + (z * rows + r) * ld + c);
+  }
+  red[lane][c4] = acc;
+  __syncthreads();
+  if (lane == 0 && valid) {
+    for (int k = 1; k < 16; ++k) acc += red[k][c4];
+    if (out_f32) {
+      float* o = (float*)out + r * ldo + c;
+      if (accumulate) acc += *(const f32x4*)o;
+      *(f32x4*)o = acc;
+    } else {
+      u16* o = (u16*)out + r * ldo + c;
+      if (accumulate) {
+        acc[0] += bf2f(o[0]); acc[1] += bf2f(o[1]); acc[2] += bf2f(o[2]); acc[3] += bf2f(o[3]);
+      }
+      o[0] = f2bf(acc[0]); o[1] = f2bf(acc[1]); o[2] = f2bf(acc[2]); o[3] = f2bf(acc[3]);
+    }
+  }
+}
+
 static bool s_smem_set = false;
 
 }  // namespace
@@ -333,7 +367,13 @@ extern "C" int ctclip_gemm(const ctclip_gemm_args* a, void* stream) {
     if (a->C2) CT_REQUIRE(aligned16(a->C2) && a->ldc2 % 8 == 0, CT_EALIGN);
     if (a->R) CT_REQUIRE(aligned16(a->R) && a->ldr % 8 == 0, CT_EALIGN);
   }
-  if (a->act == 2) CT_REQUIRE(a->N % BN == 0, CT_ESHAPE);
+  if (a->act == 2) CT_REQUIRE(a->N % 64 == 0 && a->ldc2 % 8 == 0, CT_ESHAPE);
+  {
+    const int b = a->batch > 0 ? a->batch : 1;
+    const int64_t tiles256 = ((a->M + 255) / 256) * ((a->N + 255) / 256) * split * b;
+    if (a->K % 64 == 0 && a->M >= 256 && a->N >= 256 && tiles256 >= 160 && (a->K / split) >= 64)
+      return ctclip_gemm256(a, split, b, stream);
+  }
   if (!s_smem_set) {
     (void)hipFuncSetAttribute((const void*)gemm_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
@@ -367,6 +407,12 @@ extern "C" int ctclip_reduce_slabs(const float* slabs, int64_t nslab, int64_t ro
   if (rows == 0 || cols == 0) return 0;
   CT_REQUIRE(cols % 4 == 0 && ld % 4 == 0 && ldo % 4 == 0, CT_EALIGN);
   const int64_t total = rows * (cols / 4);
+  if (total < 64 * 1024 && nslab >= 16) {
+    hipLaunchKernelGGL(reduce_slabs_skinny_kernel, dim3(cdiv(total, 64)), dim3(1024), 0, (hipStream_t)stream, slabs,
+                       nslab, rows, cols, ld, out, ldo, out_f32, accumulate);
+    CT_CHECK_LAUNCH();
+    return 0;
+  }
   const int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
   hipLaunchKernelGGL(reduce_slabs_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slabs, nslab, rows, cols,
                      ld, out, ldo, out_f32, accumulate);

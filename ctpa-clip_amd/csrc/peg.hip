@@ -15,14 +15,15 @@ namespace {
 
 struct Geo {
   int T, H, W;
-  int64_t thw;
+  int thw;
   int mode;
 };
 
-__device__ __forceinline__ int64_t canon(const Geo& g, int64_t b, int64_t p) {
+// token rows fit in 32 bits (B*T*H*W < 2^31); only the final row*D product is 64-bit
+__device__ __forceinline__ int canon(const Geo& g, int b, int p) {
   if (g.mode == 0) return b * g.thw + p;
-  const int64_t hw = p / g.T, t = p - hw * g.T;
-  return b * g.thw + t * (int64_t)(g.H * g.W) + hw;
+  const int hw = p / g.T, t = p - hw * g.T;
+  return b * g.thw + t * (g.H * g.W) + hw;
 }
 
 // forward (transpose = 0) or input-gradient (transpose = 1) of the depthwise conv
@@ -41,15 +42,16 @@ __global__ __launch_bounds__(256) void peg_kernel(const u16* __restrict__ xin, i
   if (threadIdx.x < 64) bs[threadIdx.x] = (bias && c0 + threadIdx.x < D) ? bias[c0 + threadIdx.x] : 0.f;
   __syncthreads();
   const int ch = threadIdx.x & 7;
-  const int64_t v = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const int v = blockIdx.x * 32 + (threadIdx.x >> 3);
   if (v >= ntok) return;
   const int col = c0 + ch * 8;
   if (col >= D) return;
-  const int64_t b = v / g.thw;
-  const int64_t p = v - b * g.thw;
-  const int wq = (int)(p % g.W);
-  const int hq = (int)((p / g.W) % g.H);
-  const int tq = (int)(p / ((int64_t)g.H * g.W));
+  const int b = v / g.thw;
+  const int p = v - b * g.thw;
+  const int hwq = p / g.W;
+  const int wq = p - hwq * g.W;
+  const int tq = hwq / g.H;
+  const int hq = hwq - tq * g.H;
   float acc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = TRANSPOSE ? 0.f : bs[ch * 8 + j];
@@ -65,16 +67,16 @@ __global__ __launch_bounds__(256) void peg_kernel(const u16* __restrict__ xin, i
       for (int kw = 0; kw < 3; ++kw) {
         const int ww = TRANSPOSE ? wq + 1 - kw : wq + kw - 1;
         if (ww < 0 || ww >= g.W) continue;
-        const int64_t pn = ((int64_t)tt * g.H + hh) * g.W + ww;
+        const int pn = (tt * g.H + hh) * g.W + ww;
         float xv[8];
-        unpack8(*(const u32x4*)(xin + canon(g, b, pn) * D + col), xv);
+        unpack8(*(const u32x4*)(xin + (int64_t)canon(g, b, pn) * D + col), xv);
         const int tap = (kt * 3 + kh) * 3 + kw;
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[j] += ws[tap][ch * 8 + j] * xv[j];
       }
     }
   }
-  const int64_t co = canon(g, b, p) * D + col;
+  const int64_t co = (int64_t)canon(g, b, p) * D + col;
   if (res) {
     const f32x4 a = *(const f32x4*)(res + co), bb = *(const f32x4*)(res + co + 4);
 #pragma unroll
@@ -92,7 +94,7 @@ __global__ __launch_bounds__(256) void peg_kernel(const u16* __restrict__ xin, i
 __global__ __launch_bounds__(192) void peg_wgrad_kernel(const u16* __restrict__ dout, const u16* __restrict__ xin,
                                                         int64_t ntok, int D, Geo g, int64_t tok_per_blk,
                                                         float* __restrict__ part) {
-  __shared__ float red[8][3][8][10][8];  // [tokenlane][kt][chunk][9 taps + bias][8 ch]
+  __shared__ float red[3][8][10][8];  // [kt][chunk][9 taps + bias][8 ch]
   const int tl = threadIdx.x & 7, ch = (threadIdx.x >> 3) & 7, kt = threadIdx.x >> 6;
   const int c0 = blockIdx.y * 64;
   const int col = c0 + ch * 8;
@@ -103,17 +105,18 @@ __global__ __launch_bounds__(192) void peg_wgrad_kernel(const u16* __restrict__ 
     for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) accb[j] = 0.f;
-  const int64_t v0 = (int64_t)blockIdx.x * tok_per_blk;
-  const int64_t v1 = min(ntok, v0 + tok_per_blk);
+  const int v0 = blockIdx.x * (int)tok_per_blk;
+  const int v1 = min((int)ntok, v0 + (int)tok_per_blk);
   if (col < D) {
-    for (int64_t v = v0 + tl; v < v1; v += 8) {
-      const int64_t b = v / g.thw;
-      const int64_t p = v - b * g.thw;
-      const int wq = (int)(p % g.W);
-      const int hq = (int)((p / g.W) % g.H);
-      const int tq = (int)(p / ((int64_t)g.H * g.W));
+    for (int v = v0 + tl; v < v1; v += 8) {
+      const int b = v / g.thw;
+      const int p = v - b * g.thw;
+      const int hwq = p / g.W;
+      const int wq = p - hwq * g.W;
+      const int tq = hwq / g.H;
+      const int hq = hwq - tq * g.H;
       float dv[8];
-      unpack8(*(const u32x4*)(dout + canon(g, b, p) * D + col), dv);
+      unpack8(*(const u32x4*)(dout + (int64_t)canon(g, b, p) * D + col), dv);
       if (kt == 0) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) accb[j] += dv[j];
@@ -128,34 +131,41 @@ __global__ __launch_bounds__(192) void peg_wgrad_kernel(const u16* __restrict__ 
         for (int kw = 0; kw < 3; ++kw) {
           const int ww = wq + kw - 1;
           if (ww < 0 || ww >= g.W) continue;
-          const int64_t pn = ((int64_t)tt * g.H + hh) * g.W + ww;
+          const int pn = (tt * g.H + hh) * g.W + ww;
           float xv[8];
-          unpack8(*(const u32x4*)(xin + canon(g, b, pn) * D + col), xv);
+          unpack8(*(const u32x4*)(xin + (int64_t)canon(g, b, pn) * D + col), xv);
 #pragma unroll
           for (int j = 0; j < 8; ++j) acc[kh * 3 + kw][j] += dv[j] * xv[j];
         }
       }
     }
   }
+  // fold the 8 token lanes (lane bits 0..2) with shuffles, then one LDS slot per (kt, chunk)
 #pragma unroll
   for (int i = 0; i < 9; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) red[tl][kt][ch][i][j] = acc[i][j];
+    for (int j = 0; j < 8; ++j) {
+      float v = acc[i][j];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      if (tl == 0) red[kt][ch][i][j] = v;
+    }
 #pragma unroll
-  for (int j = 0; j < 8; ++j) red[tl][kt][ch][9][j] = accb[j];
+  for (int j = 0; j < 8; ++j) {
+    float v = accb[j];
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    if (tl == 0) red[kt][ch][9][j] = v;
+  }
   __syncthreads();
   // 64 channels x 28 outputs = 1792 values; 192 threads
   for (int o = threadIdx.x; o < 64 * 28; o += 192) {
     const int c = o / 28, k = o - c * 28;
     if (c0 + c >= D) continue;
     const int chh = c >> 3, j = c & 7;
-    float s = 0.f;
-    if (k < 27) {
-      const int kt2 = k / 9, i = k - kt2 * 9;
-      for (int t = 0; t < 8; ++t) s += red[t][kt2][chh][i][j];
-    } else {
-      for (int t = 0; t < 8; ++t) s += red[t][0][chh][9][j];
-    }
+    const float s = k < 27 ? red[k / 9][chh][k % 9][j] : red[0][chh][9][j];
     part[((int64_t)blockIdx.x * D + c0 + c) * 28 + k] = s;
   }
 }
@@ -166,7 +176,7 @@ extern "C" int ctclip_peg_fwd(const void* x_bf16, const float* x_f32, int64_t B,
                               int32_t D, const float* weight, const float* bias, int32_t mode, float* out_f32,
                               void* out_bf16, void* stream) {
   CT_REQUIRE(D % 8 == 0, CT_EALIGN);
-  Geo g{T, H, W, (int64_t)T * H * W, mode};
+  Geo g{T, H, W, T * H * W, mode};
   const int64_t ntok = B * g.thw;
   dim3 grid(cdiv(ntok, 32), cdiv(D, 64));
   hipLaunchKernelGGL(peg_kernel<0>, grid, dim3(256), 0, (hipStream_t)stream, (const u16*)x_bf16, ntok, D, weight,
@@ -180,7 +190,7 @@ extern "C" int ctclip_peg_bwd_data(const void* dout_bf16, const float* dout_f32,
                                    int32_t W, int32_t D, const float* weight, int32_t mode, float* dx_f32,
                                    void* dx_bf16, void* stream) {
   CT_REQUIRE(D % 8 == 0, CT_EALIGN);
-  Geo g{T, H, W, (int64_t)T * H * W, mode};
+  Geo g{T, H, W, T * H * W, mode};
   const int64_t ntok = B * g.thw;
   dim3 grid(cdiv(ntok, 32), cdiv(D, 64));
   hipLaunchKernelGGL(peg_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, (const u16*)dout_bf16, ntok, D, weight,
@@ -193,7 +203,7 @@ extern "C" int ctclip_peg_bwd_data(const void* dout_bf16, const float* dout_f32,
 extern "C" int ctclip_peg_bwd_weight(const void* dout_bf16, const void* x_bf16, int64_t B, int32_t T, int32_t H,
                                      int32_t W, int32_t D, int32_t mode, float* part, int32_t nblk, void* stream) {
   CT_REQUIRE(D % 8 == 0, CT_EALIGN);
-  Geo g{T, H, W, (int64_t)T * H * W, mode};
+  Geo g{T, H, W, T * H * W, mode};
   const int64_t ntok = B * g.thw;
   const int64_t per = (ntok + nblk - 1) / nblk;
   dim3 grid(nblk, cdiv(D, 64));

@@ -53,18 +53,19 @@ def ff_pad(inner):
 
 
 def ff1_rowmap(inner, device):
-    """Row map of the GEGLU-interleaved W1: packed row t*128 + c  <- x row t*64+c,
-    t*128 + 64 + c <- gate row inner + t*64 + c  (-1 = zero padding)."""
+    """Row map of the GEGLU-interleaved W1: packed row t*64 + c  <- x row t*32+c,
+    t*64 + 32 + c <- gate row inner + t*32 + c  (-1 = zero padding); 32-column pairs so one
+    wave's 64 output columns always hold matching x / gate halves."""
     key = ('ff1', inner, str(device))
     if key not in _MAP_CACHE:
         P = ff_pad(inner)
         m = torch.full((2 * P,), -1, dtype=torch.int32)
-        for t in range(P // 64):
-            for c in range(64):
-                j = t * 64 + c
+        for t in range(P // 32):
+            for c in range(32):
+                j = t * 32 + c
                 if j < inner:
-                    m[t * 128 + c] = j
-                    m[t * 128 + 64 + c] = inner + j
+                    m[t * 64 + c] = j
+                    m[t * 64 + 32 + c] = inner + j
         _MAP_CACHE[key] = m.to(device)
     return _MAP_CACHE[key]
 
@@ -283,7 +284,7 @@ class VQPoolFn(torch.autograd.Function):
         cb_b = state.codebook_bf16(cb)
         ones = state.ones(D, zf.device)
         xn_b = K.l2norm_scale_fwd(zb, 1, D, ones)
-        nt = (C + 127) // 128
+        nt = (C + 63) // 64          # one (score, index) candidate per 64-code group
         cand = torch.empty(zf.shape[0], nt, 2, device=zf.device, dtype=F32)
         K.gemm_raw(zf.shape[0], C, D, xn_b, D, True, cb_b, D, True, cand, nt, act=K.ACT_ARGMAX)
         idx, xn = K.vq_select(cand, zf, cb, want_xn=training)

@@ -151,7 +151,7 @@ def nblocks_for(rows, cap=1024):
 def colsum(x, out=None, accumulate=False):
     """Column sums of x[rows, cols] (bf16 or f32) -> f32 [cols]."""
     rows, cols = x.shape
-    nb = nblocks_for(rows, 512)
+    nb = nblocks_for(rows, 256)
     part = torch.empty(nb, cols, device=x.device, dtype=F32)
     call('ctclip_colsum', ptr(x), int(x.dtype == F32), x.stride(0), rows, cols, ptr(part), nb, stream_ptr())
     if out is None:
@@ -205,7 +205,7 @@ def l2norm_scale_fwd(x, H, D, scale, out=None):
 def l2norm_scale_bwd(x, dy, H, D, scale, out):
     rows = x.shape[0]
     lpr = H * D // 8
-    nb = 512
+    nb = 256
     while (nb * 256) % lpr:
         nb += 1
     part = torch.empty(nb, D, device=x.device, dtype=F32)

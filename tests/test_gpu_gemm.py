@@ -62,29 +62,69 @@ def test_matmul_tn(K, M, N, K_):
     assert _rel(dw, dy.float().t() @ x.float()) < 1e-5
 
 
-def test_gelu_and_geglu_epilogue(K):
+@pytest.mark.parametrize('M', [384, 40000])    # 128-tile kernel / 256-tile glds kernel
+def test_gelu_and_geglu_epilogue(K, M):
     torch.manual_seed(3)
-    M, Kd = 384, 512
+    Kd, N = 512, 1024
     x = torch.randn(M, Kd, device='cuda').bfloat16()
-    w = (torch.randn(256, Kd, device='cuda') / 20).bfloat16()
-    y = K.linear(x, w, act=K.ACT_GELU, out_dtype=torch.float32)
-    ref = torch.nn.functional.gelu(x.float() @ w.float().t())
-    assert _rel(y, ref) < 1e-5
-    g = torch.empty(M, 128, device='cuda', dtype=torch.bfloat16)
+    w = (torch.randn(N, Kd, device='cuda') / 20).bfloat16()
+    pre = torch.empty(M, N, device='cuda', dtype=torch.bfloat16)
+    y = K.linear(x, w, act=K.ACT_GELU, out2=pre)
+    ref_pre = x.float() @ w.float().t()
+    assert _rel(y, torch.nn.functional.gelu(ref_pre)) < 4e-3
+    assert _rel(pre, ref_pre) < 4e-3
+    g = torch.empty(M, N // 2, device='cuda', dtype=torch.bfloat16)
     h = K.linear(x, w, act=K.ACT_GEGLU, out2=g)
-    hf = h.float()
-    ref_g = torch.cat([torch.nn.functional.gelu(hf[:, 64:128]) * hf[:, :64],
-                       torch.nn.functional.gelu(hf[:, 192:256]) * hf[:, 128:192]], 1)
+    hf = h.float().reshape(M, N // 64, 2, 32)
+    ref_g = (torch.nn.functional.gelu(hf[:, :, 1]) * hf[:, :, 0]).reshape(M, N // 2)
     assert _rel(g, ref_g) < 4e-3
-    assert _rel(h, x.float() @ w.float().t()) < 4e-3
+    assert _rel(h, ref_pre) < 4e-3
 
 
-def test_argmax_epilogue(K):
+@pytest.mark.parametrize('M,N,K_,lay', [(8192, 2816, 512, 'nt'), (4096, 512, 1408, 'nt'), (20480, 512, 512, 'nn'),
+                                        (20480, 512, 2816, 'nn'), (40960, 2816, 512, 'tn'), (65536, 512, 256, 'tn')])
+def test_large_tile_layouts(K, M, N, K_, lay):
+    """Shapes that dispatch to the 256x256 glds kernel (all three layouts, residual/bias epilogues)."""
+    torch.manual_seed(7)
+    if lay == 'nt':
+        x = torch.randn(M, K_, device='cuda').bfloat16()
+        w = torch.randn(N, K_, device='cuda').bfloat16()
+        r = torch.randn(M, N, device='cuda')
+        b = torch.randn(N, device='cuda')
+        y = K.linear(x, w, bias=b, residual=r, out_dtype=torch.float32)
+        assert _rel(y, x.float() @ w.float().t() + b + r) < 1e-5
+    elif lay == 'nn':
+        dy = torch.randn(M, N, device='cuda').bfloat16()
+        w = torch.randn(N, K_, device='cuda').bfloat16()
+        dx = K.matmul_nn(dy, w, out_dtype=torch.float32)
+        assert _rel(dx, dy.float() @ w.float()) < 1e-5
+    else:
+        dy = torch.randn(M, N, device='cuda').bfloat16()
+        x = torch.randn(M, K_, device='cuda').bfloat16()
+        dw = K.matmul_tn(dy, x)
+        assert _rel(dw, dy.float().t() @ x.float()) < 1e-5
+
+
+def test_large_tile_exact_asymmetric(K):
+    M, N, K_ = 1024, 1024, 256
+    x = (torch.arange(M * K_, device='cuda').reshape(M, K_) % 7 - 3).bfloat16()
+    w = (torch.arange(N * K_, device='cuda').reshape(N, K_) % 5 - 2).bfloat16()
+    y = K.linear(x, w, out_dtype=torch.float32)
+    assert torch.equal(y, x.float() @ w.float().t())
+    dy = (torch.arange(M * N, device='cuda').reshape(M, N) % 3 - 1).bfloat16()
+    dx = K.matmul_nn(dy, w, out_dtype=torch.float32)
+    assert torch.equal(dx, dy.float() @ w.float())
+    dw = K.matmul_tn(dy, x, split_k=8)
+    assert torch.equal(dw, dy.float().t() @ x.float())
+
+
+@pytest.mark.parametrize('M', [1000, 70000])
+def test_argmax_epilogue(K, M):
     torch.manual_seed(4)
-    M, Nc, Kd = 1000, 1024, 512
+    Nc, Kd = 1024, 512
     x = torch.randn(M, Kd, device='cuda').bfloat16()
     w = torch.randn(Nc, Kd, device='cuda').bfloat16()
-    nt = Nc // 128
+    nt = Nc // 64
     out = torch.empty(M, nt, 2, device='cuda', dtype=torch.float32)
     K.gemm_raw(M, Nc, Kd, x, Kd, True, w, Kd, True, out, nt, act=K.ACT_ARGMAX)
     vals = out[..., 0]

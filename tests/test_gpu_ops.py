@@ -191,7 +191,7 @@ def test_vq_select_and_pool(K):
     x = torch.randn(M, D, device=dev)
     cb = F.normalize(torch.randn(C, D, device=dev), dim=-1)
     xn = F.normalize(x, dim=-1)
-    nt = C // 128
+    nt = C // 64
     cand = torch.empty(M, nt, 2, device=dev)
     K.gemm_raw(M, C, D, xn.bfloat16(), D, True, cb.bfloat16(), D, True, cand, nt, act=K.ACT_ARGMAX)
     idx, xno = K.vq_select(cand, x, cb)

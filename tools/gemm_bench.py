@@ -1,0 +1,52 @@
+"""Per-shape timing of the MFMA GEMM on the contrastive step's main shapes (B = 8 tokens = 110,592).
+usage: python tools/gemm_bench.py   (GPU)"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'ctpa-clip_amd'))
+import torch  # noqa: E402
+
+from ctclip_mi355x import kernels as K  # noqa: E402
+
+M = 110592
+
+
+def timeit(fn, n=20):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(n):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n
+
+
+def main():
+    torch.manual_seed(0)
+    r = lambda *s: (torch.rand(*s, device='cuda') * 2 - 1).bfloat16()  # noqa: E731
+    x512, x1408 = r(M, 512), r(M, 1408)
+    w1, w2, wq, wkv = r(2816, 512), r(512, 1408), r(256, 512), r(512, 512)
+    g = torch.empty(M, 1408, device='cuda', dtype=torch.bfloat16)
+    res = torch.randn(M, 512, device='cuda')
+    dh = r(M, 2816)
+    cases = [
+        ('FF1 NT+GEGLU  110592x2816x512', lambda: K.linear(x512, w1, act=K.ACT_GEGLU, out2=g), 2 * M * 2816 * 512),
+        ('FF2 NT+res32  110592x512x1408', lambda: K.linear(x1408, w2, residual=res, out_dtype=torch.float32),
+         2 * M * 512 * 1408),
+        ('Q   NT        110592x256x512', lambda: K.linear(x512, wq), 2 * M * 256 * 512),
+        ('KV  NT        110592x512x512', lambda: K.linear(x512, wkv), 2 * M * 512 * 512),
+        ('dX  NN        110592x512x2816', lambda: K.matmul_nn(dh, w1), 2 * M * 512 * 2816),
+        ('dX  NN        110592x1408x512', lambda: K.matmul_nn(x512, w2), 2 * M * 1408 * 512),
+        ('dW  TN        2816x512x110592', lambda: K.matmul_tn(dh, x512), 2 * M * 512 * 2816),
+        ('dW  TN        512x512x110592', lambda: K.matmul_tn(x512, x512), 2 * M * 512 * 512),
+    ]
+    for name, fn, fl in cases:
+        ms = timeit(fn)
+        print(f'{name:34s} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s', flush=True)
+
+
+if __name__ == '__main__':
+    main()
