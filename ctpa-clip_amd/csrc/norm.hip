@@ -3,20 +3,21 @@
 // LayerNorm replaces: ct_clip/attention.py:28-35 (bias-less LayerNorm, gamma only, eps 1e-5),
 // nn.LayerNorm in FeedForward (attention.py:47) and to_patch_emb (ctvit.py:171,173), BERT's
 // LayerNorms (eps 1e-12).  One wave per row, the row held in registers (CPL chunks of 8 per
-// lane), 16-B vector loads, f32 statistics.
+// lane), 16-B vector loads, f32 statistics.  Input dtypes are template parameters (no runtime
+// branches in the loops) and gamma / beta are loaded once per lane as vectors, outside the row
+// loop (scalar per-element parameter loads serialised the first version to 1.4 TB/s).
 #include "common.h"
 #include "../../include/ctclip_hip.h"
 
 namespace {
 
-template <int CPL>
-__device__ __forceinline__ void load_row(const void* x, int x_f32, int64_t row, int64_t ld, int D, int lane,
-                                         float (&v)[CPL][8]) {
+template <int CPL, bool XF>
+__device__ __forceinline__ void load_row(const void* x, int64_t row, int64_t ld, int D, int lane, float (&v)[CPL][8]) {
 #pragma unroll
   for (int c = 0; c < CPL; ++c) {
     const int col = (c * 64 + lane) * 8;
     if (col < D) {
-      if (x_f32) {
+      if constexpr (XF) {
         const float* p = (const float*)x + row * ld + col;
         const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
 #pragma unroll
@@ -31,62 +32,83 @@ __device__ __forceinline__ void load_row(const void* x, int x_f32, int64_t row, 
   }
 }
 
+// per-lane copy of a length-D parameter vector in the same chunk layout as the row (or `dflt`)
 template <int CPL>
-__global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x, int x_f32, int64_t ldx, int64_t rows,
-                                                     int D, const float* __restrict__ gamma,
-                                                     const float* __restrict__ beta, float eps, u16* __restrict__ yb,
-                                                     int64_t ldyb, float* __restrict__ yf, int64_t ldyf,
+__device__ __forceinline__ void load_param(const float* p, int D, int lane, float dflt, float (&v)[CPL][8]) {
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    const int col = (c * 64 + lane) * 8;
+    if (p && col < D) {
+      const f32x4 a = *(const f32x4*)(p + col), b = *(const f32x4*)(p + col + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[c][j] = a[j]; v[c][4 + j] = b[j]; }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[c][j] = dflt;
+    }
+  }
+}
+
+// RPW rows per wave, all row loads issued before the reductions
+template <int CPL, int RPW, bool XF>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x, int64_t ldx, int64_t rows, int D,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     float eps, u16* __restrict__ yb, int64_t ldyb,
+                                                     float* __restrict__ yf, int64_t ldyf,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  float v[CPL][8];
-  load_row<CPL>(x, x_f32, row, ldx, D, lane, v);
-  float s = 0.f;
+  const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  float gv[CPL][8], bv[CPL][8];
+  load_param<CPL>(gamma, D, lane, 1.f, gv);
+  load_param<CPL>(beta, D, lane, 0.f, bv);
+  float v[RPW][CPL][8];
 #pragma unroll
-  for (int c = 0; c < CPL; ++c)
+  for (int r = 0; r < RPW; ++r)
+    if (row0 + r < rows) load_row<CPL, XF>(x, row0 + r, ldx, D, lane, v[r]);
+  const float invD = 1.f / D;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += v[c][j];
-  const float mean = warp_sum(s) / D;
-  float q = 0.f;
+  for (int r = 0; r < RPW; ++r) {
+    const int64_t row = row0 + r;
+    if (row >= rows) break;
+    float s = 0.f;
 #pragma unroll
-  for (int c = 0; c < CPL; ++c) {
-    const int col = (c * 64 + lane) * 8;
-    if (col < D)
+    for (int c = 0; c < CPL; ++c)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { const float d = v[c][j] - mean; q += d * d; }
-  }
-  const float var = warp_sum(q) / D;
-  const float rstd = rsqrtf(var + eps);
-  if (lane == 0) {
-    if (mean_out) mean_out[row] = mean;
-    if (rstd_out) rstd_out[row] = rstd;
-  }
+      for (int j = 0; j < 8; ++j) s += v[r][c][j];
+    const float mean = warp_sum(s) * invD;
+    float q = 0.f;
 #pragma unroll
-  for (int c = 0; c < CPL; ++c) {
-    const int col = (c * 64 + lane) * 8;
-    if (col >= D) continue;
-    float o[8];
+    for (int c = 0; c < CPL; ++c) {
+      const bool in = (c * 64 + lane) * 8 < D;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float t = (v[c][j] - mean) * rstd;
-      if (gamma) t *= gamma[col + j];
-      if (beta) t += beta[col + j];
-      o[j] = t;
+      for (int j = 0; j < 8; ++j) { const float d = in ? v[r][c][j] - mean : 0.f; q += d * d; }
     }
-    if (yb) *(u32x4*)(yb + row * ldyb + col) = pack8(o);
-    if (yf) {
-      float* p = yf + row * ldyf + col;
-      *(f32x4*)p = f32x4{o[0], o[1], o[2], o[3]};
-      *(f32x4*)(p + 4) = f32x4{o[4], o[5], o[6], o[7]};
+    const float rstd = rsqrtf(warp_sum(q) * invD + eps);
+    if (lane == 0) {
+      if (mean_out) mean_out[row] = mean;
+      if (rstd_out) rstd_out[row] = rstd;
+    }
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int col = (c * 64 + lane) * 8;
+      if (col >= D) continue;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[r][c][j] - mean) * rstd * gv[c][j] + bv[c][j];
+      if (yb) *(u32x4*)(yb + row * ldyb + col) = pack8(o);
+      if (yf) {
+        float* p = yf + row * ldyf + col;
+        *(f32x4*)p = f32x4{o[0], o[1], o[2], o[3]};
+        *(f32x4*)(p + 4) = f32x4{o[4], o[5], o[6], o[7]};
+      }
     }
   }
 }
 
 // dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)) [+ dres];  dgamma/dbeta partials.
-template <int CPL>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy, int dy_f32, int64_t lddy,
-                                                     const void* __restrict__ x, int x_f32, int64_t ldx,
+template <int CPL, bool DYF, bool XF>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy, int64_t lddy,
+                                                     const void* __restrict__ x, int64_t ldx,
                                                      const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, const float* __restrict__ gamma,
                                                      int64_t rows, int D, const float* __restrict__ dres,
@@ -95,36 +117,39 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
                                                      float* __restrict__ part_g, float* __restrict__ part_b) {
   __shared__ float red[4][2][CPL * 512];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float gv[CPL][8];
+  load_param<CPL>(gamma, D, lane, 1.f, gv);
   float ag[CPL][8], ab[CPL][8];
 #pragma unroll
   for (int c = 0; c < CPL; ++c)
 #pragma unroll
     for (int j = 0; j < 8; ++j) { ag[c][j] = 0.f; ab[c][j] = 0.f; }
+  const float invD = 1.f / D;
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < rows; row += nw) {
-    float g[CPL][8], xv[CPL][8];
-    load_row<CPL>(dy, dy_f32, row, lddy, D, lane, g);
-    load_row<CPL>(x, x_f32, row, ldx, D, lane, xv);
+    float g[CPL][8], xv[CPL][8], rv[CPL][8];
+    load_row<CPL, DYF>(dy, row, lddy, D, lane, g);
+    load_row<CPL, XF>(x, row, ldx, D, lane, xv);
+    if (dres) load_row<CPL, true>(dres, row, lddres, D, lane, rv);   // issued before the reductions
     const float mean = mean_in[row], rstd = rstd_in[row];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
-      const int col = (c * 64 + lane) * 8;
-      if (col >= D) continue;
+      const bool in = (c * 64 + lane) * 8 < D;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float xh = (xv[c][j] - mean) * rstd;
+        const float xh = in ? (xv[c][j] - mean) * rstd : 0.f;
         xv[c][j] = xh;
         ag[c][j] += g[c][j] * xh;
         ab[c][j] += g[c][j];
-        const float gg = gamma ? g[c][j] * gamma[col + j] : g[c][j];
+        const float gg = g[c][j] * gv[c][j];
         g[c][j] = gg;
         s1 += gg;
         s2 += gg * xh;
       }
     }
-    s1 = warp_sum(s1) / D;
-    s2 = warp_sum(s2) / D;
+    s1 = warp_sum(s1) * invD;
+    s2 = warp_sum(s2) * invD;
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const int col = (c * 64 + lane) * 8;
@@ -133,10 +158,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = rstd * (g[c][j] - s1 - xv[c][j] * s2);
       if (dres) {
-        const float* p = dres + row * lddres + col;
-        const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { o[j] += a[j]; o[4 + j] += b[j]; }
+        for (int j = 0; j < 8; ++j) o[j] += rv[c][j];
       }
       if (dxf) {
         float* p = dxf + row * lddxf + col;
@@ -162,7 +185,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
 }
 
 // per-head l2norm + per-dim scale:  y = x / max(||x||, 1e-12) * scale[d]     (attention.py:152-154)
-// one lane handles 8 of a head's D elements; D in {16, 32, 64}; x row stride ldx, heads at h*D.
+// one lane handles 8 of a head's D elements; D in {16, 32, 64, ..., 512}; heads at h*D.
 __global__ __launch_bounds__(256) void l2n_fwd_kernel(const u16* __restrict__ x, int64_t ldx, int64_t rows, int H,
                                                       int D, const float* __restrict__ scale, u16* __restrict__ y,
                                                       int64_t ldy) {
@@ -172,6 +195,7 @@ __global__ __launch_bounds__(256) void l2n_fwd_kernel(const u16* __restrict__ x,
   const int c = (int)(gid - row * lpr);
   if (row >= rows) return;
   const int col = c * 8, d0 = col % D;
+  const f32x4 s0 = *(const f32x4*)(scale + d0), s1v = *(const f32x4*)(scale + d0 + 4);
   float v[8];
   unpack8(*(const u32x4*)(x + row * ldx + col), v);
   float s = 0.f;
@@ -181,12 +205,11 @@ __global__ __launch_bounds__(256) void l2n_fwd_kernel(const u16* __restrict__ x,
   const float inv = 1.f / fmaxf(sqrtf(s), 1e-12f);
   float o8[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o8[j] = v[j] * inv * scale[d0 + j];
+  for (int j = 0; j < 4; ++j) { o8[j] = v[j] * inv * s0[j]; o8[4 + j] = v[4 + j] * inv * s1v[j]; }
   *(u32x4*)(y + row * ldy + col) = pack8(o8);
 }
 
-// backward of the above: dx = (du - u (u.du)) / max(||x||,eps) (only if ||x|| > eps), du = dy*scale;
-// dscale partial[d] += dy * u
+// backward of the above: dx = (du - u (u.du)) / max(||x||,eps), du = dy*scale; dscale partial[d] += dy * u
 __global__ __launch_bounds__(256) void l2n_bwd_kernel(const u16* __restrict__ x, int64_t ldx, const u16* __restrict__ dy,
                                                       int64_t lddy, int64_t rows, int H, int D,
                                                       const float* __restrict__ scale, u16* __restrict__ dx,
@@ -199,6 +222,12 @@ __global__ __launch_bounds__(256) void l2n_bwd_kernel(const u16* __restrict__ x,
   const int64_t gid0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int c = (int)(gid0 % lpr);
   const int col = c * 8, d0 = col % D;
+  float sc[8];
+  {
+    const f32x4 a = *(const f32x4*)(scale + d0), b = *(const f32x4*)(scale + d0 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { sc[j] = a[j]; sc[4 + j] = b[j]; }
+  }
   for (int64_t row = gid0 / lpr; row < rows; row += nthreads / lpr) {
     float v[8], g[8];
     unpack8(*(const u32x4*)(x + row * ldx + col), v);
@@ -214,7 +243,7 @@ __global__ __launch_bounds__(256) void l2n_bwd_kernel(const u16* __restrict__ x,
     for (int j = 0; j < 8; ++j) {
       const float u = v[j] * inv;
       acc[j] += g[j] * u;
-      du[j] = g[j] * scale[d0 + j];
+      du[j] = g[j] * sc[j];
       ud += du[j] * u;
     }
     for (int o = 1; o < D / 8; o <<= 1) ud += __shfl_xor(ud, o, 64);
@@ -246,7 +275,6 @@ __global__ __launch_bounds__(256) void l2n_bwd_kernel(const u16* __restrict__ x,
 __global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ x, int x_f32, int64_t ld, int64_t rows,
                                                      int cols, float* __restrict__ part) {
   const int nch = cols / 8;
-  // thread -> (chunk, row-lane)
   const int per_row = min(nch, 256);
   const int rl = 256 / per_row;
   const int ch0 = threadIdx.x % per_row, r0 = threadIdx.x / per_row;
@@ -258,8 +286,9 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ x,
         float v[8];
         if (x_f32) {
           const float* p = (const float*)x + r * ld + ch * 8;
+          const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = p[j];
+          for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
         } else {
           unpack8(*(const u32x4*)((const u16*)x + r * ld + ch * 8), v);
         }
@@ -284,6 +313,32 @@ __global__ __launch_bounds__(256) void colsum_kernel(const void* __restrict__ x,
 
 int ln_cpl(int D) { return (D + 511) / 512; }
 
+template <int C, int R>
+void launch_ln_fwd(bool xf, dim3 grid, hipStream_t st, const void* x, int64_t ldx, int64_t rows, int D,
+                   const float* gamma, const float* beta, float eps, u16* yb, int64_t ldyb, float* yf, int64_t ldyf,
+                   float* mean, float* rstd) {
+  if (xf)
+    hipLaunchKernelGGL((ln_fwd_kernel<C, R, true>), grid, dim3(256), 0, st, x, ldx, rows, D, gamma, beta, eps, yb,
+                       ldyb, yf, ldyf, mean, rstd);
+  else
+    hipLaunchKernelGGL((ln_fwd_kernel<C, R, false>), grid, dim3(256), 0, st, x, ldx, rows, D, gamma, beta, eps, yb,
+                       ldyb, yf, ldyf, mean, rstd);
+}
+
+template <int C>
+void launch_ln_bwd(bool dyf, bool xf, dim3 grid, hipStream_t st, const void* dy, int64_t lddy, const void* x,
+                   int64_t ldx, const float* mean, const float* rstd, const float* gamma, int64_t rows, int D,
+                   const float* dres, int64_t lddres, float* dxf, int64_t lddxf, u16* dxb, int64_t lddxb, float* pg,
+                   float* pb) {
+#define LB(A, B_) hipLaunchKernelGGL((ln_bwd_kernel<C, A, B_>), grid, dim3(256), 0, st, dy, lddy, x, ldx, mean, rstd, \
+                                     gamma, rows, D, dres, lddres, dxf, lddxf, dxb, lddxb, pg, pb)
+  if (dyf && xf) LB(true, true);
+  else if (dyf) LB(true, false);
+  else if (xf) LB(false, true);
+  else LB(false, false);
+#undef LB
+}
+
 }  // namespace
 
 extern "C" int ctclip_layernorm_fwd(const void* x, int32_t x_f32, int64_t ldx, int64_t rows, int32_t D,
@@ -292,15 +347,18 @@ extern "C" int ctclip_layernorm_fwd(const void* x, int32_t x_f32, int64_t ldx, i
   if (rows == 0) return 0;
   CT_REQUIRE(D % 8 == 0 && ldx % 8 == 0, CT_EALIGN);
   const int cpl = ln_cpl(D);
-  dim3 grid(cdiv(rows, 4));
   hipStream_t st = (hipStream_t)stream;
-#define LNF(C) hipLaunchKernelGGL(ln_fwd_kernel<C>, grid, dim3(256), 0, st, x, x_f32, ldx, rows, D, gamma, beta, eps, \
-                                  (u16*)y_bf16, ldyb, y_f32, ldyf, mean, rstd)
-  if (cpl == 1) LNF(1);
-  else if (cpl == 2) LNF(2);
-  else if (cpl <= 8) LNF(8);
-  else return CT_ESHAPE;
-#undef LNF
+  if (cpl == 1)
+    launch_ln_fwd<1, 4>(x_f32, dim3(cdiv(rows, 16)), st, x, ldx, rows, D, gamma, beta, eps, (u16*)y_bf16, ldyb,
+                        y_f32, ldyf, mean, rstd);
+  else if (cpl == 2)
+    launch_ln_fwd<2, 2>(x_f32, dim3(cdiv(rows, 8)), st, x, ldx, rows, D, gamma, beta, eps, (u16*)y_bf16, ldyb,
+                        y_f32, ldyf, mean, rstd);
+  else if (cpl <= 8)
+    launch_ln_fwd<8, 1>(x_f32, dim3(cdiv(rows, 4)), st, x, ldx, rows, D, gamma, beta, eps, (u16*)y_bf16, ldyb,
+                        y_f32, ldyf, mean, rstd);
+  else
+    return CT_ESHAPE;
   CT_CHECK_LAUNCH();
   return 0;
 }
@@ -315,12 +373,14 @@ extern "C" int ctclip_layernorm_bwd(const void* dy, int32_t dy_f32, int64_t lddy
   const int cpl = ln_cpl(D);
   dim3 grid(nblocks);
   hipStream_t st = (hipStream_t)stream;
-#define LNB(C) hipLaunchKernelGGL(ln_bwd_kernel<C>, grid, dim3(256), 0, st, dy, dy_f32, lddy, x, x_f32, ldx, mean, rstd, \
-                                  gamma, rows, D, dres, lddres, dx_f32, lddxf, (u16*)dx_bf16, lddxb, part_gamma, part_beta)
-  if (cpl == 1) LNB(1);
-  else if (cpl == 2) LNB(2);
-  else return CT_ESHAPE;  // D > 1024 not needed on the backward path (patch LN uses the folded-weight trick)
-#undef LNB
+  if (cpl == 1)
+    launch_ln_bwd<1>(dy_f32, x_f32, grid, st, dy, lddy, x, ldx, mean, rstd, gamma, rows, D, dres, lddres, dx_f32,
+                     lddxf, (u16*)dx_bf16, lddxb, part_gamma, part_beta);
+  else if (cpl == 2)
+    launch_ln_bwd<2>(dy_f32, x_f32, grid, st, dy, lddy, x, ldx, mean, rstd, gamma, rows, D, dres, lddres, dx_f32,
+                     lddxf, (u16*)dx_bf16, lddxb, part_gamma, part_beta);
+  else
+    return CT_ESHAPE;  // D > 1024 not needed on the backward path (patch LN uses the folded-weight trick)
   CT_CHECK_LAUNCH();
   return 0;
 }

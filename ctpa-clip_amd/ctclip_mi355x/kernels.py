@@ -124,8 +124,16 @@ def matmul_tn(dy, x, *, out=None, accumulate=False, split_k=None, alpha=1.0):
     if out is None:
         out = torch.zeros(N, K, device=dy.device, dtype=F32) if accumulate else \
             torch.empty(N, K, device=dy.device, dtype=F32)
-    tiles = ((N + 127) // 128) * ((K + 127) // 128)
-    s = split_for(M, tiles) if split_k is None else split_k
+    if split_k is not None:
+        s = split_k
+    elif False and N >= 256 and K >= 256 and M % 64 == 0:   # 256-tile TN measured slower (r01)
+        # 256x256-tile kernel: ~320 workgroups, >= 8 K-steps of 64 per split
+        t256 = ((N + 255) // 256) * ((K + 255) // 256)
+        s = max(1, min((320 + t256 - 1) // t256, M // 512))
+        if t256 * s < 160:
+            s = split_for(M, ((N + 127) // 128) * ((K + 127) // 128))
+    else:
+        s = split_for(M, ((N + 127) // 128) * ((K + 127) // 128))
     if s <= 1:
         gemm_raw(N, K, M, dy, dy.stride(0), False, x, x.stride(0), False, out, out.stride(0),
                  accumulate=accumulate, alpha=alpha)

@@ -48,5 +48,21 @@ def main():
         print(f'{name:34s} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s', flush=True)
 
 
-if __name__ == '__main__':
+if __name__ == '__main__' and len(sys.argv) == 1:
     main()
+
+
+def ksweep():
+    """Per-tile fixed cost vs per-K-step cost: NT GEMM, M=27648, N=2816, K in 512..4096."""
+    torch.manual_seed(0)
+    Mm, N = 27648, 2816
+    for Kd in (512, 1024, 2048, 4096):
+        x = (torch.rand(Mm, Kd, device='cuda') * 2 - 1).bfloat16()
+        w = (torch.rand(N, Kd, device='cuda') * 2 - 1).bfloat16()
+        out = torch.empty(Mm, N, device='cuda', dtype=torch.bfloat16)
+        ms = timeit(lambda: K.linear(x, w, out=out))
+        print(f'NT M={Mm} N={N} K={Kd:5d}: {ms:7.3f} ms {2 * Mm * N * Kd / ms / 1e9:8.1f} TF/s', flush=True)
+
+
+if __name__ == '__main__' and len(sys.argv) > 1 and sys.argv[1] == 'ksweep':
+    ksweep()

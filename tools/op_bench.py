@@ -1,0 +1,56 @@
+"""Isolated timing of the bandwidth-bound kernels at the step's shapes (110,592 tokens x 512)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'ctpa-clip_amd'))
+import torch  # noqa: E402
+
+from ctclip_mi355x import kernels as K  # noqa: E402
+
+M, D = 110592, 512
+
+
+def timeit(fn, n=20):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(n):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n
+
+
+def main():
+    torch.manual_seed(0)
+    xf = torch.randn(M, D, device='cuda')
+    xb = xf.bfloat16()
+    g = torch.randn(D, device='cuda')
+    b = torch.randn(D, device='cuda')
+    _, _, mean, rstd = K.layernorm_fwd(xf, g, b, 1e-5)
+    w = torch.randn(D, 1, 3, 3, 3, device='cuda') * 0.1
+    pb = torch.randn(D, device='cuda')
+    dg = torch.randn(M, 1408, device='cuda').bfloat16()
+    h = torch.randn(M, 2816, device='cuda').bfloat16()
+    qs = torch.ones(32, device='cuda')
+    cases = [
+        ('ln_fwd f32->bf16', lambda: K.layernorm_fwd(xf, g, b, 1e-5), M * D * 6),
+        ('ln_fwd f32->bf16+f32', lambda: K.layernorm_fwd(xf, g, b, 1e-5, out_f32=True), M * D * 10),
+        ('ln_bwd', lambda: K.layernorm_bwd(xb, xb, mean, rstd, g, dres=xf), M * D * (2 + 2 + 4 + 4 + 2)),
+        ('peg_fwd mode0', lambda: K.peg_fwd(xb, xf, 8, 24, 24, 24, w, pb, 0), M * D * (2 + 4 + 4 + 2)),
+        ('peg_fwd mode1', lambda: K.peg_fwd(xb, xf, 8, 24, 24, 24, w, pb, 1), M * D * (2 + 4 + 4 + 2)),
+        ('peg_bwd (data+w)', lambda: K.peg_bwd(xb, xf, xb, 8, 24, 24, 24, w, 0), M * D * (2 + 4 + 4 + 2 + 4)),
+        ('geglu_bwd', lambda: K.geglu_bwd(dg, h), M * (1408 + 2816 + 2816) * 2),
+        ('l2n_fwd', lambda: K.l2norm_scale_fwd(xb[:, :256], 8, 32, qs), M * 256 * 4),
+        ('cast f32->bf16', lambda: K.cast_bf16(xf), M * D * 6),
+        ('colsum bf16', lambda: K.colsum(xb), M * D * 2),
+    ]
+    for name, fn, nbytes in cases:
+        ms = timeit(fn)
+        print(f'{name:24s} {ms * 1e3:9.1f} us  {nbytes / ms / 1e9:7.2f} TB/s (algorithmic bytes)', flush=True)
+
+
+if __name__ == '__main__':
+    main()
