@@ -1,0 +1,69 @@
+"""Data-parallel exchange steps of the contrastive step (one process per GPU, RCCL over xGMI).
+
+The reference runs the step under accelerate/DDP (ct_clip/CTCLIPTrainer.py:185-215, 337-340):
+an all-reduce of every gradient bucket, and — through the loss — negatives drawn from the
+local batch.  Here the step has exactly three exchanges, each one collective:
+
+  1. ``gather_latents``: all-gather of the raw [B, 512] text / image latents so InfoNCE sees the
+     GLOBAL batch as negatives (every rank then computes the same global loss; ``local_rows``
+     keeps the gradient rows of this rank's pairs);
+  2. ``sum_codebook_stats``: SUM of the VQ EMA statistics (per-code counts and token sums) so every
+     rank applies the same codebook update (vector_quantize_pytorch's EMA with a synced codebook);
+  3. ``sum_grads``: ONE SUM all-reduce over the flat f32 gradient arena (trainer.FlatParams).
+
+Because every rank back-propagates only its own rows of a loss that is global, the SUM in (3)
+reproduces the single-process gradient of the global batch exactly (tests/test_dist_gloo.py
+checks this on world_size 2 with gloo).  Parameters that receive a gradient from the full
+global loss on every rank (the temperature) are divided by the world size in the backward
+(``replicated_grad_scale``) so the SUM counts them once.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def world_rank():
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def gather_latents(t_raw: torch.Tensor, i_raw: torch.Tensor):
+    """[B, Dl] x 2 on each rank -> ([world*B, Dl], [world*B, Dl]) in rank order."""
+    world, _ = world_rank()
+    if world == 1:
+        return t_raw.contiguous(), i_raw.contiguous()
+    B, Dl = t_raw.shape
+    both = torch.cat([t_raw, i_raw], 0).contiguous()
+    gathered = torch.empty(world * 2 * B, Dl, device=both.device, dtype=both.dtype)
+    if dist.get_backend() == 'gloo':
+        dist.all_gather(list(gathered.view(world, 2 * B, Dl).unbind(0)), both)
+    else:
+        dist.all_gather_into_tensor(gathered, both)
+    g = gathered.view(world, 2, B, Dl)
+    return g[:, 0].reshape(world * B, Dl).contiguous(), g[:, 1].reshape(world * B, Dl).contiguous()
+
+
+def local_rows(x: torch.Tensor, B: int) -> torch.Tensor:
+    """This rank's B rows of a [world*B, ...] global tensor."""
+    _, rank = world_rank()
+    return x[rank * B:(rank + 1) * B]
+
+
+def replicated_grad_scale() -> float:
+    world, _ = world_rank()
+    return 1.0 / world
+
+
+def sum_codebook_stats(*tensors: torch.Tensor) -> None:
+    world, _ = world_rank()
+    if world > 1:
+        for t in tensors:
+            dist.all_reduce(t)
+
+
+def sum_grads(flat_grad: torch.Tensor) -> None:
+    world, _ = world_rank()
+    if world > 1:
+        dist.all_reduce(flat_grad)

@@ -13,8 +13,8 @@ import math
 from dataclasses import dataclass
 
 import torch
-import torch.distributed as dist
 
+from . import dist_sync
 from . import kernels as K
 
 F32, BF16 = torch.float32, torch.bfloat16
@@ -295,9 +295,7 @@ class VQPoolFn(torch.autograd.Function):
             bins = torch.zeros(C, device=zf.device, dtype=F32)
             esum = torch.zeros(C, D, device=zf.device, dtype=F32)
             K.vq_ema_accum(idx, xn, bins, esum)
-            if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-                dist.all_reduce(bins)
-                dist.all_reduce(esum)
+            dist_sync.sum_codebook_stats(bins, esum)
             K.vq_ema_finalize(bins, esum, decay, cb, cluster.view(-1), cb_b)
             state.mark_codebook_fresh(cb)
         ctx.geo = geo
@@ -388,11 +386,6 @@ class TextProjFn(torch.autograd.Function):
 
 
 # ----------------------------------------------------------------------------- loss
-def _world():
-    if dist.is_available() and dist.is_initialized():
-        return dist.get_world_size(), dist.get_rank()
-    return 1, 0
-
 
 class ClipLossFn(torch.autograd.Function):
     """Symmetric InfoNCE (ct_clip/ct_clip.py:845-901).  Under torch.distributed the raw latents
@@ -400,30 +393,23 @@ class ClipLossFn(torch.autograd.Function):
     same global loss and back-propagates its own rows (gradients are then SUM-reduced)."""
 
     @staticmethod
-    def forward(ctx, t_raw, i_raw, log_temp):
-        world, rank = _world()
+    def forward(ctx, t_raw, i_raw, log_temp, impl=None):
         B = t_raw.shape[0]
-        if world > 1:
-            both = torch.cat([t_raw, i_raw], 0).contiguous()
-            gathered = torch.empty(world * 2 * B, t_raw.shape[1], device=t_raw.device, dtype=F32)
-            dist.all_gather_into_tensor(gathered, both)
-            g = gathered.view(world, 2, B, -1)
-            tg = g[:, 0].reshape(world * B, -1).contiguous()
-            ig = g[:, 1].reshape(world * B, -1).contiguous()
-        else:
-            tg, ig = t_raw.contiguous(), i_raw.contiguous()
-        loss, dt, di, dlt, tn, inn, sim = K.clip_loss(tg, ig, log_temp.reshape(1).contiguous())
-        ctx.save_for_backward(dt[rank * B:(rank + 1) * B], di[rank * B:(rank + 1) * B], dlt)
-        ctx.world = world
+        tg, ig = dist_sync.gather_latents(t_raw, i_raw)
+        # impl: the fused HIP loss (default); tests substitute a CPU restatement to exercise
+        # the exchange logic under gloo
+        loss, dt, di, dlt = (impl or K.clip_loss)(tg, ig, log_temp.reshape(1).contiguous())[:4]
+        ctx.save_for_backward(dist_sync.local_rows(dt, B), dist_sync.local_rows(di, B), dlt)
+        ctx.scale = dist_sync.replicated_grad_scale()
         return loss.reshape(())
 
     @staticmethod
     def backward(ctx, dloss):
         dt, di, dlt = ctx.saved_tensors
         s = dloss.reshape(1)
-        # log-temperature gradient: every rank holds the full global value -> divide by world so a
-        # SUM all-reduce reproduces it once.
-        return dt * s, di * s, (dlt * s / ctx.world).reshape(())
+        # log-temperature gradient: every rank holds the full global value -> scaled by 1/world so
+        # the SUM all-reduce reproduces it once.
+        return dt * s, di * s, (dlt * s * ctx.scale).reshape(()), None
 
 
 # ----------------------------------------------------------------------------- BERT

@@ -9,8 +9,8 @@ never syncs the host: the clip coefficient stays on the device).
 from __future__ import annotations
 
 import torch
-import torch.distributed as dist
 
+from . import dist_sync
 from . import kernels as K
 
 
@@ -57,7 +57,7 @@ class CTClipTrainer:
         self.lr, self.wd, self.max_grad_norm, self.betas, self.eps = lr, wd, max_grad_norm, betas, eps
         self.steps = 0
         self.norm = torch.zeros(2, device=dev, dtype=torch.float32)
-        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        self.world = dist_sync.world_rank()[0]
 
     def forward_backward(self, text, video):
         loss = self.model(text, video, device=self.device, return_loss=True)
@@ -66,8 +66,7 @@ class CTClipTrainer:
         return loss
 
     def optimizer_step(self):
-        if self.world > 1:
-            dist.all_reduce(self.flat.grad)          # SUM: ClipLossFn gives each rank its own rows
+        dist_sync.sum_grads(self.flat.grad)          # SUM: ClipLossFn gives each rank its own rows
         K.grad_norm(self.flat.grad, self.max_grad_norm if self.max_grad_norm else 0.0, self.norm)
         self.steps += 1
         K.adam(self.flat.data, self.flat.grad, self.m, self.v, lr=self.lr, b1=self.betas[0], b2=self.betas[1],

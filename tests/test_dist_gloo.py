@@ -1,0 +1,129 @@
+"""N > 1 data-parallel exchange logic on CPU (gloo, world_size 2).
+
+The GPU path runs one process per GPU over RCCL; the exchange steps themselves
+(ctclip_mi355x/dist_sync.py) are backend-agnostic host logic, exercised here with the InfoNCE
+kernel replaced by the oracle's restatement (oracle.infonce, ct_clip/ct_clip.py:845-901):
+
+  * every rank computes the same GLOBAL loss from all-gathered latents;
+  * backward through each rank's own rows + one SUM all-reduce reproduces the single-process
+    gradient of the global batch (encoder weights and the shared temperature);
+  * summed VQ EMA statistics equal the statistics of the global batch;
+  * the flat-arena trainer layout all-reduces every parameter's gradient in one collective.
+"""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import ctclip_oracle as O
+
+WORLD, B, DIN, DL = 2, 3, 16, 8
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def oracle_clip_loss(tg, ig, log_temp):
+    """Same outputs as kernels.clip_loss (loss, dt, di, dlt) from the oracle's InfoNCE."""
+    t = tg.detach().clone().requires_grad_(True)
+    i = ig.detach().clone().requires_grad_(True)
+    lt = log_temp.detach().clone().reshape(()).requires_grad_(True)
+    with torch.enable_grad():          # called inside an autograd.Function forward
+        tn = torch.nn.functional.normalize(t, dim=-1)
+        inn = torch.nn.functional.normalize(i, dim=-1)
+        loss = O.infonce(tn, inn, lt)
+        loss.backward()
+    return loss.detach().reshape(1), t.grad, i.grad, lt.grad.reshape(1)
+
+
+def _problem():
+    g = torch.Generator().manual_seed(7)
+    xt = torch.randn(WORLD * B, DIN, generator=g, dtype=torch.float64).float()
+    xi = torch.randn(WORLD * B, DIN, generator=g, dtype=torch.float64).float()
+    wt = torch.randn(DIN, DL, generator=g, dtype=torch.float64).float()
+    wi = torch.randn(DIN, DL, generator=g, dtype=torch.float64).float()
+    return xt, xi, wt, wi
+
+
+def _single_process():
+    xt, xi, wt, wi = _problem()
+    wt.requires_grad_(True)
+    wi.requires_grad_(True)
+    lt = torch.tensor(1.0, requires_grad=True)
+    loss = O.infonce(torch.nn.functional.normalize(xt @ wt, dim=-1),
+                     torch.nn.functional.normalize(xi @ wi, dim=-1), lt)
+    loss.backward()
+    return loss.detach(), wt.grad, wi.grad, lt.grad
+
+
+def _worker(rank, port, out_dir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=WORLD)
+    try:
+        from ctclip_mi355x import dist_sync
+        from ctclip_mi355x.functional import ClipLossFn
+        from ctclip_mi355x.trainer import FlatParams
+        xt, xi, wt0, wi0 = _problem()
+        wt = torch.nn.Parameter(wt0.clone())
+        wi = torch.nn.Parameter(wi0.clone())
+        lt = torch.nn.Parameter(torch.tensor(1.0))
+        flat = FlatParams([wt, wi, lt], torch.device('cpu'))
+        rows = slice(rank * B, (rank + 1) * B)
+        loss = ClipLossFn.apply(xt[rows] @ wt, xi[rows] @ wi, lt, oracle_clip_loss)
+        loss.backward()
+        flat.rebind_grads()
+        dist_sync.sum_grads(flat.grad)
+
+        ref_loss, gwt, gwi, glt = _single_process()
+        assert torch.allclose(loss.detach(), ref_loss, rtol=1e-6, atol=1e-6), (loss.item(), ref_loss.item())
+        torch.testing.assert_close(wt.grad, gwt, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(wi.grad, gwi, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(lt.grad, glt, rtol=1e-5, atol=1e-6)
+        # the arena IS the .grad storage: the single collective covered every parameter
+        assert wt.grad.data_ptr() == flat.grad.data_ptr()
+
+        # VQ EMA statistics: per-code counts and token sums of the local tokens, summed
+        C, D, n = 5, 4, 7
+        g = torch.Generator().manual_seed(11)
+        idx = torch.randint(0, C, (WORLD, n), generator=g)
+        tok = torch.randn(WORLD, n, D, generator=g)
+        bins = torch.zeros(C).index_add_(0, idx[rank], torch.ones(n))
+        esum = torch.zeros(C, D).index_add_(0, idx[rank], tok[rank])
+        dist_sync.sum_codebook_stats(bins, esum)
+        ref_bins = torch.zeros(C).index_add_(0, idx.reshape(-1), torch.ones(WORLD * n))
+        ref_esum = torch.zeros(C, D).index_add_(0, idx.reshape(-1), tok.reshape(-1, D))
+        assert torch.equal(bins, ref_bins)
+        torch.testing.assert_close(esum, ref_esum)
+
+        # gathered latents arrive in rank order
+        tg, ig = dist_sync.gather_latents(torch.full((B, DL), float(rank)), torch.full((B, DL), 10.0 + rank))
+        assert torch.equal(tg[:, 0], torch.arange(WORLD).repeat_interleave(B).float())
+        assert torch.equal(ig[:, 0], 10 + torch.arange(WORLD).repeat_interleave(B).float())
+        open(os.path.join(out_dir, f'ok{rank}'), 'w').close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_contrastive_exchange(tmp_path):
+    mp.spawn(_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    assert all((tmp_path / f'ok{r}').exists() for r in range(WORLD))
+
+
+def test_single_process_path_matches_oracle():
+    """world_size 1: the same Function with no process group is the plain global loss."""
+    from ctclip_mi355x.functional import ClipLossFn
+    xt, xi, wt0, wi0 = _problem()
+    wt = wt0.clone().requires_grad_(True)
+    wi = wi0.clone().requires_grad_(True)
+    lt = torch.tensor(1.0, requires_grad=True)
+    loss = ClipLossFn.apply(xt @ wt, xi @ wi, lt, oracle_clip_loss)
+    loss.backward()
+    ref_loss, gwt, gwi, glt = _single_process()
+    assert torch.allclose(loss.detach(), ref_loss)
+    torch.testing.assert_close(wt.grad, gwt)
+    torch.testing.assert_close(lt.grad, glt)

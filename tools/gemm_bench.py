@@ -34,6 +34,7 @@ def main():
     dh = r(M, 2816)
     cases = [
         ('FF1 NT+GEGLU  110592x2816x512', lambda: K.linear(x512, w1, act=K.ACT_GEGLU, out2=g), 2 * M * 2816 * 512),
+        ('FF1 NT plain  110592x2816x512', lambda: K.linear(x512, w1, out=dh), 2 * M * 2816 * 512),
         ('FF2 NT+res32  110592x512x1408', lambda: K.linear(x1408, w2, residual=res, out_dtype=torch.float32),
          2 * M * 512 * 1408),
         ('Q   NT        110592x256x512', lambda: K.linear(x512, wq), 2 * M * 256 * 512),
