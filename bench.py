@@ -181,10 +181,20 @@ def main():
     }
     if ff1:
         tflops = ff1['flops'] / (ff1['avg_ms'] * 1e-3) / 1e12
+        M = args.batch * 24 * 24 * 24
+        algo_bytes = 2 * (M * 512 + 2816 * 512 + M * (2816 + 1408))   # A + W1 + h + GEGLU(h), bf16
+        traffic, traffic_src = None, None
+        pmc = os.path.join(REPO, 'profiles', 'r01_ff1_pmc.json')
+        if args.batch == 8 and os.path.exists(pmc):
+            rec = json.load(open(pmc))
+            traffic = round(rec['traffic_bytes_per_launch'] / 1e9, 4)
+            traffic_src = 'profiles/r01_ff1_pmc.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, GB per launch)'
         result['roofline'] = {
-            'kernel': 'gemm_kernel<1,1> FF1 (LN-out x W1^T, GEGLU epilogue)',
+            'kernel': 'g256::gemm256_kernel<true,true> FF1 (LN-out x W1^T, GEGLU epilogue)',
             'bound': 'mfma', 'achieved': round(tflops, 1), 'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
-            'frac': round(tflops / PEAK_BF16_TFLOPS, 4), 'traffic': None,
+            'frac': round(tflops / PEAK_BF16_TFLOPS, 4), 'traffic': traffic, 'traffic_unit': 'GB',
+            'traffic_source': traffic_src, 'algorithmic_bytes': algo_bytes,
+            'hbm_frac': round(algo_bytes / (ff1['avg_ms'] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
             'avg_launch_ms': round(ff1['avg_ms'], 4), 'flops_per_launch': ff1['flops'],
             'launches': ff1['launches']}
     if vit_ms > 0:
