@@ -170,7 +170,276 @@ __global__ __launch_bounds__(192) void peg_wgrad_kernel(const u16* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Plane-streaming kernels (the fast path).  A workgroup owns HT view rows x all W columns x 64
+// channels of one batch element and walks the view-time axis.  Input planes (HT+2 rows with
+// the h halo, W+2 columns with zero padding, 64 channels, bf16) stream through a 4-slot LDS ring:
+// each input byte is fetched from L2/HBM ~(HT+2)/HT times instead of 27, and every output is
+// computed from LDS.  A thread covers SEG consecutive w positions of one 8-channel chunk and
+// slides a (SEG+2)-wide window along w, so each (kt, kh) costs SEG+2 window reads + 3 weight
+// reads for SEG outputs.  The ring slot written in step t is (t+lead+1)&3, never one of the
+// three read in step t, so one barrier per step suffices.
+// W <= 24 (one item per thread); 3 ring slots + weights = 47 KB -> 3 workgroups per CU, so the
+// base grid (8 x 12 x 8 = 768 workgroups) is resident in one round
+constexpr int HT = 2, SEG = 3, SEGW = 6, TNTH = 128, WNTH = 256, LMAX = 8, NSLOT = 3;
+
+__host__ __device__ inline int plane_bytes(int W) { return (HT + 2) * (W + 2) * 128; }
+
+// issue this thread's loads of plane tp (view coordinates) into registers
+template <int NT>
+__device__ __forceinline__ void plane_load(const u16* __restrict__ x, const Geo& g, int D, int b, int h0, int c0,
+                                           int tp, u32x4 (&reg)[LMAX * TNTH / NT]) {
+  const int nl = (HT + 2) * (g.W + 2) * 8;
+#pragma unroll
+  for (int m = 0; m < LMAX * TNTH / NT; ++m) {
+    const int i = threadIdx.x + m * NT;
+    reg[m] = u32x4{0u, 0u, 0u, 0u};
+    if (i < nl) {
+      const int k = i & 7, cw = (i >> 3) % (g.W + 2), hr = (i >> 3) / (g.W + 2);
+      const int h = h0 - 1 + hr, w = cw - 1;
+      if (h >= 0 && h < g.H && w >= 0 && w < g.W)
+        reg[m] = *(const u32x4*)(x + (int64_t)canon(g, b, (tp * g.H + h) * g.W + w) * D + c0 + k * 8);
+    }
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void plane_store(char* ring, int W, int tp, const u32x4 (&reg)[LMAX * TNTH / NT]) {
+  const int nl = (HT + 2) * (W + 2) * 8;
+  char* dst = ring + (tp % NSLOT) * plane_bytes(W);
+#pragma unroll
+  for (int m = 0; m < LMAX * TNTH / NT; ++m) {
+    const int i = threadIdx.x + m * NT;
+    if (i < nl) *(u32x4*)(dst + i * 16) = reg[m];
+  }
+}
+
+// forward (TR = 0) or input-gradient (TR = 1); grid (B * ceil(H/HT), D/64), TNTH threads
+template <int TR>
+__global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ xin, int D,
+                                                        const float* __restrict__ w, const float* __restrict__ bias,
+                                                        const float* __restrict__ res, Geo g,
+                                                        float* __restrict__ out, u16* __restrict__ outb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nht = (g.H + HT - 1) / HT;
+  const int b = blockIdx.x / nht, h0 = (blockIdx.x - b * nht) * HT, c0 = blockIdx.y * 64;
+  const int pb = plane_bytes(g.W);
+  char* ring = smem;
+  float* ws = (float*)(smem + NSLOT * pb);   // [27][64]
+  float* bs = ws + 27 * 64;
+  for (int i = threadIdx.x; i < 27 * 64; i += TNTH) {
+    const int c = i / 27, tap = i - c * 27;
+    ws[tap * 64 + c] = w[(int64_t)(c0 + c) * 27 + tap];
+  }
+  if (threadIdx.x < 64) bs[threadIdx.x] = bias ? bias[c0 + threadIdx.x] : 0.f;
+  const int lead = TR ? 2 : 0;
+  u32x4 reg[LMAX];   // LMAX * TNTH / TNTH
+  for (int tp = 0; tp <= lead && tp < g.T; ++tp) {
+    plane_load<TNTH>(xin, g, D, b, h0, c0, tp, reg);
+    plane_store<TNTH>(ring, g.W, tp, reg);
+  }
+  __syncthreads();
+  // one (row, w-segment, chunk) item per thread (tiled_ok: HT * ceil(W/SEG) * 8 <= TNTH)
+  const int ns = (g.W + SEG - 1) / SEG;
+  const int o = threadIdx.x;
+  const int ch = o & 7, s = (o >> 3) % ns, r = (o >> 3) / ns;
+  const int h = h0 + r, w0 = s * SEG;
+  const bool active = o < HT * ns * 8 && h < g.H;
+  // residual rows of this thread's outputs, prefetched one step ahead with the plane
+  auto res_load = [&](int t, f32x4 (&rv)[SEG][2]) {
+#pragma unroll
+    for (int j = 0; j < SEG; ++j) {
+      rv[j][0] = rv[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (res && active && w0 + j < g.W) {
+        const float* p = res + (int64_t)canon(g, b, (t * g.H + h) * g.W + w0 + j) * D + c0 + ch * 8;
+        rv[j][0] = *(const f32x4*)p;
+        rv[j][1] = *(const f32x4*)(p + 4);
+      }
+    }
+  };
+  f32x4 rv[SEG][2];
+  res_load(0, rv);
+  for (int t = 0; t < g.T; ++t) {
+    const int tn = t + lead + 1;
+    if (tn < g.T) plane_load<TNTH>(xin, g, D, b, h0, c0, tn, reg);
+    f32x4 rn[SEG][2];
+    if (t + 1 < g.T) res_load(t + 1, rn);
+    if (active) {
+      float acc[SEG][8];
+#pragma unroll
+      for (int j = 0; j < SEG; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[j][e] = TR ? 0.f : bs[ch * 8 + e];
+      // rolled (kt, kh) loops: one (SEG+2) x 8 window live at a time (unrolled, hipcc hoists all
+      // nine windows and the kernel runs at 1 wave/SIMD)
+#pragma unroll 1
+      for (int kt = 0; kt < 3; ++kt) {
+        const int tp = TR ? t + 2 - kt : t + kt - 2;
+        if (tp < 0 || tp >= g.T) continue;
+        const char* pl = ring + (tp % NSLOT) * pb;
+#pragma unroll 1
+        for (int kh = 0; kh < 3; ++kh) {
+          const int lr = TR ? r + 2 - kh : r + kh;
+          float xv[SEG + 2][8];
+#pragma unroll
+          for (int q = 0; q < SEG + 2; ++q) {
+            // LDS column of w0 - 1 + q; columns past W + 1 only feed outputs w >= W
+            const int cw = min(w0 + q, g.W + 1);
+            unpack8(*(const u32x4*)(pl + ((lr * (g.W + 2) + cw) * 8 + ch) * 16), xv[q]);
+          }
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const float* wp = ws + ((kt * 3 + kh) * 3 + kw) * 64 + ch * 8;
+            const f32x4 wa = *(const f32x4*)wp, wb = *(const f32x4*)(wp + 4);
+            const float wv[8] = {wa[0], wa[1], wa[2], wa[3], wb[0], wb[1], wb[2], wb[3]};
+#pragma unroll
+            for (int j = 0; j < SEG; ++j) {
+              const int q = TR ? j + 2 - kw : j + kw;
+#pragma unroll
+              for (int e = 0; e < 8; ++e) acc[j][e] += wv[e] * xv[q][e];
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < SEG; ++j) {
+        const int wq = w0 + j;
+        if (wq >= g.W) break;
+        const int64_t co = (int64_t)canon(g, b, (t * g.H + h) * g.W + wq) * D + c0 + ch * 8;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { acc[j][e] += rv[j][0][e]; acc[j][4 + e] += rv[j][1][e]; }
+        if (out) {
+          *(f32x4*)(out + co) = f32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
+          *(f32x4*)(out + co + 4) = f32x4{acc[j][4], acc[j][5], acc[j][6], acc[j][7]};
+        }
+        if (outb) *(u32x4*)(outb + co) = pack8(acc[j]);
+      }
+    }
+    // the slot of plane tn held plane tn - 3, read in this step: write it after a barrier
+    __syncthreads();
+    if (tn < g.T) plane_store<TNTH>(ring, g.W, tn, reg);
+    if (t + 1 < g.T) {
+#pragma unroll
+      for (int j = 0; j < SEG; ++j) { rv[j][0] = rn[j][0]; rv[j][1] = rn[j][1]; }
+    }
+    __syncthreads();
+  }
+}
+
+// weight/bias gradient: grid (B * ceil(H/HT), D/64), WNTH threads; thread = (row, w-segment of
+// SEGW, channel pair); part[blockIdx.x][c][28] (27 taps in (kt,kh,kw) order, then bias).
+// Channel pairs keep the 27 x 2 accumulators + windows under 128 VGPRs (4 waves/SIMD).
+__global__ __launch_bounds__(WNTH, 3) void peg_wgrad_tile_kernel(const u16* __restrict__ dout,
+                                                              const u16* __restrict__ xin, int D, Geo g,
+                                                              float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nht = (g.H + HT - 1) / HT;
+  const int b = blockIdx.x / nht, h0 = (blockIdx.x - b * nht) * HT, c0 = blockIdx.y * 64;
+  const int pb = plane_bytes(g.W);
+  char* ring = smem;
+  const int pair = threadIdx.x & 31;
+  float acc[27][2], accb[2] = {0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 27; ++i) acc[i][0] = acc[i][1] = 0.f;
+  u32x4 reg[LMAX * TNTH / WNTH];
+  plane_load<WNTH>(xin, g, D, b, h0, c0, 0, reg);
+  plane_store<WNTH>(ring, g.W, 0, reg);
+  __syncthreads();
+  const int ns = (g.W + SEGW - 1) / SEGW;
+  const int items = HT * ns * 32;
+  for (int t = 0; t < g.T; ++t) {
+    const int tn = t + 1;
+    if (tn < g.T) plane_load<WNTH>(xin, g, D, b, h0, c0, tn, reg);
+    for (int o = threadIdx.x; o < items; o += WNTH) {
+      const int s = (o >> 5) % ns, r = (o >> 5) / ns;
+      const int h = h0 + r, w0 = s * SEGW;
+      float dv[SEGW][2];
+#pragma unroll
+      for (int j = 0; j < SEGW; ++j) {
+        const int wq = w0 + j;
+        uint32_t u = 0;
+        if (h < g.H && wq < g.W)
+          u = *(const uint32_t*)(dout + (int64_t)canon(g, b, (t * g.H + h) * g.W + wq) * D + c0 + pair * 2);
+        dv[j][0] = __uint_as_float(u << 16);
+        dv[j][1] = __uint_as_float(u & 0xffff0000u);
+        accb[0] += dv[j][0];
+        accb[1] += dv[j][1];
+      }
+#pragma unroll
+      for (int kt = 0; kt < 3; ++kt) {
+        const int tp = t + kt - 2;
+        if (tp < 0) continue;
+        const char* pl = ring + (tp % NSLOT) * pb;
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          const int lr = r + kh;
+          float xv[SEGW + 2][2];
+#pragma unroll
+          for (int q = 0; q < SEGW + 2; ++q) {
+            const int cw = min(w0 + q, g.W + 1);
+            const uint32_t u = *(const uint32_t*)(pl + (lr * (g.W + 2) + cw) * 128 + pair * 4);
+            xv[q][0] = __uint_as_float(u << 16);
+            xv[q][1] = __uint_as_float(u & 0xffff0000u);
+          }
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+            for (int j = 0; j < SEGW; ++j) {
+              acc[(kt * 3 + kh) * 3 + kw][0] += dv[j][0] * xv[j + kw][0];
+              acc[(kt * 3 + kh) * 3 + kw][1] += dv[j][1] * xv[j + kw][1];
+            }
+        }
+      }
+    }
+    __syncthreads();   // slot of plane tn held plane tn - 3, read in this step
+    if (tn < g.T) plane_store<WNTH>(ring, g.W, tn, reg);
+    __syncthreads();
+  }
+  // fold the two (row, segment) items of a wave sharing a pair (lane bit 5), then the waves
+  constexpr int NWV = WNTH / 64;
+  float* red = (float*)smem;   // [NWV][64 ch][28]; the ring is dead after the last barrier
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 28; ++i)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      float v = i < 27 ? acc[i][e] : accb[e];
+      v += __shfl_xor(v, 32, 64);
+      if (lane < 32) red[(wv * 64 + pair * 2 + e) * 28 + i] = v;
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 28; i += WNTH) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NWV; ++k) s += red[k * 64 * 28 + i];
+    part[((int64_t)blockIdx.x * D + c0) * 28 + i] = s;
+  }
+}
+
+bool tiled_ok(int W, int D) {
+  return D % 64 == 0 && HT * ((W + SEG - 1) / SEG) * 8 <= TNTH && (HT + 2) * (W + 2) * 8 <= LMAX * TNTH;
+}
+
+size_t tile_smem(int W) { return (size_t)NSLOT * plane_bytes(W) + (27 * 64 + 64) * 4; }
+size_t wgrad_smem(int W) { return std::max<size_t>((size_t)NSLOT * plane_bytes(W), (WNTH / 64) * 64 * 28 * 4); }
+
+bool s_tile_attr = false;
+void tile_attrs() {
+  if (s_tile_attr) return;
+  // up to W = 30: 4 x 4 x 32 x 128 B + weights = 72 KB
+  (void)hipFuncSetAttribute((const void*)peg_tile_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+  (void)hipFuncSetAttribute((const void*)peg_tile_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+  (void)hipFuncSetAttribute((const void*)peg_wgrad_tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            80 * 1024);
+  s_tile_attr = true;
+}
+
 }  // namespace
+
+extern "C" int ctclip_peg_wgrad_slabs(int64_t B, int32_t T, int32_t H, int32_t W, int32_t D) {
+  (void)T;
+  return tiled_ok(W, D) ? (int)(B * ((H + HT - 1) / HT)) : 256;
+}
 
 extern "C" int ctclip_peg_fwd(const void* x_bf16, const float* x_f32, int64_t B, int32_t T, int32_t H, int32_t W,
                               int32_t D, const float* weight, const float* bias, int32_t mode, float* out_f32,
@@ -178,9 +447,17 @@ extern "C" int ctclip_peg_fwd(const void* x_bf16, const float* x_f32, int64_t B,
   CT_REQUIRE(D % 8 == 0, CT_EALIGN);
   Geo g{T, H, W, T * H * W, mode};
   const int64_t ntok = B * g.thw;
-  dim3 grid(cdiv(ntok, 32), cdiv(D, 64));
-  hipLaunchKernelGGL(peg_kernel<0>, grid, dim3(256), 0, (hipStream_t)stream, (const u16*)x_bf16, ntok, D, weight,
-                     bias, x_f32, g, out_f32, (u16*)out_bf16);
+  if (ntok == 0) return 0;
+  if (tiled_ok(W, D)) {
+    tile_attrs();
+    dim3 grid(B * ((H + HT - 1) / HT), D / 64);
+    hipLaunchKernelGGL(peg_tile_kernel<0>, grid, dim3(TNTH), tile_smem(W), (hipStream_t)stream, (const u16*)x_bf16,
+                       D, weight, bias, x_f32, g, out_f32, (u16*)out_bf16);
+  } else {
+    dim3 grid(cdiv(ntok, 32), cdiv(D, 64));
+    hipLaunchKernelGGL(peg_kernel<0>, grid, dim3(256), 0, (hipStream_t)stream, (const u16*)x_bf16, ntok, D, weight,
+                       bias, x_f32, g, out_f32, (u16*)out_bf16);
+  }
   CT_CHECK_LAUNCH();
   return 0;
 }
@@ -192,9 +469,17 @@ extern "C" int ctclip_peg_bwd_data(const void* dout_bf16, const float* dout_f32,
   CT_REQUIRE(D % 8 == 0, CT_EALIGN);
   Geo g{T, H, W, T * H * W, mode};
   const int64_t ntok = B * g.thw;
-  dim3 grid(cdiv(ntok, 32), cdiv(D, 64));
-  hipLaunchKernelGGL(peg_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, (const u16*)dout_bf16, ntok, D, weight,
-                     (const float*)nullptr, dout_f32, g, dx_f32, (u16*)dx_bf16);
+  if (ntok == 0) return 0;
+  if (tiled_ok(W, D)) {
+    tile_attrs();
+    dim3 grid(B * ((H + HT - 1) / HT), D / 64);
+    hipLaunchKernelGGL(peg_tile_kernel<1>, grid, dim3(TNTH), tile_smem(W), (hipStream_t)stream,
+                       (const u16*)dout_bf16, D, weight, (const float*)nullptr, dout_f32, g, dx_f32, (u16*)dx_bf16);
+  } else {
+    dim3 grid(cdiv(ntok, 32), cdiv(D, 64));
+    hipLaunchKernelGGL(peg_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, (const u16*)dout_bf16, ntok, D,
+                       weight, (const float*)nullptr, dout_f32, g, dx_f32, (u16*)dx_bf16);
+  }
   CT_CHECK_LAUNCH();
   return 0;
 }
@@ -203,12 +488,20 @@ extern "C" int ctclip_peg_bwd_data(const void* dout_bf16, const float* dout_f32,
 extern "C" int ctclip_peg_bwd_weight(const void* dout_bf16, const void* x_bf16, int64_t B, int32_t T, int32_t H,
                                      int32_t W, int32_t D, int32_t mode, float* part, int32_t nblk, void* stream) {
   CT_REQUIRE(D % 8 == 0, CT_EALIGN);
+  CT_REQUIRE(nblk == ctclip_peg_wgrad_slabs(B, T, H, W, D), CT_ESHAPE);
   Geo g{T, H, W, T * H * W, mode};
   const int64_t ntok = B * g.thw;
-  const int64_t per = (ntok + nblk - 1) / nblk;
-  dim3 grid(nblk, cdiv(D, 64));
-  hipLaunchKernelGGL(peg_wgrad_kernel, grid, dim3(192), 0, (hipStream_t)stream, (const u16*)dout_bf16,
-                     (const u16*)x_bf16, ntok, D, g, per, part);
+  if (tiled_ok(W, D)) {
+    tile_attrs();
+    dim3 grid(nblk, D / 64);
+    hipLaunchKernelGGL(peg_wgrad_tile_kernel, grid, dim3(WNTH), wgrad_smem(W), (hipStream_t)stream, (const u16*)dout_bf16,
+                       (const u16*)x_bf16, D, g, part);
+  } else {
+    const int64_t per = (ntok + nblk - 1) / nblk;
+    dim3 grid(nblk, cdiv(D, 64));
+    hipLaunchKernelGGL(peg_wgrad_kernel, grid, dim3(192), 0, (hipStream_t)stream, (const u16*)dout_bf16,
+                       (const u16*)x_bf16, ntok, D, g, per, part);
+  }
   CT_CHECK_LAUNCH();
   return 0;
 }

@@ -302,7 +302,7 @@ def peg_bwd(doutb, doutf, xb, B, T, H, W, weight, mode):
     dxb = torch.empty_like(doutb)
     call('ctclip_peg_bwd_data', ptr(doutb), ptr(doutf), B, T, H, W, D, ptr(weight), mode, ptr(dxf), ptr(dxb),
          stream_ptr())
-    nblk = 256
+    nblk = _lib.lib().ctclip_peg_wgrad_slabs(B, T, H, W, D)
     part = torch.empty(nblk, D * 28, device=xb.device, dtype=F32)
     call('ctclip_peg_bwd_weight', ptr(doutb), ptr(xb), B, T, H, W, D, mode, ptr(part), nblk, stream_ptr())
     red = torch.empty(D * 28, device=xb.device, dtype=F32)

@@ -120,8 +120,11 @@ int ctclip_peg_fwd(const void* x_bf16, const float* x_f32, int64_t B, int32_t T,
 int ctclip_peg_bwd_data(const void* dout_bf16, const float* dout_f32, int64_t B, int32_t T, int32_t H,
                         int32_t W, int32_t D, const float* weight, int32_t mode, float* dx_f32,
                         void* dx_bf16, void* stream);
+/* part: [nblk][D][28] f32 partial sums (27 taps in (kt,kh,kw) order, then bias); nblk must equal
+   ctclip_peg_wgrad_slabs(B, T, H, W, D) (one slab per (batch, 2-row tile) on the plane-streaming path). */
 int ctclip_peg_bwd_weight(const void* dout_bf16, const void* x_bf16, int64_t B, int32_t T, int32_t H,
                           int32_t W, int32_t D, int32_t mode, float* part, int32_t nblk, void* stream);
+int ctclip_peg_wgrad_slabs(int64_t B, int32_t T, int32_t H, int32_t W, int32_t D);
 
 /* ---------------------------------------------------------------- attention (attention.py:127-181)
  * softmax(scale * q.k^T + bias + mask) v per (sequence, head); q/k already l2-normalised and

@@ -80,11 +80,13 @@ def _peg_ref(x, w, b, shape, mode):
 
 
 @pytest.mark.parametrize('mode', [0, 1])
-def test_peg(K, mode):
+@pytest.mark.parametrize('shape,D', [((2, 6, 5, 7), 128),      # plane-streaming path, ragged h tile / w segment
+                                     ((1, 24, 24, 24), 512),   # base token grid (480^2 x 240 volume)
+                                     ((1, 3, 4, 40), 64),      # W > 30: general path
+                                     ((2, 2, 3, 4), 24)])      # D % 64 != 0: general path
+def test_peg(K, mode, shape, D):
     torch.manual_seed(2)
-    shape = (2, 6, 5, 7)
-    D = 128
-    M = 2 * 6 * 5 * 7
+    M = shape[0] * shape[1] * shape[2] * shape[3]
     xb = torch.randn(M, D, device=dev).bfloat16()
     xf = xb.float()
     w = torch.randn(D, 1, 3, 3, 3, device=dev) * 0.2

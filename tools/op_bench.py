@@ -35,6 +35,7 @@ def main():
     dg = torch.randn(M, 1408, device='cuda').bfloat16()
     h = torch.randn(M, 2816, device='cuda').bfloat16()
     qs = torch.ones(32, device='cuda')
+    dxf, dxb = torch.empty_like(xf), torch.empty_like(xb)
     cases = [
         ('ln_fwd f32->bf16', lambda: K.layernorm_fwd(xf, g, b, 1e-5), M * D * 6),
         ('ln_fwd f32->bf16+f32', lambda: K.layernorm_fwd(xf, g, b, 1e-5, out_f32=True), M * D * 10),
@@ -42,6 +43,9 @@ def main():
         ('peg_fwd mode0', lambda: K.peg_fwd(xb, xf, 8, 24, 24, 24, w, pb, 0), M * D * (2 + 4 + 4 + 2)),
         ('peg_fwd mode1', lambda: K.peg_fwd(xb, xf, 8, 24, 24, 24, w, pb, 1), M * D * (2 + 4 + 4 + 2)),
         ('peg_bwd (data+w)', lambda: K.peg_bwd(xb, xf, xb, 8, 24, 24, 24, w, 0), M * D * (2 + 4 + 4 + 2 + 4)),
+        ('peg_bwd data only', lambda: K.call('ctclip_peg_bwd_data', K.ptr(xb), K.ptr(xf), 8, 24, 24, 24, D,
+                                             K.ptr(w), 0, K.ptr(dxf), K.ptr(dxb), K.stream_ptr()),
+         M * D * (2 + 4 + 4 + 2)),
         ('geglu_bwd', lambda: K.geglu_bwd(dg, h), M * (1408 + 2816 + 2816) * 2),
         ('l2n_fwd', lambda: K.l2norm_scale_fwd(xb[:, :256], 8, 32, qs), M * 256 * 4),
         ('cast f32->bf16', lambda: K.cast_bf16(xf), M * D * 6),
