@@ -258,15 +258,12 @@ __global__ __launch_bounds__(256) void l2n_bwd_kernel(const u16* __restrict__ x,
 #pragma unroll
   for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = acc[j];
   __syncthreads();
-  // fold threads with the same d0 (d0 = (c*8) % D, c = gid % lpr)
+  // fold threads with the same d-chunk: chunk = (gid % lpr) % (D/8) = tid % (D/8), since
+  // D/8 divides both lpr and 256 (checked by the launcher)
   if (threadIdx.x < D) {
-    const int d = threadIdx.x;
+    const int d = threadIdx.x, nch = D >> 3;
     float s = 0.f;
-    for (int t = 0; t < 256; ++t) {
-      const int cc = (int)(((int64_t)blockIdx.x * 256 + t) % lpr);
-      const int dd = (cc * 8) % D;
-      if (d >= dd && d < dd + 8) s += red[t][d - dd];
-    }
+    for (int t = d >> 3; t < 256; t += nch) s += red[t][d & 7];
     part[(int64_t)blockIdx.x * D + d] = s;
   }
 }
@@ -402,6 +399,7 @@ extern "C" int ctclip_l2norm_scale_bwd(const void* x, int64_t ldx, const void* d
   if (rows == 0) return 0;
   const int lpr = H * D / 8;
   CT_REQUIRE((256 % lpr == 0) || (lpr % 256 == 0), CT_ESHAPE);
+  CT_REQUIRE(D % 8 == 0 && D <= 512 && 256 % (D / 8) == 0, CT_ESHAPE);
   CT_REQUIRE(((int64_t)nblocks * 256) % lpr == 0, CT_ESHAPE);
   hipLaunchKernelGGL(l2n_bwd_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, (const u16*)x, ldx,
                      (const u16*)dy, lddy, rows, H, D, scale, (u16*)dx, lddx, part_scale);

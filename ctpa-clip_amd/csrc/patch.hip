@@ -7,6 +7,8 @@
 //   W' = W*diag(gamma), b' = b + W.beta, so the same xhat also serves the weight gradient.
 // One wave per token (patch), the patch held in registers, element -> voxel offsets from a
 // small per-call table (no integer division in the loop).
+#include <type_traits>
+
 #include "common.h"
 #include "../../include/ctclip_hip.h"
 
@@ -62,6 +64,108 @@ __global__ __launch_bounds__(256) void patch_ln_kernel(const void* __restrict__ 
   }
 }
 
+// Row-strip form (the fast path, single-channel volumes): a workgroup owns PW = 4 horizontally
+// adjacent patches of one (b, t, hg) strip.  Phase 1 reads the strip's PT x P rows of 4P voxels
+// with coalesced 16-B loads and scatters the normalised voxels into LDS in patch order
+// [token][pt p1 p2]; phase 2 (one wave per patch) takes the LN statistics from LDS and writes
+// xhat as contiguous bf16 pairs.  Every voxel is read from HBM once in full 16-B segments
+// (the gather form above reads 40-B row pieces through the cache).
+constexpr int PW = 4;
+
+// int16 volumes stay raw int16 in LDS (32 KB per workgroup -> 4 per CU) and are normalised
+// when read back; all of a thread's 16-B loads are issued before the first LDS scatter.
+template <bool F32>
+__global__ __launch_bounds__(256) void patch_ln_strip_kernel(const void* __restrict__ video, int is_hu, int T,
+                                                             int Hg, int Wg, int64_t vol_stride, int H, int W,
+                                                             int PT, int P, float eps, u16* __restrict__ out) {
+  using E = typename std::conditional<F32, float, short>::type;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  E* sx = (E*)smem_raw;   // [PW][pd]
+  constexpr int VEC = F32 ? 4 : 8;
+  constexpr int NCH = PW * 4096 / VEC / 256;   // 16-B loads per thread at pd <= 4096
+  const int pd = PT * P * P;
+  // patch groups of one strip are consecutive workgroups: they share the strip's cache lines
+  int r = blockIdx.y;
+  const int hg = r % Hg; r /= Hg;
+  const int t = r % T;
+  const int b = r / T;
+  const int wg0 = blockIdx.x * PW;
+  const int ntk = min(PW, Wg - wg0);
+  const int cpr = ntk * P / VEC;   // 16-B chunks per row segment
+  const int nchunk = PT * P * cpr;
+  const int64_t base = (int64_t)b * vol_stride + ((int64_t)t * PT * H + (int64_t)hg * P) * W + (int64_t)wg0 * P;
+  u32x4 ld[NCH];
+#pragma unroll
+  for (int m = 0; m < NCH; ++m) {
+    const int c = threadIdx.x + m * 256;
+    if (c < nchunk) {
+      const int k = c % cpr, rowi = c / cpr, p1 = rowi % P, pt = rowi / P;
+      ld[m] = *(const u32x4*)((const E*)video + base + ((int64_t)pt * H + p1) * W + k * VEC);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < NCH; ++m) {
+    const int c = threadIdx.x + m * 256;
+    if (c >= nchunk) break;
+    const int k = c % cpr, rowi = c / cpr, p1 = rowi % P, pt = rowi / P;
+    const E* ev = (const E*)&ld[m];
+    int cr = k * VEC, tk = cr / P, p2 = cr - tk * P;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      sx[tk * pd + (pt * P + p1) * P + p2] = ev[j];
+      if (++p2 == P) { p2 = 0; ++tk; }
+    }
+  }
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (w >= ntk) return;
+  const E* px = sx + w * pd;
+  constexpr int NP = 32;   // pairs per lane: pd <= 4096
+  float v[NP][2];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int e = 2 * (lane + 64 * i);
+    v[i][0] = v[i][1] = 0.f;
+    if (e < pd) {
+      if constexpr (F32) {
+        const float2 u = *(const float2*)(px + e);
+        v[i][0] = u.x;
+        v[i][1] = u.y;
+      } else {
+        const uint32_t u = *(const uint32_t*)(px + e);
+        v[i][0] = (float)(short)(u & 0xffffu);
+        v[i][1] = (float)(short)(u >> 16);
+      }
+      if (is_hu) {
+        v[i][0] = fminf(fmaxf(v[i][0], -1000.f), 1000.f) / 1000.f;
+        v[i][1] = fminf(fmaxf(v[i][1], -1000.f), 1000.f) / 1000.f;
+      }
+    }
+    s += v[i][0] + v[i][1];
+  }
+  const float mean = warp_sum(s) / pd;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    if (2 * (lane + 64 * i) < pd) {
+      const float d0 = v[i][0] - mean, d1 = v[i][1] - mean;
+      q += d0 * d0 + d1 * d1;
+    }
+  }
+  const float rstd = rsqrtf(warp_sum(q) / pd + eps);
+  const int64_t tok = (((int64_t)b * T + t) * Hg + hg) * Wg + wg0 + w;
+  uint32_t* o = (uint32_t*)(out + tok * pd);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int e = 2 * (lane + 64 * i);
+    if (e < pd)
+      o[e >> 1] = (uint32_t)f2bf((v[i][0] - mean) * rstd) | ((uint32_t)f2bf((v[i][1] - mean) * rstd) << 16);
+  }
+}
+
+bool s_strip_attr = false;
+
 // Given G = dy^T . xhat  [N][K] (f32) and colsum(dy) cs[N], produce the grads of the folded
 // LayerNorm+Linear pair: dW = G*g + cs (x) b, dgamma[k] = sum_n W[n,k] G[n,k], dbeta[k] = sum_n W[n,k] cs[n].
 __global__ __launch_bounds__(256) void patch_wgrad_kernel(const float* __restrict__ G, const float* __restrict__ cs,
@@ -97,8 +201,28 @@ extern "C" int ctclip_patch_ln(const void* video, int32_t is_f32, int32_t is_hu,
   const int64_t ntok = B * T * Hg * Wg;
   const int64_t frame = (int64_t)H * W;
   const int64_t vol = (int64_t)C * F * frame;
-  hipLaunchKernelGGL(patch_ln_kernel, dim3(cdiv(ntok, 4)), dim3(256), 0, (hipStream_t)stream, video, is_f32, is_hu,
-                     ntok, T, Hg, Wg, vol, frame, W, PT, P, offs, pd, eps, (u16*)out);
+  if (ntok == 0) return 0;
+  const int vec = is_f32 ? 4 : 8;
+  if (C == 1 && pd % 2 == 0 && (PW * P) % vec == 0 && ((Wg % PW) * P) % vec == 0 && W % vec == 0) {
+    if (!s_strip_attr) {
+      (void)hipFuncSetAttribute((const void*)patch_ln_strip_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                PW * 4096 * 4);
+      (void)hipFuncSetAttribute((const void*)patch_ln_strip_kernel<false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, PW * 4096 * 4);
+      s_strip_attr = true;
+    }
+    dim3 grid(cdiv(Wg, PW), B * T * Hg);
+    const size_t sm = (size_t)PW * pd * (is_f32 ? 4 : 2);
+    if (is_f32)
+      hipLaunchKernelGGL(patch_ln_strip_kernel<true>, grid, dim3(256), sm, (hipStream_t)stream, video, is_hu, T, Hg,
+                         Wg, vol, H, W, PT, P, eps, (u16*)out);
+    else
+      hipLaunchKernelGGL(patch_ln_strip_kernel<false>, grid, dim3(256), sm, (hipStream_t)stream, video, is_hu, T,
+                         Hg, Wg, vol, H, W, PT, P, eps, (u16*)out);
+  } else {
+    hipLaunchKernelGGL(patch_ln_kernel, dim3(cdiv(ntok, 4)), dim3(256), 0, (hipStream_t)stream, video, is_f32,
+                       is_hu, ntok, T, Hg, Wg, vol, frame, W, PT, P, offs, pd, eps, (u16*)out);
+  }
   CT_CHECK_LAUNCH();
   return 0;
 }

@@ -213,7 +213,7 @@ def l2norm_scale_fwd(x, H, D, scale, out=None):
 def l2norm_scale_bwd(x, dy, H, D, scale, out):
     rows = x.shape[0]
     lpr = H * D // 8
-    nb = 256
+    nb = 2048       # 8 workgroups per CU: the row loop is load-latency bound
     while (nb * 256) % lpr:
         nb += 1
     part = torch.empty(nb, D, device=x.device, dtype=F32)
@@ -419,8 +419,14 @@ def clip_scores(t_raw, i_raw, log_temp):
 # ----------------------------------------------------------------------------- sgemm
 def sgemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, *, bias=None, alpha=1.0, act=0, slope=0.1, aux=None,
           sxm=0, sxn=0, accumulate=False):
+    # split K when the output has few 64x64 tiles and K is long (CPB weight gradients, K = 2,209)
+    tiles = ((M + 63) // 64) * ((N + 63) // 64)
+    split = 1
+    if K >= 512 and tiles < 128:
+        split = max(1, min(K // 128, 256 // tiles))
+    ws = torch.empty(split * M * N, device=A.device, dtype=F32) if split > 1 else None
     call('ctclip_sgemm', M, N, K, ptr(A), sam, sak, ptr(B), sbk, sbn, ptr(C), scm, scn, ptr(bias), alpha, act, slope,
-         ptr(aux), sxm, sxn, int(accumulate), stream_ptr())
+         ptr(aux), sxm, sxn, int(accumulate), ptr(ws), split, stream_ptr())
     return C
 
 

@@ -184,11 +184,12 @@ int ctclip_clip_scores(const float* t_raw, const float* i_raw, int32_t B, int32_
 
 /* ---------------------------------------------------------------- small exact-f32 GEMM (strided)
  * CPB MLP (attention.py:247-252,271-274) and its backward; act 1 = LeakyReLU(slope),
- * act 2 = multiply by LeakyReLU'(aux). */
+ * act 2 = multiply by LeakyReLU'(aux).  split > 1 splits K over `split` workgroup layers writing
+ * f32 slabs into `workspace` ([split][M][N]), folded in slab order (deterministic). */
 int ctclip_sgemm(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam, int64_t sak, const float* B,
                  int64_t sbk, int64_t sbn, float* C, int64_t scm, int64_t scn, const float* bias, float alpha,
                  int32_t act, float slope, const float* aux, int64_t sxm, int64_t sxn, int32_t accumulate,
-                 void* stream);
+                 float* workspace, int32_t split, void* stream);
 
 /* ---------------------------------------------------------------- BERT embeddings */
 int ctclip_embed_fwd(const int64_t* ids, int64_t B, int32_t L, int32_t Hd, const float* word, const float* pos,

@@ -250,23 +250,49 @@ def test_sgemm_cpb_mlp(K):
     dz = K.smm(g, w1, act=2, aux=h1)          # dh1 * leaky'(h1)
     ref2 = (g @ w1) * torch.where(h1 > 0, 1.0, 0.1)
     assert rel(dz, ref2) < 1e-5
-    dw = K.smm(g.t(), h1)
+    dw = K.smm(g.t(), h1)                     # K = 2,209: split-K slabs
     assert rel(dw, g.t() @ h1) < 1e-5
+    du = torch.randn(8, h2.shape[0], device=dev)
+    dw2 = K.smm(du, h2)                       # 8 x 512, K = 2,209 (one row of tiles)
+    assert rel(dw2, du @ h2) < 1e-5
+    acc = torch.randn(8, 512, device=dev)
+    ref_acc = acc + du @ h2
+    K.smm(du, h2, out=acc, accumulate=True)
+    assert rel(acc, ref_acc) < 1e-5
+
+
+def test_sgemm_exact_integers(K):
+    """Small-integer operands: every product and partial sum is exact in f32, so the MFMA path
+    must reproduce the fp64 result bit for bit (catches row/column swaps and lost K slices)."""
+    torch.manual_seed(9)
+    for (M, N, Kd) in [(70, 33, 45), (128, 64, 2209), (5, 300, 17)]:
+        a = torch.randint(-3, 4, (M, Kd), device=dev).float()
+        b = torch.randint(-3, 4, (N, Kd), device=dev).float()
+        y = K.slinear(a, b)
+        assert torch.equal(y, (a.double() @ b.double().t()).float())
+        y2 = K.smm(a.t().contiguous().t(), b.t())   # column-major A view
+        assert torch.equal(y2, (a.double() @ b.double().t()).float())
 
 
 # ----------------------------------------------------------------------------- patch embed
-def test_patch_ln(K):
+@pytest.mark.parametrize('size,f32', [(40, False),     # strip path, ragged 2-patch group
+                                      (160, False),    # strip path, full groups
+                                      (100, False),    # Wg = 5: ragged group of 1 -> gather path
+                                      (80, True)])     # f32 [-1, 1] video input
+def test_patch_ln(K, size, f32):
     torch.manual_seed(7)
-    cfg = O.ViTConfig(dim=64, image_size=40, patch_size=20, temporal_patch_size=10, frames=20)
-    hu = torch.randint(-1200, 1201, (2, 1, 20, 40, 40), dtype=torch.int16, device=dev)
+    hu = torch.randint(-1200, 1201, (2, 1, 20, size, size), dtype=torch.int16, device=dev)
     from ctclip_mi355x import layers
-    offs = layers.patch_offsets(1, 10, 20, 20, 40, 40).to(dev)
-    xh = K.patch_ln(hu, True, 10, 20, offs)
+    offs = layers.patch_offsets(1, 10, 20, 20, size, size).to(dev)
     v = O.normalize_hu(hu.cpu())
+    xh = K.patch_ln(v.to(dev) if f32 else hu, not f32, 10, 20, offs)
     b, c, f, hh, ww = v.shape
-    x = v.reshape(b, c, 2, 10, 2, 20, 2, 20).permute(0, 2, 4, 6, 1, 3, 5, 7).reshape(-1, 4000)
+    g = size // 20
+    x = v.reshape(b, c, 2, 10, g, 20, g, 20).permute(0, 2, 4, 6, 1, 3, 5, 7).reshape(-1, 4000)
     ref = F.layer_norm(x, (4000,), eps=1e-5)
     assert rel(xh.cpu(), ref) < 4e-3
+    # bf16 of the f32 LN of identical inputs: every element within one bf16 ulp
+    assert ((xh.cpu().float() - ref).abs() <= ref.abs() * 2 ** -7 + 1e-6).all()
 
 
 def test_embed(K):

@@ -48,9 +48,14 @@ def main():
          M * D * (2 + 4 + 4 + 2)),
         ('geglu_bwd', lambda: K.geglu_bwd(dg, h), M * (1408 + 2816 + 2816) * 2),
         ('l2n_fwd', lambda: K.l2norm_scale_fwd(xb[:, :256], 8, 32, qs), M * 256 * 4),
+        ('l2n_bwd', lambda: K.l2norm_scale_bwd(xb[:, :256], xb[:, 256:], 8, 32, qs, dxb[:, :256]), M * 256 * 6),
         ('cast f32->bf16', lambda: K.cast_bf16(xf), M * D * 6),
         ('colsum bf16', lambda: K.colsum(xb), M * D * 2),
     ]
+    from ctclip_mi355x import layers
+    vol = torch.randint(-1200, 1201, (8, 1, 240, 480, 480), device='cuda', dtype=torch.int32).to(torch.int16)
+    offs = layers.patch_offsets(1, 10, 20, 20, 480, 480).cuda()
+    cases.append(('patch_ln int16->bf16', lambda: K.patch_ln(vol, True, 10, 20, offs), vol.numel() * 4))
     for name, fn, nbytes in cases:
         ms = timeit(fn)
         print(f'{name:24s} {ms * 1e3:9.1f} us  {nbytes / ms / 1e9:7.2f} TB/s (algorithmic bytes)', flush=True)
