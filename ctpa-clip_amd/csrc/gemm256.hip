@@ -16,10 +16,19 @@
 
 namespace g256 {
 
-constexpr int BM = 256, BN = 256, BK = 64, NTH = 512;
-constexpr int STAGE = 64 * 1024;             // A (32 KB) + B (32 KB)
-constexpr int SMEM = 2 * STAGE;              // 128 KB
+// Two shapes of one kernel template, WR = wave rows of 128:
+//   WR = 2: 256 x 256 tile, 8 waves, 4-slot ring (128 KB LDS, 1 workgroup per CU);
+//   WR = 1: 128 x 256 tile, 4 waves, 3-slot ring (72 KB LDS, 2 workgroups per CU), so one
+//           workgroup's epilogue stores drain while the other one's MFMAs run.
+constexpr int BN = 256, BK = 32;
 constexpr int EP_LD = 68;                    // f32 staging row stride (64 cols + pad)
+template <int WR> struct Cfg {
+  static constexpr int BM = 128 * WR, NTH = 256 * WR;
+  static constexpr int ABYTES = BM * BK * 2, BBYTES = BN * BK * 2, STAGE = ABYTES + BBYTES;
+  static constexpr int NSTAGE = WR == 2 ? 4 : 3;
+  static constexpr int SMEM = NSTAGE * STAGE;
+  static constexpr int GA = ABYTES / 16 / NTH, GB = BBYTES / 16 / NTH, G = GA + GB;   // glds per thread per tile
+};
 
 struct P {
   int64_t M, N, K;
@@ -39,41 +48,47 @@ __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) 
 typedef __attribute__((address_space(1))) void gvoid;
 typedef __attribute__((address_space(3))) void lvoid;
 
-// issue this thread's 4 glds for one 256 x 64 operand tile
-template <bool KC>
+// K-contiguous image [256 rows][32 k], 64-B rows: 16-B chunk ^= (row >> 2) & 2 makes every
+// ds_read_b128 lane group of a fragment read (row = lane & 15, chunk = lane >> 4) hit 16
+// distinct 16-B bank slots (searched exhaustively over the four gfx950 lane groups)
+__device__ __forceinline__ int kc_swz(int row) { return (row >> 2) & 2; }
+
+// issue this thread's NJ glds for one ROWS x 32 operand tile (ROWS * 4 16-B chunks)
+template <bool KC, int ROWS, int NJ>
 __device__ __forceinline__ void stage_tile(char* lds, const u16* base, int64_t ld, int64_t rows, int64_t row0,
                                            int64_t k0, int w, int lane) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int c = (w * 4 + j) * 64 + lane;   // 16-B chunk index in the tile image
+  for (int j = 0; j < NJ; ++j) {
+    const int c = (w * NJ + j) * 64 + lane;   // 16-B chunk index in the tile image
     const u16* src;
     if constexpr (KC) {
-      const int row = c >> 3, pc = c & 7, lc = pc ^ ((row >> 1) & 7);
+      const int row = c >> 2, pc = c & 3, lc = pc ^ kc_swz(row);
       const int64_t gr = min(row0 + row, rows - 1);
       src = base + gr * ld + k0 + lc * 8;
     } else {
-      const int kk = c >> 5, pc = c & 31, pb = pc >> 1, half = pc & 1;
+      constexpr int CPR = ROWS / 8;             // chunks per k-row
+      const int kk = c / CPR, pc = c % CPR, pb = pc >> 1, half = pc & 1;
       const int lb = pb ^ mn_swz(kk);
       const int64_t gm = min(row0 + (int64_t)(lb * 2 + half) * 8, rows - 8);
       src = base + (k0 + kk) * ld + gm;
     }
-    __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(lds + (w * 4 + j) * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(lds + (w * NJ + j) * 1024), 16, 0, 0);
   }
 }
 
-template <bool KC>
-__device__ __forceinline__ bf16x8 frag(const char* tile, int r0, int s, int lane) {
+template <bool KC, int ROWS>
+__device__ __forceinline__ bf16x8 frag(const char* tile, int r0, int lane) {
   if constexpr (KC) {
     const int row = r0 + (lane & 15);
-    const int lc = s * 4 + (lane >> 4);
-    return *(const bf16x8*)(tile + row * 128 + ((lc ^ ((row >> 1) & 7)) << 4));
+    const int lc = lane >> 4;
+    return *(const bf16x8*)(tile + row * 64 + ((lc ^ kc_swz(row)) << 4));
   } else {
     const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
     const int m = r0 + 4 * p;
-    const int k1 = s * 32 + 8 * g + q, k2 = k1 + 4;
+    const int k1 = 8 * g + q, k2 = k1 + 4;
     const int cb = m >> 4, within = (m & 15) * 2;
-    const int o1 = k1 * 512 + ((cb ^ mn_swz(k1)) << 5) + within;
-    const int o2 = k2 * 512 + ((cb ^ mn_swz(k2)) << 5) + within;
+    const int o1 = k1 * (ROWS * 2) + ((cb ^ mn_swz(k1)) << 5) + within;
+    const int o2 = k2 * (ROWS * 2) + ((cb ^ mn_swz(k2)) << 5) + within;
     s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, tile + o1));
     s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, tile + o2));
     typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -94,14 +109,16 @@ __device__ __forceinline__ void xcd_remap(int& tx, int& ty) {
   tx = id - ty * gx;
 }
 
-template <bool AK, bool BKC>
-__global__ __launch_bounds__(NTH, 1) void gemm256_kernel(P p) {
+template <int WR, bool AK, bool BKC>
+__global__ __launch_bounds__(Cfg<WR>::NTH, 2 / WR) void gemm256_kernel(P p) {
+  using C = Cfg<WR>;
+  constexpr int NSTAGE = C::NSTAGE, STAGE = C::STAGE, G = C::G;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
   int tx, ty;
   xcd_remap(tx, ty);
   const int split = blockIdx.z % p.split_k, bidx = blockIdx.z / p.split_k;
-  const int64_t m0 = (int64_t)ty * BM, n0 = (int64_t)tx * BN;
+  const int64_t m0 = (int64_t)ty * C::BM, n0 = (int64_t)tx * BN;
   const int64_t kbeg = split * p.kper;
   const int64_t kend = min(p.K, kbeg + p.kper);
   const u16* A = p.A + bidx * p.sA;
@@ -113,39 +130,48 @@ __global__ __launch_bounds__(NTH, 1) void gemm256_kernel(P p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // NSTAGE-slot ring of 32-deep K tiles: tile kt lives in slot kt % NSTAGE; NSTAGE - 1 tiles
+  // are in flight while one is computed.  Each tile is G glds per thread; the wait before step
+  // kt leaves the younger tiles' loads outstanding (counted vmcnt, never 0 in steady state) and
+  // a raw s_barrier publishes the landed tile (a __syncthreads fence would drain every glds).
+  // The slot refilled at step kt held tile kt - 1, which every wave finished before the barrier.
   const int nk = kend > kbeg ? (int)((kend - kbeg) / BK) : 0;
-  if (nk > 0) {
-    stage_tile<AK>(smem, A, p.lda, p.M, m0, kbeg, w, lane);
-    stage_tile<BKC>(smem + 32768, B, p.ldb, p.N, n0, kbeg, w, lane);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  auto stage = [&](int t) {
+    char* st = smem + (t % NSTAGE) * STAGE;
+    const int64_t k1 = kbeg + (int64_t)t * BK;
+    stage_tile<AK, C::BM, C::GA>(st, A, p.lda, p.M, m0, k1, w, lane);
+    stage_tile<BKC, BN, C::GB>(st + C::ABYTES, B, p.ldb, p.N, n0, k1, w, lane);
+  };
+  for (int t = 0; t < NSTAGE - 1 && t < nk; ++t) stage(t);
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const char* As = smem + cur * STAGE;
-    const char* Bs = As + 32768;
-    if (kt + 1 < nk) {
-      char* nx = smem + (cur ^ 1) * STAGE;
-      const int64_t k1 = kbeg + (int64_t)(kt + 1) * BK;
-      stage_tile<AK>(nx, A, p.lda, p.M, m0, k1, w, lane);
-      stage_tile<BKC>(nx + 32768, B, p.ldb, p.N, n0, k1, w, lane);
+    if constexpr (NSTAGE == 4) {
+      if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
+      else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + NSTAGE - 1 < nk) stage(kt + NSTAGE - 1);
+    const char* As = smem + (kt % NSTAGE) * STAGE;
+    const char* Bs = As + C::ABYTES;
+    bf16x8 bfr[4];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 bfr[4];
+    for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC, BN>(Bs, wc * 64 + j * 16, lane);
+    bf16x8 af[8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(Bs, wc * 64 + j * 16, s, lane);
+    for (int i = 0; i < 8; ++i) af[i] = frag<AK, C::BM>(As, wr * 128 + i * 16, lane);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const bf16x8 af = frag<AK>(As, wr * 128 + i * 16, s, lane);
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[j], acc[i][j], 0, 0, 0);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
   }
+  __syncthreads();   // every wave's last fragment reads done before the epilogue reuses LDS
 
   // ---------------- epilogue: per-wave private staging, four 32-row quarters
   float* cs = (float*)(smem + w * (32 * EP_LD * 4));   // 8.7 KB per wave, 8 waves = 70 KB
@@ -274,14 +300,37 @@ __global__ __launch_bounds__(NTH, 1) void gemm256_kernel(P p) {
   }
 }
 
-bool s_attr = false;
-
-template <bool AK, bool BKC>
+template <int WR, bool AK, bool BKC>
 int launch(const P& p, int batch, hipStream_t st) {
-  dim3 grid(cdiv(p.N, BN), cdiv(p.M, BM), batch * p.split_k);
-  hipLaunchKernelGGL((gemm256_kernel<AK, BKC>), grid, dim3(NTH), SMEM, st, p);
+  using C = Cfg<WR>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm256_kernel<WR, AK, BKC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              C::SMEM);
+    attr = true;
+  }
+  dim3 grid(cdiv(p.N, BN), cdiv(p.M, C::BM), batch * p.split_k);
+  hipLaunchKernelGGL((gemm256_kernel<WR, AK, BKC>), grid, dim3(C::NTH), C::SMEM, st, p);
   CT_CHECK_LAUNCH();
   return 0;
+}
+
+template <int WR>
+int launch_any(const P& p, bool ak, bool bk, int batch, hipStream_t st) {
+  if (ak && bk) return launch<WR, true, true>(p, batch, st);
+  if (ak) return launch<WR, true, false>(p, batch, st);
+  if (bk) return launch<WR, false, true>(p, batch, st);
+  return launch<WR, false, false>(p, batch, st);
+}
+
+// tile shape: CTCLIP_G256_WR=2 forces the 256 x 256 form, =1 the 128 x 256 form
+int tile_rows() {
+  static int wr = -1;
+  if (wr < 0) {
+    const char* e = getenv("CTCLIP_G256_WR");
+    wr = (e && atoi(e) == 2) ? 2 : 1;
+  }
+  return wr;
 }
 
 }  // namespace g256
@@ -289,13 +338,6 @@ int launch(const P& p, int batch, hipStream_t st) {
 // called from ctclip_gemm (gemm.hip) after argument validation
 int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream) {
   using namespace g256;
-  if (!s_attr) {
-    (void)hipFuncSetAttribute((const void*)gemm256_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
-    (void)hipFuncSetAttribute((const void*)gemm256_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
-    (void)hipFuncSetAttribute((const void*)gemm256_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
-    (void)hipFuncSetAttribute((const void*)gemm256_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM);
-    s_attr = true;
-  }
   P p;
   p.M = a->M; p.N = a->N; p.K = a->K;
   p.A = (const u16*)a->A; p.lda = a->lda;
@@ -309,8 +351,6 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   int64_t kper = (a->K / BK + split - 1) / split * BK;
   p.kper = kper;
   hipStream_t st = (hipStream_t)stream;
-  if (a->a_kcontig && a->b_kcontig) return launch<true, true>(p, batch, st);
-  if (a->a_kcontig && !a->b_kcontig) return launch<true, false>(p, batch, st);
-  if (!a->a_kcontig && a->b_kcontig) return launch<false, true>(p, batch, st);
-  return launch<false, false>(p, batch, st);
+  if (tile_rows() == 2) return launch_any<2>(p, a->a_kcontig, a->b_kcontig, batch, st);
+  return launch_any<1>(p, a->a_kcontig, a->b_kcontig, batch, st);
 }

@@ -66,9 +66,9 @@ class CTCLIP(nn.Module):
 
     # ------------------------------------------------------------------ helpers
     def _visual_weight_bf16(self, W):
-        key = (W.data_ptr(), W._version)
+        from . import kernels as K
+        key = (W.data_ptr(), W._version, K.weights_epoch())
         if self._wvis[0] != key:
-            from . import kernels as K
             self._wvis = (key, K.cast_bf16(W.detach().contiguous()))
         return self._wvis[1]
 

@@ -10,6 +10,7 @@ by index arithmetic instead of transposing).
 from __future__ import annotations
 
 import math
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -18,6 +19,35 @@ from . import dist_sync
 from . import kernels as K
 
 F32, BF16 = torch.float32, torch.bfloat16
+
+
+# ----------------------------------------------------------------------------- gradient plumbing
+def gsink(p):
+    """Gradient sink of parameter ``p``: the backward kernels accumulate its gradient straight
+    into ``p.grad`` (the trainer binds every .grad to one flat f32 arena, zeroed after each
+    optimizer step) and the Function returns None for ``p`` -- no temporary gradient and no
+    AccumulateGrad add per parameter.  None when ``p`` needs no gradient."""
+    if not p.requires_grad:
+        return None
+    if p.grad is None:
+        p.grad = torch.zeros_like(p, memory_format=torch.contiguous_format)
+    return p.grad
+
+
+_SHADOW = {}
+
+
+def put_shadow(gf, gb):
+    """Register ``gb`` (bf16) as the bf16 image of the f32 gradient ``gf`` a backward returns,
+    so the producing layer's backward can take it instead of re-casting (identity-checked)."""
+    _SHADOW[id(gf)] = (weakref.ref(gf), gb)
+
+
+def take_shadow(gf):
+    e = _SHADOW.pop(id(gf), None)
+    if e is not None and e[0]() is gf:
+        return e[1]
+    return None
 
 
 # ----------------------------------------------------------------------------- geometry
@@ -104,6 +134,7 @@ class PatchEmbedFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dyf, _dyb):
         xhat, y1, mean, rstd, ln1_w, ln1_b, W, ln2_w = ctx.saved_tensors
+        take_shadow(dyf)
         _, dy1b, dg2, db2 = K.layernorm_bwd(dyf.contiguous(), y1, mean, rstd, ln2_w, dx_f32=False)
         G = K.matmul_tn(dy1b, xhat)                                     # [D, pd] f32
         cs = K.colsum(dy1b)                                             # d bias
@@ -141,27 +172,35 @@ class CPBFn(torch.autograd.Function):
         u = torch.empty(H, nb, device=rel.device, dtype=F32)
         K.sgemm(nb, H, h2.shape[1], h2, h2.stride(0), 1, w2, 1, w2.stride(0), u, 1, nb, bias=b2)
         ctx.save_for_backward(rel, w0, w1, w2, h1, h2)
+        ctx.params = (w0, b0, w1, b1, w2, b2)
         return u
 
     @staticmethod
     def backward(ctx, du):
         rel, w0, w1, w2, h1, h2 = ctx.saved_tensors
+        pw0, pb0, pw1, pb1, pw2, pb2 = ctx.params
         du = du.contiguous()
         H, nb = du.shape
         dev = du.device
         dz2 = torch.empty(nb, w2.shape[1], device=dev, dtype=F32)
         K.sgemm(nb, w2.shape[1], H, du, 1, nb, w2, w2.stride(0), 1, dz2, dz2.stride(0), 1, act=2, aux=h2,
                 sxm=h2.stride(0), sxn=1)
-        dw2 = K.smm(du, h2)
-        ones = torch.ones(nb, device=dev, dtype=F32)
-        db2 = torch.empty(H, device=dev, dtype=F32)
-        K.sgemm(H, 1, nb, du, nb, 1, ones, 1, 0, db2, 1, 1)
-        dw1 = K.smm(dz2.t(), h1)
-        db1 = K.colsum(dz2)
+        # parameter gradients accumulate straight into .grad
+        if pw2.requires_grad:
+            K.smm(du, h2, out=gsink(pw2), accumulate=True)
+        if pb2.requires_grad:
+            ones = torch.ones(nb, device=dev, dtype=F32)
+            K.sgemm(H, 1, nb, du, nb, 1, ones, 1, 0, gsink(pb2), 1, 1, accumulate=True)
+        if pw1.requires_grad:
+            K.smm(dz2.t(), h1, out=gsink(pw1), accumulate=True)
+        if pb1.requires_grad:
+            K.colsum(dz2, out=gsink(pb1), accumulate=True)
         dz1 = K.smm(dz2, w1, act=2, aux=h1)
-        dw0 = K.smm(dz1.t(), rel)
-        db0 = K.colsum(dz1)
-        return None, dw0, db0, dw1, db1, dw2, db2
+        if pw0.requires_grad:
+            K.smm(dz1.t(), rel, out=gsink(pw0), accumulate=True)
+        if pb0.requires_grad:
+            K.colsum(dz1, out=gsink(pb0), accumulate=True)
+        return None, None, None, None, None, None, None
 
 
 # ----------------------------------------------------------------------------- transformer layer
@@ -197,36 +236,38 @@ class ViTLayerFn(torch.autograd.Function):
         x3f = K.linear(g, W2p, residual=x2f, out_dtype=F32, out2=x3b)
         ctx.geo = geo
         ctx.use_bias = use_bias
+        ctx.params = (peg_w, peg_b, norm_g, q_scale, k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1, W2)
         ctx.save_for_backward(xb, x1b, m1, r1, xn, q, kv, qn, kn, o, lse, x2b, m2, r2, xn2, h, g,
-                              bias_u if use_bias else torch.empty(0), peg_w, norm_g, q_scale, k_scale,
-                              Wq_b, Wkv_b, Wo_b, ff_w, W1p, W2p, W1, W2)
+                              bias_u if use_bias else torch.empty(0), Wq_b, Wkv_b, Wo_b, W1p, W2p)
         ctx.mark_non_differentiable(x3b)
         return x3f, x3b
 
     @staticmethod
     def backward(ctx, dx3f, _dx3b):
-        (xb, x1b, m1, r1, xn, q, kv, qn, kn, o, lse, x2b, m2, r2, xn2, h, g, bias_u, peg_w, norm_g, q_scale,
-         k_scale, Wq_b, Wkv_b, Wo_b, ff_w, W1p, W2p, W1, W2) = ctx.saved_tensors
+        (xb, x1b, m1, r1, xn, q, kv, qn, kn, o, lse, x2b, m2, r2, xn2, h, g, bias_u, Wq_b, Wkv_b, Wo_b, W1p,
+         W2p) = ctx.saved_tensors
+        peg_w, peg_b, norm_g, q_scale, k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1, W2 = ctx.params
         geo = ctx.geo
         H, dh = geo.heads, geo.dim_head
         inner = H * dh
         dev = dx3f.device
+        dx3b = take_shadow(dx3f)          # bf16 image written by the next layer's PEG backward
         dx3f = dx3f.contiguous()
-        dx3b = K.cast_bf16(dx3f)
-        # feed-forward
+        if dx3b is None:
+            dx3b = K.cast_bf16(dx3f)
+        # feed-forward (weight gradients accumulate straight into the parameters' .grad)
         dg = K.matmul_nn(dx3b, W2p)
         dW2p = K.matmul_tn(dx3b, g)
         dh_ = K.geglu_bwd(dg, h)
         dxn2 = K.matmul_nn(dh_, W1p)
         dW1p = K.matmul_tn(dh_, xn2)
-        dx2f, dx2b, dffw, dffb = K.layernorm_bwd(dxn2, x2b, m2, r2, ff_w, dres=dx3f)
-        dW1 = torch.empty_like(W1)
-        K.unpack_rows(dW1p, dW1, rowmap=ff1_rowmap(W1.shape[0] // 2, dev), accumulate=False)
-        dW2 = torch.empty_like(W2)
-        K.unpack_rows(dW2p, dW2, cols=W2.shape[1], accumulate=False)
+        dx2f, dx2b, _, _ = K.layernorm_bwd(dxn2, x2b, m2, r2, ff_w, dres=dx3f, dgamma_out=gsink(ff_w),
+                                           dbeta_out=gsink(ff_b))
+        K.unpack_rows(dW1p, gsink(W1), rowmap=ff1_rowmap(W1.shape[0] // 2, dev), accumulate=True)
+        K.unpack_rows(dW2p, gsink(W2), cols=W2.shape[1], accumulate=True)
         # attention
         do = K.matmul_nn(dx2b, Wo_b)
-        dWo = K.matmul_tn(dx2b, o)
+        K.matmul_tn(dx2b, o, out=gsink(Wo), accumulate=True)
         dqn = torch.empty_like(qn)
         dkn = torch.empty_like(kn)
         dkv = torch.empty_like(kv)
@@ -236,17 +277,19 @@ class ViTLayerFn(torch.autograd.Function):
                    scale=8.0, seq=seq, bias_u=bias_u if ctx.use_bias else None, dbias_u=du,
                    grid=(geo.Hg, geo.Wg) if ctx.use_bias else (0, 0))
         dq = torch.empty_like(q)
-        dqs = K.l2norm_scale_bwd(q, dqn, H, dh, q_scale, dq)
-        dks = K.l2norm_scale_bwd(kv[:, :inner], dkn, H, dh, k_scale, dkv[:, :inner])
+        K.l2norm_scale_bwd(q, dqn, H, dh, q_scale, dq, ds_out=gsink(q_scale))
+        K.l2norm_scale_bwd(kv[:, :inner], dkn, H, dh, k_scale, dkv[:, :inner], ds_out=gsink(k_scale))
         dxn = K.matmul_nn(dq, Wq_b)
-        dWq = K.matmul_tn(dq, xn)
-        dWkv = K.matmul_tn(dkv, x1b)
+        K.matmul_tn(dq, xn, out=gsink(Wq), accumulate=True)
+        K.matmul_tn(dkv, x1b, out=gsink(Wkv), accumulate=True)
         dx1kv = K.matmul_nn(dkv, Wkv_b, residual=dx2f, out_dtype=F32)
-        dx1f, dx1b, dng, _ = K.layernorm_bwd(dxn, x1b, m1, r1, norm_g, dres=dx1kv, want_beta=False)
+        dx1f, dx1b, _, _ = K.layernorm_bwd(dxn, x1b, m1, r1, norm_g, dres=dx1kv, want_beta=False,
+                                           dgamma_out=gsink(norm_g))
         # PEG
-        dxf, _, dpw, dpb = K.peg_bwd(dx1b, dx1f, xb, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, geo.mode)
-        return (dxf, None, du, None, dpw.reshape(peg_w.shape), dpb, dng, dqs, dks, dWq, dWkv, dWo, dffw, dffb,
-                dW1, dW2)
+        dxf, dxb, dpw, dpb = K.peg_bwd(dx1b, dx1f, xb, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, geo.mode)
+        put_shadow(dxf, dxb)
+        return (dxf, None, du, None, dpw.reshape(peg_w.shape), dpb, None, None, None, None, None, None, None,
+                None, None, None)
 
 
 class NormFn(torch.autograd.Function):
@@ -256,14 +299,18 @@ class NormFn(torch.autograd.Function):
     def forward(ctx, xf, xb, gamma):
         yb, yf, mean, rstd = K.layernorm_fwd(xf, gamma, None, 1e-5, out_bf16=True, out_f32=True)
         ctx.save_for_backward(xb, mean, rstd, gamma)
+        ctx.gamma = gamma
         ctx.mark_non_differentiable(yb)
         return yf, yb
 
     @staticmethod
     def backward(ctx, dyf, _):
         xb, mean, rstd, gamma = ctx.saved_tensors
-        dxf, _, dg, _ = K.layernorm_bwd(dyf.contiguous(), xb, mean, rstd, gamma, want_beta=False, dx_bf16=False)
-        return dxf, None, dg
+        take_shadow(dyf)
+        dxf, dxb, _, _ = K.layernorm_bwd(dyf.contiguous(), xb, mean, rstd, gamma, want_beta=False,
+                                         dgamma_out=gsink(ctx.gamma))
+        put_shadow(dxf, dxb)
+        return dxf, None, None
 
 
 # ----------------------------------------------------------------------------- VQ + pooling
@@ -355,16 +402,18 @@ class ImageProjFn(torch.autograd.Function):
         K.gemm_raw(B, N, Kd, pooled_b, Kd, True, Wb, Kd, True, slabs, N, split_k=split)
         out = torch.empty(B, N, device=pooled.device, dtype=F32)
         K.reduce_slabs(slabs, out)
-        ctx.save_for_backward(pooled_b, W, Wb)
+        ctx.save_for_backward(pooled_b, Wb)
+        ctx.W = W
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        pooled_b, W, Wb = ctx.saved_tensors
+        pooled_b, Wb = ctx.saved_tensors
         dlb = K.cast_bf16(dout.contiguous())
         dpooled = K.matmul_nn(dlb, Wb, out_dtype=F32) if ctx.needs_input_grad[0] else None
-        dW = K.matmul_tn(dlb, pooled_b) if ctx.needs_input_grad[2] else None
-        return dpooled, None, dW, None
+        if ctx.needs_input_grad[2]:   # the 294,912-wide weight gradient lands in .grad directly
+            K.matmul_tn(dlb, pooled_b, out=gsink(ctx.W), accumulate=True)
+        return dpooled, None, None, None
 
 
 class TextProjFn(torch.autograd.Function):
@@ -374,6 +423,7 @@ class TextProjFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, cls, W):
         ctx.save_for_backward(cls, W)
+        ctx.W = W
         return K.slinear(cls, W)
 
     @staticmethod
@@ -381,8 +431,9 @@ class TextProjFn(torch.autograd.Function):
         cls, W = ctx.saved_tensors
         dout = dout.contiguous()
         dcls = K.smm(dout, W) if ctx.needs_input_grad[0] else None
-        dW = K.smm(dout.t(), cls) if ctx.needs_input_grad[1] else None
-        return dcls, dW
+        if ctx.needs_input_grad[1]:
+            K.smm(dout.t(), cls, out=gsink(ctx.W), accumulate=True)
+        return dcls, None
 
 
 # ----------------------------------------------------------------------------- loss
@@ -421,20 +472,20 @@ class BertEmbedFn(torch.autograd.Function):
         x = K.embed_fwd(ids, word, pos, typ[0])
         yb, yf, mean, rstd = K.layernorm_fwd(x, ln_w, ln_b, eps, out_bf16=True, out_f32=True)
         ctx.save_for_backward(ids, x, mean, rstd, ln_w)
-        ctx.shapes = (word.shape, pos.shape, typ.shape)
+        ctx.params = (word, pos, typ, ln_w, ln_b)
         ctx.mark_non_differentiable(yb)
         return yf, yb
 
     @staticmethod
     def backward(ctx, dyf, _):
         ids, x, mean, rstd, ln_w = ctx.saved_tensors
-        dx, _, dg, db = K.layernorm_bwd(dyf.contiguous(), x, mean, rstd, ln_w, dx_bf16=False)
-        ws, ps, ts = ctx.shapes
-        dword = torch.zeros(ws, device=dx.device, dtype=F32)
-        dpos = torch.zeros(ps, device=dx.device, dtype=F32)
-        dtyp = torch.zeros(ts, device=dx.device, dtype=F32)
-        K.embed_bwd(ids, dx, dword, dpos, dtyp[0])
-        return None, dword, dpos, dtyp, dg, db, None
+        word, pos, typ, _, ln_b = ctx.params
+        dx, _, _, _ = K.layernorm_bwd(dyf.contiguous(), x, mean, rstd, ln_w, dx_bf16=False,
+                                      dgamma_out=gsink(ln_w), dbeta_out=gsink(ln_b))
+        dtyp = gsink(typ)
+        # scatter-add straight into the parameters' .grad
+        K.embed_bwd(ids, dx, gsink(word), gsink(pos), dtyp[0] if dtyp is not None else None)
+        return None, None, None, None, None, None, None
 
 
 class BertLayerFn(torch.autograd.Function):
@@ -462,6 +513,7 @@ class BertLayerFn(torch.autograd.Function):
         x2b, x2f, m2, r2 = K.layernorm_fwd(b2, ln2_w, ln2_b, eps, out_bf16=True, out_f32=True)
         ctx.save_for_backward(xb, kmask, qkv, ctxv, lse, a, m1, r1, x1b, hpre, hact, b2, m2, r2, Wqkv, Wo_b, Wi_b,
                               Wout_b, ln1_w, ln2_w)
+        ctx.params = (Wq, bq, Wk, bk, Wv, bv, Wo, bo, ln1_w, ln1_b, Wi, bi, Wout, bout, ln2_w, ln2_b)
         ctx.dims = (B, L, heads, dh)
         ctx.mark_non_differentiable(x2b)
         return x2f, x2b
@@ -470,29 +522,33 @@ class BertLayerFn(torch.autograd.Function):
     def backward(ctx, dx2f, _):
         (xb, kmask, qkv, ctxv, lse, a, m1, r1, x1b, hpre, hact, b2, m2, r2, Wqkv, Wo_b, Wi_b, Wout_b, ln1_w,
          ln2_w) = ctx.saved_tensors
+        Wq, bq, Wk, bk, Wv, bv, Wo, bo, _, ln1_b, Wi, bi, Wout, bout, _, ln2_b = ctx.params
         B, L, heads, dh = ctx.dims
         Hd = heads * dh
+
+        def wgrad(dy, x, W, b):          # dW += dy^T x, db += colsum(dy), into the parameters' .grad
+            if W.requires_grad:
+                K.matmul_tn(dy, x, out=gsink(W), accumulate=True)
+            if b.requires_grad:
+                K.colsum(dy, out=gsink(b), accumulate=True)
+
         # LN2 + FF out
-        db2f, db2b, dln2w, dln2b = K.layernorm_bwd(dx2f.contiguous(), b2, m2, r2, ln2_w)
+        db2f, db2b, _, _ = K.layernorm_bwd(dx2f.contiguous(), b2, m2, r2, ln2_w, dgamma_out=gsink(ln2_w),
+                                           dbeta_out=gsink(ln2_b))
         dhact = K.matmul_nn(db2b, Wout_b)
-        dWout = K.matmul_tn(db2b, hact)
-        dbout = K.colsum(db2b)
+        wgrad(db2b, hact, Wout, bout)
         dhpre = K.gelu_bwd(dhact, hpre)
         dx1 = K.matmul_nn(dhpre, Wi_b, residual=db2f, out_dtype=F32)
-        dWi = K.matmul_tn(dhpre, x1b)
-        dbi = K.colsum(dhpre)
+        wgrad(dhpre, x1b, Wi, bi)
         # LN1 + attention out
-        daf, dab, dln1w, dln1b = K.layernorm_bwd(dx1, a, m1, r1, ln1_w)
+        daf, dab, _, _ = K.layernorm_bwd(dx1, a, m1, r1, ln1_w, dgamma_out=gsink(ln1_w), dbeta_out=gsink(ln1_b))
         dctx = K.matmul_nn(dab, Wo_b)
-        dWo = K.matmul_tn(dab, ctxv)
-        dbo = K.colsum(dab)
+        wgrad(dab, ctxv, Wo, bo)
         dqkv = torch.empty_like(qkv)
         K.attn_bwd(qkv[:, :Hd], qkv[:, Hd:2 * Hd], qkv[:, 2 * Hd:], ctxv, lse, dctx, dqkv[:, :Hd],
                    dqkv[:, Hd:2 * Hd], dqkv[:, 2 * Hd:], L=L, H=heads, D=dh, nseq=B, scale=1.0 / math.sqrt(dh),
                    seq=(1, L, 0, 1), kmask=kmask)
         dx = K.matmul_nn(dqkv, Wqkv, residual=daf, out_dtype=F32)
-        dWqkv = K.matmul_tn(dqkv, xb)
-        dbqkv = K.colsum(dqkv)
-        return (dx, None, None, None, None, None, None,
-                dWqkv[:Hd], dbqkv[:Hd], dWqkv[Hd:2 * Hd], dbqkv[Hd:2 * Hd], dWqkv[2 * Hd:], dbqkv[2 * Hd:],
-                dWo, dbo, dln1w, dln1b, dWi, dbi, dWout, dbout, dln2w, dln2b)
+        for i, (W, b) in enumerate(((Wq, bq), (Wk, bk), (Wv, bv))):
+            wgrad(dqkv[:, i * Hd:(i + 1) * Hd], xb, W, b)
+        return (dx, None, None, None, None, None, None) + (None,) * 16

@@ -181,8 +181,10 @@ def layernorm_fwd(x, gamma, beta, eps, *, out_bf16=True, out_f32=False):
     return yb, yf, mean, rstd
 
 
-def layernorm_bwd(dy, x, mean, rstd, gamma, *, dres=None, want_beta=True, dx_f32=True, dx_bf16=True):
-    """Returns (dx_f32, dx_bf16, dgamma, dbeta)."""
+def layernorm_bwd(dy, x, mean, rstd, gamma, *, dres=None, want_beta=True, dx_f32=True, dx_bf16=True,
+                  dgamma_out=None, dbeta_out=None):
+    """Returns (dx_f32, dx_bf16, dgamma, dbeta).  dgamma_out / dbeta_out: accumulate the
+    parameter gradients into these f32 tensors instead of returning fresh ones."""
     rows, D = x.shape
     nb = nblocks_for(rows, 1024)
     dxf = torch.empty(rows, D, device=x.device, dtype=F32) if dx_f32 else None
@@ -192,12 +194,12 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, *, dres=None, want_beta=True, dx_f32
     call('ctclip_layernorm_bwd', ptr(dy), int(dy.dtype == F32), dy.stride(0), ptr(x), int(x.dtype == F32),
          x.stride(0), ptr(mean), ptr(rstd), ptr(gamma), rows, D, ptr(dres),
          dres.stride(0) if dres is not None else 0, ptr(dxf), D, ptr(dxb), D, ptr(pg), ptr(pb), nb, stream_ptr())
-    dg = torch.empty(D, device=x.device, dtype=F32)
-    reduce_slabs(pg.view(nb, 1, D), dg.view(1, D))
+    dg = dgamma_out if dgamma_out is not None else torch.empty(D, device=x.device, dtype=F32)
+    reduce_slabs(pg.view(nb, 1, D), dg.view(1, D), accumulate=dgamma_out is not None)
     db = None
     if want_beta:
-        db = torch.empty(D, device=x.device, dtype=F32)
-        reduce_slabs(pb.view(nb, 1, D), db.view(1, D))
+        db = dbeta_out if dbeta_out is not None else torch.empty(D, device=x.device, dtype=F32)
+        reduce_slabs(pb.view(nb, 1, D), db.view(1, D), accumulate=dbeta_out is not None)
     return dxf, dxb, dg, db
 
 
@@ -210,7 +212,8 @@ def l2norm_scale_fwd(x, H, D, scale, out=None):
     return out
 
 
-def l2norm_scale_bwd(x, dy, H, D, scale, out):
+def l2norm_scale_bwd(x, dy, H, D, scale, out, ds_out=None):
+    """dx into `out`; returns dscale (accumulated into ds_out when given)."""
     rows = x.shape[0]
     lpr = H * D // 8
     nb = 2048       # 8 workgroups per CU: the row loop is load-latency bound
@@ -219,8 +222,8 @@ def l2norm_scale_bwd(x, dy, H, D, scale, out):
     part = torch.empty(nb, D, device=x.device, dtype=F32)
     call('ctclip_l2norm_scale_bwd', ptr(x), x.stride(0), ptr(dy), dy.stride(0), rows, H, D, ptr(scale), ptr(out),
          out.stride(0), ptr(part), nb, stream_ptr())
-    ds = torch.empty(D, device=x.device, dtype=F32)
-    reduce_slabs(part.view(nb, 1, D), ds.view(1, D))
+    ds = ds_out if ds_out is not None else torch.empty(D, device=x.device, dtype=F32)
+    reduce_slabs(part.view(nb, 1, D), ds.view(1, D), accumulate=ds_out is not None)
     return ds
 
 
@@ -473,9 +476,20 @@ def grad_norm(g, max_norm, out):
     return out
 
 
+_WEIGHTS_EPOCH = [0]
+
+
+def weights_epoch():
+    """Bumped by every optimizer update: the Adam kernel writes parameters through raw pointers,
+    invisible to torch's version counters, so caches of derived weights (bf16 copies) key on
+    (data_ptr, _version, weights_epoch())."""
+    return _WEIGHTS_EPOCH[0]
+
+
 def adam(p, g, m, v, *, lr, b1, b2, eps, wd, step, coef=None, p_bf16=None):
     call('ctclip_adam', ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, b1, b2, eps, wd, step, ptr(coef), ptr(p_bf16),
          stream_ptr())
+    _WEIGHTS_EPOCH[0] += 1
 
 
 def gelu_f32(x):
