@@ -13,13 +13,24 @@
 // so each lane owns ONE query column and its probabilities feed the P.V MFMA as the B operand
 // with a permuted key order; V (and K in the backward) are read from their row-major LDS
 // image with ds_read_b64_tr_b16 in that same permuted order.  Online softmax keeps the
-// running max/sum per lane.  The CPB bias is read from the deduplicated table u[h][bin],
-// bin = (dh + Hg-1)*(2Wg-1) + (dw + Wg-1) (2,209 entries at 24x24), and its gradient is
-// binned the same way in LDS (one global atomic per bin per workgroup).
+// running max/sum per lane, in the log2 domain (log2(e) folded into the score scale and the
+// bias table, so every probability is one v_exp_f32).
+//
+// The kernels are VALU-bound (head dim 32: 2 MFMAs of S per 32 keys against 8 softmax elements
+// per lane), so per-element work is kept to table reads:
+//   * CPB bias: bin(q, k) = (hq-hk+Hg-1)(2Wg-1) + (wq-wk+Wg-1) = C(q) - kb[k] with the position
+//     table kb[i] = (i / Wg)(2Wg-1) + i % Wg in LDS; the deduplicated bias u[h][bin] (2,209
+//     entries at 24x24, pre-scaled by log2 e) is read from LDS by that index;
+//   * key validity (padding past L, BERT key mask) is an additive 0 / -inf row in LDS;
+//   * query validity in the backward rides on lse = +inf for padded queries.
+// The bias gradient is binned with the same index arithmetic (frame-inner kernel below).
 #include "common.h"
 #include "../../include/ctclip_hip.h"
 
 namespace {
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
 
 struct AP {
   const u16* q; int64_t ldq;
@@ -40,7 +51,6 @@ struct AP {
   int L, H, nseq;
   int64_t M;
   int Hg, Wg, nbins;
-  float inv_wg;
   int n_inner;
   int64_t s_outer, s_inner, s_pos;
   int pp;                         // (seq, head) pairs per workgroup
@@ -53,11 +63,9 @@ __device__ __forceinline__ int64_t seq_row(const AP& p, int s, int i) {
   return (int64_t)(s / p.n_inner) * p.s_outer + (int64_t)(s % p.n_inner) * p.s_inner + (int64_t)i * p.s_pos;
 }
 
-__device__ __forceinline__ int bin_of(const AP& p, int hq, int wq, int key) {
-  const int hk = (int)(((float)key + 0.5f) * p.inv_wg);
-  const int wk = key - hk * p.Wg;
-  return (hq - hk + p.Hg - 1) * (2 * p.Wg - 1) + (wq - wk + p.Wg - 1);
-}
+// bias table constants: bin(q, k) = kb[q] + boff - kb[k]
+__device__ __forceinline__ int kb_of(const AP& p, int i) { return (i / p.Wg) * (2 * p.Wg - 1) + i % p.Wg; }
+__device__ __forceinline__ int boff(const AP& p) { return (p.Hg - 1) * (2 * p.Wg - 1) + p.Wg - 1; }
 
 template <int D>
 struct Img {
@@ -106,9 +114,38 @@ __device__ __forceinline__ bf16x8 pack_perm(const f32x4& a, const f32x4& b) {
 
 __device__ __forceinline__ bf16x8 gload8(const u16* p) { return __builtin_bit_cast(bf16x8, *(const u32x4*)p); }
 __device__ __forceinline__ bf16x8 zero8() { return __builtin_bit_cast(bf16x8, make_uint4(0, 0, 0, 0)); }
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// shared LDS tables of a workgroup (after the K/V or Q/dO images):
+//   ub[nbins]  bias table * log2 e        (BIAS)
+//   kb[Lp]     position table             (BIAS)
+//   madd[pp][Lp] additive key validity     (0 / -inf: padding past L, key mask)
+template <bool BIAS>
+__device__ __forceinline__ void load_tables(const AP& p, char* tab, int Lp, int tid, int h, float*& ub, int*& kb,
+                                            float*& madd) {
+  char* t = tab;
+  if (BIAS) {
+    ub = (float*)t;
+    t += ((p.nbins + 3) & ~3) * 4;   // keep kb / madd 16-B aligned for the vector reads
+    kb = (int*)t;
+    t += Lp * 4;
+    for (int i = tid; i < p.nbins; i += NT) ub[i] = p.bias_u[(int64_t)h * p.nbins + i] * LOG2E;
+    for (int i = tid; i < Lp; i += NT) kb[i] = i < p.L ? kb_of(p, i) : 0;
+  }
+  madd = (float*)t;
+  for (int pl = 0; pl < p.pp; ++pl) {
+    const int pair = blockIdx.x * p.pp + pl;
+    const int s = pair / p.H;
+    for (int i = tid; i < Lp; i += NT) {
+      bool v = i < p.L && pair < p.nseq * p.H;
+      if (v && p.kmask) v = p.kmask[(int64_t)s * p.L + i] != 0;
+      madd[pl * Lp + i] = v ? 0.f : -INFINITY;
+    }
+  }
+}
 
 // ------------------------------------------------------------------------------------ forward
-template <int D>
+template <int D, bool BIAS>
 __global__ __launch_bounds__(NT) void attn_fwd_kernel(AP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KK = D / 32, DB = D / 16, RS = Img<D>::RS;
@@ -117,7 +154,6 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(AP p) {
   const int wpp = NW / p.pp;                         // waves per pair
   const int pair_local = w / wpp, wi = w - pair_local * wpp;
   const int pair_bytes = 2 * Lp * RS;
-  float* ub = (float*)(smem + p.pp * pair_bytes);
   for (int pl = 0; pl < p.pp; ++pl) {
     const int pair = blockIdx.x * p.pp + pl;
     if (pair >= p.nseq * p.H) break;
@@ -125,18 +161,20 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(AP p) {
     stage<D>(smem + pl * pair_bytes, p.k, p.ldk, p, s, h, Lp, tid, NT);
     stage<D>(smem + pl * pair_bytes + Lp * RS, p.v, p.ldv, p, s, h, Lp, tid, NT);
   }
-  if (p.bias_u) {
-    const int h = blockIdx.x % p.H;  // pp == 1 when a bias is present
-    for (int i = tid; i < p.nbins; i += NT) ub[i] = p.bias_u[(int64_t)h * p.nbins + i];
-  }
+  float* ub = nullptr;
+  int* kb = nullptr;
+  float* madd = nullptr;
+  load_tables<BIAS>(p, smem + p.pp * pair_bytes, Lp, tid, blockIdx.x % p.H, ub, kb, madd);  // pp == 1 with BIAS
   __syncthreads();
   const int pair = blockIdx.x * p.pp + pair_local;
   if (pair >= p.nseq * p.H) return;
   const int s = pair / p.H, h = pair - s * p.H;
   const char* Kimg = smem + pair_local * pair_bytes;
   const char* Vimg = Kimg + Lp * RS;
+  const float* mrow = madd + pair_local * Lp;
   const int g = lane >> 4, li = lane & 15;
   const int nqb = (L + 15) >> 4;
+  const float sc2 = p.scale * LOG2E;
   for (int qb = wi; qb < nqb; qb += wpp) {
     const int q = qb * 16 + li;
     const bool qv = q < L;
@@ -144,8 +182,7 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(AP p) {
     bf16x8 qf[KK];
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) qf[kk] = qv ? gload8(p.q + qrow * p.ldq + h * D + kk * 32 + 8 * g) : zero8();
-    int hq = 0, wq = 0;
-    if (p.bias_u) { hq = (int)(((float)q + 0.5f) * p.inv_wg); wq = q - hq * p.Wg; }
+    const int cq = BIAS ? kb[min(q, L - 1)] + boff(p) : 0;   // padded queries: any in-range bin
     float m = -INFINITY, lsum = 0.f;
     f32x4 o[DB];
 #pragma unroll
@@ -161,29 +198,30 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(AP p) {
       }
       float cmax = -INFINITY;
 #pragma unroll
-      for (int bi = 0; bi < 2; ++bi)
+      for (int bi = 0; bi < 2; ++bi) {
+        const int k0 = kc + 16 * bi + 4 * g;
+        const f32x4 ma = *(const f32x4*)(mrow + k0);
+        int4 kbv;
+        if (BIAS) kbv = *(const int4*)(kb + k0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int key = kc + 16 * bi + 4 * g + r;
-          float x = sa[bi][r] * p.scale;
-          bool valid = key < L;
-          if (valid && p.kmask) valid = p.kmask[(int64_t)s * L + key] != 0;
-          if (valid && p.bias_u) x += ub[bin_of(p, hq, wq, key)];
-          x = valid ? x : -INFINITY;
+          float x = sa[bi][r] * sc2 + ma[r];
+          if (BIAS) x += ub[cq - kbv[r]];
           sa[bi][r] = x;
           cmax = fmaxf(cmax, x);
         }
+      }
       cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
       cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
       const float mnew = fmaxf(m, cmax);
       const float msafe = mnew == -INFINITY ? 0.f : mnew;
-      const float alpha = __expf(m - msafe);
+      const float alpha = fexp2(m - msafe);
       float psum = 0.f;
 #pragma unroll
       for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = __expf(sa[bi][r] - msafe);
+          const float e = fexp2(sa[bi][r] - msafe);
           sa[bi][r] = e;
           psum += e;
         }
@@ -207,14 +245,16 @@ __global__ __launch_bounds__(NT) void attn_fwd_kernel(AP p) {
         pk.y = pack2(o[d][2] * inv, o[d][3] * inv);
         *(uint2*)(p.out + qrow * p.ldout + h * D + d * 16 + 4 * g) = pk;
       }
-      if (g == 0 && p.lse) p.lse[(int64_t)h * p.M + qrow] = lsum > 0.f ? m + __logf(lsum) : INFINITY;
+      // natural-log LSE: ln(sum exp(x)) = (m2 + log2(lsum)) * ln 2
+      if (g == 0 && p.lse) p.lse[(int64_t)h * p.M + qrow] = lsum > 0.f ? (m + __log2f(lsum)) * LN2 : INFINITY;
     }
   }
 }
 
 // ------------------------------------------------------------------------------- backward dQ
-// also writes delta = rowsum(dO * O) and bins the bias gradient
-template <int D>
+// also writes delta = rowsum(dO * O); with BIAS, bins the bias gradient (LDS atomics; the
+// spatial shapes use the frame-inner kernel below instead)
+template <int D, bool BIAS>
 __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(AP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KK = D / 32, DB = D / 16, RS = Img<D>::RS;
@@ -223,8 +263,6 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(AP p) {
   const int wpp = NW / p.pp;
   const int pair_local = w / wpp, wi = w - pair_local * wpp;
   const int pair_bytes = 2 * Lp * RS;
-  float* ub = (float*)(smem + p.pp * pair_bytes);
-  float* bins = ub + p.nbins;
   for (int pl = 0; pl < p.pp; ++pl) {
     const int pair = blockIdx.x * p.pp + pl;
     if (pair >= p.nseq * p.H) break;
@@ -232,18 +270,23 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(AP p) {
     stage<D>(smem + pl * pair_bytes, p.k, p.ldk, p, s, h, Lp, tid, NT);
     stage<D>(smem + pl * pair_bytes + Lp * RS, p.v, p.ldv, p, s, h, Lp, tid, NT);
   }
-  if (p.bias_u) {
-    const int h = blockIdx.x % p.H;
-    for (int i = tid; i < p.nbins; i += NT) { ub[i] = p.bias_u[(int64_t)h * p.nbins + i]; bins[i] = 0.f; }
-  }
+  float* ub = nullptr;
+  int* kb = nullptr;
+  float* madd = nullptr;
+  load_tables<BIAS>(p, smem + p.pp * pair_bytes, Lp, tid, blockIdx.x % p.H, ub, kb, madd);
+  float* bins = madd + p.pp * Lp;
+  if (BIAS)
+    for (int i = tid; i < p.nbins; i += NT) bins[i] = 0.f;
   __syncthreads();
   const int pair = blockIdx.x * p.pp + pair_local;
   const bool active = pair < p.nseq * p.H;
   const int s = active ? pair / p.H : 0, h = active ? pair - s * p.H : 0;
   const char* Kimg = smem + pair_local * pair_bytes;
   const char* Vimg = Kimg + Lp * RS;
+  const float* mrow = madd + pair_local * Lp;
   const int g = lane >> 4, li = lane & 15;
   const int nqb = active ? (L + 15) >> 4 : 0;
+  const float sc2 = p.scale * LOG2E;
   for (int qb = wi; qb < nqb; qb += wpp) {
     const int q = qb * 16 + li;
     const bool qv = q < L;
@@ -265,10 +308,9 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(AP p) {
     }
     dl += __shfl_xor(dl, 16, 64);
     dl += __shfl_xor(dl, 32, 64);
-    const float lse = qv ? p.lse[(int64_t)h * p.M + qrow] : INFINITY;
+    const float lse2 = qv ? p.lse[(int64_t)h * p.M + qrow] * LOG2E : INFINITY;
     if (qv && g == 0) p.delta[(int64_t)h * p.M + qrow] = dl;
-    int hq = 0, wq = 0;
-    if (p.bias_u) { hq = (int)(((float)q + 0.5f) * p.inv_wg); wq = q - hq * p.Wg; }
+    const int cq = BIAS ? kb[min(q, L - 1)] + boff(p) : 0;
     f32x4 dq[DB];
 #pragma unroll
     for (int d = 0; d < DB; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -285,23 +327,20 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(AP p) {
         }
       }
 #pragma unroll
-      for (int bi = 0; bi < 2; ++bi)
+      for (int bi = 0; bi < 2; ++bi) {
+        const int k0 = kc + 16 * bi + 4 * g;
+        const f32x4 ma = *(const f32x4*)(mrow + k0);
+        int4 kbv;
+        if (BIAS) kbv = *(const int4*)(kb + k0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int key = kc + 16 * bi + 4 * g + r;
-          bool valid = qv && key < L;
-          if (valid && p.kmask) valid = p.kmask[(int64_t)s * L + key] != 0;
-          float ds = 0.f;
-          if (valid) {
-            int bn = 0;
-            float x = sa[bi][r] * p.scale;
-            if (p.bias_u) { bn = bin_of(p, hq, wq, key); x += ub[bn]; }
-            const float pr = __expf(x - lse);
-            ds = pr * (da[bi][r] - dl);
-            if (p.dbias_u) atomicAdd(&bins[bn], ds);
-          }
+          float x = sa[bi][r] * sc2 + ma[r];
+          if (BIAS) x += ub[cq - kbv[r]];
+          const float ds = fexp2(x - lse2) * (da[bi][r] - dl);   // 0 for masked keys / padded queries
+          if (BIAS && p.dbias_u && qv) atomicAdd(&bins[cq - kbv[r]], ds);
           sa[bi][r] = ds * p.scale;
         }
+      }
       const bf16x8 dsb = pack_perm(sa[0], sa[1]);
 #pragma unroll
       for (int d = 0; d < DB; ++d)
@@ -317,7 +356,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(AP p) {
       }
     }
   }
-  if (p.dbias_u) {
+  if (BIAS && p.dbias_u) {
     __syncthreads();
     const int hh = blockIdx.x % p.H;
     for (int i = tid; i < p.nbins; i += NT) {
@@ -328,7 +367,9 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(AP p) {
 }
 
 // ----------------------------------------------------------------------------- backward dK dV
-template <int D>
+// lane owns a key; elements run over queries.  Padded queries carry lse = +inf (probability 0);
+// a masked / padded key adds -inf through kadd.
+template <int D, bool BIAS>
 __global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(AP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KK = D / 32, DB = D / 16, RS = Img<D>::RS;
@@ -337,7 +378,6 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(AP p) {
   const int wpp = NW / p.pp;
   const int pair_local = w / wpp, wi = w - pair_local * wpp;
   const int pair_bytes = 2 * Lp * RS + 2 * Lp * 4;
-  float* ub = (float*)(smem + p.pp * pair_bytes);
   for (int pl = 0; pl < p.pp; ++pl) {
     const int pair = blockIdx.x * p.pp + pl;
     if (pair >= p.nseq * p.H) break;
@@ -350,14 +390,14 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(AP p) {
     for (int i = tid; i < Lp; i += NT) {
       const bool v = i < L;
       const int64_t r = v ? seq_row(p, s, i) : 0;
-      ls[i] = v ? p.lse[(int64_t)h * p.M + r] : INFINITY;
+      ls[i] = v ? p.lse[(int64_t)h * p.M + r] * LOG2E : INFINITY;
       dls[i] = v ? p.delta[(int64_t)h * p.M + r] : 0.f;
     }
   }
-  if (p.bias_u) {
-    const int h = blockIdx.x % p.H;
-    for (int i = tid; i < p.nbins; i += NT) ub[i] = p.bias_u[(int64_t)h * p.nbins + i];
-  }
+  float* ub = nullptr;
+  int* kb = nullptr;
+  float* madd = nullptr;
+  load_tables<BIAS>(p, smem + p.pp * pair_bytes, Lp, tid, blockIdx.x % p.H, ub, kb, madd);
   __syncthreads();
   const int pair = blockIdx.x * p.pp + pair_local;
   if (pair >= p.nseq * p.H) return;
@@ -368,19 +408,20 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(AP p) {
   const float* dls = ls + Lp;
   const int g = lane >> 4, li = lane & 15;
   const int nkb = (L + 15) >> 4;
-  for (int kb = wi; kb < nkb; kb += wpp) {
-    const int key = kb * 16 + li;
-    bool kv = key < L;
-    if (kv && p.kmask) kv = p.kmask[(int64_t)s * L + key] != 0;
-    const int64_t krow = key < L ? seq_row(p, s, key) : 0;
+  const float sc2 = p.scale * LOG2E;
+  for (int kbk = wi; kbk < nkb; kbk += wpp) {
+    const int key = kbk * 16 + li;
+    const bool kin = key < L;
+    const float kadd = madd[pair_local * Lp + key];
+    const int64_t krow = kin ? seq_row(p, s, key) : 0;
     bf16x8 kf[KK], vf[KK];
 #pragma unroll
     for (int kk = 0; kk < KK; ++kk) {
-      kf[kk] = key < L ? gload8(p.k + krow * p.ldk + h * D + kk * 32 + 8 * g) : zero8();
-      vf[kk] = key < L ? gload8(p.v + krow * p.ldv + h * D + kk * 32 + 8 * g) : zero8();
+      kf[kk] = kin ? gload8(p.k + krow * p.ldk + h * D + kk * 32 + 8 * g) : zero8();
+      vf[kk] = kin ? gload8(p.v + krow * p.ldv + h * D + kk * 32 + 8 * g) : zero8();
     }
-    int hk = 0, wk = 0;
-    if (p.bias_u) { hk = (int)(((float)key + 0.5f) * p.inv_wg); wk = key - hk * p.Wg; }
+    // bin(q, key) = kb[q] - ck
+    const int ck = BIAS && kin ? kb[key] - boff(p) : 0;
     f32x4 dk[DB], dv[DB];
 #pragma unroll
     for (int d = 0; d < DB; ++d) { dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[d] = f32x4{0.f, 0.f, 0.f, 0.f}; }
@@ -398,24 +439,22 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(AP p) {
       }
       // element (bi, r): query = qc + 16bi + 4g + r, key = this lane's key
 #pragma unroll
-      for (int bi = 0; bi < 2; ++bi)
+      for (int bi = 0; bi < 2; ++bi) {
+        const int q0 = qc + 16 * bi + 4 * g;
+        const f32x4 lv = *(const f32x4*)(ls + q0);
+        const f32x4 dlv = *(const f32x4*)(dls + q0);
+        int4 qbv;
+        if (BIAS) qbv = *(const int4*)(kb + q0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int qi = qc + 16 * bi + 4 * g + r;
-          float pr = 0.f, ds = 0.f;
-          if (kv && qi < L) {
-            float x = sa[bi][r] * p.scale;
-            if (p.bias_u) {
-              const int hq = (int)(((float)qi + 0.5f) * p.inv_wg);
-              const int wq = qi - hq * p.Wg;
-              x += ub[(hq - hk + p.Hg - 1) * (2 * p.Wg - 1) + (wq - wk + p.Wg - 1)];
-            }
-            pr = __expf(x - ls[qi]);
-            ds = pr * (da[bi][r] - dls[qi]);
-          }
+          float x = sa[bi][r] * sc2 + kadd;
+          if (BIAS) x += ub[qbv[r] - ck];
+          const float pr = fexp2(x - lv[r]);
+          const float ds = pr * (da[bi][r] - dlv[r]);
           sa[bi][r] = pr;
           da[bi][r] = ds * p.scale;
         }
+      }
       const bf16x8 pa = pack_perm(sa[0], sa[1]);
       const bf16x8 dsa = pack_perm(da[0], da[1]);
 #pragma unroll
@@ -424,10 +463,10 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(AP p) {
         dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsa, trfrag<D>(Qimg, qc, d * 16, lane), dk[d], 0, 0, 0);
       }
     }
-    // C[key][d]: rows = keys kb*16 + 4g + r, col = d*16 + li
+    // C[key][d]: rows = keys kbk*16 + 4g + r, col = d*16 + li
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int kr = kb * 16 + 4 * g + r;
+      const int kr = kbk * 16 + 4 * g + r;
       if (kr >= L) continue;
       const int64_t row = seq_row(p, s, kr);
 #pragma unroll
@@ -458,22 +497,30 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_bias_kernel(AP p, int nfc) {
   char* Kimg = smem;
   char* Vimg = smem + Lp * RS;
   float* ub = (float*)(smem + 2 * Lp * RS);
-  float* bins = ub + p.nbins;
-  float* xch = bins + p.nbins;   // [4 waves][64 lanes][8] dq exchange
-  for (int i = tid; i < p.nbins; i += NT) { ub[i] = p.bias_u[(int64_t)h * p.nbins + i]; bins[i] = 0.f; }
+  const int nb4 = (p.nbins + 3) & ~3;
+  float* bins = ub + nb4;
+  int* kb = (int*)(bins + nb4);
+  float* madd = (float*)(kb + Lp);
+  float* xch = madd + Lp;   // [4 waves][64 lanes][8] dq exchange
+  for (int i = tid; i < p.nbins; i += NT) { ub[i] = p.bias_u[(int64_t)h * p.nbins + i] * LOG2E; bins[i] = 0.f; }
+  for (int i = tid; i < Lp; i += NT) {
+    kb[i] = i < L ? kb_of(p, i) : 0;
+    madd[i] = i < L ? 0.f : -INFINITY;
+  }
   const int g = lane >> 4, li = lane & 15;
   const int q = qg * 64 + qsub * 16 + li;
   const bool qv = q < L;
-  const int hq = (int)(((float)q + 0.5f) * p.inv_wg), wq = q - hq * p.Wg;
+  const float sc2 = p.scale * LOG2E;
   f32x4 acc[MAXCH][2];
 #pragma unroll
   for (int c = 0; c < MAXCH; ++c) { acc[c][0] = f32x4{0.f, 0.f, 0.f, 0.f}; acc[c][1] = f32x4{0.f, 0.f, 0.f, 0.f}; }
   const int f0 = (int)((int64_t)p.nseq * fc / nfc), f1 = (int)((int64_t)p.nseq * (fc + 1) / nfc);
+  __syncthreads();
+  const int cq = kb[min(q, L - 1)] + boff(p);
   for (int s = f0; s < f1; ++s) {
     __syncthreads();   // previous frame's LDS reads done
     stage<D>(Kimg, p.k, p.ldk, p, s, h, Lp, tid, NT);
     stage<D>(Vimg, p.v, p.ldv, p, s, h, Lp, tid, NT);
-    __syncthreads();
     const int64_t qrow = qv ? seq_row(p, s, q) : 0;
     bf16x8 qf, df;
     float dl = 0.f;
@@ -489,8 +536,9 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_bias_kernel(AP p, int nfc) {
     }
     dl += __shfl_xor(dl, 16, 64);
     dl += __shfl_xor(dl, 32, 64);
-    const float lse = qv ? p.lse[(int64_t)h * p.M + qrow] : INFINITY;
+    const float lse2 = qv ? p.lse[(int64_t)h * p.M + qrow] * LOG2E : INFINITY;
     if (qv && g == 0 && khalf == 0) p.delta[(int64_t)h * p.M + qrow] = dl;
+    __syncthreads();
     f32x4 dq[DB];
 #pragma unroll
     for (int d = 0; d < DB; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -508,18 +556,18 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_bias_kernel(AP p, int nfc) {
                                                            f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         }
 #pragma unroll
-        for (int bi = 0; bi < 2; ++bi)
+        for (int bi = 0; bi < 2; ++bi) {
+          const int k0 = kc + 16 * bi + 4 * g;
+          const int4 kbv = *(const int4*)(kb + k0);
+          const f32x4 ma = *(const f32x4*)(madd + k0);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int key = kc + 16 * bi + 4 * g + r;
-            float ds = 0.f;
-            if (qv && key < L) {
-              const float x = sa[bi][r] * p.scale + ub[bin_of(p, hq, wq, key)];
-              ds = __expf(x - lse) * (da[bi][r] - dl);
-            }
+            const float x = sa[bi][r] * sc2 + ma[r] + ub[cq - kbv[r]];
+            const float ds = fexp2(x - lse2) * (da[bi][r] - dl);
             acc[ci][bi][r] += ds;
             sa[bi][r] = ds * p.scale;
           }
+        }
         const bf16x8 dsb = pack_perm(sa[0], sa[1]);
 #pragma unroll
         for (int d = 0; d < DB; ++d)
@@ -558,7 +606,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_bias_kernel(AP p, int nfc) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int key = c * 32 + 16 * bi + 4 * g + r;
-            if (key < L) atomicAdd(&bins[bin_of(p, hq, wq, key)], acc[ci][bi][r]);
+            if (key < L) atomicAdd(&bins[cq - kb[key]], acc[ci][bi][r]);
           }
       }
     }
@@ -572,11 +620,21 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_bias_kernel(AP p, int nfc) {
 
 bool s_attr = false;
 
-template <int D>
+template <int D, bool BIAS>
+void set_attrs_b() {
+  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<D, BIAS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D, BIAS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<D, BIAS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+}
+
 void set_attrs() {
-  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<D>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  set_attrs_b<32, false>();
+  set_attrs_b<32, true>();
+  set_attrs_b<64, false>();
+  set_attrs_b<64, true>();
   (void)hipFuncSetAttribute((const void*)attn_bwd_dq_bias_kernel<9>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024);
 }
@@ -600,10 +658,9 @@ int fill(AP& p, const ctclip_attn_args* a) {
   p.L = a->L; p.H = a->H; p.nseq = a->nseq; p.M = a->M;
   p.Hg = a->grid_h; p.Wg = a->grid_w;
   p.nbins = (2 * a->grid_h - 1) * (2 * a->grid_w - 1);
-  p.inv_wg = a->grid_w > 0 ? 1.f / (float)a->grid_w : 0.f;
   p.n_inner = a->n_inner > 0 ? a->n_inner : 1;
   p.s_outer = a->s_outer; p.s_inner = a->s_inner; p.s_pos = a->s_pos;
-  if (p.bias_u && a->grid_h * a->grid_w != a->L) return CT_ESHAPE;
+  if (p.bias_u && (a->grid_w <= 0 || a->grid_h * a->grid_w != a->L)) return CT_ESHAPE;
   // pairs per workgroup: enough (seq, head) pairs that every wave has query blocks
   const int nqb = (a->L + 15) / 16;
   int pp = NW / std::max(1, std::min(NW, nqb));
@@ -613,21 +670,47 @@ int fill(AP& p, const ctclip_attn_args* a) {
   return 0;
 }
 
+// LDS bytes of the tables after the images: [BIAS: ub + kb] + madd[pp][Lp] (+ bins for dq)
+size_t table_bytes(const AP& p, int Lp, bool bins) {
+  size_t b = (size_t)p.pp * Lp * 4;
+  const size_t nb4 = (size_t)((p.nbins + 3) & ~3);
+  if (p.bias_u) b += nb4 * 4 + (size_t)Lp * 4 + (bins ? nb4 * 4 : 0);
+  return b;
+}
+
+template <int D>
+void launch_fwd(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
+  if (p.bias_u) hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(NT), lds, st, p);
+  else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(NT), lds, st, p);
+}
+
+template <int D>
+void launch_dq(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
+  if (p.bias_u) hipLaunchKernelGGL((attn_bwd_dq_kernel<D, true>), grid, dim3(NT), lds, st, p);
+  else hipLaunchKernelGGL((attn_bwd_dq_kernel<D, false>), grid, dim3(NT), lds, st, p);
+}
+
+template <int D>
+void launch_dkv(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
+  if (p.bias_u) hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, true>), grid, dim3(NT), lds, st, p);
+  else hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, false>), grid, dim3(NT), lds, st, p);
+}
+
 }  // namespace
 
 extern "C" int ctclip_attn_fwd(const ctclip_attn_args* a, void* stream) {
   AP p;
   int rc = fill(p, a);
   if (rc) return rc;
-  if (!s_attr) { set_attrs<32>(); set_attrs<64>(); s_attr = true; }
+  if (!s_attr) { set_attrs(); s_attr = true; }
   const int Lp = (p.L + 31) & ~31;
   const int pairs = p.nseq * p.H;
   const size_t RSb = a->D * 2 + 16;
-  const size_t lds = (size_t)p.pp * 2 * Lp * RSb + (p.bias_u ? p.nbins * 4 : 0);
+  const size_t lds = (size_t)p.pp * 2 * Lp * RSb + table_bytes(p, Lp, false);
   if (lds > 160 * 1024) return CT_ESHAPE;
   dim3 grid(cdiv(pairs, p.pp));
-  if (a->D == 32) hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(NT), lds, (hipStream_t)stream, p);
-  else hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(NT), lds, (hipStream_t)stream, p);
+  if (a->D == 32) launch_fwd<32>(p, grid, lds, (hipStream_t)stream);
+  else launch_fwd<64>(p, grid, lds, (hipStream_t)stream);
   CT_CHECK_LAUNCH();
   return 0;
 }
@@ -636,33 +719,34 @@ extern "C" int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream) {
   AP p;
   int rc = fill(p, a);
   if (rc) return rc;
-  if (!s_attr) { set_attrs<32>(); set_attrs<64>(); s_attr = true; }
+  if (!s_attr) { set_attrs(); s_attr = true; }
   const int Lp = (p.L + 31) & ~31;
   const int pairs = p.nseq * p.H;
   const size_t RSb = a->D * 2 + 16;
-  const size_t lds1 = (size_t)p.pp * 2 * Lp * RSb + (p.bias_u ? 2 * p.nbins * 4 : 0);
-  const size_t lds2 = (size_t)p.pp * (2 * Lp * RSb + 2 * Lp * 4) + (p.bias_u ? p.nbins * 4 : 0);
+  const size_t lds1 = (size_t)p.pp * 2 * Lp * RSb + table_bytes(p, Lp, true);
+  const size_t lds2 = (size_t)p.pp * (2 * Lp * RSb + 2 * Lp * 4) + table_bytes(p, Lp, false);
   if (lds1 > 160 * 1024 || lds2 > 160 * 1024) return CT_ESHAPE;
   dim3 grid(cdiv(pairs, p.pp));
   hipStream_t st = (hipStream_t)stream;
   const int nc = Lp / 32;
-  if (a->D == 32 && p.bias_u && p.dbias_u && (nc + 1) / 2 <= 9) {
+  if (a->D == 32 && p.bias_u && p.dbias_u && !p.kmask && (nc + 1) / 2 <= 9) {
     // frame-inner dQ + bias-gradient kernel (see attn_bwd_dq_bias_kernel)
     const int nqg = cdiv(p.L, 64);
     int nfc = std::max(1, std::min(p.nseq, (2 * 256 + p.H * nqg - 1) / (p.H * nqg)));
-    const size_t lds = (size_t)2 * Lp * RSb + 2 * (size_t)p.nbins * 4 + 4 * 64 * 8 * 4;
+    const size_t lds = (size_t)2 * Lp * RSb + 2 * (size_t)((p.nbins + 3) & ~3) * 4 + 2 * (size_t)Lp * 4 +
+                       4 * 64 * 8 * 4;
     if (lds > 160 * 1024) return CT_ESHAPE;
     hipLaunchKernelGGL(attn_bwd_dq_bias_kernel<9>, dim3(p.H, nqg, nfc), dim3(NT), lds, st, p, nfc);
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<32>, grid, dim3(NT), lds2, st, p);
+    launch_dkv<32>(p, grid, lds2, st);
     CT_CHECK_LAUNCH();
     return 0;
   }
   if (a->D == 32) {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<32>, grid, dim3(NT), lds1, st, p);
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<32>, grid, dim3(NT), lds2, st, p);
+    launch_dq<32>(p, grid, lds1, st);
+    launch_dkv<32>(p, grid, lds2, st);
   } else {
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<64>, grid, dim3(NT), lds1, st, p);
-    hipLaunchKernelGGL(attn_bwd_dkv_kernel<64>, grid, dim3(NT), lds2, st, p);
+    launch_dq<64>(p, grid, lds1, st);
+    launch_dkv<64>(p, grid, lds2, st);
   }
   CT_CHECK_LAUNCH();
   return 0;

@@ -52,6 +52,13 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   r.w = pack2(f[6], f[7]);
   return r;
 }
+__device__ __forceinline__ uint2 pack4(const float* f) { return make_uint2(pack2(f[0], f[1]), pack2(f[2], f[3])); }
+__device__ __forceinline__ void unpack4(const uint2& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16);
+  f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16);
+  f[3] = __uint_as_float(v.y & 0xffff0000u);
+}
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float gelu_erf_grad(float x) {

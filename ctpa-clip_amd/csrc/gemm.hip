@@ -371,7 +371,8 @@ extern "C" int ctclip_gemm(const ctclip_gemm_args* a, void* stream) {
   {
     const int b = a->batch > 0 ? a->batch : 1;
     const int64_t tiles256 = ((a->M + 255) / 256) * ((a->N + 255) / 256) * split * b;
-    if (a->K % 64 == 0 && a->M >= 256 && a->N >= 256 && tiles256 >= 160 && (a->K / split) >= 64)
+    if (a->K % 64 == 0 && a->M >= 256 && a->N >= 256 && tiles256 >= 160 && (a->K / split) >= 64 &&
+        (!a->bias || aligned16(a->bias)))
       return ctclip_gemm256(a, split, b, stream);
   }
   if (!s_smem_set) {

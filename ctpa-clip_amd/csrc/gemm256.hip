@@ -41,6 +41,8 @@ struct P {
   float alpha; int act; int accumulate; int split_k;
   int64_t sA, sB, sC, sC2, sR;
   int64_t kper;
+  int debug;     // diagnostic knob (CTCLIP_G256_DEBUG): 1 = skip the epilogue, 2 = skip the main loop
+  int stagger;   // start delay (s_sleep units of 64 cycles) for the second co-resident workgroup
 };
 
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
@@ -135,7 +137,15 @@ __global__ __launch_bounds__(Cfg<WR>::NTH, 2 / WR) void gemm256_kernel(P p) {
   // kt leaves the younger tiles' loads outstanding (counted vmcnt, never 0 in steady state) and
   // a raw s_barrier publishes the landed tile (a __syncthreads fence would drain every glds).
   // The slot refilled at step kt held tile kt - 1, which every wave finished before the barrier.
-  const int nk = kend > kbeg ? (int)((kend - kbeg) / BK) : 0;
+  const int nk = (kend > kbeg && !(p.debug & 2)) ? (int)((kend - kbeg) / BK) : 0;
+  // the first dispatch round holds two workgroups per CU (WR = 1); delaying the second one
+  // offsets their store-heavy epilogues against each other's MFMA main loops
+  if (p.stagger > 0) {
+    const int lin = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const int ncu = 256;
+    if (lin >= ncu && lin < 2 * ncu)
+      for (int s = 0; s < p.stagger; s += 64) __builtin_amdgcn_s_sleep(64);
+  }
   auto stage = [&](int t) {
     char* st = smem + (t % NSTAGE) * STAGE;
     const int64_t k1 = kbeg + (int64_t)t * BK;
@@ -172,6 +182,13 @@ __global__ __launch_bounds__(Cfg<WR>::NTH, 2 / WR) void gemm256_kernel(P p) {
     __builtin_amdgcn_s_setprio(0);
   }
   __syncthreads();   // every wave's last fragment reads done before the epilogue reuses LDS
+  if (p.debug & 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
 
   // ---------------- epilogue: per-wave private staging, four 32-row quarters
   float* cs = (float*)(smem + w * (32 * EP_LD * 4));   // 8.7 KB per wave, 8 waves = 70 KB
@@ -350,6 +367,15 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   p.sA = a->sA; p.sB = a->sB; p.sC = a->sC; p.sC2 = a->sC2; p.sR = a->sR;
   int64_t kper = (a->K / BK + split - 1) / split * BK;
   p.kper = kper;
+  static int dbg = -1, stag = 0;
+  if (dbg < 0) {
+    const char* e = getenv("CTCLIP_G256_DEBUG");
+    dbg = e ? atoi(e) : 0;
+    const char* s = getenv("CTCLIP_G256_STAGGER");
+    stag = s ? atoi(s) : 0;
+  }
+  p.debug = dbg;
+  p.stagger = tile_rows() == 1 ? stag : 0;
   hipStream_t st = (hipStream_t)stream;
   if (tile_rows() == 2) return launch_any<2>(p, a->a_kcontig, a->b_kcontig, batch, st);
   return launch_any<1>(p, a->a_kcontig, a->b_kcontig, batch, st);
