@@ -111,86 +111,11 @@ __device__ __forceinline__ void xcd_remap(int& tx, int& ty) {
   tx = id - ty * gx;
 }
 
-template <int WR, bool AK, bool BKC>
-__global__ __launch_bounds__(Cfg<WR>::NTH, 2 / WR) void gemm256_kernel(P p) {
-  using C = Cfg<WR>;
-  constexpr int NSTAGE = C::NSTAGE, STAGE = C::STAGE, G = C::G;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
-  int tx, ty;
-  xcd_remap(tx, ty);
-  const int split = blockIdx.z % p.split_k, bidx = blockIdx.z / p.split_k;
-  const int64_t m0 = (int64_t)ty * C::BM, n0 = (int64_t)tx * BN;
-  const int64_t kbeg = split * p.kper;
-  const int64_t kend = min(p.K, kbeg + p.kper);
-  const u16* A = p.A + bidx * p.sA;
-  const u16* B = p.B + bidx * p.sB;
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // NSTAGE-slot ring of 32-deep K tiles: tile kt lives in slot kt % NSTAGE; NSTAGE - 1 tiles
-  // are in flight while one is computed.  Each tile is G glds per thread; the wait before step
-  // kt leaves the younger tiles' loads outstanding (counted vmcnt, never 0 in steady state) and
-  // a raw s_barrier publishes the landed tile (a __syncthreads fence would drain every glds).
-  // The slot refilled at step kt held tile kt - 1, which every wave finished before the barrier.
-  const int nk = (kend > kbeg && !(p.debug & 2)) ? (int)((kend - kbeg) / BK) : 0;
-  // the first dispatch round holds two workgroups per CU (WR = 1); delaying the second one
-  // offsets their store-heavy epilogues against each other's MFMA main loops
-  if (p.stagger > 0) {
-    const int lin = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-    const int ncu = 256;
-    if (lin >= ncu && lin < 2 * ncu)
-      for (int s = 0; s < p.stagger; s += 64) __builtin_amdgcn_s_sleep(64);
-  }
-  auto stage = [&](int t) {
-    char* st = smem + (t % NSTAGE) * STAGE;
-    const int64_t k1 = kbeg + (int64_t)t * BK;
-    stage_tile<AK, C::BM, C::GA>(st, A, p.lda, p.M, m0, k1, w, lane);
-    stage_tile<BKC, BN, C::GB>(st + C::ABYTES, B, p.ldb, p.N, n0, k1, w, lane);
-  };
-  for (int t = 0; t < NSTAGE - 1 && t < nk; ++t) stage(t);
-  for (int kt = 0; kt < nk; ++kt) {
-    if constexpr (NSTAGE == 4) {
-      if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
-      else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (kt + NSTAGE - 1 < nk) stage(kt + NSTAGE - 1);
-    const char* As = smem + (kt % NSTAGE) * STAGE;
-    const char* Bs = As + C::ABYTES;
-    bf16x8 bfr[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC, BN>(Bs, wc * 64 + j * 16, lane);
-    bf16x8 af[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) af[i] = frag<AK, C::BM>(As, wr * 128 + i * 16, lane);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  }
-  __syncthreads();   // every wave's last fragment reads done before the epilogue reuses LDS
-  if (p.debug & 1) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
-    return;
-  }
-
-  // ---------------- epilogue: per-wave private staging, four 32-row quarters
+// Shared epilogue: wave (wr, wc) owns output rows m0 + wr*128 + [0,128), cols n0 + wc*64 + [0,64);
+// acc[i][j] is the 16x16 block (i, j) of that region in the MFMA 16x16 C layout.  Stages each
+// 32-row quarter through a wave-private LDS region (8.7 KB per wave) and writes 16-B row chunks.
+__device__ __forceinline__ void epilogue(const P& p, f32x4 (&acc)[8][4], char* smem, int w, int wr, int wc, int lane,
+                                         int64_t m0, int64_t n0, int split, int bidx) {
   float* cs = (float*)(smem + w * (32 * EP_LD * 4));   // 8.7 KB per wave, 8 waves = 70 KB
   const int64_t wrow0 = m0 + wr * 128, wcol0 = n0 + wc * 64;
   const bool slab = p.split_k > 1;
@@ -318,6 +243,501 @@ __global__ __launch_bounds__(Cfg<WR>::NTH, 2 / WR) void gemm256_kernel(P p) {
 }
 
 template <int WR, bool AK, bool BKC>
+__global__ __launch_bounds__(Cfg<WR>::NTH, 2 / WR) void gemm256_kernel(P p) {
+  using C = Cfg<WR>;
+  constexpr int NSTAGE = C::NSTAGE, STAGE = C::STAGE, G = C::G;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
+  int tx, ty;
+  xcd_remap(tx, ty);
+  const int split = blockIdx.z % p.split_k, bidx = blockIdx.z / p.split_k;
+  const int64_t m0 = (int64_t)ty * C::BM, n0 = (int64_t)tx * BN;
+  const int64_t kbeg = split * p.kper;
+  const int64_t kend = min(p.K, kbeg + p.kper);
+  const u16* A = p.A + bidx * p.sA;
+  const u16* B = p.B + bidx * p.sB;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // NSTAGE-slot ring of 32-deep K tiles: tile kt lives in slot kt % NSTAGE; NSTAGE - 1 tiles
+  // are in flight while one is computed.  Each tile is G glds per thread; the wait before step
+  // kt leaves the younger tiles' loads outstanding (counted vmcnt, never 0 in steady state) and
+  // a raw s_barrier publishes the landed tile (a __syncthreads fence would drain every glds).
+  // The slot refilled at step kt held tile kt - 1, which every wave finished before the barrier.
+  const int nk = (kend > kbeg && !(p.debug & 2)) ? (int)((kend - kbeg) / BK) : 0;
+  // the first dispatch round holds two workgroups per CU (WR = 1); delaying the second one
+  // offsets their store-heavy epilogues against each other's MFMA main loops
+  if (p.stagger > 0) {
+    const int lin = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    const int ncu = 256;
+    if (lin >= ncu && lin < 2 * ncu)
+      for (int s = 0; s < p.stagger; s += 64) __builtin_amdgcn_s_sleep(64);
+  }
+  auto stage = [&](int t) {
+    char* st = smem + (t % NSTAGE) * STAGE;
+    const int64_t k1 = kbeg + (int64_t)t * BK;
+    stage_tile<AK, C::BM, C::GA>(st, A, p.lda, p.M, m0, k1, w, lane);
+    stage_tile<BKC, BN, C::GB>(st + C::ABYTES, B, p.ldb, p.N, n0, k1, w, lane);
+  };
+  for (int t = 0; t < NSTAGE - 1 && t < nk; ++t) stage(t);
+  for (int kt = 0; kt < nk; ++kt) {
+    if constexpr (NSTAGE == 4) {
+      if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
+      else if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + NSTAGE - 1 < nk) stage(kt + NSTAGE - 1);
+    const char* As = smem + (kt % NSTAGE) * STAGE;
+    const char* Bs = As + C::ABYTES;
+    bf16x8 bfr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC, BN>(Bs, wc * 64 + j * 16, lane);
+    bf16x8 af[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = frag<AK, C::BM>(As, wr * 128 + i * 16, lane);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  __syncthreads();   // every wave's last fragment reads done before the epilogue reuses LDS
+  if (p.debug & 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+
+  epilogue(p, acc, smem, w, wr, wc, lane, m0, n0, split, bidx);
+}
+
+
+// ============================================================================================
+// 8-phase 256 x 256 x 64 kernel (1 workgroup per CU, 8 waves as 2 (M) x 4 (N), wave tile
+// 128 x 64 = four 64 x 32 quadrants).  Each K-tile is computed in 4 PHASES, one quadrant per
+// phase (16 MFMAs per wave); a phase is [load segment: fragment ds_reads + one half-tile of
+// glds] s_barrier [compute segment: 16 MFMAs] s_barrier.  Waves 4-7 run one barrier behind
+// waves 0-3, so on every SIMD one wave's MFMA segment overlaps its partner's load segment.
+//
+// LDS: two 64 KB buffers (even / odd K-tiles), each = four 16 KB half-tiles A0 A1 B0 B1.
+// A half h holds the block rows {h*64 + [0,64)} u {128 + h*64 + [0,64)} (quadrant row h of
+// both wave rows); B half h the block cols {wc*64 + h*32 + [0,32)} for wc = 0..3.  Quadrant
+// order per tile: (m0,n0) reads A0+B0, (m0,n1) reads B1, (m1,n1) reads A1, (m1,n0) reads none
+// (B0 frags kept in registers), so each half's last read is at a known phase.
+// Restage schedule (phase p of the 8-phase iteration i, tiles 2i in E, 2i+1 in O):
+//   p0 B1->O(2i+1)  p1 A1->O(2i+1)  p2 A0->E(2i+2)  p3 B0->E(2i+2) + wait O complete
+//   p4 B1->E(2i+2)  p5 A1->E(2i+2)  p6 A0->O(2i+3)  p7 B0->O(2i+3) + wait E complete
+// Every restage is >= 2 phases after the last read of that half (WAR safe under the one-
+// barrier stagger); every wait retires a buffer one phase before its first read (RAW), with
+// two younger half-tiles (4 glds) left in flight: s_waitcnt vmcnt(4), never 0 in the loop.
+// ============================================================================================
+namespace p8 {
+constexpr int BM = 256, BNN = 256, BKK = 64, NTH = 512;
+constexpr int HALF = 128 * 64 * 2;   // 16 KB
+constexpr int TILEB = 4 * HALF;      // 64 KB per buffer
+constexpr int SMEM = 2 * TILEB;      // 128 KB
+enum { A0 = 0, A1 = 1, B0 = 2, B1 = 3 };
+
+__device__ __forceinline__ int kswz(int row) { return (row >> 1) & 7; }
+
+// block-local row of half-local row j: A halves interleave 64-row groups, B halves 32-col groups
+template <bool ISA>
+__device__ __forceinline__ int half_row(int j, int h) {
+  if constexpr (ISA) return (j >> 6) * 128 + h * 64 + (j & 63);
+  else return (j >> 5) * 64 + h * 32 + (j & 31);
+}
+
+// this thread's 2 glds of one 128-row x 64-k half-tile
+template <bool KC, bool ISA>
+__device__ __forceinline__ void stage_half(char* dst, const u16* base, int64_t ld, int64_t rows, int64_t row0,
+                                           int64_t k0, int h, int w, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int c = (w * 2 + j) * 64 + lane;
+    const u16* src;
+    if constexpr (KC) {
+      const int r = c >> 3, pc = c & 7, lc = pc ^ kswz(r);
+      const int64_t gr = min(row0 + half_row<ISA>(r, h), rows - 1);
+      src = base + gr * ld + k0 + lc * 8;
+    } else {
+      const int kk = c >> 4, pc = c & 15, pb = pc >> 1, hf = pc & 1;
+      const int lb = pb ^ mn_swz(kk);
+      const int64_t gm = min(row0 + half_row<ISA>(lb * 16 + hf * 8, h), rows - 8);
+      src = base + (k0 + kk) * ld + gm;
+    }
+    __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(dst + (w * 2 + j) * 1024), 16, 0, 0);
+  }
+}
+
+// A-operand-layout fragment (16 rows x 32 k) of half-local rows r0 + blk*16 + [0,16), k-substep s.
+// K-contiguous image [128 rows][64 k]: ds_read_b128 at row r, 16-B chunk (s*4 + lane/16) ^ kswz(r);
+// the swizzle depends only on lane bits, so blocks are plain immediate offsets (blk * 2 KB).
+// MN-contiguous image [64 k][128 rows] via ds_read_b64_tr_b16: the per-lane byte offset of block 0
+// is mn_base(); block blk flips bits 5-6 (32-B block index ^ blk, legal because r0 / 16 has its
+// low bits clear), the k-substep adds 8 KB and the second k-quad adds 1 KB.
+template <bool KC>
+__device__ __forceinline__ int frag_base(int r0, int lane) {
+  if constexpr (KC) {
+    const int r = r0 + (lane & 15);
+    return r * 128 + (((lane >> 4) ^ kswz(r)) << 4);
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+    const int k1 = 8 * g + q;
+    return k1 * 256 + (((r0 >> 4) ^ mn_swz(k1)) << 5) + pp * 8;
+  }
+}
+template <bool KC>
+__device__ __forceinline__ bf16x8 hfrag(const char* half, int base, int blk, int s) {
+  if constexpr (KC) {
+    // chunk s*4 + c ^ sw = (c ^ sw) ^ (s*4): the k-substep flips bit 6 of the byte offset
+    return *(const bf16x8*)(half + ((base + blk * 2048) ^ (s << 6)));
+  } else {
+    const char* p0 = half + (base ^ (blk << 5)) + s * 8192;
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, p0));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, p0 + 1024));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
+__device__ __forceinline__ void bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+}  // namespace p8
+
+// Epilogue for the TRANSPOSED accumulator layout of gemm8p (MFMA operands swapped, so block
+// (i, j) holds D^T): lane l owns output row m = l & 15 of 16-row block i and the 4 consecutive
+// columns 16 j + 4 g + [0, 4) (g = l >> 4).  No LDS staging: f32 outputs are 16-B stores per
+// block; bf16 outputs pair blocks (j, j+1) with v_permlane16_swap so every lane stores 16
+// contiguous bytes (lanes g = 0,1,2,3 -> columns 16j, 16j+16, 16j+8, 16j+24 of the pair).
+__device__ __forceinline__ uint2 pk4(const float* v) { return make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3])); }
+
+// one permlane16 pair: lanes g=0..3 end with 16 contiguous bytes at column offset pair_coff(g)
+__device__ __forceinline__ u32x4 pair_swap(const float* x4, const float* y4) {
+  const uint2 x = pk4(x4), y = pk4(y4);
+  const auto r0 = __builtin_amdgcn_permlane16_swap(x.x, y.x, false, false);
+  const auto r1 = __builtin_amdgcn_permlane16_swap(x.y, y.y, false, false);
+  return make_uint4(r0[0], r1[0], r0[1], r1[1]);
+}
+__device__ __forceinline__ int pair_coff(int g) { return ((g & 1) ? 16 : 0) + ((g & 2) ? 8 : 0); }
+
+// store one row's 4 j-blocks x 4 cols as bf16; rowp = row base at the wave's first column c0
+__device__ __forceinline__ void store_row_bf16(u16* rowp, const float (&v)[4][4], int g, bool ok, int64_t c0,
+                                               int64_t N) {
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp) {
+    const u32x4 d = pair_swap(v[2 * jp], v[2 * jp + 1]);
+    const int coff = 32 * jp + pair_coff(g);
+    if (ok && c0 + coff < N) *(u32x4*)(rowp + coff) = d;
+  }
+}
+
+__device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int wr, int wc, int lane, int64_t m0,
+                                           int64_t n0, int split, int bidx) {
+  const int m = lane & 15, g = lane >> 4;
+  const int64_t wrow0 = m0 + wr * 128, wcol0 = n0 + wc * 64;
+  const int64_t cl = wcol0 + 4 * g;          // this lane's column in block j: cl + 16 j
+  float bias[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (p.bias && p.split_k <= 1 && p.act != 3 && cl + 16 * j < p.N) b = *(const f32x4*)(p.bias + cl + 16 * j);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[j][r] = b[r];
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int64_t gm = wrow0 + i * 16 + m;
+    const bool rok = gm < p.M;
+    float v[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[j][r] = acc[i][j][r] * p.alpha;
+    if (p.act == 3) {
+      // argmax over the wave's 64 columns of row gm (first-max tie-break): 16 values per lane,
+      // then across the 4 lanes g = 0..3 that hold the same row
+      float best = -INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = 16 * j + 4 * g + r;
+          if (wcol0 + c < p.N && (v[j][r] > best || (v[j][r] == best && c < bi))) { best = v[j][r]; bi = c; }
+        }
+#pragma unroll
+      for (int o = 16; o <= 32; o <<= 1) {
+        const float ob = __shfl_xor(best, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+      }
+      if (g == 0 && rok && wcol0 < p.N) {
+        float2* out = (float2*)p.C + bidx * p.sC;
+        out[gm * p.ldc + (wcol0 >> 6)] = make_float2(best, __int_as_float((int)(wcol0 + bi)));
+      }
+      continue;
+    }
+    if (p.split_k > 1) {
+      float* Cf = (float*)p.C + (int64_t)split * p.M * p.ldc + bidx * p.sC + gm * p.ldc + cl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (rok && cl + 16 * j < p.N) *(f32x4*)(Cf + 16 * j) = f32x4{v[j][0], v[j][1], v[j][2], v[j][3]};
+      continue;
+    }
+    if (p.act == 2) {
+      // GEGLU in 32-column pairs: blocks 0,1 = x, blocks 2,3 = gate; h keeps both halves
+      store_row_bf16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N);
+      float gg[2][4];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float xb = bf2f(f2bf(v[j][r])), gb = bf2f(f2bf(v[j + 2][r]));
+          gg[j][r] = gelu_erf(gb) * xb;
+        }
+      const u32x4 d = pair_swap(gg[0], gg[1]);
+      if (rok && wcol0 < p.N) *(u32x4*)(p.C2 + bidx * p.sC2 + gm * p.ldc2 + (wcol0 >> 1) + pair_coff(g)) = d;
+      continue;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[j][r] += bias[j][r];
+    if (p.R) {
+      if (p.r_f32) {
+        const float* Rp = (const float*)p.R + bidx * p.sR + gm * p.ldr + cl;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (rok && cl + 16 * j < p.N) {
+            const f32x4 a = *(const f32x4*)(Rp + 16 * j);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[j][r] += a[r];
+          }
+      } else {
+        const u16* Rp = (const u16*)p.R + bidx * p.sR + gm * p.ldr + cl;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (rok && cl + 16 * j < p.N) {
+            float rr[4];
+            unpack4(*(const uint2*)(Rp + 16 * j), rr);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[j][r] += rr[r];
+          }
+      }
+    }
+    if (p.act == 1) {
+      if (p.C2) store_row_bf16(p.C2 + bidx * p.sC2 + gm * p.ldc2 + wcol0, v, g, rok, wcol0, p.N);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[j][r] = gelu_erf(v[j][r]);
+    }
+    if (p.c_f32) {
+      float* Cf = (float*)p.C + bidx * p.sC + gm * p.ldc + cl;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (rok && cl + 16 * j < p.N) {
+          if (p.accumulate) {
+            const f32x4 a = *(const f32x4*)(Cf + 16 * j);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[j][r] += a[r];
+          }
+          *(f32x4*)(Cf + 16 * j) = f32x4{v[j][0], v[j][1], v[j][2], v[j][3]};
+        }
+    } else {
+      u16* Cb = (u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0;
+      if (p.accumulate) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (rok && cl + 16 * j < p.N) {
+            float rr[4];
+            unpack4(*(const uint2*)(Cb + 16 * j + 4 * g), rr);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[j][r] += rr[r];
+          }
+      }
+      store_row_bf16(Cb, v, g, rok, wcol0, p.N);
+    }
+    if (p.C2 && p.act == 0) store_row_bf16(p.C2 + bidx * p.sC2 + gm * p.ldc2 + wcol0, v, g, rok, wcol0, p.N);
+  }
+}
+
+// TR = true: MFMA operands swapped (transposed accumulator) + the LDS-free epilogue_t, used for
+// bf16 outputs; TR = false: the LDS-staged row-chunk epilogue, used for f32 / residual / argmax
+// outputs (measured faster there: full-row f32 chunks, one argmax pass per staged quarter).
+template <bool AK, bool BKC, bool TR>
+__global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
+  using namespace p8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
+  int tx, ty;
+  xcd_remap(tx, ty);
+  const int split = blockIdx.z % p.split_k, bidx = blockIdx.z / p.split_k;
+  const int64_t m0 = (int64_t)ty * BM, n0 = (int64_t)tx * BNN;
+  const int64_t kbeg = split * p.kper;
+  const int64_t kend = min(p.K, kbeg + p.kper);
+  const u16* A = p.A + bidx * p.sA;
+  const u16* B = p.B + bidx * p.sB;
+  const int nk = (kend > kbeg && !(p.debug & 2)) ? (int)((kend - kbeg) / BKK) : 0;
+  // desynchronise the CUs: half of the first dispatch round (every other workgroup within each
+  // XCD) starts p.stagger x ~2k cycles late, so later rounds' store-heavy epilogues on those CUs
+  // fall under the other half's MFMA main loops instead of all CUs storing at once
+  if (p.stagger > 0) {
+    const int lin = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    if (lin < 256 && ((lin >> 3) & 1))
+      for (int s = 0; s < p.stagger; ++s) __builtin_amdgcn_s_sleep(32);
+  }
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int which, int t) {
+    if (t >= nk) return;
+    char* dst = smem + (t & 1) * TILEB + which * HALF;
+    const int64_t k0 = kbeg + (int64_t)t * BKK;
+    if (which < 2) stage_half<AK, true>(dst, A, p.lda, p.M, m0, k0, which, w, lane);
+    else stage_half<BKC, false>(dst, B, p.ldb, p.N, n0, k0, which - 2, w, lane);
+  };
+
+  bf16x8 a[4][2], b0[2][2], b1[2][2];
+
+  const int abase = frag_base<AK>(wr * 64, lane), bbase = frag_base<BKC>(wc * 32, lane);
+  // load segment of quadrant q of the tile in buffer `buf`
+  auto load_frags = [&](int buf, int q) {
+    const char* base = smem + buf * TILEB;
+    if (q == 0 || q == 2) {
+      const char* ah = base + (q == 0 ? A0 : A1) * HALF;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) a[ii][s] = hfrag<AK>(ah, abase, ii, s);
+    }
+    if (q == 0) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) b0[jj][s] = hfrag<BKC>(base + B0 * HALF, bbase, jj, s);
+    }
+    if (q == 1) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) b1[jj][s] = hfrag<BKC>(base + B1 * HALF, bbase, jj, s);
+    }
+  };
+  // compute segment: quadrant q = (mi, ni) in order (0,0) (0,1) (1,1) (1,0)
+  auto mma = [&](int q) {
+    const int mi = (q == 0 || q == 1) ? 0 : 1;
+    const int ni = (q == 1 || q == 2) ? 1 : 0;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const bf16x8 bb = ni ? b1[jj][s] : b0[jj][s];
+          acc[mi * 4 + ii][ni * 2 + jj] =
+              TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb, a[ii][s], acc[mi * 4 + ii][ni * 2 + jj], 0, 0, 0)
+                 : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ii][s], bb, acc[mi * 4 + ii][ni * 2 + jj], 0, 0, 0);
+        }
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto wait_ahead = [&](bool younger_issued) {
+    if (younger_issued) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  auto compute_phase = [&]() {
+    bar();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: tile 0 complete in E, tile 1's A0/B0 halves in flight
+  if (nk > 0) {
+    stage(A0, 0); stage(A1, 0); stage(B0, 0); stage(B1, 0);
+    stage(A0, 1); stage(B0, 1);
+    wait_ahead(nk > 1);
+  }
+  bar();
+  if (wr == 1) bar();   // the stagger: waves 4-7 run one barrier behind
+
+  for (int i = 0; 2 * i < nk; ++i) {
+    const int te = 2 * i, to = 2 * i + 1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      load_frags(0, q);
+      if (q == 0) stage(B1, to);
+      if (q == 1) stage(A1, to);
+      if (q == 2) stage(A0, te + 2);
+      if (q == 3) { stage(B0, te + 2); if (to < nk) wait_ahead(te + 2 < nk); }
+      compute_phase();
+      mma(q);
+      bar();
+    }
+    if (to < nk) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        load_frags(1, q);
+        if (q == 0) stage(B1, te + 2);
+        if (q == 1) stage(A1, te + 2);
+        if (q == 2) stage(A0, to + 2);
+        if (q == 3) { stage(B0, to + 2); if (te + 2 < nk) wait_ahead(to + 2 < nk); }
+        compute_phase();
+        mma(q);
+        bar();
+      }
+    }
+  }
+  if (wr == 0) bar();   // balance the stagger barrier
+  __syncthreads();      // every wave's last fragment reads done before the epilogue reuses LDS
+  if (p.debug & 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+  if constexpr (TR) epilogue_t(p, acc, wr, wc, lane, m0, n0, split, bidx);
+  else epilogue(p, acc, smem, w, wr, wc, lane, m0, n0, split, bidx);
+}
+
+template <bool AK, bool BKC, bool TR>
+int launch8(const P& p, int batch, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<AK, BKC, TR>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              p8::SMEM);
+    attr = true;
+  }
+  dim3 grid(cdiv(p.N, p8::BNN), cdiv(p.M, p8::BM), batch * p.split_k);
+  hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, TR>), grid, dim3(p8::NTH), p8::SMEM, st, p);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int WR, bool AK, bool BKC>
 int launch(const P& p, int batch, hipStream_t st) {
   using C = Cfg<WR>;
   static bool attr = false;
@@ -340,14 +760,25 @@ int launch_any(const P& p, bool ak, bool bk, int batch, hipStream_t st) {
   return launch<WR, false, false>(p, batch, st);
 }
 
-// tile shape: CTCLIP_G256_WR=2 forces the 256 x 256 form, =1 the 128 x 256 form
-int tile_rows() {
-  static int wr = -1;
-  if (wr < 0) {
-    const char* e = getenv("CTCLIP_G256_WR");
-    wr = (e && atoi(e) == 2) ? 2 : 1;
+// kernel variant: 8 = 8-phase 256 x 256 x 64 (default), 1 = 128 x 256 x 32 (2 WG/CU),
+// 2 = 256 x 256 x 32 4-slot ring.  CTCLIP_GEMM_VARIANT or ctclip_gemm_set_variant() select it.
+static int g_variant = -1;
+static int g_stagger8 = -1;   // 8-phase start stagger (units of s_sleep(32)); -1 = default
+int variant() {
+  if (g_variant < 0) {
+    const char* e = getenv("CTCLIP_GEMM_VARIANT");
+    g_variant = e ? atoi(e) : 8;
+    if (g_variant != 1 && g_variant != 2) g_variant = 8;
   }
-  return wr;
+  return g_variant;
+}
+int tile_rows() { return variant() == 2 ? 2 : 1; }
+
+template <bool AK>
+int launch8_any(const P& p, bool bk, int batch, hipStream_t st) {
+  const bool tr = !p.c_f32 && p.split_k <= 1 && p.act != 3 && !p.R;
+  if (tr) return bk ? launch8<AK, true, true>(p, batch, st) : launch8<AK, false, true>(p, batch, st);
+  return bk ? launch8<AK, true, false>(p, batch, st) : launch8<AK, false, false>(p, batch, st);
 }
 
 }  // namespace g256
@@ -365,8 +796,8 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   p.R = a->R; p.ldr = a->ldr; p.r_f32 = a->r_f32;
   p.alpha = a->alpha; p.act = a->act; p.accumulate = a->accumulate; p.split_k = split;
   p.sA = a->sA; p.sB = a->sB; p.sC = a->sC; p.sC2 = a->sC2; p.sR = a->sR;
-  int64_t kper = (a->K / BK + split - 1) / split * BK;
-  p.kper = kper;
+  const int kstep = variant() == 8 ? p8::BKK : BK;
+  p.kper = (a->K / kstep + split - 1) / split * kstep;
   static int dbg = -1, stag = 0;
   if (dbg < 0) {
     const char* e = getenv("CTCLIP_G256_DEBUG");
@@ -375,8 +806,27 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
     stag = s ? atoi(s) : 0;
   }
   p.debug = dbg;
-  p.stagger = tile_rows() == 1 ? stag : 0;
+  // 8-phase default: stagger only the GEGLU GEMM, whose epilogue (h + g stores + erf) is long
+  // enough that desynchronised CUs pay off (r01 sweep: 0.52 -> 0.48 ms at B = 8; neutral to
+  // slightly negative on the plain / residual epilogues)
+  p.stagger = variant() == 8 ? (g_stagger8 >= 0 ? g_stagger8 : (a->act == 2 ? 4 : 0)) : (tile_rows() == 1 ? stag : 0);
   hipStream_t st = (hipStream_t)stream;
+  if (variant() == 8)
+    return a->a_kcontig ? launch8_any<true>(p, a->b_kcontig, batch, st) : launch8_any<false>(p, a->b_kcontig, batch, st);
   if (tile_rows() == 2) return launch_any<2>(p, a->a_kcontig, a->b_kcontig, batch, st);
   return launch_any<1>(p, a->a_kcontig, a->b_kcontig, batch, st);
+}
+
+// diagnostic: 8-phase kernel start stagger (see gemm8p_kernel); returns the previous value
+extern "C" int ctclip_gemm_set_stagger(int v) {
+  const int old = g256::g_stagger8;
+  g256::g_stagger8 = v;
+  return old;
+}
+
+// diagnostic: select the large-tile kernel variant at run time (returns the previous one)
+extern "C" int ctclip_gemm_set_variant(int v) {
+  const int old = g256::variant();
+  if (v == 1 || v == 2 || v == 8) g256::g_variant = v;
+  return old;
 }

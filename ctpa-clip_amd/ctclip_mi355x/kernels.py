@@ -126,10 +126,11 @@ def matmul_tn(dy, x, *, out=None, accumulate=False, split_k=None, alpha=1.0):
             torch.empty(N, K, device=dy.device, dtype=F32)
     if split_k is not None:
         s = split_k
-    elif False and N >= 256 and K >= 256 and M % 64 == 0:   # 256-tile TN measured slower (r01)
-        # 256x256-tile kernel: ~320 workgroups, >= 8 K-steps of 64 per split
+    elif N >= 256 and K >= 256 and M % 64 == 0 and M >= 64 * 1024:
+        # 8-phase 256x256x64 kernel (gemm256.hip): one wave of <= 256 workgroups (one per CU),
+        # each reducing a long K-chunk; the slabs are summed by reduce_slabs
         t256 = ((N + 255) // 256) * ((K + 255) // 256)
-        s = max(1, min((320 + t256 - 1) // t256, M // 512))
+        s = max(1, 256 // t256)
         if t256 * s < 160:
             s = split_for(M, ((N + 127) // 128) * ((K + 127) // 128))
     else:

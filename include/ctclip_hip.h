@@ -55,6 +55,11 @@ typedef struct {
   int64_t sA, sB, sC, sC2, sR;      /* batch strides in elements */
 } ctclip_gemm_args;
 int ctclip_gemm(const ctclip_gemm_args* a, void* stream);
+/* diagnostic: large-tile kernel variant (8 = 8-phase 256x256x64 default, 1 = 128x256x32,
+ * 2 = 256x256x32); returns the previous one.  Every variant computes bit-identical results. */
+int ctclip_gemm_set_variant(int variant);
+/* diagnostic: start stagger of the 8-phase kernel (units of ~2k cycles); returns the previous */
+int ctclip_gemm_set_stagger(int units);
 
 /* sum f32 slabs [s][rows][ld] -> out (f32 or bf16), optional accumulate into f32 out */
 int ctclip_reduce_slabs(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,

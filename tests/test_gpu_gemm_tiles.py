@@ -1,0 +1,142 @@
+"""Large-tile MFMA GEMM paths (gemm256.hip) at shapes that dispatch to them (>= 160 tiles of
+256 x 256): every layout and fused epilogue vs a plain torch fp32 reference, and the 8-phase
+256x256x64 kernel bit-identical to the 128x256x32 kernel (same MFMA k-order per accumulator)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def K():
+    from ctclip_mi355x import kernels
+    return kernels
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+
+
+def _variants(K, fn):
+    from ctclip_mi355x import _lib
+    outs = {}
+    prev = _lib.lib().ctclip_gemm_set_variant(8)
+    try:
+        for v in (8, 1):
+            _lib.lib().ctclip_gemm_set_variant(v)
+            outs[v] = fn()
+            torch.cuda.synchronize()
+    finally:
+        _lib.lib().ctclip_gemm_set_variant(prev)
+    return outs
+
+
+def _raw(K, M, N, Kd, A, lda, ak, B, ldb, bk, C, ldc, **kw):
+    K._gemm_raw(M, N, Kd, A, lda, ak, B, ldb, bk, C, ldc, **kw)
+    return C
+
+
+@pytest.mark.parametrize('M,N,Kd', [(4000, 2816, 512), (8192, 1536, 1408), (5000, 2048, 192)])
+def test_nt_bias_residual(K, M, N, Kd):
+    torch.manual_seed(0)
+    x = torch.randn(M, Kd, device='cuda').bfloat16()
+    w = torch.randn(N, Kd, device='cuda').bfloat16()
+    b = torch.randn(N, device='cuda')
+    r = torch.randn(M, N, device='cuda')
+    outs = _variants(K, lambda: K.linear(x, w, bias=b, residual=r, out_dtype=torch.float32))
+    ref = x.float() @ w.float().t() + b + r
+    assert _rel(outs[8], ref) < 1e-5
+    assert torch.equal(outs[8], outs[1])
+
+
+@pytest.mark.parametrize('ak,bk', [(True, False), (False, True), (False, False)])
+def test_layouts(K, ak, bk):
+    torch.manual_seed(1)
+    M, N, Kd = 3000, 3328, 704
+    A = torch.randn(M, Kd, device='cuda').bfloat16()
+    B = torch.randn(N, Kd, device='cuda').bfloat16()
+    Am = A if ak else A.t().contiguous()
+    Bm = B if bk else B.t().contiguous()
+
+    def run():
+        C = torch.empty(M, N, device='cuda', dtype=torch.float32)
+        return _raw(K, M, N, Kd, Am, Am.stride(0), ak, Bm, Bm.stride(0), bk, C, N)
+    outs = _variants(K, run)
+    ref = A.float() @ B.float().t()
+    assert _rel(outs[8], ref) < 1e-5
+    assert torch.equal(outs[8], outs[1])
+
+
+def test_tn_split_slabs(K):
+    torch.manual_seed(2)
+    M, N, Kd = 65536, 512, 512          # dW[N, Kd] = dy^T x over 65536 tokens
+    dy = torch.randn(M, N, device='cuda').bfloat16()
+    x = torch.randn(M, Kd, device='cuda').bfloat16()
+    outs = _variants(K, lambda: K.matmul_tn(dy, x, split_k=40))
+    ref = dy.float().t() @ x.float()
+    assert _rel(outs[8], ref) < 1e-5
+    assert torch.allclose(outs[8], outs[1], rtol=0, atol=1e-3)
+
+
+def test_nn_accumulate_shadow(K):
+    torch.manual_seed(3)
+    M, N, Kd = 10000, 2816, 1024
+    dy = torch.randn(M, N, device='cuda').bfloat16()
+    w = torch.randn(N, Kd, device='cuda').bfloat16()
+    base = torch.randn(M, Kd, device='cuda')
+
+    def run():
+        C = base.clone()
+        return K.matmul_nn(dy, w, out=C, accumulate=True)
+    outs = _variants(K, run)
+    ref = base + dy.float() @ w.float()
+    assert _rel(outs[8], ref) < 1e-5
+    assert torch.equal(outs[8], outs[1])
+
+
+def test_geglu_and_gelu(K):
+    torch.manual_seed(4)
+    M, N, Kd = 6000, 2816, 512
+    x = torch.randn(M, Kd, device='cuda').bfloat16()
+    w = (torch.randn(N, Kd, device='cuda') * 0.05).bfloat16()
+
+    def geglu():
+        g = torch.empty(M, N // 2, device='cuda', dtype=torch.bfloat16)
+        h = K.linear(x, w, act=K.ACT_GEGLU, out2=g)
+        return torch.cat([h.float(), g.float()], 1)
+    outs = _variants(K, geglu)
+    h = (x.float() @ w.float().t()).bfloat16().float()
+    hv = h.view(M, N // 64, 2, 32)
+    g = (torch.nn.functional.gelu(hv[:, :, 1]) * hv[:, :, 0]).reshape(M, N // 2)
+    assert _rel(outs[8][:, :N], h) < 1e-2
+    assert _rel(outs[8][:, N:], g) < 1e-2
+    assert torch.equal(outs[8], outs[1])
+
+    def gelu():
+        pre = torch.empty(M, N, device='cuda', dtype=torch.bfloat16)
+        y = K.linear(x, w, act=K.ACT_GELU, out2=pre)
+        return torch.cat([y.float(), pre.float()], 1)
+    o2 = _variants(K, gelu)
+    pre = x.float() @ w.float().t()
+    assert _rel(o2[8][:, :N], torch.nn.functional.gelu(pre)) < 1e-2
+    assert torch.equal(o2[8], o2[1])
+
+
+def test_batched_argmax(K):
+    torch.manual_seed(5)
+    nb, M, N, Kd = 2, 4096, 2560, 512
+    A = torch.randn(nb, M, Kd, device='cuda').bfloat16()
+    B = torch.randn(N, Kd, device='cuda').bfloat16()
+
+    def run():
+        C = torch.empty(nb, M, N // 64, 2, device='cuda', dtype=torch.float32)
+        K._gemm_raw(M, N, Kd, A, Kd, True, B, Kd, True, C, N // 64, act=K.ACT_ARGMAX if hasattr(K, 'ACT_ARGMAX')
+                    else 3, batch=nb, sA=M * Kd, sB=0, sC=M * (N // 64))
+        return C
+    outs = _variants(K, run)
+    assert torch.equal(outs[8], outs[1])
+    ref = (A.float() @ B.float().t()).view(nb, M, N // 64, 64)
+    idx = outs[8][..., 1].view(torch.int32).long()
+    best = ref.argmax(-1) + torch.arange(N // 64, device='cuda') * 64
+    agree = (idx == best).float().mean().item()
+    assert agree > 0.999, agree

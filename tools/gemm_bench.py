@@ -42,9 +42,36 @@ def main():
         ('dX  NN        110592x512x2816', lambda: K.matmul_nn(dh, w1), 2 * M * 512 * 2816),
         ('dX  NN        110592x1408x512', lambda: K.matmul_nn(x512, w2), 2 * M * 1408 * 512),
         ('dW  TN        2816x512x110592', lambda: K.matmul_tn(dh, x512), 2 * M * 512 * 2816),
+        ('dW  TN s4     2816x512x110592', lambda: K.matmul_tn(dh, x512, split_k=4), 2 * M * 512 * 2816),
+        ('dW  TN s40    512x512x110592', lambda: K.matmul_tn(x512, x512, split_k=40), 2 * M * 512 * 512),
         ('dW  TN        512x512x110592', lambda: K.matmul_tn(x512, x512), 2 * M * 512 * 512),
     ]
+    from ctclip_mi355x import _lib
+    variants = [v for v in os.environ.get('GEMM_VARIANTS', '8,1').split(',')]
     for name, fn, fl in cases:
+        row = []
+        for v in variants:   # '8' or '8s<stagger>'
+            vv, _, st = v.partition('s')
+            _lib.lib().ctclip_gemm_set_variant(int(vv))
+            _lib.lib().ctclip_gemm_set_stagger(int(st) if st else -1)
+            ms = timeit(fn)
+            row.append(f'v{v} {ms:7.3f} ms {fl / ms / 1e9:7.1f} TF/s')
+        print(f'{name:34s} ' + ' | '.join(row), flush=True)
+    _lib.lib().ctclip_gemm_set_variant(8)
+    _lib.lib().ctclip_gemm_set_stagger(-1)
+    if os.environ.get('NO_LIB'):
+        return
+    # hipBLASLt (torch.matmul) on the same shapes, for a library reference point
+    lib = [
+        ('lib FF1 NT  110592x2816x512', lambda: torch.matmul(x512, w1.t()), 2 * M * 2816 * 512),
+        ('lib FF2 NT  110592x512x1408', lambda: torch.matmul(x1408, w2.t()), 2 * M * 512 * 1408),
+        ('lib Q   NT  110592x256x512', lambda: torch.matmul(x512, wq.t()), 2 * M * 256 * 512),
+        ('lib dX  NN  110592x512x2816', lambda: torch.matmul(dh, w1), 2 * M * 512 * 2816),
+        ('lib dW  TN  2816x512x110592', lambda: torch.matmul(dh.t(), x512), 2 * M * 512 * 2816),
+        ('lib sq  NT  8192x8192x8192', lambda: torch.matmul(sq, sq.t()), 2 * 8192 ** 3),
+    ]
+    sq = r(8192, 8192)
+    for name, fn, fl in lib:
         ms = timeit(fn)
         print(f'{name:34s} {ms:8.3f} ms  {fl / ms / 1e9:8.1f} TF/s', flush=True)
 

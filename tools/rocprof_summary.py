@@ -21,7 +21,7 @@ def main():
     print(f'{"kernel":72s} {"calls":>7s} {"total_ms":>10s} {"avg_us":>9s} {"%":>6s}')
     for name, calls, tot, avg, pct in rows:
         print(f'{short(name):72s} {calls:7d} {tot / 1e3:10.3f} {avg:9.2f} {pct:6.2f}')
-    print(f'{"TOTAL":72s} {"":7s} {total / 1e3:10.3f}   (per step: {total / 1e3 / steps:.2f} ms over {steps:g} steps)')
+    print(f'{"TOTAL":72s} {"":7s} {total / 1e3:10.3f}   (per step: {total / 1e3 / steps:.2f} ms over {steps:g} profiled steps incl. warmup)')
 
 
 if __name__ == '__main__':
