@@ -201,6 +201,30 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
     return;
   }
   const bool slab = p.split_k > 1;
+  if (p.act == 4) {
+    // GEGLU backward fused into dg = dy . W2 (see gemm256.hip): 8 g-columns per thread
+    for (int it = 0; it < (BM * BN / 8) / NTH; ++it) {
+      const int c = t + NTH * it;
+      const int row = c >> 4, cc = (c & 15) * 8;
+      const int64_t gm = m0 + row, gn = n0 + cc;
+      if (gm >= p.M || gn >= p.N) continue;
+      const int64_t tg = gn >> 5, cw = gn & 31;
+      const u16* hr = (const u16*)p.R + bidx * p.sR + gm * p.ldr + tg * 64 + cw;
+      u16* dr = (u16*)p.C + bidx * p.sC + gm * p.ldc + tg * 64 + cw;
+      float x[8], gt[8], ox[8], og[8];
+      unpack8(*(const u32x4*)hr, x);
+      unpack8(*(const u32x4*)(hr + 32), gt);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = bf2f(f2bf(cs[row * CS_LD + cc + j] * p.alpha));
+        ox[j] = d * gelu_erf(gt[j]);
+        og[j] = d * x[j] * gelu_erf_grad(gt[j]);
+      }
+      *(u32x4*)dr = pack8(ox);
+      *(u32x4*)(dr + 32) = pack8(og);
+    }
+    return;
+  }
   for (int it = 0; it < (BM * BN / 8) / NTH; ++it) {
     const int c = t + NTH * it;
     const int row = c >> 4, cc = (c & 15) * 8;
@@ -347,6 +371,68 @@ __global__ __launch_bounds__(1024) void reduce_slabs_skinny_kernel(const float* 
   }
 }
 
+// Split-K combine with the full GEMM epilogue (bias, residual, GELU + pre-activation, f32 /
+// bf16 output, accumulate, bf16 shadow): out = epilogue(sum_z slabs[z]).  Each thread owns 8
+// consecutive columns of one row.  Lets skinny GEMMs (M = 1024 text-tower tokens) split K over
+// 4-6x more workgroups than they have output tiles.
+__global__ __launch_bounds__(256) void reduce_slabs_ep_kernel(const float* __restrict__ s, int64_t nslab,
+                                                              int64_t rows, int64_t cols, int64_t ld, P p) {
+  const int64_t n8 = cols / 8;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= rows * n8) return;
+  const int64_t r = i / n8, c = (i - r * n8) * 8;
+  float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t z = 0; z < nslab; ++z) {
+    const float* sp = s + (z * rows + r) * ld + c;
+    const f32x4 a = *(const f32x4*)sp, b = *(const f32x4*)(sp + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] += a[j]; v[4 + j] += b[j]; }
+  }
+  if (p.bias) {
+    const f32x4 a = *(const f32x4*)(p.bias + c), b = *(const f32x4*)(p.bias + c + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] += a[j]; v[4 + j] += b[j]; }
+  }
+  if (p.R) {
+    if (p.r_f32) {
+      const float* Rp = (const float*)p.R + r * p.ldr + c;
+      const f32x4 a = *(const f32x4*)Rp, b = *(const f32x4*)(Rp + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] += a[j]; v[4 + j] += b[j]; }
+    } else {
+      float rr[8];
+      unpack8(*(const u32x4*)((const u16*)p.R + r * p.ldr + c), rr);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += rr[j];
+    }
+  }
+  if (p.act == 1) {
+    if (p.C2) *(u32x4*)(p.C2 + r * p.ldc2 + c) = pack8(v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
+  }
+  if (p.c_f32) {
+    float* Cf = (float*)p.C + r * p.ldc + c;
+    if (p.accumulate) {
+      const f32x4 a = *(const f32x4*)Cf, b = *(const f32x4*)(Cf + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] += a[j]; v[4 + j] += b[j]; }
+    }
+    *(f32x4*)Cf = f32x4{v[0], v[1], v[2], v[3]};
+    *(f32x4*)(Cf + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  } else {
+    u16* Cb = (u16*)p.C + r * p.ldc + c;
+    if (p.accumulate) {
+      float rr[8];
+      unpack8(*(const u32x4*)Cb, rr);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += rr[j];
+    }
+    *(u32x4*)Cb = pack8(v);
+  }
+  if (p.C2 && p.act == 0) *(u32x4*)(p.C2 + r * p.ldc2 + c) = pack8(v);
+}
+
 static bool s_smem_set = false;
 
 }  // namespace
@@ -368,10 +454,11 @@ extern "C" int ctclip_gemm(const ctclip_gemm_args* a, void* stream) {
     if (a->R) CT_REQUIRE(aligned16(a->R) && a->ldr % 8 == 0, CT_EALIGN);
   }
   if (a->act == 2) CT_REQUIRE(a->N % 64 == 0 && a->ldc2 % 8 == 0, CT_ESHAPE);
+  if (a->act == 4) CT_REQUIRE(a->N % 32 == 0 && a->R && !a->r_f32 && !a->c_f32 && a->split_k <= 1, CT_EINVAL);
   {
     const int b = a->batch > 0 ? a->batch : 1;
     const int64_t tiles256 = ((a->M + 255) / 256) * ((a->N + 255) / 256) * split * b;
-    if (a->K % 64 == 0 && a->M >= 256 && a->N >= 256 && tiles256 >= 160 && (a->K / split) >= 64 &&
+    if (a->K % 64 == 0 && a->M >= 256 && a->N >= 256 && tiles256 >= 160 && (split == 1 || (a->K / split) >= 512) &&
         (!a->bias || aligned16(a->bias)))
       return ctclip_gemm256(a, split, b, stream);
   }
@@ -401,6 +488,27 @@ extern "C" int ctclip_gemm(const ctclip_gemm_args* a, void* stream) {
   if (a->a_kcontig && !a->b_kcontig) return launch<true, false>(p, batch, st);
   if (!a->a_kcontig && a->b_kcontig) return launch<false, true>(p, batch, st);
   return launch<false, false>(p, batch, st);
+}
+
+extern "C" int ctclip_reduce_slabs_ep(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,
+                                      const ctclip_gemm_args* a, void* stream) {
+  if (rows == 0 || cols == 0) return 0;
+  CT_REQUIRE(a && (a->act == 0 || a->act == 1), CT_EINVAL);
+  CT_REQUIRE(cols % 8 == 0 && ld % 4 == 0 && a->ldc % 8 == 0 && aligned16(slabs) && aligned16(a->C), CT_EALIGN);
+  if (a->bias) CT_REQUIRE(aligned16(a->bias), CT_EALIGN);
+  if (a->R) CT_REQUIRE(aligned16(a->R) && a->ldr % 8 == 0, CT_EALIGN);
+  if (a->C2) CT_REQUIRE(aligned16(a->C2) && a->ldc2 % 8 == 0, CT_EALIGN);
+  P p{};
+  p.C = a->C; p.ldc = a->ldc; p.c_f32 = a->c_f32;
+  p.C2 = (u16*)a->C2; p.ldc2 = a->ldc2;
+  p.bias = a->bias;
+  p.R = a->R; p.ldr = a->ldr; p.r_f32 = a->r_f32;
+  p.act = a->act; p.accumulate = a->accumulate;
+  const int64_t total = rows * (cols / 8);
+  hipLaunchKernelGGL(reduce_slabs_ep_kernel, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream, slabs, nslab,
+                     rows, cols, ld, p);
+  CT_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int ctclip_reduce_slabs(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,

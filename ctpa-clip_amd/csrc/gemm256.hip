@@ -449,6 +449,10 @@ __device__ __forceinline__ void store_row_bf16(u16* rowp, const float (&v)[4][4]
   }
 }
 
+// MODE (compile time, so each variant's row loop stays small enough to unroll fully and the
+// accumulator never leaves registers): 0 = general (bias / residual / GELU / f32 or bf16 /
+// accumulate / shadow), 2 = GEGLU, 3 = argmax, 4 = GEGLU backward, 5 = split-K slab.
+template <int MODE>
 __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int wr, int wc, int lane, int64_t m0,
                                            int64_t n0, int split, int bidx) {
   const int m = lane & 15, g = lane >> 4;
@@ -471,7 +475,7 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[j][r] = acc[i][j][r] * p.alpha;
-    if (p.act == 3) {
+    if constexpr (MODE == 3) {
       // argmax over the wave's 64 columns of row gm (first-max tie-break): 16 values per lane,
       // then across the 4 lanes g = 0..3 that hold the same row
       float best = -INFINITY;
@@ -495,14 +499,14 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
       }
       continue;
     }
-    if (p.split_k > 1) {
+    if constexpr (MODE == 5) {
       float* Cf = (float*)p.C + (int64_t)split * p.M * p.ldc + bidx * p.sC + gm * p.ldc + cl;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (rok && cl + 16 * j < p.N) *(f32x4*)(Cf + 16 * j) = f32x4{v[j][0], v[j][1], v[j][2], v[j][3]};
       continue;
     }
-    if (p.act == 2) {
+    if constexpr (MODE == 2) {
       // GEGLU in 32-column pairs: blocks 0,1 = x, blocks 2,3 = gate; h keeps both halves
       store_row_bf16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N);
       float gg[2][4];
@@ -517,6 +521,7 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
       if (rok && wcol0 < p.N) *(u32x4*)(p.C2 + bidx * p.sC2 + gm * p.ldc2 + (wcol0 >> 1) + pair_coff(g)) = d;
       continue;
     }
+    if constexpr (MODE != 0) continue;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -577,6 +582,64 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
       store_row_bf16(Cb, v, g, rok, wcol0, p.N);
     }
     if (p.C2 && p.act == 0) store_row_bf16(p.C2 + bidx * p.sC2 + gm * p.ldc2 + wcol0, v, g, rok, wcol0, p.N);
+  }
+}
+
+// GEGLU backward fused into dg = dy . W2 (TR layout): the accumulator is dg over g-space
+// columns; block pair (0,1) is 32-group t0 = wcol0 / 32, pair (2,3) group t0 + 1.  dg is
+// rounded to bf16 (as the stand-alone geglu_bwd reads it) and permlane-paired so every lane
+// owns 8 consecutive g-columns: one 16-B load of h's x part, one of its gate part, one 16-B
+// store each of dh.  The next row block's h loads are issued before this block's math.
+__device__ __forceinline__ void epilogue_geglu_bwd(const P& p, f32x4 (&acc)[8][4], int wr, int wc, int lane,
+                                                   int64_t m0, int64_t n0, int bidx) {
+  const int m = lane & 15, g = lane >> 4;
+  const int64_t wrow0 = m0 + wr * 128, wcol0 = n0 + wc * 64, t0 = wcol0 >> 5;
+  const int co = pair_coff(g);
+  const u16* hb = (const u16*)p.R + bidx * p.sR;
+  u16* db = (u16*)p.C + bidx * p.sC;
+  u32x4 hx[2][2], hg[2][2];
+  auto load = [&](int i, int b) {
+    const int64_t gm = wrow0 + i * 16 + m;
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      const int64_t t = t0 + jp;
+      if (gm < p.M && t * 32 < p.N) {
+        const u16* hp = hb + gm * p.ldr + t * 64 + co;
+        hx[b][jp] = *(const u32x4*)hp;
+        hg[b][jp] = *(const u32x4*)(hp + 32);
+      } else {
+        hx[b][jp] = make_uint4(0, 0, 0, 0);
+        hg[b][jp] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  load(0, 0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int b = i & 1;
+    if (i + 1 < 8) load(i + 1, b ^ 1);
+    const int64_t gm = wrow0 + i * 16 + m;
+#pragma unroll
+    for (int jp = 0; jp < 2; ++jp) {
+      float v0[4], v1[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { v0[r] = acc[i][2 * jp][r] * p.alpha; v1[r] = acc[i][2 * jp + 1][r] * p.alpha; }
+      float d[8], x[8], gt[8], ox[8], og[8];
+      unpack8(pair_swap(v0, v1), d);
+      unpack8(hx[b][jp], x);
+      unpack8(hg[b][jp], gt);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        ox[k] = d[k] * gelu_erf(gt[k]);
+        og[k] = d[k] * x[k] * gelu_erf_grad(gt[k]);
+      }
+      const int64_t t = t0 + jp;
+      if (gm < p.M && t * 32 < p.N) {
+        u16* dp = db + gm * p.ldc + t * 64 + co;
+        *(u32x4*)dp = pack8(ox);
+        *(u32x4*)(dp + 32) = pack8(og);
+      }
+    }
   }
 }
 
@@ -719,7 +782,11 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
       for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
   }
-  if constexpr (TR) epilogue_t(p, acc, wr, wc, lane, m0, n0, split, bidx);
+  if constexpr (TR) {
+    if (p.act == 2) epilogue_t<2>(p, acc, wr, wc, lane, m0, n0, split, bidx);
+    else if (p.act == 4) epilogue_geglu_bwd(p, acc, wr, wc, lane, m0, n0, bidx);
+    else epilogue_t<0>(p, acc, wr, wc, lane, m0, n0, split, bidx);
+  }
   else epilogue(p, acc, smem, w, wr, wc, lane, m0, n0, split, bidx);
 }
 
@@ -776,7 +843,7 @@ int tile_rows() { return variant() == 2 ? 2 : 1; }
 
 template <bool AK>
 int launch8_any(const P& p, bool bk, int batch, hipStream_t st) {
-  const bool tr = !p.c_f32 && p.split_k <= 1 && p.act != 3 && !p.R;
+  const bool tr = p.act == 4 || (!p.c_f32 && p.split_k <= 1 && p.act != 3 && !p.R);
   if (tr) return bk ? launch8<AK, true, true>(p, batch, st) : launch8<AK, false, true>(p, batch, st);
   return bk ? launch8<AK, true, false>(p, batch, st) : launch8<AK, false, false>(p, batch, st);
 }
@@ -796,7 +863,7 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   p.R = a->R; p.ldr = a->ldr; p.r_f32 = a->r_f32;
   p.alpha = a->alpha; p.act = a->act; p.accumulate = a->accumulate; p.split_k = split;
   p.sA = a->sA; p.sB = a->sB; p.sC = a->sC; p.sC2 = a->sC2; p.sR = a->sR;
-  const int kstep = variant() == 8 ? p8::BKK : BK;
+  const int kstep = (variant() == 8 || a->act == 4) ? p8::BKK : BK;
   p.kper = (a->K / kstep + split - 1) / split * kstep;
   static int dbg = -1, stag = 0;
   if (dbg < 0) {
@@ -811,7 +878,7 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   // slightly negative on the plain / residual epilogues)
   p.stagger = variant() == 8 ? (g_stagger8 >= 0 ? g_stagger8 : (a->act == 2 ? 4 : 0)) : (tile_rows() == 1 ? stag : 0);
   hipStream_t st = (hipStream_t)stream;
-  if (variant() == 8)
+  if (variant() == 8 || a->act == 4)
     return a->a_kcontig ? launch8_any<true>(p, a->b_kcontig, batch, st) : launch8_any<false>(p, a->b_kcontig, batch, st);
   if (tile_rows() == 2) return launch_any<2>(p, a->a_kcontig, a->b_kcontig, batch, st);
   return launch_any<1>(p, a->a_kcontig, a->b_kcontig, batch, st);

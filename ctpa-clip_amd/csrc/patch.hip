@@ -20,7 +20,7 @@ __global__ __launch_bounds__(256) void patch_ln_kernel(const void* __restrict__ 
                                                        int64_t ntok, int T, int Hg, int Wg, int64_t vol_stride,
                                                        int64_t frame_elems, int W, int PT, int P,
                                                        const int32_t* __restrict__ offs, int pd, float eps,
-                                                       u16* __restrict__ out) {
+                                                       u16* __restrict__ out, int64_t ldo) {
   const int lane = threadIdx.x & 63;
   const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (tok >= ntok) return;
@@ -56,12 +56,13 @@ __global__ __launch_bounds__(256) void patch_ln_kernel(const void* __restrict__ 
     if (e < pd) { const float d = v[i] - mean; q += d * d; }
   }
   const float rstd = rsqrtf(warp_sum(q) / pd + eps);
-  u16* o = out + tok * pd;
+  u16* o = out + tok * ldo;
 #pragma unroll
   for (int i = 0; i < MAXC; ++i) {
     const int e = lane + 64 * i;
     if (e < pd) o[e] = f2bf((v[i] - mean) * rstd);
   }
+  for (int e = pd + lane; e < ldo; e += 64) o[e] = 0;   // K padding of the patch-embed GEMM
 }
 
 // Row-strip form (the fast path, single-channel volumes): a workgroup owns PW = 4 horizontally
@@ -77,7 +78,8 @@ constexpr int PW = 4;
 template <bool F32>
 __global__ __launch_bounds__(256) void patch_ln_strip_kernel(const void* __restrict__ video, int is_hu, int T,
                                                              int Hg, int Wg, int64_t vol_stride, int H, int W,
-                                                             int PT, int P, float eps, u16* __restrict__ out) {
+                                                             int PT, int P, float eps, u16* __restrict__ out,
+                                                             int64_t ldo) {
   using E = typename std::conditional<F32, float, short>::type;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   E* sx = (E*)smem_raw;   // [PW][pd]
@@ -155,13 +157,14 @@ __global__ __launch_bounds__(256) void patch_ln_strip_kernel(const void* __restr
   }
   const float rstd = rsqrtf(warp_sum(q) / pd + eps);
   const int64_t tok = (((int64_t)b * T + t) * Hg + hg) * Wg + wg0 + w;
-  uint32_t* o = (uint32_t*)(out + tok * pd);
+  uint32_t* o = (uint32_t*)(out + tok * ldo);
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
     const int e = 2 * (lane + 64 * i);
     if (e < pd)
       o[e >> 1] = (uint32_t)f2bf((v[i][0] - mean) * rstd) | ((uint32_t)f2bf((v[i][1] - mean) * rstd) << 16);
   }
+  for (int e = pd + 2 * lane; e < ldo; e += 128) o[e >> 1] = 0u;   // K padding of the patch-embed GEMM
 }
 
 bool s_strip_attr = false;
@@ -193,9 +196,11 @@ __global__ __launch_bounds__(256) void patch_wgrad_kernel(const float* __restric
 
 extern "C" int ctclip_patch_ln(const void* video, int32_t is_f32, int32_t is_hu, int64_t B, int32_t C, int32_t F,
                                int32_t H, int32_t W, int32_t PT, int32_t P, const int32_t* offs, float eps,
-                               void* out, void* stream) {
+                               void* out, int64_t ldo, void* stream) {
   const int pd = C * PT * P * P;
   CT_REQUIRE(pd <= 64 * MAXC, CT_ESHAPE);
+  if (ldo <= 0) ldo = pd;
+  CT_REQUIRE(ldo >= pd && ldo % 2 == 0, CT_ESHAPE);
   CT_REQUIRE(F % PT == 0 && H % P == 0 && W % P == 0, CT_ESHAPE);
   const int T = F / PT, Hg = H / P, Wg = W / P;
   const int64_t ntok = B * T * Hg * Wg;
@@ -215,13 +220,13 @@ extern "C" int ctclip_patch_ln(const void* video, int32_t is_f32, int32_t is_hu,
     const size_t sm = (size_t)PW * pd * (is_f32 ? 4 : 2);
     if (is_f32)
       hipLaunchKernelGGL(patch_ln_strip_kernel<true>, grid, dim3(256), sm, (hipStream_t)stream, video, is_hu, T, Hg,
-                         Wg, vol, H, W, PT, P, eps, (u16*)out);
+                         Wg, vol, H, W, PT, P, eps, (u16*)out, ldo);
     else
       hipLaunchKernelGGL(patch_ln_strip_kernel<false>, grid, dim3(256), sm, (hipStream_t)stream, video, is_hu, T,
-                         Hg, Wg, vol, H, W, PT, P, eps, (u16*)out);
+                         Hg, Wg, vol, H, W, PT, P, eps, (u16*)out, ldo);
   } else {
     hipLaunchKernelGGL(patch_ln_kernel, dim3(cdiv(ntok, 4)), dim3(256), 0, (hipStream_t)stream, video, is_f32,
-                       is_hu, ntok, T, Hg, Wg, vol, frame, W, PT, P, offs, pd, eps, (u16*)out);
+                       is_hu, ntok, T, Hg, Wg, vol, frame, W, PT, P, offs, pd, eps, (u16*)out, ldo);
   }
   CT_CHECK_LAUNCH();
   return 0;

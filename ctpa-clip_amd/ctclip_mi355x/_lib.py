@@ -58,6 +58,7 @@ _SIGS = {
     'ctclip_gemm': [ctypes.POINTER(GemmArgs), c_vp],
     'ctclip_gemm_set_variant': [c_i32],
     'ctclip_gemm_set_stagger': [c_i32],
+    'ctclip_reduce_slabs_ep': [c_vp, c_i64, c_i64, c_i64, c_i64, ctypes.POINTER(GemmArgs), c_vp],
     'ctclip_reduce_slabs': [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp],
     'ctclip_layernorm_fwd': [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_f32, c_vp, c_i64, c_vp, c_i64,
                              c_vp, c_vp, c_vp],
@@ -73,7 +74,8 @@ _SIGS = {
     'ctclip_gelu_f32': [c_vp, c_vp, c_i64, c_vp],
     'ctclip_cast_f32_bf16': [c_vp, c_vp, c_i64, c_vp],
     'ctclip_add_f32': [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
-    'ctclip_patch_ln': [c_vp, c_i32, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp, c_vp],
+    'ctclip_patch_ln': [c_vp, c_i32, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp, c_i64,
+                        c_vp],
     'ctclip_patch_wgrad': [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp],
     'ctclip_peg_fwd': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp],
     'ctclip_peg_bwd_data': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp],

@@ -122,10 +122,13 @@ class PatchEmbedFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, video, ln1_w, ln1_b, W, b, ln2_w, ln2_b, PT, P, is_hu, offs):
-        xhat = K.patch_ln(video, is_hu, PT, P, offs)                   # [M, pd] bf16
-        Wp = K.pack_rows(W, W.shape[0], W.shape[1], colscale=ln1_w)    # bf16 [D, pd]
+        pd = W.shape[1]
+        kp = (pd + 63) // 64 * 64                                      # K padded to the 64-deep GEMM step
+        xhat_p = K.patch_ln(video, is_hu, PT, P, offs, ld=kp)          # [M, kp] bf16, zero pad columns
+        xhat = xhat_p[:, :pd]
+        Wp = K.pack_rows(W, W.shape[0], kp, colscale=ln1_w)            # bf16 [D, kp], zero pad columns
         bp = K.slinear(ln1_b.view(1, -1), W, bias=b).view(-1)          # f32 [D]
-        y1 = K.linear(xhat, Wp, bias=bp, out_dtype=F32)                 # [M, D]
+        y1 = K.linear(xhat_p, Wp, bias=bp, out_dtype=F32)               # [M, D]
         yb, yf, mean, rstd = K.layernorm_fwd(y1, ln2_w, ln2_b, 1e-5, out_bf16=True, out_f32=True)
         ctx.save_for_backward(xhat, y1, mean, rstd, ln1_w, ln1_b, W, ln2_w)
         ctx.mark_non_differentiable(yb)
@@ -256,9 +259,8 @@ class ViTLayerFn(torch.autograd.Function):
         if dx3b is None:
             dx3b = K.cast_bf16(dx3f)
         # feed-forward (weight gradients accumulate straight into the parameters' .grad)
-        dg = K.matmul_nn(dx3b, W2p)
+        dh_ = K.matmul_nn_geglu_bwd(dx3b, W2p, h)      # dg = dx3 . W2 and the GEGLU backward, fused
         dW2p = K.matmul_tn(dx3b, g)
-        dh_ = K.geglu_bwd(dg, h)
         dxn2 = K.matmul_nn(dh_, W1p)
         dW1p = K.matmul_tn(dh_, xn2)
         dx2f, dx2b, _, _ = K.layernorm_bwd(dxn2, x2b, m2, r2, ff_w, dres=dx3f, dgamma_out=gsink(ff_w),

@@ -10,7 +10,7 @@ from ._lib import GemmArgs, call, ptr, stream_ptr
 BF16 = torch.bfloat16
 F32 = torch.float32
 
-ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_ARGMAX = 0, 1, 2, 3
+ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_ARGMAX, ACT_GEGLU_BWD = 0, 1, 2, 3, 4
 
 
 def _chk(t, name, dtype=None):
@@ -69,6 +69,20 @@ def gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, *, C2=None, 
 def _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, *, C2=None, ldc2=0, bias=None,
               R=None, ldr=0, alpha=1.0, act=ACT_NONE, accumulate=False, split_k=1, batch=1,
               sA=0, sB=0, sC=0, sC2=0, sR=0):
+    s = _auto_split(M, N, K, act, split_k, batch, accumulate, C)
+    if s > 1:
+        # skinny GEMM (text tower, M = B * L tokens): split K into f32 slabs over ~4x more
+        # workgroups than output tiles, then combine with the epilogue in one pass
+        slabs = torch.empty(s, M, N, device=C.device, dtype=F32)
+        _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, slabs, N, alpha=alpha, split_k=s)
+        a = GemmArgs()
+        a.C, a.ldc, a.c_f32 = ptr(C), ldc, int(C.dtype == F32)
+        a.C2, a.ldc2 = ptr(C2), ldc2
+        a.bias = ptr(bias)
+        a.R, a.ldr, a.r_f32 = ptr(R), ldr, int(R is not None and R.dtype == F32)
+        a.act, a.accumulate = act, int(accumulate)
+        call('ctclip_reduce_slabs_ep', ptr(slabs), s, M, N, N, _lib.ctypes.byref(a), stream_ptr())
+        return
     a = GemmArgs()
     a.M, a.N, a.K = M, N, K
     a.A, a.lda, a.a_kcontig = ptr(A), lda, int(a_kcontig)
@@ -80,6 +94,16 @@ def _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, *, C2=None,
     a.alpha, a.act, a.accumulate, a.split_k, a.batch = alpha, act, int(accumulate), split_k, batch
     a.sA, a.sB, a.sC, a.sC2, a.sR = sA, sB, sC, sC2, sR
     call('ctclip_gemm', _lib.ctypes.byref(a), stream_ptr())
+
+
+def _auto_split(M, N, K, act, split_k, batch, accumulate, C):
+    """split-K factor for an epilogue GEMM that fills too few CUs with 128 x 128 tiles."""
+    if split_k != 1 or batch != 1 or act not in (ACT_NONE, ACT_GELU) or K < 512 or N % 8 or C.stride(-1) != 1:
+        return 1
+    tiles = ((M + 127) // 128) * ((N + 127) // 128)
+    if tiles >= 128 or M * N > (1 << 22):
+        return 1
+    return max(1, min(256 // tiles, K // 256))
 
 
 def linear(x, w, *, bias=None, residual=None, out=None, out_dtype=BF16, act=ACT_NONE, out2=None, alpha=1.0,
@@ -160,7 +184,7 @@ def nblocks_for(rows, cap=1024):
 def colsum(x, out=None, accumulate=False):
     """Column sums of x[rows, cols] (bf16 or f32) -> f32 [cols]."""
     rows, cols = x.shape
-    nb = nblocks_for(rows, 256)
+    nb = int(max(1, min(256, rows // 8)))   # >= 8 rows per block: short (text-tower) inputs fill the chip
     part = torch.empty(nb, cols, device=x.device, dtype=F32)
     call('ctclip_colsum', ptr(x), int(x.dtype == F32), x.stride(0), rows, cols, ptr(part), nb, stream_ptr())
     if out is None:
@@ -229,6 +253,19 @@ def l2norm_scale_bwd(x, dy, H, D, scale, out, ds_out=None):
 
 
 # ----------------------------------------------------------------------------- elementwise
+def matmul_nn_geglu_bwd(dy, w2p, h, out=None):
+    """dh = geglu_bwd(dy @ w2p, h) in one GEMM (act 4): dy [M, D] bf16, w2p [D, G] (the padded
+    FeedForward W2), h [M, 2G] the GEGLU pre-activation; returns dh [M, 2G] bf16."""
+    M, D = dy.shape
+    G = w2p.shape[1]
+    assert w2p.shape[0] == D and h.shape == (M, 2 * G)
+    if out is None:
+        out = torch.empty(M, 2 * G, device=dy.device, dtype=BF16)
+    gemm_raw(M, G, D, dy, dy.stride(0), True, w2p, w2p.stride(0), False, out, out.stride(0), R=h, ldr=h.stride(0),
+             act=ACT_GEGLU_BWD)
+    return out
+
+
 def geglu_bwd(dg, h, out=None):
     rows, gcols = dg.shape
     if out is None:
@@ -273,13 +310,15 @@ def add_f32(a, b, out=None, out_bf16=None):
 
 
 # ----------------------------------------------------------------------------- patch embed
-def patch_ln(video, is_hu, PT, P, offs, eps=1e-5):
+def patch_ln(video, is_hu, PT, P, offs, eps=1e-5, ld=None):
+    """LayerNorm'd patch rows [tokens, ld] bf16 (columns pd..ld-1 zero: K padding for the GEMM)."""
     B, C, Fr, H, W = video.shape
     T, Hg, Wg = Fr // PT, H // P, W // P
     pd = C * PT * P * P
-    out = torch.empty(B * T * Hg * Wg, pd, device=video.device, dtype=BF16)
+    ld = pd if ld is None else ld
+    out = torch.empty(B * T * Hg * Wg, ld, device=video.device, dtype=BF16)
     call('ctclip_patch_ln', ptr(video), int(video.dtype == F32), int(is_hu), B, C, Fr, H, W, PT, P, ptr(offs), eps,
-         ptr(out), stream_ptr())
+         ptr(out), ld, stream_ptr())
     return out
 
 

@@ -36,7 +36,9 @@ int ctclip_device_arch(char* buf, int n); /* writes gcnArchName of the current d
  * (ct_clip/ct_clip.py:685) and all their backward GEMMs.
  *   a_kcontig = 1: A[m*lda + k]   (row-major M x K);   0: A[k*lda + m]  (K x M)
  *   b_kcontig = 1: B[n*ldb + k]   (nn.Linear weight);  0: B[k*ldb + n]  (K x N)
- *   act: 0 none, 1 gelu(erf), 2 geglu (tile-interleaved pairs), 3 argmax
+ *   act: 0 none, 1 gelu(erf), 2 geglu (tile-interleaved pairs), 3 argmax,
+ *        4 geglu backward: acc = dg (N = g-space columns, N % 32 == 0), R = h (bf16, the
+ *          act-2 pre-activation), C = dh (bf16, h's layout) — replaces dg + geglu_bwd
  *   split_k > 1: C is an f32 slab array [split_k][M][ldc] of partial sums (no epilogue).
  */
 typedef struct {
@@ -64,6 +66,10 @@ int ctclip_gemm_set_stagger(int units);
 /* sum f32 slabs [s][rows][ld] -> out (f32 or bf16), optional accumulate into f32 out */
 int ctclip_reduce_slabs(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,
                         void* out, int64_t ldo, int32_t out_f32, int32_t accumulate, void* stream);
+/* split-K combine with the GEMM epilogue of `ep` (C, ldc, c_f32, C2, ldc2, bias, R, ldr, r_f32,
+ * act in {0, 1}, accumulate; M/N/K/A/B ignored): C = epilogue(sum_z slabs[z][rows][ld]) */
+int ctclip_reduce_slabs_ep(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,
+                           const ctclip_gemm_args* ep, void* stream);
 
 
 /* ---------------------------------------------------------------- LayerNorm family
@@ -108,10 +114,12 @@ int ctclip_add_f32(const float* a, const float* b, float* y, void* y_bf16, int64
 /* ---------------------------------------------------------------- patch embedding
  * int16 HU (is_hu: clamp(-1000,1000)/1000.f, ct_clip/data.py:150-152) or f32 video
  * (B, C, F, H, W) -> xhat (B*T*Hg*Wg, C*PT*P*P) bf16 = LayerNorm statistics applied
- * (ctvit.py:170-171).  offs[e] = voxel offset of patch element e from the patch origin. */
+ * (ctvit.py:170-171).  offs[e] = voxel offset of patch element e from the patch origin.
+ * ldo = xhat row stride in elements (>= patch dim, even; <= 0 means patch dim); columns
+ * [patch dim, ldo) are written as zeros (K padding for the 64-deep patch-embed GEMM). */
 int ctclip_patch_ln(const void* video, int32_t is_f32, int32_t is_hu, int64_t B, int32_t C, int32_t F,
                     int32_t H, int32_t W, int32_t PT, int32_t P, const int32_t* offs, float eps,
-                    void* xhat, void* stream);
+                    void* xhat, int64_t ldo, void* stream);
 int ctclip_patch_wgrad(const float* G, const float* colsum_dy, const float* W, const float* gamma,
                        const float* beta, int32_t N, int32_t K, float* dW, float* dgamma, float* dbeta,
                        int32_t accumulate, void* stream);

@@ -140,3 +140,30 @@ def test_batched_argmax(K):
     best = ref.argmax(-1) + torch.arange(N // 64, device='cuda') * 64
     agree = (idx == best).float().mean().item()
     assert agree > 0.999, agree
+
+
+@pytest.mark.parametrize('M', [6000, 300])     # 8-phase kernel / 128-tile kernel
+def test_geglu_bwd_fused(K, M):
+    """act 4: dh = geglu_bwd(dy . W2p, h) in one GEMM == the two-kernel path, bit for bit."""
+    torch.manual_seed(6)
+    D, G = 512, 1408
+    dy = (torch.randn(M, D, device='cuda') * 0.1).bfloat16()
+    w2p = (torch.randn(D, G, device='cuda') * 0.05).bfloat16()
+    h = torch.randn(M, 2 * G, device='cuda').bfloat16()
+    fused = K.matmul_nn_geglu_bwd(dy, w2p, h)
+    ref = K.geglu_bwd(K.matmul_nn(dy, w2p), h)
+    if M >= 1024:
+        assert torch.equal(fused, ref)
+    else:   # the stand-alone small GEMM runs split-K (different f32 summation order)
+        assert _rel(fused, ref) < 5e-3
+    # and against torch fp32 math on the bf16-rounded dg
+    dg = (dy.float() @ w2p.float()).bfloat16().float()
+    hv = h.float().view(M, G // 32, 2, 32)
+    x, gt = hv[:, :, 0], hv[:, :, 1]
+    d = dg.view(M, G // 32, 32)
+    cdf = 0.5 * (1 + torch.erf(gt / 2 ** 0.5))
+    pdf = torch.exp(-0.5 * gt * gt) / (2 * torch.pi) ** 0.5
+    ox = d * torch.nn.functional.gelu(gt)
+    og = d * x * (cdf + gt * pdf)
+    refm = torch.stack([ox, og], 2).reshape(M, 2 * G)
+    assert _rel(fused, refm) < 1e-2

@@ -293,6 +293,10 @@ def test_patch_ln(K, size, f32):
     assert rel(xh.cpu(), ref) < 4e-3
     # bf16 of the f32 LN of identical inputs: every element within one bf16 ulp
     assert ((xh.cpu().float() - ref).abs() <= ref.abs() * 2 ** -7 + 1e-6).all()
+    # padded row stride (the patch-embed GEMM's K = 4032): same values, zero pad columns
+    xp = K.patch_ln(v.to(dev) if f32 else hu, not f32, 10, 20, offs, ld=4032)
+    assert torch.equal(xp[:, :4000].cpu(), xh.cpu())
+    assert (xp[:, 4000:] == 0).all()
 
 
 def test_embed(K):

@@ -41,6 +41,8 @@ def main():
         ('KV  NT        110592x512x512', lambda: K.linear(x512, wkv), 2 * M * 512 * 512),
         ('dX  NN        110592x512x2816', lambda: K.matmul_nn(dh, w1), 2 * M * 512 * 2816),
         ('dX  NN        110592x1408x512', lambda: K.matmul_nn(x512, w2), 2 * M * 1408 * 512),
+        ('dG+geglu_bwd  fused', lambda: K.matmul_nn_geglu_bwd(x512, w2, dh), 2 * M * 1408 * 512),
+        ('dG+geglu_bwd  2-kernel', lambda: K.geglu_bwd(K.matmul_nn(x512, w2), dh), 2 * M * 1408 * 512),
         ('dW  TN        2816x512x110592', lambda: K.matmul_tn(dh, x512), 2 * M * 512 * 2816),
         ('dW  TN s4     2816x512x110592', lambda: K.matmul_tn(dh, x512, split_k=4), 2 * M * 512 * 2816),
         ('dW  TN s40    512x512x110592', lambda: K.matmul_tn(x512, x512, split_k=40), 2 * M * 512 * 512),
