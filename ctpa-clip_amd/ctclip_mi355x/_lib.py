@@ -12,7 +12,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libctclip_hip.so')
+# CTCLIP_HIP_LIB: an alternative in-tree build (A/B timing in tools/); never a fallback
+LIB_PATH = os.environ.get('CTCLIP_HIP_LIB') or os.path.join(_HERE, 'libctclip_hip.so')
 _LIB = None
 
 c_i64 = ctypes.c_int64
