@@ -8,6 +8,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from . import dist_sync
 from . import functional as Fn
 
 
@@ -103,12 +104,15 @@ class Transformer(nn.Module):
         self.norm_out = LayerNorm(dim)
         self.heads = heads
         self.dim_head = dim_head
+        self.ready_tag = None   # gradient bucket tag (dist_sync.mark_ready), set by CTViT
 
     def run(self, xf, xb, geo, attn_bias=None):
         """x: (f32 master, bf16 shadow) rows in canonical order; returns norm_out(x) as (f32, bf16)."""
-        for peg, attn, _, ff in self.layers:
+        for li, (peg, attn, _, ff) in enumerate(self.layers):
             xf, xb = Fn.ViTLayerFn.apply(
                 xf, xb, attn_bias, geo, peg.dsconv.weight, peg.dsconv.bias, attn.norm.gamma, attn.q_scale,
                 attn.k_scale, attn.to_q.weight, attn.to_kv.weight, attn.to_out.weight, ff[0].weight, ff[0].bias,
                 ff[1].weight, ff[4].weight)
+            if li == 0 and self.ready_tag:   # the stack's layer .grads are final after layer 0's backward
+                dist_sync.mark_ready(xf, self.ready_tag)
         return Fn.NormFn.apply(xf, xb, self.norm_out.gamma)

@@ -13,6 +13,7 @@ from dataclasses import dataclass
 import torch
 from torch import nn
 
+from . import dist_sync
 from . import functional as Fn
 
 
@@ -108,6 +109,7 @@ class BertModel(nn.Module):
         xf, xb = Fn.BertEmbedFn.apply(ids, e.word_embeddings.weight, e.position_embeddings.weight,
                                       e.token_type_embeddings.weight, e.LayerNorm.weight, e.LayerNorm.bias,
                                       c.layer_norm_eps)
+        dist_sync.mark_ready(xf, 'text')   # every BERT .grad is final once the embeddings' backward ran
         for lyr in self.encoder.layer:
             a = lyr.attention
             xf, xb = Fn.BertLayerFn.apply(

@@ -78,8 +78,10 @@ class CTCLIP(nn.Module):
     def encode(self, text, image):
         """Text + image towers and raw latents: (enc_text (B,L,768), pooled (B, h*w*d),
         text_raw (B, dl), image_raw (B, dl))."""
-        enc_text = self.text_transformer(text.input_ids, attention_mask=text.attention_mask)[0]
+        # image tower first: the text tower's nodes are then newer, so the backward runs BERT
+        # first and its gradient bucket all-reduces under the 3D-ViT backward (dist_sync)
         pooled, pooled_b = self.visual_transformer.encode_pooled(image)
+        enc_text = self.text_transformer(text.input_ids, attention_mask=text.attention_mask)[0]
         cls = enc_text[:, 0, :]
         t_raw = Fn.TextProjFn.apply(cls.contiguous() if not cls.is_contiguous() else cls, self.to_text_latent.weight)
         W = self.to_visual_latent.weight
@@ -109,6 +111,14 @@ class CTCLIP(nn.Module):
             from . import kernels as K
             return K.clip_scores(t_raw.contiguous(), i_raw.contiguous(), self.temperature.detach().reshape(1))
         return Fn.ClipLossFn.apply(t_raw, i_raw, self.temperature)
+
+    def grad_buckets(self):
+        """Gradient all-reduce buckets in the order the backward finalises them (dist_sync)."""
+        vt = self.visual_transformer
+        return [('text', list(self.text_transformer.parameters())),
+                ('vit_temporal', list(vt.enc_temporal_transformer.parameters())),
+                ('vit_spatial', list(vt.enc_spatial_transformer.parameters())),
+                ('rest', list(self.parameters()))]
 
     def _pool_tokens(self, tokens):
         """mean over t + flatten of already-quantised tokens (ct_clip.py:724,740)."""

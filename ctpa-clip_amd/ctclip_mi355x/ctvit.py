@@ -78,6 +78,8 @@ class CTViT(nn.Module):
         kw = dict(dim_head=dim_head, heads=heads, peg=True, peg_causal=True)
         self.enc_spatial_transformer = Transformer(dim, depth=spatial_depth, **kw)
         self.enc_temporal_transformer = Transformer(dim, depth=temporal_depth, **kw)
+        self.enc_spatial_transformer.ready_tag = 'vit_spatial'     # gradient buckets (dist_sync)
+        self.enc_temporal_transformer.ready_tag = 'vit_temporal'
         self.vq = VectorQuantize(dim=dim, codebook_size=codebook_size, use_cosine_sim=True)
         self.to_pixels_first_frame = nn.Sequential(nn.Linear(dim, pdf), _Slot())
         self.to_pixels = nn.Sequential(nn.Linear(dim, pd), _Slot())

@@ -67,3 +67,74 @@ def sum_grads(flat_grad: torch.Tensor) -> None:
     world, _ = world_rank()
     if world > 1:
         dist.all_reduce(flat_grad)
+
+
+# ------------------------------------------------------------------ backward-overlapped buckets
+# SURVEY §8(e) "Overlap": the image tower runs forward first and the text tower second, so the
+# autograd engine (which runs the most recently created node first) back-propagates BERT before
+# the 3D-ViT.  Each tower (or stack) marks the autograd node after which its parameters' .grad
+# are final (``mark_ready``); the trainer's ``BucketedGradSync`` then launches that bucket's SUM
+# all-reduce asynchronously (RCCL runs it on its own stream after the kernels already queued)
+# while the rest of the backward keeps the compute stream busy.  Buckets are launched in one
+# fixed order on every rank, so the collectives always match.
+_READY = {}
+
+
+def mark_ready(t: torch.Tensor, tag: str) -> None:
+    """Called in a forward: once ``t``'s producing node has run its backward, every parameter of
+    bucket ``tag`` has its final gradient.  No-op unless a trainer armed ``tag``."""
+    cb = _READY.get(tag)
+    if cb is None or t.grad_fn is None or not torch.is_grad_enabled():
+        return
+    t.grad_fn.register_hook(lambda grad_inputs, grad_outputs: cb(tag))
+
+
+def disarm() -> None:
+    _READY.clear()
+
+
+class BucketedGradSync:
+    """SUM all-reduce of a flat gradient arena in contiguous buckets [(tag, offset, numel)],
+    each launched as soon as its ``mark_ready`` node has run (the last bucket at ``finish``)."""
+
+    def __init__(self, flat_grad: torch.Tensor, buckets, before_launch=None, force=False):
+        self.grad = flat_grad
+        self.buckets = list(buckets)
+        self.before_launch = before_launch   # fold stray (non-arena) grads of a bucket
+        self.force = force                   # arm the hooks even at world 1 (tests)
+        self.launched = []
+        self.works = []
+        self.log = []
+
+    def _launch(self, tag):
+        if tag in self.launched:
+            return
+        # buckets go out in their fixed order: an early hook also launches every earlier bucket
+        for t, off, n in self.buckets:
+            if t in self.launched:
+                continue
+            if self.before_launch is not None:
+                self.before_launch(t)
+            self.launched.append(t)
+            self.log.append(t)
+            world, _ = world_rank()
+            if world > 1:
+                self.works.append(dist.all_reduce(self.grad[off:off + n], async_op=True))
+            if t == tag:
+                break
+
+    def arm(self):
+        world, _ = world_rank()
+        self.launched, self.works, self.log = [], [], []
+        if world > 1 or self.force:
+            for t, _, _ in self.buckets[:-1]:
+                _READY[t] = self._launch
+
+    def finish(self):
+        for t, _, _ in self.buckets:
+            _READY.pop(t, None)
+        if self.buckets:
+            self._launch(self.buckets[-1][0])
+        for w in self.works:
+            w.wait()
+        self.works = []

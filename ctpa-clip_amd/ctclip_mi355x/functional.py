@@ -290,7 +290,11 @@ class ViTLayerFn(torch.autograd.Function):
         # PEG
         dxf, dxb, dpw, dpb = K.peg_bwd(dx1b, dx1f, xb, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, geo.mode)
         put_shadow(dxf, dxb)
-        return (dxf, None, du, None, dpw.reshape(peg_w.shape), dpb, None, None, None, None, None, None, None,
+        if peg_w.requires_grad:          # into .grad here too, so the layer's grads are final when
+            gsink(peg_w).add_(dpw.reshape(peg_w.shape))   # its node returns (dist_sync buckets)
+        if peg_b.requires_grad:
+            gsink(peg_b).add_(dpb)
+        return (dxf, None, du, None, None, None, None, None, None, None, None, None, None,
                 None, None, None)
 
 

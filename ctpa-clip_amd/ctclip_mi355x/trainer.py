@@ -32,9 +32,12 @@ class FlatParams:
             self.views.append((off, k, g))
             off += k
 
-    def rebind_grads(self):
+    def rebind_grads(self, only=None):
         """Make sure every .grad is (still) the arena view; fold stray grads back in."""
+        sel = None if only is None else {id(p) for p in only}
         for p, (off, k, g) in zip(self.params, self.views):
+            if sel is not None and id(p) not in sel:
+                continue
             if p.grad is None:
                 p.grad = g
             elif p.grad.data_ptr() != g.data_ptr():
@@ -42,16 +45,45 @@ class FlatParams:
                 p.grad = g
 
 
+def grad_buckets(model):
+    """[(tag, params)] with every parameter in exactly one bucket, in the model's readiness order
+    (``model.grad_buckets()``, e.g. CTCLIP: text, vit_temporal, vit_spatial, rest)."""
+    spec = model.grad_buckets() if hasattr(model, 'grad_buckets') else [('all', list(model.parameters()))]
+    seen, out = set(), []
+    for tag, ps in spec:
+        mine = []
+        for p in ps:
+            if id(p) not in seen:
+                seen.add(id(p))
+                mine.append(p)
+        out.append((tag, mine))
+    rest = [p for p in model.parameters() if id(p) not in seen]
+    if rest:
+        out[-1][1].extend(rest)
+    return out
+
+
 class CTClipTrainer:
     """Optimiser + step for a ``ctclip_mi355x.CTCLIP``.  Hyper-parameters default to the
     reference's (CTCLIPTrainer.py:203-205, optimizer.py:24: Adam lr 1.25e-6, betas (0.9, 0.99),
     eps 1e-8, wd 0, clip 0.5)."""
 
-    def __init__(self, model, lr=1.25e-6, wd=0.0, max_grad_norm=0.5, betas=(0.9, 0.99), eps=1e-8):
+    def __init__(self, model, lr=1.25e-6, wd=0.0, max_grad_norm=0.5, betas=(0.9, 0.99), eps=1e-8,
+                 overlap_grad_sync=True):
         self.model = model
         dev = next(model.parameters()).device
         self.device = dev
-        self.flat = FlatParams(model.parameters(), dev)
+        # arena order = gradient bucket order, so every bucket is one contiguous slice
+        groups = grad_buckets(model) if overlap_grad_sync else [('all', list(model.parameters()))]
+        self.flat = FlatParams([p for _, ps in groups for p in ps], dev)
+        segs, off, self.bucket_params = [], 0, {}
+        for tag, ps in groups:
+            n = sum(p.numel() for p in ps if p.requires_grad)
+            if n:
+                segs.append((tag, off, n))
+                self.bucket_params[tag] = [p for p in ps if p.requires_grad]
+            off += n
+        self.grad_sync = dist_sync.BucketedGradSync(self.flat.grad, segs, before_launch=self._fold_bucket)
         self.m = torch.zeros_like(self.flat.data)
         self.v = torch.zeros_like(self.flat.data)
         self.lr, self.wd, self.max_grad_norm, self.betas, self.eps = lr, wd, max_grad_norm, betas, eps
@@ -59,14 +91,23 @@ class CTClipTrainer:
         self.norm = torch.zeros(2, device=dev, dtype=torch.float32)
         self.world = dist_sync.world_rank()[0]
 
+    def _fold_bucket(self, tag):
+        self.flat.rebind_grads(self.bucket_params.get(tag, ()))
+
     def forward_backward(self, text, video):
-        loss = self.model(text, video, device=self.device, return_loss=True)
-        loss.backward()
-        self.flat.rebind_grads()
+        self.grad_sync.arm()
+        try:
+            loss = self.model(text, video, device=self.device, return_loss=True)
+            loss.backward()
+        except BaseException:
+            dist_sync.disarm()
+            raise
         return loss
 
     def optimizer_step(self):
-        dist_sync.sum_grads(self.flat.grad)          # SUM: ClipLossFn gives each rank its own rows
+        # SUM (ClipLossFn gives each rank its own rows): buckets already in flight since their
+        # tower's backward finished; the last one goes out here and all are waited on
+        self.grad_sync.finish()
         K.grad_norm(self.flat.grad, self.max_grad_norm if self.max_grad_norm else 0.0, self.norm)
         self.steps += 1
         K.adam(self.flat.data, self.flat.grad, self.m, self.v, lr=self.lr, b1=self.betas[0], b2=self.betas[1],

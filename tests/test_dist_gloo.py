@@ -127,3 +127,85 @@ def test_single_process_path_matches_oracle():
     assert torch.allclose(loss.detach(), ref_loss)
     torch.testing.assert_close(wt.grad, gwt)
     torch.testing.assert_close(lt.grad, glt)
+
+
+# ------------------------------------------------------------------ backward-overlapped buckets
+class _SinkMM(torch.autograd.Function):
+    """x @ w whose weight gradient is accumulated straight into w.grad inside backward, like the
+    HIP layer Functions (functional.gsink)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x @ w
+
+    @staticmethod
+    def backward(ctx, g):
+        from ctclip_mi355x.functional import gsink
+        x, w = ctx.saved_tensors
+        gsink(w).add_(x.t() @ g)
+        return g @ w.t(), None
+
+
+class _Toy(torch.nn.Module):
+    """Two 2-layer 'towers' + a temperature, image tower first as in CTCLIP.encode."""
+
+    def __init__(self):
+        super().__init__()
+        g = torch.Generator().manual_seed(3)
+        mk = lambda *s: torch.nn.Parameter(torch.randn(*s, generator=g, dtype=torch.float64).float())  # noqa: E731
+        self.wt1, self.wt2, self.wi1, self.wi2 = mk(DIN, DIN), mk(DIN, DL), mk(DIN, DIN), mk(DIN, DL)
+        self.lt = torch.nn.Parameter(torch.tensor(1.0))
+
+    def grad_buckets(self):
+        return [('text', [self.wt1, self.wt2]), ('image', [self.wi1, self.wi2]), ('rest', [self.lt])]
+
+    def forward(self, text, video, device=None, return_loss=True):
+        from ctclip_mi355x import dist_sync
+        from ctclip_mi355x.functional import ClipLossFn
+        h = _SinkMM.apply(video, self.wi1)
+        dist_sync.mark_ready(h, 'image')
+        i = _SinkMM.apply(h, self.wi2)
+        u = _SinkMM.apply(text, self.wt1)
+        dist_sync.mark_ready(u, 'text')
+        t = _SinkMM.apply(u, self.wt2)
+        return ClipLossFn.apply(t, i, self.lt, oracle_clip_loss)
+
+
+def _bucket_worker(rank, port, out_dir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=WORLD)
+    try:
+        from ctclip_mi355x.trainer import CTClipTrainer
+        xt, xi, _, _ = _problem()
+        model = _Toy()
+        ref = _Toy()
+        tr = CTClipTrainer(model)
+        # arena order follows the buckets, each bucket one contiguous slice
+        assert [t for t, _, _ in tr.grad_sync.buckets] == ['text', 'image', 'rest']
+        assert model.wt1.grad.data_ptr() == tr.flat.grad.data_ptr()
+        rows = slice(rank * B, (rank + 1) * B)
+        for step in range(2):     # hooks re-arm every step
+            tr.flat.grad.zero_()
+            tr.forward_backward(xt[rows], xi[rows])
+            # the text and image buckets went out from autograd hooks during the backward, the
+            # image one after the text one (BERT-first backward order); 'rest' waits for finish
+            assert tr.grad_sync.launched == ['text', 'image'], tr.grad_sync.launched
+            tr.grad_sync.finish()
+            assert tr.grad_sync.launched == ['text', 'image', 'rest']
+        t = _SinkMM.apply(_SinkMM.apply(xt, ref.wt1), ref.wt2)
+        i = _SinkMM.apply(_SinkMM.apply(xi, ref.wi1), ref.wi2)
+        loss = O.infonce(torch.nn.functional.normalize(t, dim=-1), torch.nn.functional.normalize(i, dim=-1), ref.lt)
+        loss.backward()
+        for name in ('wt1', 'wt2', 'wi1', 'wi2', 'lt'):
+            torch.testing.assert_close(getattr(model, name).grad, getattr(ref, name).grad, rtol=1e-5, atol=1e-6)
+        open(os.path.join(out_dir, f'ok{rank}'), 'w').close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_bucketed_overlap(tmp_path):
+    """Gradient buckets all-reduced from autograd hooks during the backward (dist_sync.
+    BucketedGradSync) reproduce the single-process global-batch gradient."""
+    mp.spawn(_bucket_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    assert all((tmp_path / f'ok{r}').exists() for r in range(WORLD))

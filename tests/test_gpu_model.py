@@ -166,3 +166,32 @@ def test_trainer_step_runs(setup):
     assert not torch.equal(before, p.detach())
     assert p.data_ptr() >= tr.flat.data.data_ptr()
     assert tr.norm[0].item() > 0
+
+
+def test_grad_buckets_final_when_launched(setup):
+    """Backward-overlapped gradient sync (dist_sync.BucketedGradSync): with the
+    hooks forced on at world 1, each bucket's gradient slice at the moment its hook launches the
+    all-reduce must already equal its final value (bit-exact), the hooks must fire in bucket
+    order during the backward (BERT first), and only the last bucket waits for finish()."""
+    cfg, model, hu, ids, mask, text = setup
+    from ctclip_mi355x.trainer import CTClipTrainer
+    tr = CTClipTrainer(model, lr=1e-4)
+    gs = tr.grad_sync
+    assert [t for t, _, _ in gs.buckets] == ['text', 'vit_temporal', 'vit_spatial', 'rest']
+    snaps = {}
+    fold = gs.before_launch
+
+    def snap(tag):
+        fold(tag)
+        _, off, n = next(b for b in gs.buckets if b[0] == tag)
+        snaps[tag] = tr.flat.grad[off:off + n].clone()
+    gs.before_launch = snap
+    gs.force = True
+    tr.flat.grad.zero_()
+    tr.forward_backward(text, hu.cuda())
+    assert gs.launched == ['text', 'vit_temporal', 'vit_spatial'], gs.launched
+    gs.finish()
+    torch.cuda.synchronize()
+    for tag, off, n in gs.buckets:
+        assert torch.equal(snaps[tag], tr.flat.grad[off:off + n]), tag
+        assert snaps[tag].abs().sum().item() > 0, tag
