@@ -341,27 +341,39 @@ __global__ __launch_bounds__(WNTH, 3) void peg_wgrad_tile_kernel(const u16* __re
   float acc[27][2], accb[2] = {0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 27; ++i) acc[i][0] = acc[i][1] = 0.f;
-  u32x4 reg[LMAX * TNTH / WNTH];
-  plane_load<WNTH>(xin, g, D, b, h0, c0, 0, reg);
-  plane_store<WNTH>(ring, g.W, 0, reg);
-  __syncthreads();
+  // planes two steps ahead (regA = plane t+1, regB = plane t+2), this thread's dout one step
+  // ahead (one (row, segment) item per thread: wgrad_ok)
+  u32x4 regA[LMAX * TNTH / WNTH], regB[LMAX * TNTH / WNTH];
+  plane_load<WNTH>(xin, g, D, b, h0, c0, 0, regA);
+  plane_store<WNTH>(ring, g.W, 0, regA);
+  if (g.T > 1) plane_load<WNTH>(xin, g, D, b, h0, c0, 1, regA);
   const int ns = (g.W + SEGW - 1) / SEGW;
   const int items = HT * ns * 32;
+  const int o = threadIdx.x;
+  const int s = (o >> 5) % ns, r = (o >> 5) / ns;
+  const int h = h0 + r, w0 = s * SEGW;
+  const bool act = o < items && h < g.H;
+  auto dload = [&](int t, uint32_t (&u)[SEGW]) {
+#pragma unroll
+    for (int j = 0; j < SEGW; ++j) {
+      u[j] = 0;
+      if (act && w0 + j < g.W)
+        u[j] = *(const uint32_t*)(dout + (int64_t)canon(g, b, (t * g.H + h) * g.W + w0 + j) * D + c0 + pair * 2);
+    }
+  };
+  uint32_t du[SEGW], dn[SEGW];
+  dload(0, du);
+  __syncthreads();
   for (int t = 0; t < g.T; ++t) {
     const int tn = t + 1;
-    if (tn < g.T) plane_load<WNTH>(xin, g, D, b, h0, c0, tn, reg);
-    for (int o = threadIdx.x; o < items; o += WNTH) {
-      const int s = (o >> 5) % ns, r = (o >> 5) / ns;
-      const int h = h0 + r, w0 = s * SEGW;
+    if (tn + 1 < g.T) plane_load<WNTH>(xin, g, D, b, h0, c0, tn + 1, regB);
+    if (tn < g.T) dload(tn, dn);
+    if (act) {
       float dv[SEGW][2];
 #pragma unroll
       for (int j = 0; j < SEGW; ++j) {
-        const int wq = w0 + j;
-        uint32_t u = 0;
-        if (h < g.H && wq < g.W)
-          u = *(const uint32_t*)(dout + (int64_t)canon(g, b, (t * g.H + h) * g.W + wq) * D + c0 + pair * 2);
-        dv[j][0] = __uint_as_float(u << 16);
-        dv[j][1] = __uint_as_float(u & 0xffff0000u);
+        dv[j][0] = __uint_as_float(du[j] << 16);
+        dv[j][1] = __uint_as_float(du[j] & 0xffff0000u);
         accb[0] += dv[j][0];
         accb[1] += dv[j][1];
       }
@@ -392,7 +404,11 @@ __global__ __launch_bounds__(WNTH, 3) void peg_wgrad_tile_kernel(const u16* __re
       }
     }
     __syncthreads();   // slot of plane tn held plane tn - 3, read in this step
-    if (tn < g.T) plane_store<WNTH>(ring, g.W, tn, reg);
+    if (tn < g.T) plane_store<WNTH>(ring, g.W, tn, regA);
+#pragma unroll
+    for (int m = 0; m < LMAX * TNTH / WNTH; ++m) regA[m] = regB[m];
+#pragma unroll
+    for (int j = 0; j < SEGW; ++j) du[j] = dn[j];
     __syncthreads();
   }
   // fold the two (row, segment) items of a wave sharing a pair (lane bit 5), then the waves
@@ -417,7 +433,8 @@ __global__ __launch_bounds__(WNTH, 3) void peg_wgrad_tile_kernel(const u16* __re
 }
 
 bool tiled_ok(int W, int D) {
-  return D % 64 == 0 && HT * ((W + SEG - 1) / SEG) * 8 <= TNTH && (HT + 2) * (W + 2) * 8 <= LMAX * TNTH;
+  return D % 64 == 0 && HT * ((W + SEG - 1) / SEG) * 8 <= TNTH && (HT + 2) * (W + 2) * 8 <= LMAX * TNTH &&
+         HT * ((W + SEGW - 1) / SEGW) * 32 <= WNTH;   // wgrad: one item per thread
 }
 
 size_t tile_smem(int W) { return (size_t)NSLOT * plane_bytes(W) + (27 * 64 + 64) * 4; }
