@@ -123,7 +123,62 @@ __global__ void clip_scores_kernel(const float* __restrict__ t_raw, const float*
   }
 }
 
+// Zero-shot scoring (ct_clip/ctclip_inference.py:305-315 over the eval branch ct_clip.py:805-807):
+// one workgroup per image row n; the image latent is l2-normalised once, then every wave takes
+// prompt pairs j: s = temp * <t_norm, i_norm> for "present" (row 2j) and "not present" (2j+1),
+// prob = softmax over the pair, entry 0.  The image latent stays in LDS; F.normalize eps 1e-12.
+__global__ __launch_bounds__(256) void zero_shot_kernel(const float* __restrict__ t_raw, const float* __restrict__ i_raw,
+                                                        int P, int Dl, const float* __restrict__ log_temp,
+                                                        float* __restrict__ scores, float* __restrict__ probs) {
+  extern __shared__ float img[];
+  __shared__ float red[4];
+  const int n = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float ii = 0.f;
+  for (int k = threadIdx.x; k < Dl; k += 256) {
+    const float y = i_raw[(int64_t)n * Dl + k];
+    img[k] = y;
+    ii += y * y;
+  }
+  ii = warp_sum(ii);
+  if (lane == 0) red[w] = ii;
+  __syncthreads();
+  const float inorm = fmaxf(sqrtf(red[0] + red[1] + red[2] + red[3]), 1e-12f);
+  const float temp = expf(log_temp[0]);
+  for (int j = w; j < P; j += 4) {
+    float s[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float* t = t_raw + (int64_t)(2 * j + e) * Dl;
+      float tt = 0.f, ti = 0.f;
+      for (int k = lane; k < Dl; k += 64) {
+        const float x = t[k];
+        tt += x * x;
+        ti += x * img[k];
+      }
+      tt = warp_sum(tt);
+      ti = warp_sum(ti);
+      s[e] = ti / (fmaxf(sqrtf(tt), 1e-12f) * inorm) * temp;
+    }
+    if (lane == 0) {
+      const float m = fmaxf(s[0], s[1]), e0 = expf(s[0] - m), e1 = expf(s[1] - m);
+      scores[((int64_t)n * P + j) * 2] = s[0];
+      scores[((int64_t)n * P + j) * 2 + 1] = s[1];
+      probs[(int64_t)n * P + j] = e0 / (e0 + e1);
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" int ctclip_zero_shot(const float* t_raw, const float* i_raw, int32_t P, int32_t N, int32_t Dl,
+                                const float* log_temp, float* scores, float* probs, void* stream) {
+  CT_REQUIRE(P >= 0 && N >= 0 && Dl > 0 && Dl <= 8192, CT_ESHAPE);
+  if (P == 0 || N == 0) return 0;
+  hipLaunchKernelGGL(zero_shot_kernel, dim3(N), dim3(256), (size_t)Dl * 4, (hipStream_t)stream, t_raw, i_raw, P, Dl,
+                     log_temp, scores, probs);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int ctclip_clip_loss(const float* t_raw, const float* i_raw, int32_t Bg, int32_t Dl, const float* log_temp,
                                 float* t_norm, float* i_norm, float* loss, float* dt_raw, float* di_raw,

@@ -92,6 +92,7 @@ _SIGS = {
     'ctclip_vq_ema_finalize': [c_vp, c_vp, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp],
     'ctclip_clip_loss': [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     'ctclip_clip_scores': [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp],
+    'ctclip_zero_shot': [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp],
     'ctclip_sgemm': [c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_f32,
                      c_i32, c_f32, c_vp, c_i64, c_i64, c_i32, c_vp, c_i32, c_vp],
     'ctclip_embed_fwd': [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],

@@ -452,8 +452,29 @@ def clip_loss(t_raw, i_raw, log_temp):
     return loss, dt, di, dlt, tn, inn, sim
 
 
+def zero_shot(t_raw, i_raw, log_temp):
+    """Raw prompt latents [2P, Dl] (pairs present / not present) x raw image latents [N, Dl] ->
+    (probs [N, P], scores [N, P, 2]); ct_clip/ctclip_inference.py:305-315."""
+    P2, Dl = t_raw.shape
+    N = i_raw.shape[0]
+    if P2 % 2 or i_raw.shape[1] != Dl:
+        raise ValueError(f'zero_shot: prompt latents {tuple(t_raw.shape)} must be pairs of {tuple(i_raw.shape)} rows')
+    t_raw, i_raw = t_raw.float().contiguous(), i_raw.float().contiguous()
+    scores = torch.empty(N, P2 // 2, 2, device=t_raw.device, dtype=F32)
+    probs = torch.empty(N, P2 // 2, device=t_raw.device, dtype=F32)
+    call('ctclip_zero_shot', ptr(t_raw), ptr(i_raw), P2 // 2, N, Dl, ptr(log_temp.float().contiguous()), ptr(scores),
+         ptr(probs), stream_ptr())
+    return probs, scores
+
+
 def clip_scores(t_raw, i_raw, log_temp):
     B, Dl = t_raw.shape
+    if i_raw.shape[0] != B:
+        # einsum('b d, b d -> b') broadcasts a batch-1 operand (the zero-shot call,
+        # ct_clip/ctclip_inference.py:310: 2 prompts x 1 volume)
+        if i_raw.shape[0] != 1:
+            raise ValueError(f'clip_scores: batch {B} vs {i_raw.shape[0]} do not broadcast')
+        i_raw = i_raw.expand(B, Dl).contiguous()
     out = torch.empty(B, device=t_raw.device, dtype=F32)
     call('ctclip_clip_scores', ptr(t_raw), ptr(i_raw), B, Dl, ptr(log_temp), ptr(out), stream_ptr())
     return out

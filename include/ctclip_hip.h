@@ -194,6 +194,12 @@ int ctclip_clip_loss(const float* t_raw, const float* i_raw, int32_t Bg, int32_t
 /* eval branch einsum('b d, b d -> b') * temp (ct_clip.py:805-807) */
 int ctclip_clip_scores(const float* t_raw, const float* i_raw, int32_t B, int32_t Dl, const float* log_temp,
                        float* out, void* stream);
+/* zero-shot pathology scoring, replaces the per-volume x per-pathology loop of
+ * ct_clip/ctclip_inference.py:305-315 (CTCLIP.forward eval branch on a 2-prompt pair, softmax
+ * over the pair, 'present' entry): t_raw [2P][Dl] raw prompt latents (rows 2j / 2j+1 = "present" /
+ * "not present" of pathology j), i_raw [N][Dl] raw image latents -> scores [N][P][2], probs [N][P] */
+int ctclip_zero_shot(const float* t_raw, const float* i_raw, int32_t P, int32_t N, int32_t Dl, const float* log_temp,
+                     float* scores, float* probs, void* stream);
 
 /* ---------------------------------------------------------------- small exact-f32 GEMM (strided)
  * CPB MLP (attention.py:247-252,271-274) and its backward; act 1 = LeakyReLU(slope),

@@ -352,6 +352,39 @@ def eval_scores(sd, ids, mask, video, cfg: ClipConfig):
     return (out['text_latents'] * out['image_latents']).sum(-1) * sd['temperature'].exp()
 
 
+# ----------------------------------------------------------------------------- zero-shot
+# ct_clip/ctclip_inference.py:286-290
+PATHOLOGIES = ('Medical material', 'Arterial wall calcification', 'Cardiomegaly', 'Pericardial effusion',
+               'Coronary artery wall calcification', 'Hiatal hernia', 'Lymphadenopathy', 'Emphysema',
+               'Atelectasis', 'Lung nodule', 'Lung opacity', 'Pulmonary Embolism', 'Pleural effusion',
+               'Mosaic attenuation pattern', 'Peribronchial thickening', 'Consolidation', 'Bronchiectasis',
+               'Interlobular septal thickening')
+
+
+def zero_shot(sd, ids, mask, video, cfg: ClipConfig, force_ind=None):
+    """Zero-shot pathology scoring, the loop of ``ct_clip/ctclip_inference.py:291-318``: for each
+    volume (batch 1) and each pathology, the prompt pair ("<p> is present.", "<p> is not
+    present.") -- rows (2j, 2j+1) of ``ids`` / ``mask`` -- goes through ``CTCLIP.forward`` in eval
+    mode (``einsum('b d, b d -> b') * temp`` with the one image broadcast over the 2 texts,
+    ``ct_clip.py:805-807``), then ``softmax(dim=0)`` (``ctclip_inference.py:92-104,312``) and the
+    'present' entry is kept (``:315``).  The reference re-encodes the identical volume for every
+    pathology; eval mode is deterministic, so the volume is encoded once here.
+    Returns (probs [N, P], scores [N, P, 2])."""
+    n, P = video.shape[0], ids.shape[0] // 2
+    enc_text = bert_forward(sd, 'text_transformer.', ids, mask, cfg.bert)
+    temp = sd['temperature'].exp()
+    probs, scores = torch.empty(n, P), torch.empty(n, P, 2)
+    for v in range(n):
+        fi = None if force_ind is None else force_ind[v:v + 1]
+        enc_image, _, _, _ = ctvit_forward(sd, 'visual_transformer.', video[v:v + 1], cfg.vit, False, None, fi)
+        for j in range(P):
+            t_lat, i_lat = clip_latents(sd, enc_text[2 * j:2 * j + 2], enc_image)
+            s = (t_lat * i_lat).sum(-1) * temp                     # (2,): the image row broadcasts
+            scores[v, j] = s
+            probs[v, j] = torch.softmax(s, dim=0)[0]
+    return probs, scores
+
+
 # ----------------------------------------------------------------------------- weights recipe
 def trainable_prefixes():
     """``ct_clip/fine_tuning_ctclip.py:6-14``: only visual_transformer and text_transformer

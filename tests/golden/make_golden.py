@@ -210,12 +210,45 @@ def shrink_base(out_keys_keep=None):
     pass
 
 
+def run_zero_shot(V, C):
+    """Zero-shot fixture (tiny config): the reference's own eval loop of
+    ct_clip/ctclip_inference.py:305-315 -- per volume (batch 1) and per pathology, CTCLIP.forward on
+    the 2-prompt pair, softmax over the pair, keep entry 0.  Prompt ids are synthetic (the
+    CXR-BERT tokenizer is not available offline): rows (2j, 2j+1) = pathology j's pair."""
+    cfg = O.TINY
+    clip = build_reference(cfg, V, C)
+    sd = W.make_state_dict(cfg)
+    clip.load_state_dict(sd, strict=True)
+    clip.eval()
+    n, P = 2, 3
+    hu = W.make_hu(n, cfg.vit, seed=77)
+    video = O.normalize_hu(hu)
+    ids, mask = W.make_text(2 * P, 16, cfg.bert.vocab_size, seed=99, ragged=True)
+    probs, scores = torch.empty(n, P), torch.empty(n, P, 2)
+    with torch.no_grad():
+        for v in range(n):
+            for j in range(P):
+                s = clip(_Text(ids[2 * j:2 * j + 2], mask[2 * j:2 * j + 2]), video[v:v + 1], device='cpu')
+                scores[v, j] = s
+                probs[v, j] = torch.nn.Softmax(dim=0)(s)[0]
+    out = {'in.hu': hu, 'in.ids': ids, 'in.mask': mask, 'out.probs': probs, 'out.scores': scores}
+    path = os.path.join(HERE, 'golden_zeroshot_tiny.safetensors')
+    save_file({k: v.contiguous() for k, v in out.items()}, path,
+              metadata={'generator': 'tests/golden/make_golden.py --zero-shot',
+                        'reference': 'sharonct/CTPA-CLIP @ 2025-06-20 (ct_clip/ctclip_inference.py:305-315)'})
+    print('zero-shot probs', probs.tolist(), '->', path)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--base', action='store_true', help='also write the base-config B=2 fixture')
+    ap.add_argument('--zero-shot', action='store_true', help='only write the zero-shot fixture')
     args = ap.parse_args()
     torch.set_num_threads(os.cpu_count())
     A, V, C = import_reference()
+    if args.zero_shot:
+        run_zero_shot(V, C)
+        return
     run(O.TINY, batch=4, text_len=16, ragged=True, with_grads=True, tag='tiny', V=V, C=C,
         save_full_state=False)
     if args.base:

@@ -195,3 +195,38 @@ def test_grad_buckets_final_when_launched(setup):
     for tag, off, n in gs.buckets:
         assert torch.equal(snaps[tag], tr.flat.grad[off:off + n]), tag
         assert snaps[tag].abs().sum().item() > 0, tag
+
+
+def test_zero_shot_matches_oracle(setup):
+    """Zero-shot pathology scoring (ct_clip/ctclip_inference.py:305-315): the HIP path (prompt
+    latents once, one image encode per volume, ctclip_zero_shot kernel) vs the oracle's loop,
+    with the oracle forced onto the HIP path's VQ indices; probabilities / scores within 1e-3.
+    Also the reference's direct call shape: 2 prompts x 1 volume broadcast -> (2,) scores."""
+    cfg, model, hu, ids, mask, text = setup
+    from ctclip_mi355x.zero_shot import ZeroShotClassifier, PATHOLOGIES
+    P = 3
+    pids, pmask = W.make_text(2 * P, 32, cfg.bert.vocab_size, seed=99, ragged=True)
+    zs = ZeroShotClassifier(model, pathologies=PATHOLOGIES[:P])
+    zs.set_prompts(types.SimpleNamespace(input_ids=pids.cuda(), attention_mask=pmask.cuda()))
+    model.train()          # predict() must switch to eval (no EMA update) and restore the mode
+    cb0 = model.visual_transformer.vq._codebook.embed.detach().clone()
+    probs, scores = zs.predict(hu.cuda())
+    idx = model.visual_transformer.vq.state.last_indices.cpu()
+    assert model.training
+    assert torch.equal(cb0, model.visual_transformer.vq._codebook.embed)
+    torch.cuda.synchronize()
+    # the model's CURRENT weights (earlier tests in this module take optimizer steps)
+    sd = {k: v.detach().float().cpu() for k, v in model.state_dict().items()}
+    with torch.no_grad():
+        rp, rs = O.zero_shot(sd, pids, pmask, O.normalize_hu(hu), cfg, force_ind=idx.reshape(hu.shape[0], -1))
+    assert probs.shape == (hu.shape[0], P) and scores.shape == (hu.shape[0], P, 2)
+    assert (scores.cpu() - rs).abs().max().item() < 1e-3
+    assert (probs.cpu() - rp).abs().max().item() < 1e-3
+    # the reference's own per-pathology call: CTCLIP.forward(2 prompts, 1 volume) in eval mode
+    model.eval()
+    with torch.no_grad():
+        pair = types.SimpleNamespace(input_ids=pids[:2].cuda(), attention_mask=pmask[:2].cuda())
+        s2 = model(pair, hu[:1].cuda(), return_loss=False)
+    model.train()
+    assert s2.shape == (2,)
+    assert (s2.cpu() - scores[0, 0].cpu()).abs().max().item() < 1e-4

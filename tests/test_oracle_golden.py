@@ -104,3 +104,18 @@ def test_base_b2_matches_reference(golden_base):
     mism = (out['indices'].to(torch.int32) != g['out.vq_indices']).float().mean().item()
     assert mism < 1e-3, mism
     _close(out['loss'].reshape(1), g['out.loss'], 1e-4)
+
+
+def test_zero_shot_matches_reference():
+    """Zero-shot scoring (ct_clip/ctclip_inference.py:305-315, eval branch ct_clip.py:805-807):
+    the oracle's restatement (one image encode per volume) against the reference's own
+    per-volume x per-pathology loop (golden_zeroshot_tiny, tests/golden/make_golden.py --zero-shot)."""
+    from safetensors.torch import load_file
+    import os
+    g = load_file(os.path.join(os.path.dirname(__file__), 'golden', 'golden_zeroshot_tiny.safetensors'))
+    cfg = O.TINY
+    sd = W.make_state_dict(cfg)
+    probs, scores = O.zero_shot(sd, g['in.ids'], g['in.mask'], O.normalize_hu(g['in.hu']), cfg)
+    _close(scores, g['out.scores'], 1e-5)
+    _close(probs, g['out.probs'], 1e-6)
+    assert O.PATHOLOGIES[11] == 'Pulmonary Embolism' and len(O.PATHOLOGIES) == 18
