@@ -52,6 +52,17 @@ class AttnArgs(ctypes.Structure):
     ]
 
 
+class ResampleArgs(ctypes.Structure):
+    _fields_ = [
+        ('src', c_vp), ('src_dtype', c_i32),
+        ('D', c_i64), ('H', c_i64), ('W', c_i64), ('sd', c_i64), ('sh', c_i64), ('sw', c_i64),
+        ('Dn', c_i64), ('Hn', c_i64), ('Wn', c_i64), ('Do', c_i64), ('Ho', c_i64), ('Wo', c_i64),
+        ('od', c_i64), ('oh', c_i64), ('ow', c_i64),
+        ('slope', ctypes.c_double), ('intercept', ctypes.c_double),
+        ('mode', c_i32), ('fill', c_f32),
+    ]
+
+
 # name -> argtypes (restype is always int32)
 _SIGS = {
     'ctclip_version': [],
@@ -93,6 +104,7 @@ _SIGS = {
     'ctclip_clip_loss': [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     'ctclip_clip_scores': [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp],
     'ctclip_zero_shot': [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp],
+    'ctclip_resample_volume': [ctypes.POINTER(ResampleArgs), c_vp, c_vp],
     'ctclip_sgemm': [c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_f32,
                      c_i32, c_f32, c_vp, c_i64, c_i64, c_i32, c_vp, c_i32, c_vp],
     'ctclip_embed_fwd': [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],

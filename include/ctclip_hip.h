@@ -223,6 +223,32 @@ int ctclip_grad_norm(const float* g, int64_t n, float max_norm, float* part, int
 int ctclip_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
                 float wd, int32_t step, const float* coef, void* p_bf16, void* stream);
 
+/* ---------------------------------------------------------------- volume preprocessing
+ * Replaces the host-side per-sample loader arithmetic:
+ *   mode 0 = ct_clip/data.py:114-192 (CTReportDataset.npz_img_to_tensor after the metadata
+ *            lookup): slope*x + intercept -> resize_array (data.py:15-40, F.interpolate trilinear,
+ *            align_corners=False) -> clip(-1000, 1000) / 1000 -> centre crop / pad (fill) ->
+ *            (D, H, W) f32.  f64 arithmetic for int16 / f64 sources (numpy promotion), f32 for f32.
+ *   mode 1 = data_prep/preprocess_train.py:67-104 (process_file): f32(clip(slope*x + intercept) /
+ *            1000) -> resize_array in f32; output = the resized volume.
+ * The source is read through (d, h, w) element strides (the npz scan is (H, W, D): sd = 1,
+ * sh = W*D, sw = D).  Output voxel (d, h, w) takes resized voxel (d-od, h-oh, w-ow), or `fill`
+ * outside [0,Dn) x [0,Hn) x [0,Wn).  The host computes Dn/Hn/Wn and the offsets exactly as the
+ * reference does (ctclip_mi355x/preprocess.py). */
+enum { CTCLIP_F32 = 0, CTCLIP_I16 = 1, CTCLIP_F64 = 2 };
+typedef struct {
+  const void* src; int32_t src_dtype;
+  int64_t D, H, W;          /* source extents in the (d, h, w) view */
+  int64_t sd, sh, sw;       /* source strides, elements */
+  int64_t Dn, Hn, Wn;       /* resized extents (interpolation target) */
+  int64_t Do, Ho, Wo;       /* output extents */
+  int64_t od, oh, ow;       /* output index - resized index (crop / pad placement) */
+  double slope, intercept;
+  int32_t mode;
+  float fill;
+} ctclip_resample_args;
+int ctclip_resample_volume(const ctclip_resample_args* a, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

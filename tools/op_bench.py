@@ -36,7 +36,12 @@ def main():
     h = torch.randn(M, 2816, device='cuda').bfloat16()
     qs = torch.ones(32, device='cuda')
     dxf, dxb = torch.empty_like(xf), torch.empty_like(xb)
+    from ctclip_mi355x.preprocess import ct_volume_to_tensor
+    scan = torch.randint(-1100, 2000, (512, 512, 300), device='cuda', dtype=torch.int16)
+    vol = torch.empty(1, 240, 480, 480, device='cuda')
     cases = [
+        ('resample 512x512x300 i16 -> 240x480x480 (f64)',
+         lambda: ct_volume_to_tensor(scan, 1.0, -1024.0, 0.7, 1.25, out=vol), scan.numel() * 2 + vol.numel() * 4),
         ('ln_fwd f32->bf16', lambda: K.layernorm_fwd(xf, g, b, 1e-5), M * D * 6),
         ('ln_fwd f32->bf16+f32', lambda: K.layernorm_fwd(xf, g, b, 1e-5, out_f32=True), M * D * 10),
         ('ln_bwd', lambda: K.layernorm_bwd(xb, xb, mean, rstd, g, dres=xf), M * D * (2 + 2 + 4 + 4 + 2)),
