@@ -696,6 +696,219 @@ void launch_dkv(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
   else hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, false>), grid, dim3(NT), lds, st, p);
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Short sequences (L <= 32, head dim 32, no bias / key mask): the temporal transformer's
+// attention (24 frames per (b, h, w) sequence).  One WAVE per (sequence, head) holds the whole
+// problem: Q, K, V (and dO, O) of the pair are read once as MFMA row fragments (32 rows,
+// zero past L) and every product is a single 32-deep MFMA block set -- no online softmax, no key
+// loop.  The backward is fused (dQ, dK, dV in one pass, no delta pre-pass): it computes the
+// scores twice, in S^T layout (lane = query: P^T, dP^T, dS^T feed dQ^T = K^T dS^T) and in S
+// layout (lane = key: P, dP, dS feed dV^T = dO^T P and dK^T = Q^T dS), so every MFMA operand is
+// a row fragment (loaded straight from HBM in MFMA operand layout) or a ds_read_b64_tr_b16 column
+// fragment of a wave-private LDS image, and the accumulators are consumed where they lie.  Four
+// waves (four heads of one sequence) per workgroup.
+constexpr int SW = 4;                          // waves per workgroup
+constexpr int SIMG = 32 * Img<32>::RS;         // one 32 x 32 bf16 image (2,560 B)
+
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// row fragments of rows 16u + (lane & 15), d chunk lane >> 4 (zero past L): exactly the MFMA
+// operand layout of rowfrag(), read straight from HBM (16 B per lane per block)
+__device__ __forceinline__ void load_rows(bf16x8 (&f)[2], const u16* x, int64_t ld, const AP& p, int s, int h,
+                                          int lane) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int r = 16 * u + (lane & 15);
+    f[u] = r < p.L ? gload8(x + seq_row(p, s, r) * ld + h * 32 + 8 * (lane >> 4)) : zero8();
+  }
+}
+
+// the same fragments into a wave-private image (for the trfrag column reads)
+__device__ __forceinline__ void put_rows(char* img, const bf16x8 (&f)[2], int lane) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) *(bf16x8*)(img + (16 * u + (lane & 15)) * Img<32>::RS + (lane >> 4) * 16) = f[u];
+}
+
+__global__ __launch_bounds__(SW * 64) void attn_small_fwd_kernel(AP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int pair = blockIdx.x * SW + w;
+  if (pair >= p.nseq * p.H) return;            // wave-uniform; no workgroup barriers below
+  const int s = pair / p.H, h = pair - s * p.H;
+  char* Vi = smem + w * SIMG;
+  bf16x8 qr[2], kr[2], vr[2];
+  load_rows(qr, p.q, p.ldq, p, s, h, lane);
+  load_rows(kr, p.k, p.ldk, p, s, h, lane);
+  load_rows(vr, p.v, p.ldv, p, s, h, lane);
+  put_rows(Vi, vr, lane);
+  const int i = lane & 15, g = lane >> 4;
+  const float c2 = p.scale * LOG2E;
+  const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
+  // S^T blocks (key block kb, query block qb): lane column = query 16qb + i, rows = keys 16kb + 4g + r
+  f32x4 st[2][2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) st[kb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr[kb], qr[qb], z4, 0, 0, 0);
+  wave_lds_sync();
+  // V^T column fragments (d block db): lane row d = 16db + i, keys 4g + 0..3 and 16 + 4g + 0..3
+  const bf16x8 vt[2] = {trfrag<32>(Vi, 0, 0, lane), trfrag<32>(Vi, 0, 16, lane)};
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float x = (16 * kb + 4 * g + r < p.L) ? st[kb][qb][r] * c2 : -INFINITY;
+        st[kb][qb][r] = x;
+        m = fmaxf(m, x);
+      }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = fexp2(st[kb][qb][r] - m);
+        st[kb][qb][r] = e;
+        l += e;
+      }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const bf16x8 pf = pack_perm(st[0][qb], st[1][qb]);       // P^T: keys in the trfrag order
+    const int q = 16 * qb + i;
+    const float inv = 1.f / l;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      // O^T block: lane column = query q, rows d = 16db + 4g + r
+      const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt[db], pf, z4, 0, 0, 0);
+      if (q < p.L) {
+        const float o4[4] = {ot[0] * inv, ot[1] * inv, ot[2] * inv, ot[3] * inv};
+        *(uint2*)(p.out + seq_row(p, s, q) * p.ldout + h * 32 + 16 * db + 4 * g) = pack4(o4);
+      }
+    }
+    if (g == 0 && q < p.L && p.lse) p.lse[(int64_t)h * p.M + seq_row(p, s, q)] = (m + __log2f(l)) * LN2;
+  }
+}
+
+__global__ __launch_bounds__(SW * 64) void attn_small_bwd_kernel(AP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int pair = blockIdx.x * SW + w;
+  if (pair >= p.nseq * p.H) return;
+  const int s = pair / p.H, h = pair - s * p.H;
+  char* Qi = smem + w * (3 * SIMG + 256);
+  char* Ki = Qi + SIMG;
+  char* Di = Ki + SIMG;                         // dO
+  float* lse2 = (float*)(Di + SIMG);            // [32] lse * log2 e (+inf past L)
+  float* dlt = lse2 + 32;                       // [32] delta = rowsum(dO * O)
+  const int i = lane & 15, g = lane >> 4;
+  bf16x8 qr[2], kr[2], vr[2], dr[2], orr[2];
+  load_rows(qr, p.q, p.ldq, p, s, h, lane);
+  load_rows(kr, p.k, p.ldk, p, s, h, lane);
+  load_rows(vr, p.v, p.ldv, p, s, h, lane);
+  load_rows(dr, p.dout, p.lddo, p, s, h, lane);
+  load_rows(orr, p.o, p.ldo, p, s, h, lane);
+  float lq[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = 16 * u + i;
+    lq[u] = q < p.L ? p.lse[(int64_t)h * p.M + seq_row(p, s, q)] * LOG2E : INFINITY;
+  }
+  put_rows(Qi, qr, lane);
+  put_rows(Ki, kr, lane);
+  put_rows(Di, dr, lane);
+  // delta per query row 16u + i: partial dot of this lane's 8 d, summed over the 4 chunks g
+  float dq[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    float dd = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dd += (float)orr[u][e] * (float)dr[u][e];
+    dd += __shfl_xor(dd, 16, 64);
+    dd += __shfl_xor(dd, 32, 64);
+    dq[u] = dd;
+    if (g == 0) {
+      dlt[16 * u + i] = dd;
+      lse2[16 * u + i] = lq[u];
+    }
+  }
+  const float c2 = p.scale * LOG2E;
+  const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
+  // ---- S^T layout (lane = query): dQ^T[d][q] = scale * sum_k K^T[d][k] dS^T[k][q]
+  bf16x8 dsf[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    f32x4 ds[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      const f32x4 sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr[kb], qr[qb], z4, 0, 0, 0);
+      const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vr[kb], dr[qb], z4, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool kv = 16 * kb + 4 * g + r < p.L;
+        const float pr = kv ? fexp2(sv[r] * c2 - lq[qb]) : 0.f;   // 0 for padded queries (lq = +inf)
+        ds[kb][r] = pr * (dp[r] - dq[qb]);
+      }
+    }
+    dsf[qb] = pack_perm(ds[0], ds[1]);
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int q = 16 * qb + i;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag<32>(Ki, 0, 16 * db, lane), dsf[qb], z4, 0, 0, 0);
+      if (q < p.L) {
+        const float d4[4] = {acc[0] * p.scale, acc[1] * p.scale, acc[2] * p.scale, acc[3] * p.scale};
+        *(uint2*)(p.dq + seq_row(p, s, q) * p.lddq + h * 32 + 16 * db + 4 * g) = pack4(d4);
+      }
+    }
+  }
+  // ---- S layout (lane = key): dV^T = dO^T P, dK^T = scale * Q^T dS
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb) {
+    const int k = 16 * kb + i;
+    const bool kv = k < p.L;
+    f32x4 pm[2], ds[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const f32x4 sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qr[qb], kr[kb], z4, 0, 0, 0);
+      const f32x4 dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dr[qb], vr[kb], z4, 0, 0, 0);
+      const f32x4 l4 = *(const f32x4*)(lse2 + 16 * qb + 4 * g);
+      const f32x4 d4 = *(const f32x4*)(dlt + 16 * qb + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pr = kv ? fexp2(sv[r] * c2 - l4[r]) : 0.f;
+        pm[qb][r] = pr;
+        ds[qb][r] = pr * (dp[r] - d4[r]);
+      }
+    }
+    const bf16x8 pf = pack_perm(pm[0], pm[1]), dsk = pack_perm(ds[0], ds[1]);
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const f32x4 dv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag<32>(Di, 0, 16 * db, lane), pf, z4, 0, 0, 0);
+      const f32x4 dk = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag<32>(Qi, 0, 16 * db, lane), dsk, z4, 0, 0, 0);
+      if (kv) {
+        const int64_t row = seq_row(p, s, k);
+        const float v4[4] = {dv[0], dv[1], dv[2], dv[3]};
+        const float k4[4] = {dk[0] * p.scale, dk[1] * p.scale, dk[2] * p.scale, dk[3] * p.scale};
+        *(uint2*)(p.dv + row * p.lddv + h * 32 + 16 * db + 4 * g) = pack4(v4);
+        *(uint2*)(p.dk + row * p.lddk + h * 32 + 16 * db + 4 * g) = pack4(k4);
+      }
+    }
+  }
+}
+
+bool small_ok(const AP& p, int D) { return D == 32 && p.L <= 32 && !p.bias_u && !p.kmask; }
+
 }  // namespace
 
 extern "C" int ctclip_attn_fwd(const ctclip_attn_args* a, void* stream) {
@@ -705,6 +918,12 @@ extern "C" int ctclip_attn_fwd(const ctclip_attn_args* a, void* stream) {
   if (!s_attr) { set_attrs(); s_attr = true; }
   const int Lp = (p.L + 31) & ~31;
   const int pairs = p.nseq * p.H;
+  if (small_ok(p, a->D)) {
+    hipLaunchKernelGGL(attn_small_fwd_kernel, dim3(cdiv(pairs, SW)), dim3(SW * 64), (size_t)SW * SIMG,
+                       (hipStream_t)stream, p);
+    CT_CHECK_LAUNCH();
+    return 0;
+  }
   const size_t RSb = a->D * 2 + 16;
   const size_t lds = (size_t)p.pp * 2 * Lp * RSb + table_bytes(p, Lp, false);
   if (lds > 160 * 1024) return CT_ESHAPE;
@@ -728,6 +947,12 @@ extern "C" int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream) {
   if (lds1 > 160 * 1024 || lds2 > 160 * 1024) return CT_ESHAPE;
   dim3 grid(cdiv(pairs, p.pp));
   hipStream_t st = (hipStream_t)stream;
+  if (small_ok(p, a->D)) {
+    hipLaunchKernelGGL(attn_small_bwd_kernel, dim3(cdiv(pairs, SW)), dim3(SW * 64), (size_t)SW * (3 * SIMG + 256), st,
+                       p);
+    CT_CHECK_LAUNCH();
+    return 0;
+  }
   const int nc = Lp / 32;
   if (a->D == 32 && p.bias_u && p.dbias_u && !p.kmask && (nc + 1) / 2 <= 9) {
     // frame-inner dQ + bias-gradient kernel (see attn_bwd_dq_bias_kernel)

@@ -137,7 +137,7 @@ def _cpb_table(H, gh, gw):
     return u, bins
 
 
-@pytest.mark.parametrize('case', ['spatial', 'spatial_small', 'temporal', 'bert'])
+@pytest.mark.parametrize('case', ['spatial', 'spatial_small', 'temporal', 'temporal_l5_h3', 'temporal_l32', 'bert'])
 def test_attention(K, case):
     torch.manual_seed(3)
     if case.startswith('spatial'):
@@ -150,9 +150,11 @@ def test_attention(K, case):
         bias = u[:, bins]
         kmask = None
         grid = (gh, gw)
-    elif case == 'temporal':
-        B, T, HW = 2, 24, 20
-        L, H, D, nseq = T, 8, 32, B * HW
+    elif case.startswith('temporal'):
+        # fused short-sequence kernels (attn_small_*): L <= 32, one wave per (sequence, head);
+        # ragged pair counts (nseq * H not a multiple of the 4 waves of a workgroup)
+        B, T, HW, H = {'temporal': (2, 24, 20, 8), 'temporal_l5_h3': (1, 5, 7, 3), 'temporal_l32': (3, 32, 3, 8)}[case]
+        L, D, nseq = T, 32, B * HW
         M = B * T * HW
         seq = (HW, T * HW, 1, HW)
         scale, u, bias, kmask, grid = 8.0, None, None, None, (0, 0)
