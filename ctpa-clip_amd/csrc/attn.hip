@@ -120,7 +120,7 @@ __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(
 //   ub[nbins]  bias table * log2 e        (BIAS)
 //   kb[Lp]     position table             (BIAS)
 //   madd[pp][Lp] additive key validity     (0 / -inf: padding past L, key mask)
-template <bool BIAS>
+template <bool BIAS, int NTH = NT>
 __device__ __forceinline__ void load_tables(const AP& p, char* tab, int Lp, int tid, int h, float*& ub, int*& kb,
                                             float*& madd) {
   char* t = tab;
@@ -129,14 +129,14 @@ __device__ __forceinline__ void load_tables(const AP& p, char* tab, int Lp, int 
     t += ((p.nbins + 3) & ~3) * 4;   // keep kb / madd 16-B aligned for the vector reads
     kb = (int*)t;
     t += Lp * 4;
-    for (int i = tid; i < p.nbins; i += NT) ub[i] = p.bias_u[(int64_t)h * p.nbins + i] * LOG2E;
-    for (int i = tid; i < Lp; i += NT) kb[i] = i < p.L ? kb_of(p, i) : 0;
+    for (int i = tid; i < p.nbins; i += NTH) ub[i] = p.bias_u[(int64_t)h * p.nbins + i] * LOG2E;
+    for (int i = tid; i < Lp; i += NTH) kb[i] = i < p.L ? kb_of(p, i) : 0;
   }
   madd = (float*)t;
   for (int pl = 0; pl < p.pp; ++pl) {
     const int pair = blockIdx.x * p.pp + pl;
     const int s = pair / p.H;
-    for (int i = tid; i < Lp; i += NT) {
+    for (int i = tid; i < Lp; i += NTH) {
       bool v = i < p.L && pair < p.nseq * p.H;
       if (v && p.kmask) v = p.kmask[(int64_t)s * p.L + i] != 0;
       madd[pl * Lp + i] = v ? 0.f : -INFINITY;
@@ -145,26 +145,28 @@ __device__ __forceinline__ void load_tables(const AP& p, char* tab, int Lp, int 
 }
 
 // ------------------------------------------------------------------------------------ forward
-template <int D, bool BIAS>
-__global__ __launch_bounds__(NT) void attn_fwd_kernel(AP p) {
+// W waves per workgroup: 12 for the spatial (BIAS) shapes, whose 36 query blocks then split
+// evenly (3 per wave) at 12 waves per CU; 8 otherwise.
+template <int D, bool BIAS, int W = (BIAS ? 12 : NW)>
+__global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int KK = D / 32, DB = D / 16, RS = Img<D>::RS;
+  constexpr int KK = D / 32, DB = D / 16, RS = Img<D>::RS, NTH = W * 64;
   const int L = p.L, Lp = (L + 31) & ~31;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wpp = NW / p.pp;                         // waves per pair
+  const int wpp = W / p.pp;                          // waves per pair
   const int pair_local = w / wpp, wi = w - pair_local * wpp;
   const int pair_bytes = 2 * Lp * RS;
   for (int pl = 0; pl < p.pp; ++pl) {
     const int pair = blockIdx.x * p.pp + pl;
     if (pair >= p.nseq * p.H) break;
     const int s = pair / p.H, h = pair - s * p.H;
-    stage<D>(smem + pl * pair_bytes, p.k, p.ldk, p, s, h, Lp, tid, NT);
-    stage<D>(smem + pl * pair_bytes + Lp * RS, p.v, p.ldv, p, s, h, Lp, tid, NT);
+    stage<D>(smem + pl * pair_bytes, p.k, p.ldk, p, s, h, Lp, tid, NTH);
+    stage<D>(smem + pl * pair_bytes + Lp * RS, p.v, p.ldv, p, s, h, Lp, tid, NTH);
   }
   float* ub = nullptr;
   int* kb = nullptr;
   float* madd = nullptr;
-  load_tables<BIAS>(p, smem + p.pp * pair_bytes, Lp, tid, blockIdx.x % p.H, ub, kb, madd);  // pp == 1 with BIAS
+  load_tables<BIAS, NTH>(p, smem + p.pp * pair_bytes, Lp, tid, blockIdx.x % p.H, ub, kb, madd);  // pp == 1 with BIAS
   __syncthreads();
   const int pair = blockIdx.x * p.pp + pair_local;
   if (pair >= p.nseq * p.H) return;
@@ -369,13 +371,14 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(AP p) {
 // ----------------------------------------------------------------------------- backward dK dV
 // lane owns a key; elements run over queries.  Padded queries carry lse = +inf (probability 0);
 // a masked / padded key adds -inf through kadd.
-template <int D, bool BIAS>
-__global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(AP p) {
+// W waves per workgroup as in attn_fwd_kernel (12 for the spatial shapes: 3 key blocks per wave)
+template <int D, bool BIAS, int W = (BIAS ? 12 : NW)>
+__global__ __launch_bounds__(W * 64) void attn_bwd_dkv_kernel(AP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int KK = D / 32, DB = D / 16, RS = Img<D>::RS;
+  constexpr int KK = D / 32, DB = D / 16, RS = Img<D>::RS, NTH = W * 64;
   const int L = p.L, Lp = (L + 31) & ~31;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wpp = NW / p.pp;
+  const int wpp = W / p.pp;
   const int pair_local = w / wpp, wi = w - pair_local * wpp;
   const int pair_bytes = 2 * Lp * RS + 2 * Lp * 4;
   for (int pl = 0; pl < p.pp; ++pl) {
@@ -383,11 +386,11 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(AP p) {
     if (pair >= p.nseq * p.H) break;
     const int s = pair / p.H, h = pair - s * p.H;
     char* base = smem + pl * pair_bytes;
-    stage<D>(base, p.q, p.ldq, p, s, h, Lp, tid, NT);
-    stage<D>(base + Lp * RS, p.dout, p.lddo, p, s, h, Lp, tid, NT);
+    stage<D>(base, p.q, p.ldq, p, s, h, Lp, tid, NTH);
+    stage<D>(base + Lp * RS, p.dout, p.lddo, p, s, h, Lp, tid, NTH);
     float* ls = (float*)(base + 2 * Lp * RS);
     float* dls = ls + Lp;
-    for (int i = tid; i < Lp; i += NT) {
+    for (int i = tid; i < Lp; i += NTH) {
       const bool v = i < L;
       const int64_t r = v ? seq_row(p, s, i) : 0;
       ls[i] = v ? p.lse[(int64_t)h * p.M + r] * LOG2E : INFINITY;
@@ -397,7 +400,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dkv_kernel(AP p) {
   float* ub = nullptr;
   int* kb = nullptr;
   float* madd = nullptr;
-  load_tables<BIAS>(p, smem + p.pp * pair_bytes, Lp, tid, blockIdx.x % p.H, ub, kb, madd);
+  load_tables<BIAS, NTH>(p, smem + p.pp * pair_bytes, Lp, tid, blockIdx.x % p.H, ub, kb, madd);
   __syncthreads();
   const int pair = blockIdx.x * p.pp + pair_local;
   if (pair >= p.nseq * p.H) return;
@@ -680,7 +683,7 @@ size_t table_bytes(const AP& p, int Lp, bool bins) {
 
 template <int D>
 void launch_fwd(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
-  if (p.bias_u) hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(NT), lds, st, p);
+  if (p.bias_u) hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(12 * 64), lds, st, p);
   else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(NT), lds, st, p);
 }
 
@@ -692,7 +695,7 @@ void launch_dq(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
 
 template <int D>
 void launch_dkv(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
-  if (p.bias_u) hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, true>), grid, dim3(NT), lds, st, p);
+  if (p.bias_u) hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, true>), grid, dim3(12 * 64), lds, st, p);
   else hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, false>), grid, dim3(NT), lds, st, p);
 }
 
