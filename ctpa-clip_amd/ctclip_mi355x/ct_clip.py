@@ -14,6 +14,7 @@ import torch
 from torch import nn
 
 from . import functional as Fn
+from . import streams
 
 
 def l2norm(t):
@@ -79,11 +80,10 @@ class CTCLIP(nn.Module):
         """Text + image towers and raw latents: (enc_text (B,L,768), pooled (B, h*w*d),
         text_raw (B, dl), image_raw (B, dl))."""
         # image tower first: the text tower's nodes are then newer, so the backward runs BERT
-        # first and its gradient bucket all-reduces under the 3D-ViT backward (dist_sync)
+        # first and its gradient bucket all-reduces under the 3D-ViT backward (dist_sync).  BERT
+        # itself runs on the text stream, beside the image tower (streams.py).
         pooled, pooled_b = self.visual_transformer.encode_pooled(image)
-        enc_text = self.text_transformer(text.input_ids, attention_mask=text.attention_mask)[0]
-        cls = enc_text[:, 0, :]
-        t_raw = Fn.TextProjFn.apply(cls.contiguous() if not cls.is_contiguous() else cls, self.to_text_latent.weight)
+        enc_text, t_raw = self._text(text, image.device)
         W = self.to_visual_latent.weight
         i_raw = self._project(W, self._visual_weight_bf16(W), pooled, pooled_b)
         return enc_text, pooled, t_raw, i_raw
@@ -111,6 +111,26 @@ class CTCLIP(nn.Module):
             from . import kernels as K
             return K.clip_scores(t_raw.contiguous(), i_raw.contiguous(), self.temperature.detach().reshape(1))
         return Fn.ClipLossFn.apply(t_raw, i_raw, self.temperature)
+
+    def _text(self, text, dev):
+        """BERT + CLS projection, on the text stream when there is one: (enc_text, text_raw)."""
+        ts = streams.text_stream(dev)
+        ids, mask = text.input_ids, text.attention_mask
+        if ts is None:
+            enc_text = self.text_transformer(ids, attention_mask=mask)[0]
+            return enc_text, Fn.TextProjFn.apply(enc_text[:, 0, :].contiguous(), self.to_text_latent.weight)
+        main = torch.cuda.current_stream(dev)
+        ts.wait_stream(main)                      # ids / mask (and the weights) are ready
+        for t in (ids, mask):
+            if t is not None and t.is_cuda:
+                t.record_stream(ts)
+        with torch.cuda.stream(ts):
+            enc_text = self.text_transformer(ids, attention_mask=mask)[0]
+            t_raw = Fn.TextProjFn.apply(enc_text[:, 0, :].contiguous(), self.to_text_latent.weight)
+        main.wait_stream(ts)                      # the loss / scores read them on the main stream
+        enc_text.record_stream(main)
+        t_raw.record_stream(main)
+        return enc_text, t_raw
 
     def grad_buckets(self):
         """Gradient all-reduce buckets in the order the backward finalises them (dist_sync)."""

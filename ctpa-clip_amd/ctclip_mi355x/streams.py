@@ -1,0 +1,35 @@
+"""The text tower's own HIP stream.
+
+BERT at 8 x 128 tokens is a chain of small launches (M = 1,024 rows: a few dozen workgroups
+each) that leave most of the 256 CUs idle, while the 3D-ViT's launches fill the chip.  The two
+towers are independent until the loss, so ``CTCLIP.encode`` enqueues BERT (and the CLS
+projection) on this second stream right after the image tower: the dispatcher runs BERT's
+workgroups beside the ViT's.  Autograd runs every node's backward on the stream of its forward,
+so BERT's backward (first in autograd order) also overlaps the ViT backward, and
+its gradient bucket's all-reduce is ordered after it on this stream.
+``CTCLIP_TEXT_STREAM=0`` keeps everything on the current stream."""
+from __future__ import annotations
+
+import os
+
+import torch
+
+ENABLED = os.environ.get('CTCLIP_TEXT_STREAM', '1') != '0'
+_STREAMS = {}
+
+
+def text_stream(dev):
+    """The text-tower stream of ``dev`` (None when disabled or not a GPU device)."""
+    if not ENABLED or dev.type != 'cuda':
+        return None
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx not in _STREAMS:
+        _STREAMS[idx] = torch.cuda.Stream(idx)
+    return _STREAMS[idx]
+
+
+def join_text(dev):
+    """Order the current stream after all work queued on the text stream so far."""
+    s = text_stream(dev)
+    if s is not None:
+        torch.cuda.current_stream(dev).wait_stream(s)

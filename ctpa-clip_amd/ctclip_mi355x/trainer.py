@@ -11,6 +11,7 @@ from __future__ import annotations
 import torch
 
 from . import dist_sync
+from . import streams
 from . import kernels as K
 
 
@@ -106,7 +107,9 @@ class CTClipTrainer:
 
     def optimizer_step(self):
         # SUM (ClipLossFn gives each rank its own rows): buckets already in flight since their
-        # tower's backward finished; the last one goes out here and all are waited on
+        # tower's backward finished; the last one goes out here and all are waited on.  BERT's
+        # backward ran on the text stream (streams.py): order the norm / Adam after it.
+        streams.join_text(self.device)
         self.grad_sync.finish()
         K.grad_norm(self.flat.grad, self.max_grad_norm if self.max_grad_norm else 0.0, self.norm)
         self.steps += 1
