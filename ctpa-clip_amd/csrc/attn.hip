@@ -960,7 +960,18 @@ extern "C" int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream) {
   if (a->D == 32 && p.bias_u && p.dbias_u && !p.kmask && (nc + 1) / 2 <= 9) {
     // frame-inner dQ + bias-gradient kernel (see attn_bwd_dq_bias_kernel)
     const int nqg = cdiv(p.L, 64);
-    int nfc = std::max(1, std::min(p.nseq, (2 * 256 + p.H * nqg - 1) / (p.H * nqg)));
+    // frame chunks: at least two workgroups per CU, then (up to twice that) the count whose last
+    // dispatch round is fullest -- 72 x 14 = 1,008 workgroups = 3.94 rounds of 256 at the base
+    // shape (measured: nfc 8 / 14 / 28 -> spatial backward 1,109 / 1,074 / 1,242 us)
+    const int per = p.H * nqg;
+    const int lo = std::max(1, std::min(p.nseq, (2 * 256 + per - 1) / per));
+    int nfc = lo;
+    double best = 0.0;
+    for (int f = lo; f <= std::min(p.nseq, 2 * lo); ++f) {
+      const long wgs = (long)per * f, rounds = (wgs + 255) / 256;
+      const double eff = (double)wgs / (double)(rounds * 256);
+      if (eff > best + 1e-3) { best = eff; nfc = f; }
+    }
     const size_t lds = (size_t)2 * Lp * RSb + 2 * (size_t)((p.nbins + 3) & ~3) * 4 + 2 * (size_t)Lp * 4 +
                        4 * 64 * 8 * 4;
     if (lds > 160 * 1024) return CT_ESHAPE;

@@ -15,6 +15,7 @@ from torch import nn
 
 from . import dist_sync
 from . import functional as Fn
+from . import streams
 
 
 @dataclass
@@ -98,7 +99,30 @@ class BertModel(nn.Module):
             if isinstance(m, nn.Linear):
                 nn.init.zeros_(m.bias)
 
-    def forward(self, input_ids, attention_mask=None, **_):
+    def forward(self, input_ids, attention_mask=None, ready=None, **_):
+        """Runs on the text stream (streams.py) when there is one: ordered after ``ready`` (an event
+        of the calling stream; default: everything queued on it so far) and after the previous
+        optimizer step's Adam of these weights (queued on the text stream); the calling stream
+        waits for the result before it returns.  Backward nodes run on the same text stream."""
+        dev = input_ids.device
+        ts = streams.text_stream(dev)
+        if ts is None:
+            return self._forward(input_ids, attention_mask)
+        cur = torch.cuda.current_stream(dev)
+        if ready is not None:
+            ts.wait_event(ready)
+        else:
+            ts.wait_stream(cur)
+        for t in (input_ids, attention_mask):
+            if t is not None and t.is_cuda:
+                t.record_stream(ts)
+        with torch.cuda.stream(ts):
+            out = self._forward(input_ids, attention_mask)
+        cur.wait_stream(ts)
+        out[0].record_stream(cur)
+        return out
+
+    def _forward(self, input_ids, attention_mask=None):
         c = self.config
         B, L = input_ids.shape
         ids = input_ids.to(torch.int64).contiguous()

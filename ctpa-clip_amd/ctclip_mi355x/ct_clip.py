@@ -82,8 +82,9 @@ class CTCLIP(nn.Module):
         # image tower first: the text tower's nodes are then newer, so the backward runs BERT
         # first and its gradient bucket all-reduces under the 3D-ViT backward (dist_sync).  BERT
         # itself runs on the text stream, beside the image tower (streams.py).
+        ready = torch.cuda.current_stream(image.device).record_event() if streams.text_stream(image.device) else None
         pooled, pooled_b = self.visual_transformer.encode_pooled(image)
-        enc_text, t_raw = self._text(text, image.device)
+        enc_text, t_raw = self._text(text, image.device, ready)
         W = self.to_visual_latent.weight
         i_raw = self._project(W, self._visual_weight_bf16(W), pooled, pooled_b)
         return enc_text, pooled, t_raw, i_raw
@@ -112,25 +113,12 @@ class CTCLIP(nn.Module):
             return K.clip_scores(t_raw.contiguous(), i_raw.contiguous(), self.temperature.detach().reshape(1))
         return Fn.ClipLossFn.apply(t_raw, i_raw, self.temperature)
 
-    def _text(self, text, dev):
-        """BERT + CLS projection, on the text stream when there is one: (enc_text, text_raw)."""
-        ts = streams.text_stream(dev)
-        ids, mask = text.input_ids, text.attention_mask
-        if ts is None:
-            enc_text = self.text_transformer(ids, attention_mask=mask)[0]
-            return enc_text, Fn.TextProjFn.apply(enc_text[:, 0, :].contiguous(), self.to_text_latent.weight)
-        main = torch.cuda.current_stream(dev)
-        ts.wait_stream(main)                      # ids / mask (and the weights) are ready
-        for t in (ids, mask):
-            if t is not None and t.is_cuda:
-                t.record_stream(ts)
-        with torch.cuda.stream(ts):
-            enc_text = self.text_transformer(ids, attention_mask=mask)[0]
-            t_raw = Fn.TextProjFn.apply(enc_text[:, 0, :].contiguous(), self.to_text_latent.weight)
-        main.wait_stream(ts)                      # the loss / scores read them on the main stream
-        enc_text.record_stream(main)
-        t_raw.record_stream(main)
-        return enc_text, t_raw
+    def _text(self, text, dev, ready=None):
+        """BERT (on the text stream, see BertModel.forward) + CLS projection: (enc_text, text_raw).
+        ``ready``: an event recorded on the main stream BEFORE the image tower was queued (ids,
+        mask and weights are ready there), so BERT does not wait for the image tower."""
+        enc_text = self.text_transformer(text.input_ids, attention_mask=text.attention_mask, ready=ready)[0]
+        return enc_text, Fn.TextProjFn.apply(enc_text[:, 0, :].contiguous(), self.to_text_latent.weight)
 
     def grad_buckets(self):
         """Gradient all-reduce buckets in the order the backward finalises them (dist_sync)."""

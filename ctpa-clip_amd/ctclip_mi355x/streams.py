@@ -6,7 +6,9 @@ towers are independent until the loss, so ``CTCLIP.encode`` enqueues BERT (and t
 projection) on this second stream right after the image tower: the dispatcher runs BERT's
 workgroups beside the ViT's.  Autograd runs every node's backward on the stream of its forward,
 so BERT's backward (first in autograd order) also overlaps the ViT backward, and
-its gradient bucket's all-reduce is ordered after it on this stream.
+its gradient bucket's all-reduce is ordered after it on this stream.  The optimizer step queues
+the text bucket's Adam here too, so the next step's image tower does not wait for it (the next
+BertModel.forward, on this stream, does).
 ``CTCLIP_TEXT_STREAM=0`` keeps everything on the current stream."""
 from __future__ import annotations
 

@@ -113,9 +113,28 @@ class CTClipTrainer:
         self.grad_sync.finish()
         K.grad_norm(self.flat.grad, self.max_grad_norm if self.max_grad_norm else 0.0, self.norm)
         self.steps += 1
-        K.adam(self.flat.data, self.flat.grad, self.m, self.v, lr=self.lr, b1=self.betas[0], b2=self.betas[1],
-               eps=self.eps, wd=self.wd, step=self.steps, coef=self.norm)
-        self.flat.grad.zero_()
+        # the text bucket's Adam (and grad reset) goes on the text stream: the next step's image
+        # tower does not wait for it, the next step's BERT (same stream) does
+        ts = streams.text_stream(self.device)
+        text = [b for b in self.grad_sync.buckets if b[0] == 'text'] if ts is not None else []
+        done = []
+        if text:
+            _, off, n = text[0]
+            ts.wait_stream(torch.cuda.current_stream(self.device))   # clip coefficient ready
+            with torch.cuda.stream(ts):
+                self._adam(off, n)
+            done.append((off, n))
+        lo = 0
+        for off, n in sorted(done) + [(self.flat.numel, 0)]:
+            if off > lo:
+                self._adam(lo, off - lo)
+            lo = off + n
+
+    def _adam(self, off, n):
+        sl = slice(off, off + n)
+        K.adam(self.flat.data[sl], self.flat.grad[sl], self.m[sl], self.v[sl], lr=self.lr, b1=self.betas[0],
+               b2=self.betas[1], eps=self.eps, wd=self.wd, step=self.steps, coef=self.norm)
+        self.flat.grad[sl].zero_()
 
     def train_step(self, text, video):
         """One contrastive step; returns the loss tensor (no host sync)."""
