@@ -2,9 +2,9 @@
 
 BERT at 8 x 128 tokens is a chain of small launches (M = 1,024 rows: a few dozen workgroups
 each) that leave most of the 256 CUs idle, while the 3D-ViT's launches fill the chip.  The two
-towers are independent until the loss, so ``CTCLIP.encode`` enqueues BERT (and the CLS
-projection) on this second stream right after the image tower: the dispatcher runs BERT's
-workgroups beside the ViT's.  Autograd runs every node's backward on the stream of its forward,
+towers are independent until the loss, so ``BertModel.forward`` runs on this second stream,
+ordered after an event ``CTCLIP.encode`` records before it queues the image tower: the
+dispatcher runs BERT's workgroups beside the ViT's.  Autograd runs every node's backward on the stream of its forward,
 so BERT's backward (first in autograd order) also overlaps the ViT backward, and
 its gradient bucket's all-reduce is ordered after it on this stream.  The optimizer step queues
 the text bucket's Adam here too, so the next step's image tower does not wait for it (the next
