@@ -40,6 +40,8 @@ def parse():
     ap.add_argument('--text-len', type=int, default=128)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-batch', type=int, default=2)
+    ap.add_argument('--dist-backend', default='nccl', choices=['nccl', 'gloo'],
+                    help='gloo: rehearse the N>1 path with several ranks sharing one GPU (not a bench number)')
     return ap.parse_args()
 
 
@@ -100,11 +102,13 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    dev = torch.device('cuda', local)
+    dev = torch.device('cuda', local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
+    if world > 1:
+        if args.dist_backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group('gloo')
 
     from ctclip_mi355x.models import build_ctclip, set_finetune_trainable
     from ctclip_mi355x.trainer import CTClipTrainer
@@ -152,6 +156,14 @@ def main():
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
+    # every rank must hold identical parameters (one SUM all-reduce of identical-order buckets)
+    in_sync = None
+    if world > 1:
+        ck = trainer.flat.data.double().sum().reshape(1)
+        lo, hi = ck.clone(), ck.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        in_sync = bool(lo.item() == hi.item())
     ff1 = K.TIMER.summary('ff1')
     vit_ms = sum(s.elapsed_time(e) for s, e in vit_events) / max(1, len(vit_events))
     loss_v = float(loss.item())
@@ -179,6 +191,10 @@ def main():
                    'parallelism': f'dp{world}', 'infonce_negatives': 'global batch (RCCL all-gather)'},
         'loss': round(loss_v, 5),
     }
+    if in_sync is not None:
+        result['ranks_in_sync'] = in_sync
+    if args.dist_backend != 'nccl':
+        result['note'] = f'{args.dist_backend} rehearsal: {world} ranks on {torch.cuda.device_count()} GPU(s)'
     if ff1:
         tflops = ff1['flops'] / (ff1['avg_ms'] * 1e-3) / 1e12
         M = args.batch * 24 * 24 * 24
