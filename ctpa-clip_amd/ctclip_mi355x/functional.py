@@ -17,6 +17,7 @@ import torch
 
 from . import dist_sync
 from . import kernels as K
+from . import streams
 
 F32, BF16 = torch.float32, torch.bfloat16
 
@@ -334,6 +335,7 @@ class VQPoolFn(torch.autograd.Function):
         D = zf.shape[1]
         C = embed.shape[-2]
         cb = embed.view(C, D)
+        streams.join_aux(zf.device)     # the previous step's EMA update of the codebook
         cb_b = state.codebook_bf16(cb)
         ones = state.ones(D, zf.device)
         xn_b = K.l2norm_scale_fwd(zb, 1, D, ones)
@@ -345,11 +347,24 @@ class VQPoolFn(torch.autograd.Function):
         pooled, pooled_b = K.vq_pool(idx, cb, geo.B, geo.T, HW)
         tokens = K.vq_gather(idx, cb) if want_tokens else torch.empty(0, device=zf.device)
         if training:
-            bins = torch.zeros(C, device=zf.device, dtype=F32)
-            esum = torch.zeros(C, D, device=zf.device, dtype=F32)
-            K.vq_ema_accum(idx, xn, bins, esum)
-            dist_sync.sum_codebook_stats(bins, esum)
-            K.vq_ema_finalize(bins, esum, decay, cb, cluster.view(-1), cb_b)
+            # EMA update on the auxiliary stream (streams.py): after the pool / gather above have
+            # read the pre-update codebook, beside the rest of this step
+            aux = streams.aux_stream(zf.device)
+
+            def ema():
+                bins = torch.zeros(C, device=zf.device, dtype=F32)
+                esum = torch.zeros(C, D, device=zf.device, dtype=F32)
+                K.vq_ema_accum(idx, xn, bins, esum)
+                dist_sync.sum_codebook_stats(bins, esum)
+                K.vq_ema_finalize(bins, esum, decay, cb, cluster.view(-1), cb_b)
+            if aux is None:
+                ema()
+            else:
+                aux.wait_stream(torch.cuda.current_stream(zf.device))
+                for t in (idx, xn, cb, cluster, cb_b):
+                    t.record_stream(aux)
+                with torch.cuda.stream(aux):
+                    ema()
             state.mark_codebook_fresh(cb)
         ctx.geo = geo
         ctx.D = D

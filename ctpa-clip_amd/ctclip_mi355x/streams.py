@@ -9,7 +9,11 @@ so BERT's backward (first in autograd order) also overlaps the Vi
 its gradient bucket's all-reduce is ordered after it on this stream.  The optimizer step queues
 the text bucket's Adam here too, so the next step's image tower does not wait for it (the next
 BertModel.forward, on this stream, does).
-``CTCLIP_TEXT_STREAM=0`` keeps everything on the current stream."""
+``CTCLIP_TEXT_STREAM=0`` keeps everything on the current stream.
+
+A third, auxiliary stream takes the vector quantiser's EMA codebook update (statistics, their
+all-reduce at N > 1, finalize): nothing reads the updated codebook before the next step's VQ,
+which waits for it (``join_aux``)."""
 from __future__ import annotations
 
 import os
@@ -33,5 +37,25 @@ def text_stream(dev):
 def join_text(dev):
     """Order the current stream after all work queued on the text stream so far."""
     s = text_stream(dev)
+    if s is not None:
+        torch.cuda.current_stream(dev).wait_stream(s)
+
+
+_AUX = {}
+AUX_ENABLED = ENABLED and os.environ.get('CTCLIP_AUX_STREAM', '1') != '0'
+
+
+def aux_stream(dev):
+    """The auxiliary stream of ``dev`` (None when disabled or not a GPU device)."""
+    if not AUX_ENABLED or dev.type != 'cuda':
+        return None
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx not in _AUX:
+        _AUX[idx] = torch.cuda.Stream(idx)
+    return _AUX[idx]
+
+
+def join_aux(dev):
+    s = aux_stream(dev)
     if s is not None:
         torch.cuda.current_stream(dev).wait_stream(s)

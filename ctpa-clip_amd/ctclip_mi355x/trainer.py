@@ -110,6 +110,7 @@ class CTClipTrainer:
         # tower's backward finished; the last one goes out here and all are waited on.  BERT's
         # backward ran on the text stream (streams.py): order the norm / Adam after it.
         streams.join_text(self.device)
+        streams.join_aux(self.device)     # the VQ EMA update (already done by now; keeps state coherent)
         self.grad_sync.finish()
         K.grad_norm(self.flat.grad, self.max_grad_norm if self.max_grad_norm else 0.0, self.norm)
         self.steps += 1
