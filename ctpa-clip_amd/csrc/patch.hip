@@ -194,6 +194,82 @@ __global__ __launch_bounds__(256) void patch_wgrad_kernel(const float* __restric
 
 }  // namespace
 
+namespace {
+
+// CTViT.to_pixels' Rearrange 'b t h w (c pt p1 p2) -> b c (t pt) (h p1) (w p2)' (ct_clip/ctvit.py:
+// 194-197) fused with F.mse_loss(video, recon) (:451) and its gradient: one wave per token row;
+// element e of the row lands at voxel base + offs[e] (the patch_ln map, inverted).  Writes the
+// squared-error sum of the row (part[tok]), optionally the gradient 2 (pix - video) / n in the
+// row layout and the reconstruction in the video layout.
+__global__ __launch_bounds__(256) void unpatch_mse_kernel(const float* __restrict__ pix, int64_t ldp,
+                                                          const void* __restrict__ video, int is_f32, int is_hu,
+                                                          int64_t ntok, int T, int Hg, int Wg, int64_t vol_stride,
+                                                          int64_t frame_elems, int W, int PT, int P,
+                                                          const int32_t* __restrict__ offs, int pd, float gscale,
+                                                          float* __restrict__ grad, int64_t ldg,
+                                                          float* __restrict__ recon, float* __restrict__ part) {
+  const int lane = threadIdx.x & 63;
+  const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tok >= ntok) return;
+  int64_t r = tok;
+  const int wg = (int)(r % Wg); r /= Wg;
+  const int hg = (int)(r % Hg); r /= Hg;
+  const int t = (int)(r % T);
+  const int64_t b = r / T;
+  const int64_t base = b * vol_stride + (int64_t)t * PT * frame_elems + (int64_t)hg * P * W + (int64_t)wg * P;
+  const float* row = pix + tok * ldp;
+  float sq = 0.f;
+  for (int e = lane; e < pd; e += 64) {
+    const int64_t a = base + offs[e];
+    float x = is_f32 ? ((const float*)video)[a] : (float)((const short*)video)[a];
+    if (is_hu) x = fminf(fmaxf(x, -1000.f), 1000.f) / 1000.f;
+    const float y = row[e], d = y - x;
+    sq += d * d;
+    if (grad) grad[tok * ldg + e] = gscale * d;
+    if (recon) recon[a] = y;
+  }
+  sq = warp_sum(sq);
+  if (lane == 0) part[tok] = sq;
+}
+
+// mean of the row sums (one workgroup, f64 accumulation: deterministic)
+__global__ __launch_bounds__(256) void mse_finish_kernel(const float* __restrict__ part, int64_t n, double inv,
+                                                         float* __restrict__ loss) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) s += part[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = (float)(red[0] * inv);
+}
+
+}  // namespace
+
+extern "C" int ctclip_unpatch_mse(const float* pix, int64_t ldp, const void* video, int32_t is_f32, int32_t is_hu,
+                                  int64_t B, int32_t C, int32_t F, int32_t H, int32_t W, int32_t PT, int32_t P,
+                                  const int32_t* offs, float* grad, int64_t ldg, float* recon, float* part,
+                                  float* loss, void* stream) {
+  const int pd = C * PT * P * P;
+  CT_REQUIRE(pix && video && offs && part && loss, CT_EINVAL);
+  CT_REQUIRE(F % PT == 0 && H % P == 0 && W % P == 0 && ldp >= pd && (!grad || ldg >= pd), CT_ESHAPE);
+  const int T = F / PT, Hg = H / P, Wg = W / P;
+  const int64_t ntok = B * T * Hg * Wg;
+  if (ntok == 0) return 0;
+  const int64_t frame = (int64_t)H * W, vol = (int64_t)C * F * frame;
+  const int64_t n = B * vol;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(unpatch_mse_kernel, dim3(cdiv(ntok, 4)), dim3(256), 0, st, pix, ldp, video, is_f32, is_hu, ntok,
+                     T, Hg, Wg, vol, frame, W, PT, P, offs, pd, (float)(2.0 / (double)n), grad, ldg, recon, part);
+  hipLaunchKernelGGL(mse_finish_kernel, dim3(1), dim3(256), 0, st, part, ntok, 1.0 / (double)n, loss);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+
 extern "C" int ctclip_patch_ln(const void* video, int32_t is_f32, int32_t is_hu, int64_t B, int32_t C, int32_t F,
                                int32_t H, int32_t W, int32_t PT, int32_t P, const int32_t* offs, float eps,
                                void* out, int64_t ldo, void* stream) {

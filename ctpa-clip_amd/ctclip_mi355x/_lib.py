@@ -89,6 +89,8 @@ _SIGS = {
     'ctclip_patch_ln': [c_vp, c_i32, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp, c_i64,
                         c_vp],
     'ctclip_patch_wgrad': [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp],
+    'ctclip_unpatch_mse': [c_vp, c_i64, c_vp, c_i32, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp,
+                           c_vp, c_i64, c_vp, c_vp, c_vp, c_vp],
     'ctclip_peg_fwd': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp],
     'ctclip_peg_bwd_data': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp],
     'ctclip_peg_bwd_weight': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp],

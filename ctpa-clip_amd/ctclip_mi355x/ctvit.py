@@ -9,6 +9,7 @@ import torch
 from torch import nn
 
 from . import functional as Fn
+from . import kernels as K
 from .attention import ContinuousPositionBias, Transformer
 from .layers import patch_offsets
 
@@ -137,18 +138,62 @@ class CTViT(nn.Module):
         c = self.vq._codebook
         return c.embed, c.cluster_size
 
+    def _decode_rows(self, zf, geo):
+        """CTViT.decode (ct_clip/ctvit.py:333-366) on canonical token rows: the encoder's temporal
+        then spatial transformers again (same raw-reshape PEG view, CPB bias) -> (f32, bf16)."""
+        xf, xb = zf, K.cast_bf16(zf.detach())
+        g_tm = Fn.Geo(geo.B, geo.T, geo.Hg, geo.Wg, self.heads, self.dim_head, 1)
+        xf, xb = self.enc_temporal_transformer.run(xf, xb, g_tm)
+        bias_u = self.spatial_rel_pos_bias(geo.Hg, geo.Wg)
+        return self.enc_spatial_transformer.run(xf, xb, geo, bias_u)
+
+    def decode(self, tokens):
+        """``CTViT.decode`` (ct_clip/ctvit.py:333-375): tokens (b, t, h, w, d) or (b, t*h*w, d)
+        -> reconstructed video (b, c, t*pt, h*p1, w*p2) f32."""
+        hg, wg = self.patch_height_width
+        b = tokens.shape[0]
+        z = tokens.reshape(-1, self.dim).float().contiguous()
+        T = z.shape[0] // (b * hg * wg)
+        geo = Fn.Geo(b, T, hg, wg, self.heads, self.dim_head, 0)
+        xf, xb = self._decode_rows(z, geo)
+        W, bias = self.to_pixels[0].weight, self.to_pixels[0].bias
+        Wb = Fn.bf(W)
+        pix = K.linear(xb, Wb, bias=bias, out_dtype=torch.float32)
+        c, pt, p = self.channels, self.temporal_patch_size, self.patch_size[0]
+        # Rearrange 'b t h w (c pt p1 p2) -> b c (t pt) (h p1) (w p2)' (ctvit.py:196)
+        return (pix.view(b, T, hg, wg, c, pt, p, p).permute(0, 4, 1, 5, 2, 6, 3, 7)
+                .reshape(b, c, T * pt, hg * p, wg * p))
+
     def forward(self, video, mask=None, return_recons=False, return_recons_only=False, return_discr_loss=False,
                 apply_grad_penalty=True, return_only_codebook_ids=False, return_encoded_tokens=False):
-        """``CTViT.forward`` (ct_clip/ctvit.py:377-436): the encoder path
-        (return_encoded_tokens / return_only_codebook_ids)."""
+        """``CTViT.forward`` (ct_clip/ctvit.py:377-451): the encoder path (return_encoded_tokens /
+        return_only_codebook_ids) and, with ``use_vgg_and_gan=False``, the VQ-VAE reconstruction
+        path (MSE loss; return_recons / return_recons_only)."""
         if mask is not None:
             raise NotImplementedError('frame masks are not used on the CT-CLIP path')
-        if not (return_encoded_tokens or return_only_codebook_ids):
-            raise NotImplementedError('reconstruction / GAN losses are outside the contrastive hot path')
+        if return_discr_loss or self.use_vgg_and_gan:
+            raise NotImplementedError('the GAN / perceptual losses (VGG16 weights) are out of scope')
+        if video.ndim == 4:
+            video = video.unsqueeze(2)
         zf, zb, geo = self.encode_tokens(video)
         emb, cs = self._codebook_tensors()
+        want_tokens = not return_only_codebook_ids
         _, _, toks = Fn.VQPoolFn.apply(zf, zb, emb, cs, geo, self.training, self.vq.decay, self.vq.state,
-                                       return_encoded_tokens)
+                                       want_tokens)
         if return_only_codebook_ids:
             return self.vq.state.last_indices.view(geo.B, -1).long()
-        return toks.view(geo.B, geo.T, geo.Hg, geo.Wg, self.dim)
+        if return_encoded_tokens:
+            return toks.view(geo.B, geo.T, geo.Hg, geo.Wg, self.dim)
+        # reconstruction (ctvit.py:436-451): decode the quantised tokens, MSE against the input
+        xf, xb = self._decode_rows(toks, geo)
+        is_hu = video.dtype == torch.int16
+        vid = video if is_hu else video.float().contiguous()
+        want_recon = return_recons or return_recons_only
+        loss, recon = Fn.ReconFn.apply(xf, xb, self.to_pixels[0].weight, self.to_pixels[0].bias, vid, is_hu,
+                                       self.temporal_patch_size, self.patch_size[0],
+                                       self._offsets(vid.shape, vid.device), want_recon)
+        if return_recons_only:
+            return recon
+        if return_recons:
+            return loss, recon
+        return loss

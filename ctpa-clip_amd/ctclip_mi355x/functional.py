@@ -149,6 +149,40 @@ class PatchEmbedFn(torch.autograd.Function):
         return None, dg1, db1, dW, cs, dg2, db2, None, None, None, None
 
 
+# ----------------------------------------------------------------------------- reconstruction
+class ReconFn(torch.autograd.Function):
+    """``CTViT.to_pixels`` (ct_clip/ctvit.py:194-197: Linear(dim -> c*pt*p1*p2) + Rearrange to the
+    video layout) and ``F.mse_loss(video, recon)`` (ctvit.py:451) as one node: the Linear is an MFMA
+    GEMM with the bias epilogue, the rearrange + squared error + its gradient one HIP pass
+    (``ctclip_unpatch_mse``) that never materialises the reconstruction unless it is returned.
+    Returns (loss, recon or an empty tensor); the recon is not differentiable (the reference
+    returns it detached from the loss as ``recon_video.clone()`` for logging)."""
+
+    @staticmethod
+    def forward(ctx, xf, xb, W, b, video, is_hu, PT, P, offs, want_recon):
+        Wb = bf(W)
+        pix = K.linear(xb, Wb, bias=b, out_dtype=F32)                   # [M, c*pt*p1*p2]
+        loss, g, recon = K.unpatch_mse(pix, video, is_hu, PT, P, offs, want_grad=True, want_recon=want_recon)
+        ctx.save_for_backward(xb, Wb, g)
+        ctx.W, ctx.b = W, b
+        if recon is None:
+            recon = torch.empty(0, device=xf.device)
+        ctx.mark_non_differentiable(recon)
+        return loss.reshape(()), recon
+
+    @staticmethod
+    def backward(ctx, dloss, _drecon):
+        xb, Wb, g = ctx.saved_tensors
+        dpix = g * dloss                      # d loss / d pix, scaled by the incoming gradient
+        dpb = K.cast_bf16(dpix)
+        if ctx.W.requires_grad:
+            K.matmul_tn(dpb, xb, out=gsink(ctx.W), accumulate=True)
+        if ctx.b.requires_grad:
+            K.colsum(dpix, out=gsink(ctx.b), accumulate=True)
+        dx = K.matmul_nn(dpb, Wb, out_dtype=F32)
+        return dx, None, None, None, None, None, None, None, None, None
+
+
 # ----------------------------------------------------------------------------- CPB
 def cpb_table(h, w, device):
     """Unique relative offsets of an h x w grid, log-spaced (ct_clip/attention.py:261-267):

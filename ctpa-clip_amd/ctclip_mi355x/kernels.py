@@ -322,6 +322,21 @@ def patch_ln(video, is_hu, PT, P, offs, eps=1e-5, ld=None):
     return out
 
 
+def unpatch_mse(pix, video, is_hu, PT, P, offs, want_grad=True, want_recon=False):
+    """(loss [1] f32, grad [tokens, pd] or None, recon (B,C,F,H,W) or None) of
+    F.mse_loss(video, rearrange(pix)) -- the inverse patch map of patch_ln."""
+    B, C, Fr, H, W = video.shape
+    pd = C * PT * P * P
+    n = pix.shape[0]
+    grad = torch.empty(n, pd, device=pix.device, dtype=F32) if want_grad else None
+    recon = torch.empty(B, C, Fr, H, W, device=pix.device, dtype=F32) if want_recon else None
+    part = torch.empty(n, device=pix.device, dtype=F32)
+    loss = torch.empty(1, device=pix.device, dtype=F32)
+    call('ctclip_unpatch_mse', ptr(pix), pix.stride(0), ptr(video), int(video.dtype == F32), int(is_hu), B, C, Fr, H, W,
+         PT, P, ptr(offs), ptr(grad), pd, ptr(recon), ptr(part), ptr(loss), stream_ptr())
+    return loss, grad, recon
+
+
 def patch_wgrad(G, cs, W, g, b, dW, dg, db, accumulate=True):
     N, K = G.shape
     call('ctclip_patch_wgrad', ptr(G), ptr(cs), ptr(W), ptr(g), ptr(b), N, K, ptr(dW), ptr(dg), ptr(db),

@@ -123,6 +123,15 @@ int ctclip_patch_ln(const void* video, int32_t is_f32, int32_t is_hu, int64_t B,
 int ctclip_patch_wgrad(const float* G, const float* colsum_dy, const float* W, const float* gamma,
                        const float* beta, int32_t N, int32_t K, float* dW, float* dgamma, float* dbeta,
                        int32_t accumulate, void* stream);
+/* reconstruction loss of the VQ-VAE path: to_pixels' Rearrange
+ * 'b t h w (c pt p1 p2) -> b c (t pt) (h p1) (w p2)' (ct_clip/ctvit.py:194-197) fused with
+ * F.mse_loss(video, recon) (ctvit.py:451).  pix [tokens][ldp] f32 (the to_pixels Linear output);
+ * video as for ctclip_patch_ln; offs its element->voxel table.  Writes loss[0] = mean squared
+ * error, part[tokens] (workspace: per-row sums), optionally grad [tokens][ldg] = d loss / d pix and
+ * recon (B, C, F, H, W) f32. */
+int ctclip_unpatch_mse(const float* pix, int64_t ldp, const void* video, int32_t is_f32, int32_t is_hu, int64_t B,
+                       int32_t C, int32_t F, int32_t H, int32_t W, int32_t PT, int32_t P, const int32_t* offs,
+                       float* grad, int64_t ldg, float* recon, float* part, float* loss, void* stream);
 
 /* ---------------------------------------------------------------- PEG (attention.py:56-84)
  * causal depthwise 3x3x3 conv + residual on canonical (b,t,h,w) token rows; mode 0 = spatial

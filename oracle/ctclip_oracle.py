@@ -277,6 +277,35 @@ def ctvit_forward(sd, p, video, cfg: ViTConfig, training, trace=None, force_ind=
     return q.reshape(b, t, h, w, d), ind, ne, ncs
 
 
+def ctvit_decode(sd, p, tokens, cfg: ViTConfig):
+    """``CTViT.decode`` (``ct_clip/ctvit.py:333-375``): the ENCODER's temporal then spatial
+    transformers run again on the quantised tokens (temporal on '(b h w) t d' with the same raw-
+    reshape PEG view, spatial with the CPB bias), then ``to_pixels`` (``:194-197``): Linear(dim ->
+    c*pt*p1*p2) and 'b t h w (c pt p1 p2) -> b c (t pt) (h p1) (w p2)'."""
+    b, t, h, w, d = tokens.shape
+    video_shape = (b, t, h, w)
+    x = tokens.permute(0, 2, 3, 1, 4).reshape(b * h * w, t, d)
+    x = transformer_forward(sd, p + 'enc_temporal_transformer.', x, cfg.temporal_depth, cfg.heads,
+                            cfg.dim_head, video_shape, None)
+    x = x.reshape(b, h, w, t, d).permute(0, 3, 1, 2, 4).reshape(b * t, h * w, d)
+    bias = cpb_forward(sd, p + 'spatial_rel_pos_bias.', h, w, cfg.cpb_layers)
+    x = transformer_forward(sd, p + 'enc_spatial_transformer.', x, cfg.spatial_depth, cfg.heads,
+                            cfg.dim_head, video_shape, bias)
+    y = F.linear(x.reshape(b, t, h, w, d), sd[p + 'to_pixels.0.weight'], sd[p + 'to_pixels.0.bias'])
+    c, pt, ps = cfg.channels, cfg.temporal_patch_size, cfg.patch_size
+    y = y.reshape(b, t, h, w, c, pt, ps, ps).permute(0, 4, 1, 5, 2, 6, 3, 7)
+    return y.reshape(b, c, t * pt, h * ps, w * ps)
+
+
+def ctvit_recon(sd, p, video, cfg: ViTConfig, training, force_ind=None):
+    """``CTViT.forward(video, return_recons=True)`` with ``use_vgg_and_gan=False``
+    (``ct_clip/ctvit.py:377-451``): patch embed -> encode -> VQ (STE) -> decode ->
+    ``F.mse_loss(video, recon)``.  Returns (loss, recon, indices, new_embed, new_cluster_size)."""
+    tokens, ind, ne, ncs = ctvit_forward(sd, p, video, cfg, training, None, force_ind)
+    recon = ctvit_decode(sd, p, tokens, cfg)
+    return F.mse_loss(video, recon), recon, ind, ne, ncs
+
+
 # ----------------------------------------------------------------------------- BERT
 def bert_forward(sd, p, ids, mask, cfg: BertConfig):
     """BERT-base encoder as called at ``ct_clip/ct_clip.py:685-686`` (third-party

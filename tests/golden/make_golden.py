@@ -239,15 +239,47 @@ def run_zero_shot(V, C):
     print('zero-shot probs', probs.tolist(), '->', path)
 
 
+def run_recon(V, C):
+    """Reconstruction fixture (tiny config): the reference CTViT built with
+    use_vgg_and_gan=False, forward(video, return_recons=True) in train mode (ct_clip/ctvit.py:
+    377-451: encode -> VQ -> decode -> MSE), its loss / recon / VQ indices and parameter grads."""
+    cfg = O.TINY
+    clip = build_reference(cfg, V, C)
+    sd = W.make_state_dict(cfg)
+    clip.load_state_dict(sd, strict=True)
+    vit = clip.visual_transformer
+    vit.train()
+    cap = {}
+    vit.vq.register_forward_hook(lambda m, i, o: cap.__setitem__('vq_indices', o[1].detach().clone()))
+    hu = W.make_hu(2, cfg.vit, seed=55)
+    video = O.normalize_hu(hu)
+    loss, recon = vit(video, return_recons=True)
+    loss.backward()
+    out = {'in.hu': hu, 'out.loss': loss.detach().reshape(1), 'out.recon': recon.detach(),
+           'out.vq_indices': cap['vq_indices']}
+    for n, prm in vit.named_parameters():
+        if prm.grad is not None:
+            out['grad.visual_transformer.' + n] = prm.grad.detach().clone()
+    path = os.path.join(HERE, 'golden_recon_tiny.safetensors')
+    save_file({k: v.contiguous() for k, v in out.items()}, path,
+              metadata={'generator': 'tests/golden/make_golden.py --recon',
+                        'reference': 'sharonct/CTPA-CLIP @ 2025-06-20 (ct_clip/ctvit.py:333-451)'})
+    print('recon loss', float(loss), 'grads', sum(k.startswith('grad.') for k in out), '->', path)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--base', action='store_true', help='also write the base-config B=2 fixture')
     ap.add_argument('--zero-shot', action='store_true', help='only write the zero-shot fixture')
+    ap.add_argument('--recon', action='store_true', help='only write the reconstruction fixture')
     args = ap.parse_args()
     torch.set_num_threads(os.cpu_count())
     A, V, C = import_reference()
     if args.zero_shot:
         run_zero_shot(V, C)
+        return
+    if args.recon:
+        run_recon(V, C)
         return
     run(O.TINY, batch=4, text_len=16, ragged=True, with_grads=True, tag='tiny', V=V, C=C,
         save_full_state=False)

@@ -230,3 +230,52 @@ def test_zero_shot_matches_oracle(setup):
     model.train()
     assert s2.shape == (2,)
     assert (s2.cpu() - scores[0, 0].cpu()).abs().max().item() < 1e-4
+
+
+def test_recon_matches_oracle(setup):
+    """VQ-VAE reconstruction path (ct_clip/ctvit.py:333-451 with
+    use_vgg_and_gan=False): CTViT.forward(video, return_recons=True) -> (MSE loss, recon) and its
+    backward against the oracle's ctvit_recon, the oracle forced onto the HIP path's VQ indices and
+    given the pre-step weights.  Loss within 1e-3 relative, recon 3e-2 (the pre-VQ tokens are within
+    2e-2 after the 8 encoder layers; the decoder adds 8 more bf16 layers), grads within 5 %."""
+    cfg, model, hu, ids, mask, text = setup
+    vit = model.visual_transformer
+    sd = {k: v.detach().float().cpu().clone() for k, v in model.state_dict().items()}
+    for prm in vit.parameters():
+        prm.grad = None
+    px = list(vit.to_pixels.parameters())      # frozen on the contrastive path (set_finetune_trainable)
+    for prm in px:
+        prm.requires_grad_(True)
+    vit.train()
+    loss, recon = vit(hu.cuda(), return_recons=True)
+    idx = vit.vq.state.last_indices.cpu()
+    loss.backward()
+    torch.cuda.synchronize()
+    # the reference's return_recons_only / decode() agree with the fused path
+    assert recon.shape == (hu.shape[0], 1, cfg.vit.frames, cfg.vit.image_size, cfg.vit.image_size)
+    p = 'visual_transformer.'
+    names = ['to_pixels.0.weight', 'to_pixels.0.bias', 'enc_spatial_transformer.layers.1.3.1.weight',
+             'enc_temporal_transformer.layers.0.1.to_q.weight', 'to_patch_emb.2.weight']
+    for n in names:
+        sd[p + n].requires_grad_(True)
+    rl, rr, _, _, _ = O.ctvit_recon(sd, p, O.normalize_hu(hu), cfg.vit, training=True,
+                                    force_ind=idx.reshape(hu.shape[0], -1))
+    rl.backward()
+    assert abs(loss.item() - rl.item()) <= 1e-3 * abs(rl.item()), (loss.item(), rl.item())
+    assert rel(recon, rr) < 3e-2, rel(recon, rr)     # 8 more bf16 transformer layers than the latents
+    named = dict(vit.named_parameters())
+    for n in names:
+        r = rel(named[n].grad, sd[p + n].grad)
+        print(f'{n}: grad rel err {r:.2e}')
+        assert r < 5e-2, (n, r)
+    for prm in vit.parameters():
+        prm.grad = None
+    for prm in px:
+        prm.requires_grad_(False)
+    # eval: the public decode() of the encoded tokens equals the fused return_recons_only path
+    vit.eval()
+    with torch.no_grad():
+        r1 = vit(hu.cuda(), return_recons_only=True)
+        r2 = vit.decode(vit(hu.cuda(), return_encoded_tokens=True))
+    vit.train()
+    assert torch.equal(r1, r2)

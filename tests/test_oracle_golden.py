@@ -119,3 +119,29 @@ def test_zero_shot_matches_reference():
     _close(scores, g['out.scores'], 1e-5)
     _close(probs, g['out.probs'], 1e-6)
     assert O.PATHOLOGIES[11] == 'Pulmonary Embolism' and len(O.PATHOLOGIES) == 18
+
+
+def test_recon_matches_reference():
+    """VQ-VAE reconstruction (ct_clip/ctvit.py:333-451, use_vgg_and_gan=False):
+    the oracle's decode + MSE against the reference's own forward(video, return_recons=True) and
+    backward (golden_recon_tiny, tests/golden/make_golden.py --recon)."""
+    from safetensors.torch import load_file
+    import os
+    g = load_file(os.path.join(os.path.dirname(__file__), 'golden', 'golden_recon_tiny.safetensors'))
+    cfg = O.TINY
+    sd = W.make_state_dict(cfg)
+    p = 'visual_transformer.'
+    for k, v in sd.items():
+        if ('grad.' + k) in g:
+            v.requires_grad_(True)
+    loss, recon, ind, _, _ = O.ctvit_recon(sd, p, O.normalize_hu(g['in.hu']), cfg.vit, training=True)
+    assert torch.equal(ind.reshape(g['out.vq_indices'].shape), g['out.vq_indices'])
+    _close(loss.detach().reshape(1), g['out.loss'], 1e-5)
+    _close(recon.detach(), g['out.recon'], 1e-5)
+    loss.backward()
+    n = 0
+    for k, v in sd.items():
+        if ('grad.' + k) in g and v.grad is not None:
+            _close(v.grad, g['grad.' + k], 2e-4)
+            n += 1
+    assert n >= 40, n
