@@ -99,11 +99,12 @@ class BertModel(nn.Module):
             if isinstance(m, nn.Linear):
                 nn.init.zeros_(m.bias)
 
-    def forward(self, input_ids, attention_mask=None, ready=None, **_):
-        """Runs on the text stream (streams.py) when there is one: ordered after ``ready`` (an event
+    def forward(self, input_ids, attention_mask=None, join=True, ready=None, **_):
+        """Runs on the text stream (streams.py) when there is one, ordered after ``ready`` (an event
         of the calling stream; default: everything queued on it so far) and after the previous
-        optimizer step's Adam of these weights (queued on the text stream); the calling stream
-        waits for the result before it returns.  Backward nodes run on the same text stream."""
+        optimizer step's Adam of these weights (queued on the text stream).  ``join``: the calling
+        stream waits for the result before this returns; with join=False the caller joins later
+        (``streams.join_text``).  Backward nodes run on the text stream."""
         dev = input_ids.device
         ts = streams.text_stream(dev)
         if ts is None:
@@ -118,8 +119,9 @@ class BertModel(nn.Module):
                 t.record_stream(ts)
         with torch.cuda.stream(ts):
             out = self._forward(input_ids, attention_mask)
-        cur.wait_stream(ts)
         out[0].record_stream(cur)
+        if join:
+            cur.wait_stream(ts)
         return out
 
     def _forward(self, input_ids, attention_mask=None):

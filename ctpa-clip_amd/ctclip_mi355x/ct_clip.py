@@ -17,6 +17,14 @@ from . import functional as Fn
 from . import streams
 
 
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
 def l2norm(t):
     return nn.functional.normalize(t, dim=-1)
 
@@ -56,6 +64,8 @@ class CTCLIP(nn.Module):
         self.to_visual_latent_extra = copy.deepcopy(self.to_visual_latent)
         self.multiview_loss_weight = multiview_loss_weight
         self._wvis = (None, None)
+        self.defer_text_backward = False     # set by CTClipTrainer (see encode)
+        self._deferred_text = None
 
     # ------------------------------------------------------------------ checkpoint
     def load(self, path):
@@ -79,12 +89,32 @@ class CTCLIP(nn.Module):
     def encode(self, text, image):
         """Text + image towers and raw latents: (enc_text (B,L,768), pooled (B, h*w*d),
         text_raw (B, dl), image_raw (B, dl))."""
-        # image tower first: the text tower's nodes are then newer, so the backward runs BERT
-        # first and its gradient bucket all-reduces under the 3D-ViT backward (dist_sync).  BERT
-        # itself runs on the text stream, beside the image tower (streams.py).
-        ready = torch.cuda.current_stream(image.device).record_event() if streams.text_stream(image.device) else None
+        # The host queues the image tower first (its ~16 ms of GPU work keep this stream busy while
+        # the host queues BERT's many small launches), BERT on the text stream (streams.py) ordered
+        # only after an event taken before the image tower, so the two run side by side.
+        dev = image.device
+        ready = torch.cuda.current_stream(dev).record_event() if streams.text_stream(dev) else None
         pooled, pooled_b = self.visual_transformer.encode_pooled(image)
-        enc_text, t_raw = self._text(text, image.device, ready)
+        enc_text = self.text_transformer(text.input_ids, attention_mask=text.attention_mask, join=False,
+                                         ready=ready)[0]
+        ts = streams.text_stream(dev)
+        with torch.cuda.stream(ts) if ts is not None else _nullctx():
+            t_raw = Fn.TextProjFn.apply(enc_text[:, 0, :].contiguous(), self.to_text_latent.weight)
+        streams.join_text(dev)
+        if ts is not None:
+            t_raw.record_stream(torch.cuda.current_stream(dev))
+        if self.defer_text_backward and torch.is_grad_enabled() and t_raw.requires_grad:
+            # the trainer back-propagates the text tower AFTER the loss / 3D-ViT graph
+            # (CTClipTrainer.forward_backward): the long ViT chain is queued first, and BERT's
+            # backward, queued while the GPU still works through it, runs beside it on the text
+            # stream -- ordered only after an event taken when the loss produced its gradient
+            leaf = t_raw.detach().requires_grad_(True)
+            d = self._deferred_text = [t_raw, leaf, None]
+            if ts is not None:
+                def mark(g):
+                    d[2] = torch.cuda.current_stream(dev).record_event()
+                leaf.register_hook(mark)
+            t_raw = leaf
         W = self.to_visual_latent.weight
         i_raw = self._project(W, self._visual_weight_bf16(W), pooled, pooled_b)
         return enc_text, pooled, t_raw, i_raw
@@ -113,20 +143,34 @@ class CTCLIP(nn.Module):
             return K.clip_scores(t_raw.contiguous(), i_raw.contiguous(), self.temperature.detach().reshape(1))
         return Fn.ClipLossFn.apply(t_raw, i_raw, self.temperature)
 
-    def _text(self, text, dev, ready=None):
-        """BERT (on the text stream, see BertModel.forward) + CLS projection: (enc_text, text_raw).
-        ``ready``: an event recorded on the main stream BEFORE the image tower was queued (ids,
-        mask and weights are ready there), so BERT does not wait for the image tower."""
-        enc_text = self.text_transformer(text.input_ids, attention_mask=text.attention_mask, ready=ready)[0]
-        return enc_text, Fn.TextProjFn.apply(enc_text[:, 0, :].contiguous(), self.to_text_latent.weight)
+    def backward_deferred_text(self):
+        """Back-propagate the text tower whose graph ``encode`` detached (defer_text_backward).
+        On the text stream, after the event the loss's backward recorded for its gradient: the
+        autograd engine then sees producer and consumer on the same stream and adds no wait on the
+        main stream (which would serialise BERT after the whole 3D-ViT backward)."""
+        d, self._deferred_text = self._deferred_text, None
+        if d is None or d[1].grad is None:
+            return
+        t_raw, leaf, ev = d
+        g = leaf.grad
+        ts = streams.text_stream(g.device)
+        if ts is None or ev is None:
+            torch.autograd.backward(t_raw, g)
+            return
+        ts.wait_event(ev)
+        g.record_stream(ts)
+        with torch.cuda.stream(ts):
+            torch.autograd.backward(t_raw, g)
 
     def grad_buckets(self):
-        """Gradient all-reduce buckets in the order the backward finalises them (dist_sync)."""
+        """Gradient all-reduce buckets in the order the backward finalises them (dist_sync): the
+        3D-ViT's temporal stack, spatial stack, the rest of the image tower (patch embed, CPB),
+        then BERT (back-propagated last, see encode)."""
         vt = self.visual_transformer
-        return [('text', list(self.text_transformer.parameters())),
-                ('vit_temporal', list(vt.enc_temporal_transformer.parameters())),
+        return [('vit_temporal', list(vt.enc_temporal_transformer.parameters())),
                 ('vit_spatial', list(vt.enc_spatial_transformer.parameters())),
-                ('rest', list(self.parameters()))]
+                ('vit_rest', list(vt.parameters())),
+                ('text', list(self.parameters()))]
 
     def _pool_tokens(self, tokens):
         """mean over t + flatten of already-quantised tokens (ct_clip.py:724,740)."""

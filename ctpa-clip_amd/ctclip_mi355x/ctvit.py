@@ -8,6 +8,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from . import dist_sync
 from . import functional as Fn
 from . import kernels as K
 from .attention import ContinuousPositionBias, Transformer
@@ -116,11 +117,13 @@ class CTViT(nn.Module):
         xf, xb = Fn.PatchEmbedFn.apply(video, pe[1].weight, pe[1].bias, pe[2].weight, pe[2].bias, pe[3].weight,
                                        pe[3].bias, self.temporal_patch_size, self.patch_size[0], is_hu,
                                        self._offsets(video.shape, video.device))
+        dist_sync.mark_ready(xf, 'vit_rest')   # with the CPB node below: the rest of the image tower
         hg, wg = self.patch_height_width
         T = F // self.temporal_patch_size
         g_sp = Fn.Geo(B, T, hg, wg, self.heads, self.dim_head, 0)
         g_tm = Fn.Geo(B, T, hg, wg, self.heads, self.dim_head, 1)
         bias_u = self.spatial_rel_pos_bias(hg, wg)                       # ctvit.py:317
+        dist_sync.mark_ready(bias_u, 'vit_rest')
         xf, xb = self.enc_spatial_transformer.run(xf, xb, g_sp, bias_u)   # ctvit.py:319
         zf, zb = self.enc_temporal_transformer.run(xf, xb, g_tm)         # ctvit.py:327
         return zf, zb, g_sp
@@ -145,6 +148,7 @@ class CTViT(nn.Module):
         g_tm = Fn.Geo(geo.B, geo.T, geo.Hg, geo.Wg, self.heads, self.dim_head, 1)
         xf, xb = self.enc_temporal_transformer.run(xf, xb, g_tm)
         bias_u = self.spatial_rel_pos_bias(geo.Hg, geo.Wg)
+        dist_sync.mark_ready(bias_u, 'vit_rest')
         return self.enc_spatial_transformer.run(xf, xb, geo, bias_u)
 
     def decode(self, tokens):

@@ -70,32 +70,43 @@ def sum_grads(flat_grad: torch.Tensor) -> None:
 
 
 # ------------------------------------------------------------------ backward-overlapped buckets
-# SURVEY §8(e) "Overlap": the image tower runs forward first and the text tower second, so the
-# autograd engine (which runs the most recently created node first) back-propagates BERT before
-# the 3D-ViT.  Each tower (or stack) marks the autograd node after which its parameters' .grad
-# are final (``mark_ready``); the trainer's ``BucketedGradSync`` then launches that bucket's SUM
-# all-reduce asynchronously (RCCL runs it on its own stream after the kernels already queued)
-# while the rest of the backward keeps the compute stream busy.  Buckets are launched in one
-# fixed order on every rank, so the collectives always match.
+# SURVEY §8(e) "Overlap": CTCLIP.encode queues the text tower first (on its own stream) and the
+# image tower second, so the autograd engine (which runs the most recently created node first)
+# queues the whole 3D-ViT backward before BERT's.  Each tower (or stack) marks the autograd node
+# after which its parameters' .grad are final (``mark_ready``); the trainer's
+# ``BucketedGradSync`` then launches that bucket's SUM all-reduce asynchronously (RCCL orders it
+# after the kernels already queued on the hook's stream) while the rest of the backward keeps the
+# GPU busy.  Buckets are launched in one fixed order on every rank, so the collectives match.
 _READY = {}
+_PENDING = {}
 
 
 def mark_ready(t: torch.Tensor, tag: str) -> None:
-    """Called in a forward: once ``t``'s producing node has run its backward, every parameter of
-    bucket ``tag`` has its final gradient.  No-op unless a trainer armed ``tag``."""
+    """Called in a forward: once ``t``'s producing node has run its backward, the parameters of
+    bucket ``tag`` it owns have their final gradient.  A bucket marked on several nodes (e.g. the
+    patch embedding and the CPB MLP) launches after the last of them.  No-op unless a trainer
+    armed ``tag``."""
     cb = _READY.get(tag)
     if cb is None or t.grad_fn is None or not torch.is_grad_enabled():
         return
-    t.grad_fn.register_hook(lambda grad_inputs, grad_outputs: cb(tag))
+    _PENDING[tag] = _PENDING.get(tag, 0) + 1
+
+    def fired(grad_inputs, grad_outputs):
+        _PENDING[tag] -= 1
+        if _PENDING[tag] == 0:
+            cb(tag)
+    t.grad_fn.register_hook(fired)
 
 
 def disarm() -> None:
     _READY.clear()
+    _PENDING.clear()
 
 
 class BucketedGradSync:
     """SUM all-reduce of a flat gradient arena in contiguous buckets [(tag, offset, numel)],
-    each launched as soon as its ``mark_ready`` node has run (the last bucket at ``finish``)."""
+    each launched as soon as its ``mark_ready`` node has run; ``finish`` launches whatever no
+    hook launched (a tower without gradients, world 1) and waits for all of them."""
 
     def __init__(self, flat_grad: torch.Tensor, buckets, before_launch=None, force=False):
         self.grad = flat_grad
@@ -127,12 +138,14 @@ class BucketedGradSync:
         world, _ = world_rank()
         self.launched, self.works, self.log = [], [], []
         if world > 1 or self.force:
-            for t, _, _ in self.buckets[:-1]:
+            for t, _, _ in self.buckets:
                 _READY[t] = self._launch
+                _PENDING[t] = 0
 
     def finish(self):
         for t, _, _ in self.buckets:
             _READY.pop(t, None)
+            _PENDING.pop(t, None)
         if self.buckets:
             self._launch(self.buckets[-1][0])
         for w in self.works:

@@ -132,6 +132,7 @@ class PatchEmbedFn(torch.autograd.Function):
         y1 = K.linear(xhat_p, Wp, bias=bp, out_dtype=F32)               # [M, D]
         yb, yf, mean, rstd = K.layernorm_fwd(y1, ln2_w, ln2_b, 1e-5, out_bf16=True, out_f32=True)
         ctx.save_for_backward(xhat, y1, mean, rstd, ln1_w, ln1_b, W, ln2_w)
+        ctx.b, ctx.ln2_w, ctx.ln2_b = b, ln2_w, ln2_b
         ctx.mark_non_differentiable(yb)
         return yf, yb
 
@@ -142,11 +143,15 @@ class PatchEmbedFn(torch.autograd.Function):
         _, dy1b, dg2, db2 = K.layernorm_bwd(dyf.contiguous(), y1, mean, rstd, ln2_w, dx_f32=False)
         G = K.matmul_tn(dy1b, xhat)                                     # [D, pd] f32
         cs = K.colsum(dy1b)                                             # d bias
-        dW = torch.empty_like(W)
-        dg1 = torch.empty_like(ln1_w)
-        db1 = torch.empty_like(ln1_b)
-        K.patch_wgrad(G, cs, W, ln1_w, ln1_b, dW, dg1, db1, accumulate=False)
-        return None, dg1, db1, dW, cs, dg2, db2, None, None, None, None
+        # straight into .grad (gsink), so the node's parameters are final when it returns
+        # (dist_sync buckets fire on the node's post-hook, before any AccumulateGrad would run)
+        sinks = [gsink(t) for t in (W, ln1_w, ln1_b)]
+        tmp = [s_ if s_ is not None else torch.zeros_like(t) for s_, t in zip(sinks, (W, ln1_w, ln1_b))]
+        K.patch_wgrad(G, cs, W, ln1_w, ln1_b, tmp[0], tmp[1], tmp[2], accumulate=True)
+        for t, g_ in ((ctx.b, cs), (ctx.ln2_w, dg2), (ctx.ln2_b, db2)):
+            if t.requires_grad:
+                gsink(t).add_(g_)
+        return None, None, None, None, None, None, None, None, None, None, None
 
 
 # ----------------------------------------------------------------------------- reconstruction

@@ -97,12 +97,20 @@ class CTClipTrainer:
 
     def forward_backward(self, text, video):
         self.grad_sync.arm()
+        defer = hasattr(self.model, 'backward_deferred_text')
+        if defer:
+            self.model.defer_text_backward = True
         try:
             loss = self.model(text, video, device=self.device, return_loss=True)
-            loss.backward()
+            loss.backward()                      # loss + 3D-ViT
+            if defer:
+                self.model.backward_deferred_text()   # then BERT (text stream), beside the ViT tail
         except BaseException:
             dist_sync.disarm()
             raise
+        finally:
+            if defer:
+                self.model.defer_text_backward = False
         return loss
 
     def optimizer_step(self):

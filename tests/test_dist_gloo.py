@@ -189,7 +189,8 @@ def _bucket_worker(rank, port, out_dir):
             tr.flat.grad.zero_()
             tr.forward_backward(xt[rows], xi[rows])
             # the text and image buckets went out from autograd hooks during the backward, the
-            # image one after the text one (BERT-first backward order); 'rest' waits for finish
+            # image one after the text one (the toy's text tower is the newer); 'rest' has no
+            # hook and goes out in finish
             assert tr.grad_sync.launched == ['text', 'image'], tr.grad_sync.launched
             tr.grad_sync.finish()
             assert tr.grad_sync.launched == ['text', 'image', 'rest']

@@ -172,12 +172,12 @@ def test_grad_buckets_final_when_launched(setup):
     """Backward-overlapped gradient sync (dist_sync.BucketedGradSync): with the
     hooks forced on at world 1, each bucket's gradient slice at the moment its hook launches the
     all-reduce must already equal its final value (bit-exact), the hooks must fire in bucket
-    order during the backward (BERT first), and only the last bucket waits for finish()."""
+    order during the backward (3D-ViT stacks, rest of the image tower, then BERT)."""
     cfg, model, hu, ids, mask, text = setup
     from ctclip_mi355x.trainer import CTClipTrainer
     tr = CTClipTrainer(model, lr=1e-4)
     gs = tr.grad_sync
-    assert [t for t, _, _ in gs.buckets] == ['text', 'vit_temporal', 'vit_spatial', 'rest']
+    assert [t for t, _, _ in gs.buckets] == ['vit_temporal', 'vit_spatial', 'vit_rest', 'text']
     snaps = {}
     fold = gs.before_launch
 
@@ -189,7 +189,7 @@ def test_grad_buckets_final_when_launched(setup):
     gs.force = True
     tr.flat.grad.zero_()
     tr.forward_backward(text, hu.cuda())
-    assert gs.launched == ['text', 'vit_temporal', 'vit_spatial'], gs.launched
+    assert gs.launched == ['vit_temporal', 'vit_spatial', 'vit_rest', 'text'], gs.launched
     gs.finish()
     torch.cuda.synchronize()
     for tag, off, n in gs.buckets:
