@@ -176,11 +176,14 @@ __global__ __launch_bounds__(256) void patch_wgrad_kernel(const float* __restric
                                                           const float* __restrict__ bt, int N, int K,
                                                           float* __restrict__ dW, float* __restrict__ dg,
                                                           float* __restrict__ db, int accumulate) {
+  // grid (K / 256, row chunks): dW is elementwise; dg / db partial sums of the chunk go out with
+  // one atomic add per column (the launcher zeroes them first when not accumulating)
   const int k = blockIdx.x * 256 + threadIdx.x;
   if (k >= K) return;
+  const int n0 = (int)((int64_t)N * blockIdx.y / gridDim.y), n1 = (int)((int64_t)N * (blockIdx.y + 1) / gridDim.y);
   float sg = 0.f, sb = 0.f;
   const float gk = g[k], bk = bt[k];
-  for (int n = 0; n < N; ++n) {
+  for (int n = n0; n < n1; ++n) {
     const float Gv = G[(int64_t)n * K + k], w = Wt[(int64_t)n * K + k];
     sg += w * Gv;
     sb += w * cs[n];
@@ -188,8 +191,8 @@ __global__ __launch_bounds__(256) void patch_wgrad_kernel(const float* __restric
     float* p = dW + (int64_t)n * K + k;
     *p = accumulate ? *p + d : d;
   }
-  dg[k] = accumulate ? dg[k] + sg : sg;
-  db[k] = accumulate ? db[k] + sb : sb;
+  atomicAdd(dg + k, sg);
+  atomicAdd(db + k, sb);
 }
 
 }  // namespace
@@ -311,8 +314,13 @@ extern "C" int ctclip_patch_ln(const void* video, int32_t is_f32, int32_t is_hu,
 extern "C" int ctclip_patch_wgrad(const float* G, const float* cs, const float* Wt, const float* g, const float* b,
                                   int32_t N, int32_t K, float* dW, float* dg, float* db, int32_t accumulate,
                                   void* stream) {
-  hipLaunchKernelGGL(patch_wgrad_kernel, dim3(cdiv(K, 256)), dim3(256), 0, (hipStream_t)stream, G, cs, Wt, g, b, N,
-                     K, dW, dg, db, accumulate);
+  if (!accumulate) {
+    (void)hipMemsetAsync(dg, 0, (size_t)K * 4, (hipStream_t)stream);
+    (void)hipMemsetAsync(db, 0, (size_t)K * 4, (hipStream_t)stream);
+  }
+  const int nch = std::max(1, std::min(N, 32));   // 16 column blocks x 32 row chunks at 512 x 4000
+  hipLaunchKernelGGL(patch_wgrad_kernel, dim3(cdiv(K, 256), nch), dim3(256), 0, (hipStream_t)stream, G, cs, Wt, g, b,
+                     N, K, dW, dg, db, accumulate);
   CT_CHECK_LAUNCH();
   return 0;
 }
