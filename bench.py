@@ -206,7 +206,7 @@ def main():
             traffic = round(rec['traffic_bytes_per_launch'] / 1e9, 4)
             traffic_src = 'profiles/r01_ff1_pmc.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, GB per launch)'
         result['roofline'] = {
-            'kernel': 'g256::gemm8p_kernel<true,true,true> FF1 (LN-out x W1^T, GEGLU epilogue)',
+            'kernel': 'g256::gemm8p_kernel<true,true,2> FF1 (LN-out x W1^T, GEGLU epilogue)',
             'bound': 'mfma', 'achieved': round(tflops, 1), 'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
             'frac': round(tflops / PEAK_BF16_TFLOPS, 4), 'traffic': traffic, 'traffic_unit': 'GB',
             'traffic_source': traffic_src, 'algorithmic_bytes': algo_bytes,

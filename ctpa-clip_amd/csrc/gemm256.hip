@@ -43,6 +43,8 @@ struct P {
   int64_t kper;
   int debug;     // diagnostic knob (CTCLIP_G256_DEBUG): 1 = skip the epilogue, 2 = skip the main loop
   int stagger;   // start delay (s_sleep units of 64 cycles) for the second co-resident workgroup
+  int gz;        // batch * split_k (8-phase tile count = ceil(N/256) * ceil(M/256) * gz)
+  int persist;   // 8-phase: persistent workgroups (one per CU) walking the tile sequence
 };
 
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
@@ -348,7 +350,8 @@ namespace p8 {
 constexpr int BM = 256, BNN = 256, BKK = 64, NTH = 512;
 constexpr int HALF = 128 * 64 * 2;   // 16 KB
 constexpr int TILEB = 4 * HALF;      // 64 KB per buffer
-constexpr int SMEM = 2 * TILEB;      // 128 KB
+// LDS: two 64 KB buffers (E, O)
+constexpr int SMEM_P = TILEB + 8 * 32 * EP_LD * 4;   // persistent: E + (O + staging overhang) = 132 KB
 enum { A0 = 0, A1 = 1, B0 = 2, B1 = 3 };
 
 __device__ __forceinline__ int kswz(int row) { return (row >> 1) & 7; }
@@ -590,6 +593,9 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
 // rounded to bf16 (as the stand-alone geglu_bwd reads it) and permlane-paired so every lane
 // owns 8 consecutive g-columns: one 16-B load of h's x part, one of its gate part, one 16-B
 // store each of dh.  The next row block's h loads are issued before this block's math.
+#ifndef GEGLU_BWD_LA
+#define GEGLU_BWD_LA 1
+#endif
 __device__ __forceinline__ void epilogue_geglu_bwd(const P& p, f32x4 (&acc)[8][4], int wr, int wc, int lane,
                                                    int64_t m0, int64_t n0, int bidx) {
   const int m = lane & 15, g = lane >> 4;
@@ -597,7 +603,8 @@ __device__ __forceinline__ void epilogue_geglu_bwd(const P& p, f32x4 (&acc)[8][4
   const int co = pair_coff(g);
   const u16* hb = (const u16*)p.R + bidx * p.sR;
   u16* db = (u16*)p.C + bidx * p.sC;
-  u32x4 hx[2][2], hg[2][2];
+  constexpr int LA = GEGLU_BWD_LA;   // row blocks of h loads in flight ahead of the math
+  u32x4 hx[LA + 1][2], hg[LA + 1][2];
   auto load = [&](int i, int b) {
     const int64_t gm = wrow0 + i * 16 + m;
 #pragma unroll
@@ -613,11 +620,12 @@ __device__ __forceinline__ void epilogue_geglu_bwd(const P& p, f32x4 (&acc)[8][4
       }
     }
   };
-  load(0, 0);
+#pragma unroll
+  for (int i = 0; i < LA; ++i) load(i, i);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int b = i & 1;
-    if (i + 1 < 8) load(i + 1, b ^ 1);
+    const int b = i % (LA + 1);
+    if (i + LA < 8) load(i + LA, (i + LA) % (LA + 1));
     const int64_t gm = wrow0 + i * 16 + m;
 #pragma unroll
     for (int jp = 0; jp < 2; ++jp) {
@@ -646,28 +654,54 @@ __device__ __forceinline__ void epilogue_geglu_bwd(const P& p, f32x4 (&acc)[8][4
 // TR = true: MFMA operands swapped (transposed accumulator) + the LDS-free epilogue_t, used for
 // bf16 outputs; TR = false: the LDS-staged row-chunk epilogue, used for f32 / residual / argmax
 // outputs (measured faster there: full-row f32 chunks, one argmax pass per staged quarter).
-template <bool AK, bool BKC, bool TR>
+//
+// Persistent over tiles (p.persist): the grid is at most one workgroup per CU and each walks the
+// XCD-remapped tile sequence wg, wg + grid, ...  After a tile's last MFMA the workgroup issues
+// the NEXT tile's prologue loads (TR: tile 0 + tile 1's A0/B0, as the cold prologue; non-TR:
+// tile 0 into buffer E, the epilogue staging lives in buffer O and beyond) and only then runs
+// this tile's epilogue, so the load latency and the store drain overlap instead of adding up.
+struct Tile {
+  int64_t m0, n0, kbeg;
+  int nk, split, bidx;
+};
+
+__device__ __forceinline__ Tile tile_at(const P& p, int lin, int gx, int gy, int ntiles) {
+  // XCD-aware remap of the linear tile index (round-robin dispatch: lin & 7 = XCD), so each
+  // XCD walks a contiguous range of tiles (x fastest, then y, then batch / split)
+  int id = lin;
+  if (ntiles >= 16) {
+    const int xcd = lin & 7, q = ntiles >> 3, r = ntiles & 7;
+    id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (lin >> 3);
+  }
+  const int gxy = gx * gy, z = id / gxy, rem = id - z * gxy, ty = rem / gx, tx = rem - ty * gx;
+  Tile t;
+  t.split = z % p.split_k;
+  t.bidx = z / p.split_k;
+  t.m0 = (int64_t)ty * p8::BM;
+  t.n0 = (int64_t)tx * p8::BNN;
+  t.kbeg = t.split * p.kper;
+  const int64_t kend = min(p.K, t.kbeg + p.kper);
+  t.nk = (kend > t.kbeg && !(p.debug & 2)) ? (int)((kend - t.kbeg) / p8::BKK) : 0;
+  return t;
+}
+
+template <bool AK, bool BKC, int EP>
 __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
   using namespace p8;
+  constexpr bool TR = EP >= 0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 2, wc = w & 3;
-  int tx, ty;
-  xcd_remap(tx, ty);
-  const int split = blockIdx.z % p.split_k, bidx = blockIdx.z / p.split_k;
-  const int64_t m0 = (int64_t)ty * BM, n0 = (int64_t)tx * BNN;
-  const int64_t kbeg = split * p.kper;
-  const int64_t kend = min(p.K, kbeg + p.kper);
-  const u16* A = p.A + bidx * p.sA;
-  const u16* B = p.B + bidx * p.sB;
-  const int nk = (kend > kbeg && !(p.debug & 2)) ? (int)((kend - kbeg) / BKK) : 0;
+  const int gx = (int)((p.N + BNN - 1) / BNN), gy = (int)((p.M + BM - 1) / BM);
+  const int ntiles = gx * gy * p.gz;
+  int lin = p.persist ? (int)blockIdx.x : (int)((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);
+  const int lstride = p.persist ? (int)gridDim.x : ntiles;
+  if (lin >= ntiles) return;
+  Tile T = tile_at(p, lin, gx, gy, ntiles);
   // desynchronise the CUs: half of the first dispatch round (every other workgroup within each
   // XCD) starts p.stagger x ~2k cycles late, so later rounds' store-heavy epilogues on those CUs
   // fall under the other half's MFMA main loops instead of all CUs storing at once
-  if (p.stagger > 0) {
-    const int lin = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-    if (lin < 256 && ((lin >> 3) & 1))
-      for (int s = 0; s < p.stagger; ++s) __builtin_amdgcn_s_sleep(32);
-  }
+  if (p.stagger > 0 && lin < 256 && ((lin >> 3) & 1))
+    for (int s = 0; s < p.stagger; ++s) __builtin_amdgcn_s_sleep(32);
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -675,13 +709,14 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto stage = [&](int which, int t) {
-    if (t >= nk) return;
+  auto stage_of = [&](const Tile& tl, int which, int t) {
+    if (t >= tl.nk) return;
     char* dst = smem + (t & 1) * TILEB + which * HALF;
-    const int64_t k0 = kbeg + (int64_t)t * BKK;
-    if (which < 2) stage_half<AK, true>(dst, A, p.lda, p.M, m0, k0, which, w, lane);
-    else stage_half<BKC, false>(dst, B, p.ldb, p.N, n0, k0, which - 2, w, lane);
+    const int64_t k0 = tl.kbeg + (int64_t)t * BKK;
+    if (which < 2) stage_half<AK, true>(dst, p.A + tl.bidx * p.sA, p.lda, p.M, tl.m0, k0, which, w, lane);
+    else stage_half<BKC, false>(dst, p.B + tl.bidx * p.sB, p.ldb, p.N, tl.n0, k0, which - 2, w, lane);
   };
+  auto stage = [&](int which, int t) { stage_of(T, which, t); };
 
   bf16x8 a[4][2], b0[2][2], b1[2][2];
 
@@ -737,69 +772,96 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  // prologue: tile 0 complete in E, tile 1's A0/B0 halves in flight
-  if (nk > 0) {
-    stage(A0, 0); stage(A1, 0); stage(B0, 0); stage(B1, 0);
-    stage(A0, 1); stage(B0, 1);
-    wait_ahead(nk > 1);
-  }
-  bar();
-  if (wr == 1) bar();   // the stagger: waves 4-7 run one barrier behind
+  // cold prologue: tile 0 complete in E, tile 1's A0/B0 halves in flight
+  stage(A0, 0); stage(A1, 0); stage(B0, 0); stage(B1, 0);
+  stage(A0, 1); stage(B0, 1);
+  wait_ahead(T.nk > 1);
 
-  for (int i = 0; 2 * i < nk; ++i) {
-    const int te = 2 * i, to = 2 * i + 1;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      load_frags(0, q);
-      if (q == 0) stage(B1, to);
-      if (q == 1) stage(A1, to);
-      if (q == 2) stage(A0, te + 2);
-      if (q == 3) { stage(B0, te + 2); if (to < nk) wait_ahead(te + 2 < nk); }
-      compute_phase();
-      mma(q);
-      bar();
-    }
-    if (to < nk) {
+  while (true) {
+    const int nk = T.nk;
+    bar();
+    if (wr == 1) bar();   // the stagger: waves 4-7 run one barrier behind
+    for (int i = 0; 2 * i < nk; ++i) {
+      const int te = 2 * i, to = 2 * i + 1;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        load_frags(1, q);
-        if (q == 0) stage(B1, te + 2);
-        if (q == 1) stage(A1, te + 2);
-        if (q == 2) stage(A0, to + 2);
-        if (q == 3) { stage(B0, to + 2); if (te + 2 < nk) wait_ahead(to + 2 < nk); }
+        load_frags(0, q);
+        if (q == 0) stage(B1, to);
+        if (q == 1) stage(A1, to);
+        if (q == 2) stage(A0, te + 2);
+        if (q == 3) { stage(B0, te + 2); if (to < nk) wait_ahead(te + 2 < nk); }
         compute_phase();
         mma(q);
         bar();
       }
+      if (to < nk) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          load_frags(1, q);
+          if (q == 0) stage(B1, te + 2);
+          if (q == 1) stage(A1, te + 2);
+          if (q == 2) stage(A0, to + 2);
+          if (q == 3) { stage(B0, to + 2); if (te + 2 < nk) wait_ahead(to + 2 < nk); }
+          compute_phase();
+          mma(q);
+          bar();
+        }
+      }
     }
-  }
-  if (wr == 0) bar();   // balance the stagger barrier
-  __syncthreads();      // every wave's last fragment reads done before the epilogue reuses LDS
-  if (p.debug & 1) {
+    if (wr == 0) bar();   // balance the stagger barrier
+    __syncthreads();      // every wave's last fragment reads done before LDS is refilled / reused
+    lin += lstride;
+    const bool more = lin < ntiles;
+    if (more) {
+      const Tile nx = tile_at(p, lin, gx, gy, ntiles);
+      stage_of(nx, A0, 0); stage_of(nx, A1, 0); stage_of(nx, B0, 0); stage_of(nx, B1, 0);
+      if constexpr (TR) { stage_of(nx, A0, 1); stage_of(nx, B0, 1); }
+    }
+    if (p.debug & 1) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+    } else if constexpr (EP == 2) {
+      epilogue_t<2>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
+    } else if constexpr (EP == 4) {
+      epilogue_geglu_bwd(p, acc, wr, wc, lane, T.m0, T.n0, T.bidx);
+    } else if constexpr (EP == 0) {
+      epilogue_t<0>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
+    } else {
+      // staging in buffer O and beyond (the next tile's tile 0 is landing in E)
+      epilogue(p, acc, smem + TILEB, w, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
+    }
+    if (!more) break;
+    T = tile_at(p, lin, gx, gy, ntiles);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
-    return;
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (!TR) {
+      __syncthreads();    // every wave's staging reads of O done before tile 1 lands there
+      stage(A0, 1); stage(B0, 1);
+    }
+    wait_ahead(T.nk > 1);
   }
-  if constexpr (TR) {
-    if (p.act == 2) epilogue_t<2>(p, acc, wr, wc, lane, m0, n0, split, bidx);
-    else if (p.act == 4) epilogue_geglu_bwd(p, acc, wr, wc, lane, m0, n0, bidx);
-    else epilogue_t<0>(p, acc, wr, wc, lane, m0, n0, split, bidx);
-  }
-  else epilogue(p, acc, smem, w, wr, wc, lane, m0, n0, split, bidx);
 }
 
-template <bool AK, bool BKC, bool TR>
+template <bool AK, bool BKC, int EP>
 int launch8(const P& p, int batch, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<AK, BKC, TR>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              p8::SMEM);
+    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<AK, BKC, EP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              p8::SMEM_P);
     attr = true;
   }
-  dim3 grid(cdiv(p.N, p8::BNN), cdiv(p.M, p8::BM), batch * p.split_k);
-  hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, TR>), grid, dim3(p8::NTH), p8::SMEM, st, p);
+  const int64_t ntiles = cdiv(p.N, p8::BNN) * cdiv(p.M, p8::BM) * (int64_t)p.gz;
+  if (p.persist) {
+    dim3 grid((unsigned)(ntiles < 256 ? ntiles : 256));
+    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP>), grid, dim3(p8::NTH), p8::SMEM_P, st, p);
+  } else {
+    dim3 grid(cdiv(p.N, p8::BNN), cdiv(p.M, p8::BM), batch * p.split_k);
+    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP>), grid, dim3(p8::NTH), p8::SMEM_P, st, p);
+  }
   CT_CHECK_LAUNCH();
   return 0;
 }
@@ -831,6 +893,7 @@ int launch_any(const P& p, bool ak, bool bk, int batch, hipStream_t st) {
 // 2 = 256 x 256 x 32 4-slot ring.  CTCLIP_GEMM_VARIANT or ctclip_gemm_set_variant() select it.
 static int g_variant = -1;
 static int g_stagger8 = -1;   // 8-phase start stagger (units of s_sleep(32)); -1 = default
+static int g_persist = -1;    // 8-phase persistent tile loop (CTCLIP_GEMM_PERSIST, default on)
 int variant() {
   if (g_variant < 0) {
     const char* e = getenv("CTCLIP_GEMM_VARIANT");
@@ -841,11 +904,21 @@ int variant() {
 }
 int tile_rows() { return variant() == 2 ? 2 : 1; }
 
+// epilogue kind, one kernel instantiation each (so the accumulator registers never share a
+// kernel with another epilogue's live ranges): -1 = LDS-staged rows (f32 / residual / argmax /
+// split-K slabs), 0 = transposed bf16, 2 = transposed GEGLU, 4 = transposed GEGLU backward
+template <bool AK, bool BKC>
+int launch8_ep(const P& p, int batch, hipStream_t st) {
+  if (p.act == 4) return launch8<AK, BKC, 4>(p, batch, st);
+  const bool tr = !p.c_f32 && p.split_k <= 1 && p.act != 3 && !p.R;
+  if (!tr) return launch8<AK, BKC, -1>(p, batch, st);
+  if (p.act == 2) return launch8<AK, BKC, 2>(p, batch, st);
+  return launch8<AK, BKC, 0>(p, batch, st);
+}
+
 template <bool AK>
 int launch8_any(const P& p, bool bk, int batch, hipStream_t st) {
-  const bool tr = p.act == 4 || (!p.c_f32 && p.split_k <= 1 && p.act != 3 && !p.R);
-  if (tr) return bk ? launch8<AK, true, true>(p, batch, st) : launch8<AK, false, true>(p, batch, st);
-  return bk ? launch8<AK, true, false>(p, batch, st) : launch8<AK, false, false>(p, batch, st);
+  return bk ? launch8_ep<AK, true>(p, batch, st) : launch8_ep<AK, false>(p, batch, st);
 }
 
 }  // namespace g256
@@ -873,6 +946,12 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
     stag = s ? atoi(s) : 0;
   }
   p.debug = dbg;
+  if (g_persist < 0) {
+    const char* e = getenv("CTCLIP_GEMM_PERSIST");
+    g_persist = e ? (atoi(e) != 0) : 1;
+  }
+  p.gz = batch * split;
+  p.persist = g_persist;
   // 8-phase default: stagger only the GEGLU GEMM, whose epilogue (h + g stores + erf) is long
   // enough that desynchronised CUs pay off (r01 sweep: 0.52 -> 0.48 ms at B = 8; neutral to
   // slightly negative on the plain / residual epilogues)
@@ -888,6 +967,13 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
 extern "C" int ctclip_gemm_set_stagger(int v) {
   const int old = g256::g_stagger8;
   g256::g_stagger8 = v;
+  return old;
+}
+
+// diagnostic: 8-phase persistent tile loop on / off; returns the previous value
+extern "C" int ctclip_gemm_set_persist(int v) {
+  const int old = g256::g_persist;
+  g256::g_persist = v != 0;
   return old;
 }
 

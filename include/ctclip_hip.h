@@ -62,6 +62,9 @@ int ctclip_gemm(const ctclip_gemm_args* a, void* stream);
 int ctclip_gemm_set_variant(int variant);
 /* diagnostic: start stagger of the 8-phase kernel (units of ~2k cycles); returns the previous */
 int ctclip_gemm_set_stagger(int units);
+/* diagnostic: 8-phase kernel as persistent workgroups walking the tile sequence (1, default) or
+ * one workgroup per tile (0); returns the previous setting.  Results are identical. */
+int ctclip_gemm_set_persist(int on);
 
 /* sum f32 slabs [s][rows][ld] -> out (f32 or bf16), optional accumulate into f32 out */
 int ctclip_reduce_slabs(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,

@@ -18,16 +18,27 @@ def _rel(a, b):
 
 
 def _variants(K, fn):
+    """Outputs of the 8-phase kernel (persistent, key 8) and the 128x256x32 kernel (key 1); the
+    8-phase kernel with one workgroup per tile must match the persistent one bit for bit."""
     from ctclip_mi355x import _lib
     outs = {}
-    prev = _lib.lib().ctclip_gemm_set_variant(8)
+    lib = _lib.lib()
+    prev, prev_p = lib.ctclip_gemm_set_variant(8), lib.ctclip_gemm_set_persist(1)
+    snap = lambda o: o.clone() if torch.is_tensor(o) else o  # noqa: E731
     try:
         for v in (8, 1):
-            _lib.lib().ctclip_gemm_set_variant(v)
-            outs[v] = fn()
+            lib.ctclip_gemm_set_variant(v)
+            outs[v] = snap(fn())
             torch.cuda.synchronize()
+        lib.ctclip_gemm_set_variant(8)
+        lib.ctclip_gemm_set_persist(0)
+        single = snap(fn())
+        torch.cuda.synchronize()
     finally:
-        _lib.lib().ctclip_gemm_set_variant(prev)
+        lib.ctclip_gemm_set_variant(prev)
+        lib.ctclip_gemm_set_persist(prev_p if prev_p >= 0 else 1)
+    if torch.is_tensor(single):
+        assert torch.equal(single, outs[8]), 'persistent 8-phase GEMM differs from one workgroup per tile'
     return outs
 
 
@@ -36,7 +47,7 @@ def _raw(K, M, N, Kd, A, lda, ak, B, ldb, bk, C, ldc, **kw):
     return C
 
 
-@pytest.mark.parametrize('M,N,Kd', [(4000, 2816, 512), (8192, 1536, 1408), (5000, 2048, 192)])
+@pytest.mark.parametrize('M,N,Kd', [(4000, 2816, 512), (8192, 1536, 1408), (5000, 2048, 192), (9000, 2816, 512)])
 def test_nt_bias_residual(K, M, N, Kd):
     torch.manual_seed(0)
     x = torch.randn(M, Kd, device='cuda').bfloat16()

@@ -52,8 +52,9 @@ def main():
     variants = [v for v in os.environ.get('GEMM_VARIANTS', '8,1').split(',')]
     for name, fn, fl in cases:
         row = []
-        for v in variants:   # '8' or '8s<stagger>'
-            vv, _, st = v.partition('s')
+        for v in variants:   # '8' or '8s<stagger>', 'n' suffix = not persistent
+            vv, _, st = v.rstrip('n').partition('s')
+            _lib.lib().ctclip_gemm_set_persist(0 if v.endswith('n') else 1)
             _lib.lib().ctclip_gemm_set_variant(int(vv))
             _lib.lib().ctclip_gemm_set_stagger(int(st) if st else -1)
             ms = timeit(fn)
@@ -61,6 +62,7 @@ def main():
         print(f'{name:34s} ' + ' | '.join(row), flush=True)
     _lib.lib().ctclip_gemm_set_variant(8)
     _lib.lib().ctclip_gemm_set_stagger(-1)
+    _lib.lib().ctclip_gemm_set_persist(1)
     if os.environ.get('NO_LIB'):
         return
     # hipBLASLt (torch.matmul) on the same shapes, for a library reference point
