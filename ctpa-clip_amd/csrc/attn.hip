@@ -181,7 +181,10 @@ __device__ __forceinline__ void load_tables(const AP& p, char* tab, int Lp, int 
 // ------------------------------------------------------------------------------------ forward
 // W waves per workgroup: 12 for the spatial (BIAS) shapes, whose 36 query blocks then split
 // evenly (3 per wave) at 12 waves per CU; 8 otherwise.
-template <int D, bool BIAS, int W = (BIAS ? 12 : NW)>
+// RUN (bias shapes with Wg % 4 == 0 and L % 32 == 0): the 4 keys a lane scores per MFMA block
+// are consecutive in one grid row, so their bins are cq - kb[k0] - 0..3 -- one table read and one
+// address for all four bias reads (fixed offsets) -- and there are no padded keys to mask.
+template <int D, bool BIAS, int W = (BIAS ? 12 : NW), bool RUN = false>
 __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KK = D / 32, DB = D / 16, RS = Img<D>::RS, NTH = W * 64;
@@ -236,6 +239,16 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
 #pragma unroll
       for (int bi = 0; bi < 2; ++bi) {
         const int k0 = kc + 16 * bi + 4 * g;
+        if constexpr (RUN) {
+          const float* up = ub + (cq - kb[k0] - 3);   // up[3 - r] = ub[bin(q, k0 + r)]
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float x = sa[bi][r] * sc2 + up[3 - r];
+            sa[bi][r] = x;
+            cmax = fmaxf(cmax, x);
+          }
+          continue;
+        }
         const f32x4 ma = *(const f32x4*)(mrow + k0);
         int4 kbv;
         if (BIAS) kbv = *(const int4*)(kb + k0);
@@ -406,7 +419,7 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(AP p) {
 // lane owns a key; elements run over queries.  Padded queries carry lse = +inf (probability 0);
 // a masked / padded key adds -inf through kadd.
 // W waves per workgroup as in attn_fwd_kernel (12 for the spatial shapes: 3 key blocks per wave)
-template <int D, bool BIAS, int W = (BIAS ? 12 : NW)>
+template <int D, bool BIAS, int W = (BIAS ? 12 : NW), bool RUN = false>
 __global__ __launch_bounds__(W * 64) void attn_bwd_dkv_kernel(AP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KK = D / 32, DB = D / 16, RS = Img<D>::RS, NTH = W * 64;
@@ -480,11 +493,15 @@ __global__ __launch_bounds__(W * 64) void attn_bwd_dkv_kernel(AP p) {
         const f32x4 lv = *(const f32x4*)(ls + q0);
         const f32x4 dlv = *(const f32x4*)(dls + q0);
         int4 qbv;
-        if (BIAS) qbv = *(const int4*)(kb + q0);
+        const float* up = nullptr;
+        if constexpr (RUN) up = ub + (kb[q0] - ck);   // up[r] = ub[bin(q0 + r, key)]
+        else if (BIAS) qbv = *(const int4*)(kb + q0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float x = sa[bi][r] * sc2 + kadd;
-          if (BIAS) x += ub[qbv[r] - ck];
+          float x;
+          if constexpr (RUN) x = sa[bi][r] * sc2 + up[r];
+          else x = sa[bi][r] * sc2 + kadd;
+          if (BIAS && !RUN) x += ub[qbv[r] - ck];
           const float pr = fexp2(x - lv[r]);
           const float ds = pr * (da[bi][r] - dlv[r]);
           sa[bi][r] = pr;
@@ -521,7 +538,7 @@ __global__ __launch_bounds__(W * 64) void attn_bwd_dkv_kernel(AP p) {
 // frame-summed dS of their (16 queries x L/2 keys) tile in registers, and bin it to the
 // (2gh-1)(2gw-1) offsets once at the end (LDS atomics, then one global atomic per bin).
 // dQ of each frame is complete inside the workgroup (the two key halves meet in LDS).
-template <int MAXCH>   // max 32-key chunks per key half
+template <int MAXCH, bool RUN = false>   // max 32-key chunks per key half; RUN as attn_fwd_kernel
 __global__ __launch_bounds__(NT) void attn_bwd_dq_bias_kernel(AP p, int nfc) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int D = 32, RS = Img<D>::RS, DB = 2;
@@ -593,11 +610,18 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_bias_kernel(AP p, int nfc) {
 #pragma unroll
         for (int bi = 0; bi < 2; ++bi) {
           const int k0 = kc + 16 * bi + 4 * g;
-          const int4 kbv = *(const int4*)(kb + k0);
-          const f32x4 ma = *(const f32x4*)(madd + k0);
+          int4 kbv;
+          f32x4 ma;
+          const float* up = nullptr;
+          if constexpr (RUN) {
+            up = ub + (cq - kb[k0] - 3);   // up[3 - r] = ub[bin(q, k0 + r)]
+          } else {
+            kbv = *(const int4*)(kb + k0);
+            ma = *(const f32x4*)(madd + k0);
+          }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float x = sa[bi][r] * sc2 + ma[r] + ub[cq - kbv[r]];
+            const float x = RUN ? sa[bi][r] * sc2 + up[3 - r] : sa[bi][r] * sc2 + ma[r] + ub[cq - kbv[r]];
             const float ds = fexp2(x - lse2) * (da[bi][r] - dl);
             acc[ci][bi][r] += ds;
             sa[bi][r] = ds * p.scale;
@@ -672,7 +696,16 @@ void set_attrs() {
   set_attrs_b<64, true>();
   (void)hipFuncSetAttribute((const void*)attn_bwd_dq_bias_kernel<9>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dq_bias_kernel<9, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<32, true, 12, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<32, true, 12, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
+
+// bias shapes whose 4-key / 4-query MFMA groups never straddle a grid row and have no padding
+bool run_ok(const AP& p) { return p.bias_u && p.Wg % 4 == 0 && p.L % 32 == 0; }
 
 int fill(AP& p, const ctclip_attn_args* a) {
   if (a->D != 32 && a->D != 64) return CT_ESHAPE;
@@ -715,6 +748,12 @@ size_t table_bytes(const AP& p, int Lp, bool bins) {
 
 template <int D>
 void launch_fwd(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
+  if constexpr (D == 32) {
+    if (run_ok(p)) {
+      hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true>), grid, dim3(12 * 64), lds, st, p);
+      return;
+    }
+  }
   if (p.bias_u) hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(12 * 64), lds, st, p);
   else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(NT), lds, st, p);
 }
@@ -727,6 +766,12 @@ void launch_dq(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
 
 template <int D>
 void launch_dkv(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
+  if constexpr (D == 32) {
+    if (run_ok(p)) {
+      hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, true, 12, true>), grid, dim3(12 * 64), lds, st, p);
+      return;
+    }
+  }
   if (p.bias_u) hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, true>), grid, dim3(12 * 64), lds, st, p);
   else hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, false>), grid, dim3(NT), lds, st, p);
 }
@@ -1007,7 +1052,8 @@ extern "C" int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream) {
     const size_t lds = (size_t)2 * Lp * RSb + 2 * (size_t)((p.nbins + 3) & ~3) * 4 + 2 * (size_t)Lp * 4 +
                        4 * 64 * 8 * 4;
     if (lds > 160 * 1024) return CT_ESHAPE;
-    hipLaunchKernelGGL(attn_bwd_dq_bias_kernel<9>, dim3(p.H, nqg, nfc), dim3(NT), lds, st, p, nfc);
+    if (run_ok(p)) hipLaunchKernelGGL((attn_bwd_dq_bias_kernel<9, true>), dim3(p.H, nqg, nfc), dim3(NT), lds, st, p, nfc);
+    else hipLaunchKernelGGL((attn_bwd_dq_bias_kernel<9>), dim3(p.H, nqg, nfc), dim3(NT), lds, st, p, nfc);
     launch_dkv<32>(p, grid, lds2, st);
     CT_CHECK_LAUNCH();
     return 0;

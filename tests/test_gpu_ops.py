@@ -137,11 +137,12 @@ def _cpb_table(H, gh, gw):
     return u, bins
 
 
-@pytest.mark.parametrize('case', ['spatial', 'spatial_small', 'temporal', 'temporal_l5_h3', 'temporal_l32', 'bert'])
+@pytest.mark.parametrize('case', ['spatial', 'spatial_small', 'spatial_8x8', 'temporal', 'temporal_l5_h3', 'temporal_l32', 'bert'])
 def test_attention(K, case):
     torch.manual_seed(3)
     if case.startswith('spatial'):
-        gh = gw = 24 if case == 'spatial' else 6
+        # 24 x 24 and 8 x 8 take the row-run bias path (Wg % 4 == 0, L % 32 == 0), 6 x 6 the general one
+        gh = gw = {'spatial': 24, 'spatial_small': 6, 'spatial_8x8': 8}[case]
         L, H, D, nseq = gh * gw, 8, 32, 3
         M = nseq * L
         seq = (1, L, 0, 1)
