@@ -167,7 +167,109 @@ __global__ __launch_bounds__(256) void patch_ln_strip_kernel(const void* __restr
   for (int e = pd + 2 * lane; e < ldo; e += 128) o[e >> 1] = 0u;   // K padding of the patch-embed GEMM
 }
 
+// x / 1000.f, correctly rounded, for the clamped HU range: one reciprocal product and one fma
+// correction (checked against IEEE division for every integer in [-1000, 1000]:
+// tests/test_hu_divide.py) instead of the ~10-instruction division sequence
+__device__ __forceinline__ float div1000(float x) {
+#pragma clang fp contract(off)
+  const float R = 1.0f / 1000.0f;
+  const float q0 = x * R;
+  const float r = __builtin_fmaf(-q0, 1000.0f, x);
+  return __builtin_fmaf(r, R, q0);
+}
+
+// P = 20 strip kernel (the CT-CLIP patch): the strip stays in LDS in its natural [PT*P rows]
+// [ntk*P columns] layout -- one ds_write_b128 per 16-B load instead of a per-voxel scatter --
+// and phase 2 maps pair j of a patch to (row j / 10, column 2 (j % 10)) with constant divisors.
+template <bool F32>
+__global__ __launch_bounds__(256) void patch_ln_strip20_kernel(const void* __restrict__ video, int is_hu, int T,
+                                                               int Hg, int Wg, int64_t vol_stride, int H, int W,
+                                                               int PT, float eps, u16* __restrict__ out,
+                                                               int64_t ldo) {
+  using E = typename std::conditional<F32, float, short>::type;
+  constexpr int P = 20, VEC = F32 ? 4 : 8;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  E* sx = (E*)smem_raw;   // [PT * P][ntk * P]
+  constexpr int NCH = PW * 4096 / VEC / 256;
+  const int pd = PT * P * P;
+  int r = blockIdx.y;
+  const int hg = r % Hg; r /= Hg;
+  const int t = r % T;
+  const int b = r / T;
+  const int wg0 = blockIdx.x * PW;
+  const int ntk = min(PW, Wg - wg0);
+  const int sw = ntk * P, cpr = sw / VEC;
+  const int nchunk = PT * P * cpr;
+  const int64_t base = (int64_t)b * vol_stride + ((int64_t)t * PT * H + (int64_t)hg * P) * W + (int64_t)wg0 * P;
+  // branch-free loads (clamped chunk index), all in flight before the first LDS write
+  u32x4 ld[NCH];
+#pragma unroll
+  for (int m = 0; m < NCH; ++m) {
+    const int c = min((int)threadIdx.x + m * 256, nchunk - 1);
+    const int k = c % cpr, rowi = c / cpr, p1 = rowi % P, pt = rowi / P;
+    ld[m] = *(const u32x4*)((const E*)video + base + ((int64_t)pt * H + p1) * W + k * VEC);
+  }
+  __builtin_amdgcn_sched_barrier(0);   // keep the scheduler from pairing each load with its write
+  // unconditional writes (lanes past the strip rewrite the last chunk with its own bytes), so the
+  // loads are not sunk into per-chunk branches and serialised behind their writes
+#pragma unroll
+  for (int m = 0; m < NCH; ++m) {
+    const int c = min((int)threadIdx.x + m * 256, nchunk - 1);
+    *(u32x4*)(sx + c * VEC) = ld[m];   // row c / cpr, column (c % cpr) * VEC
+  }
+  __syncthreads();
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (w >= ntk) return;
+  const E* px = sx + w * P;
+  constexpr int NP = 32;   // pairs per lane: pd <= 4096
+  float v[NP][2];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int j = lane + 64 * i;
+    v[i][0] = v[i][1] = 0.f;
+    if (2 * j < pd) {
+      const int row = j / (P / 2), col = 2 * (j - row * (P / 2));
+      const E* e = px + row * sw + col;
+      if constexpr (F32) {
+        const float2 u = *(const float2*)e;
+        v[i][0] = u.x;
+        v[i][1] = u.y;
+      } else {
+        const uint32_t u = *(const uint32_t*)e;
+        v[i][0] = (float)(short)(u & 0xffffu);
+        v[i][1] = (float)(short)(u >> 16);
+      }
+      if (is_hu) {
+        v[i][0] = div1000(fminf(fmaxf(v[i][0], -1000.f), 1000.f));
+        v[i][1] = div1000(fminf(fmaxf(v[i][1], -1000.f), 1000.f));
+      }
+    }
+    s += v[i][0] + v[i][1];
+  }
+  const float mean = warp_sum(s) / pd;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    if (2 * (lane + 64 * i) < pd) {
+      const float d0 = v[i][0] - mean, d1 = v[i][1] - mean;
+      q += d0 * d0 + d1 * d1;
+    }
+  }
+  const float rstd = rsqrtf(warp_sum(q) / pd + eps);
+  const int64_t tok = (((int64_t)b * T + t) * Hg + hg) * Wg + wg0 + w;
+  uint32_t* o = (uint32_t*)(out + tok * ldo);
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int e = 2 * (lane + 64 * i);
+    if (e < pd)
+      o[e >> 1] = (uint32_t)f2bf((v[i][0] - mean) * rstd) | ((uint32_t)f2bf((v[i][1] - mean) * rstd) << 16);
+  }
+  for (int e = pd + 2 * lane; e < ldo; e += 128) o[e >> 1] = 0u;   // K padding of the patch-embed GEMM
+}
+
 bool s_strip_attr = false;
+bool s_strip20_attr = false;
 
 // Given G = dy^T . xhat  [N][K] (f32) and colsum(dy) cs[N], produce the grads of the folded
 // LayerNorm+Linear pair: dW = G*g + cs (x) b, dgamma[k] = sum_n W[n,k] G[n,k], dbeta[k] = sum_n W[n,k] cs[n].
@@ -297,7 +399,21 @@ extern "C" int ctclip_patch_ln(const void* video, int32_t is_f32, int32_t is_hu,
     }
     dim3 grid(cdiv(Wg, PW), B * T * Hg);
     const size_t sm = (size_t)PW * pd * (is_f32 ? 4 : 2);
-    if (is_f32)
+    if (P == 20) {
+      if (!s_strip20_attr) {
+        (void)hipFuncSetAttribute((const void*)patch_ln_strip20_kernel<true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, PW * 4096 * 4);
+        (void)hipFuncSetAttribute((const void*)patch_ln_strip20_kernel<false>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, PW * 4096 * 4);
+        s_strip20_attr = true;
+      }
+      if (is_f32)
+        hipLaunchKernelGGL(patch_ln_strip20_kernel<true>, grid, dim3(256), sm, (hipStream_t)stream, video, is_hu, T,
+                           Hg, Wg, vol, H, W, PT, eps, (u16*)out, ldo);
+      else
+        hipLaunchKernelGGL(patch_ln_strip20_kernel<false>, grid, dim3(256), sm, (hipStream_t)stream, video, is_hu, T,
+                           Hg, Wg, vol, H, W, PT, eps, (u16*)out, ldo);
+    } else if (is_f32)
       hipLaunchKernelGGL(patch_ln_strip_kernel<true>, grid, dim3(256), sm, (hipStream_t)stream, video, is_hu, T, Hg,
                          Wg, vol, H, W, PT, P, eps, (u16*)out, ldo);
     else

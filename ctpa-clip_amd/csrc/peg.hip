@@ -185,32 +185,46 @@ constexpr int HT = 2, SEG = 3, SEGW = 6, TNTH = 128, WNTH = 256, LMAX = 8, NSLOT
 
 __host__ __device__ inline int plane_bytes(int W) { return (HT + 2) * (W + 2) * 128; }
 
-// issue this thread's loads of plane tp (view coordinates) into registers
-template <int NT>
-__device__ __forceinline__ void plane_load(const u16* __restrict__ x, const Geo& g, int D, int b, int h0, int c0,
-                                           int tp, u32x4 (&reg)[LMAX * TNTH / NT]) {
+// issue this thread's loads of plane tp (view coordinates) into registers.  The loads are
+// unconditional (out-of-plane / padding slots re-read the tensor's first chunk) and the zero
+// padding is applied in plane_store from the returned bit mask: a conditional load (value or
+// zero) makes the compiler merge the two with register copies right after the load, i.e. an
+// immediate s_waitcnt vmcnt(0) that serialises the prefetch with the step it should overlap.
+// BF = false keeps conditional loads (zero in the register, mask all ones): the weight-gradient
+// kernel, whose register budget (3 workgroups per CU) the branch-free form overflows (measured
+// 107 -> 126 us there, while the conv kernels gain 174 -> 156 us)
+template <int NT, bool BF = true>
+__device__ __forceinline__ unsigned plane_load(const u16* __restrict__ x, const Geo& g, int D, int b, int h0, int c0,
+                                               int tp, u32x4 (&reg)[LMAX * TNTH / NT]) {
   const int nl = (HT + 2) * (g.W + 2) * 8;
+  unsigned valid = BF ? 0u : ~0u;
 #pragma unroll
   for (int m = 0; m < LMAX * TNTH / NT; ++m) {
     const int i = threadIdx.x + m * NT;
-    reg[m] = u32x4{0u, 0u, 0u, 0u};
-    if (i < nl) {
-      const int k = i & 7, cw = (i >> 3) % (g.W + 2), hr = (i >> 3) / (g.W + 2);
-      const int h = h0 - 1 + hr, w = cw - 1;
-      if (h >= 0 && h < g.H && w >= 0 && w < g.W)
-        reg[m] = *(const u32x4*)(x + (int64_t)canon(g, b, (tp * g.H + h) * g.W + w) * D + c0 + k * 8);
+    const int k = i & 7, cw = (i >> 3) % (g.W + 2), hr = (i >> 3) / (g.W + 2);
+    const int h = h0 - 1 + hr, w = cw - 1;
+    const bool ok = i < nl && h >= 0 && h < g.H && w >= 0 && w < g.W;
+    if constexpr (BF) {
+      const int64_t row = ok ? (int64_t)canon(g, b, (tp * g.H + h) * g.W + w) : 0;
+      reg[m] = *(const u32x4*)(x + row * D + c0 + k * 8);
+      valid |= (unsigned)ok << m;
+    } else {
+      reg[m] = u32x4{0u, 0u, 0u, 0u};
+      if (ok) reg[m] = *(const u32x4*)(x + (int64_t)canon(g, b, (tp * g.H + h) * g.W + w) * D + c0 + k * 8);
     }
   }
+  return valid;
 }
 
 template <int NT>
-__device__ __forceinline__ void plane_store(char* ring, int W, int tp, const u32x4 (&reg)[LMAX * TNTH / NT]) {
+__device__ __forceinline__ void plane_store(char* ring, int W, int tp, const u32x4 (&reg)[LMAX * TNTH / NT],
+                                            unsigned valid) {
   const int nl = (HT + 2) * (W + 2) * 8;
   char* dst = ring + (tp % NSLOT) * plane_bytes(W);
 #pragma unroll
   for (int m = 0; m < LMAX * TNTH / NT; ++m) {
     const int i = threadIdx.x + m * NT;
-    if (i < nl) *(u32x4*)(dst + i * 16) = reg[m];
+    if (i < nl) *(u32x4*)(dst + i * 16) = ((valid >> m) & 1) ? reg[m] : u32x4{0u, 0u, 0u, 0u};
   }
 }
 
@@ -234,9 +248,10 @@ __global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ 
   if (threadIdx.x < 64) bs[threadIdx.x] = bias ? bias[c0 + threadIdx.x] : 0.f;
   const int lead = TR ? 2 : 0;
   u32x4 reg[LMAX];   // LMAX * TNTH / TNTH
+  unsigned rvalid = 0;
   for (int tp = 0; tp <= lead && tp < g.T; ++tp) {
-    plane_load<TNTH>(xin, g, D, b, h0, c0, tp, reg);
-    plane_store<TNTH>(ring, g.W, tp, reg);
+    rvalid = plane_load<TNTH>(xin, g, D, b, h0, c0, tp, reg);
+    plane_store<TNTH>(ring, g.W, tp, reg, rvalid);
   }
   __syncthreads();
   // one (row, w-segment, chunk) item per thread (tiled_ok: HT * ceil(W/SEG) * 8 <= TNTH)
@@ -246,24 +261,25 @@ __global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ 
   const int h = h0 + r, w0 = s * SEG;
   const bool active = o < HT * ns * 8 && h < g.H;
   // residual rows of this thread's outputs, prefetched one step ahead with the plane
+  // (unconditional loads as in plane_load; rows without a residual read w[0..7] and are masked)
   auto res_load = [&](int t, f32x4 (&rv)[SEG][2]) {
 #pragma unroll
     for (int j = 0; j < SEG; ++j) {
-      rv[j][0] = rv[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (res && active && w0 + j < g.W) {
-        const float* p = res + (int64_t)canon(g, b, (t * g.H + h) * g.W + w0 + j) * D + c0 + ch * 8;
-        rv[j][0] = *(const f32x4*)p;
-        rv[j][1] = *(const f32x4*)(p + 4);
-      }
+      const bool ok = res && active && w0 + j < g.W;
+      const float* p = ok ? res + (int64_t)canon(g, b, (t * g.H + h) * g.W + w0 + j) * D + c0 + ch * 8 : w;
+      rv[j][0] = *(const f32x4*)p;
+      rv[j][1] = *(const f32x4*)(p + 4);
     }
   };
+  const bool has_res = res != nullptr;
   f32x4 rv[SEG][2];
   res_load(0, rv);
   for (int t = 0; t < g.T; ++t) {
     const int tn = t + lead + 1;
-    if (tn < g.T) plane_load<TNTH>(xin, g, D, b, h0, c0, tn, reg);
+    // always issued (the last steps re-read plane T-1, never stored) so no branch merges `reg`
+    const unsigned nvalid = plane_load<TNTH>(xin, g, D, b, h0, c0, min(tn, g.T - 1), reg);
     f32x4 rn[SEG][2];
-    if (t + 1 < g.T) res_load(t + 1, rn);
+    res_load(min(t + 1, g.T - 1), rn);
     if (active) {
       float acc[SEG][8];
 #pragma unroll
@@ -306,8 +322,10 @@ __global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ 
         const int wq = w0 + j;
         if (wq >= g.W) break;
         const int64_t co = (int64_t)canon(g, b, (t * g.H + h) * g.W + wq) * D + c0 + ch * 8;
+        if (has_res) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { acc[j][e] += rv[j][0][e]; acc[j][4 + e] += rv[j][1][e]; }
+          for (int e = 0; e < 4; ++e) { acc[j][e] += rv[j][0][e]; acc[j][4 + e] += rv[j][1][e]; }
+        }
         if (out) {
           *(f32x4*)(out + co) = f32x4{acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
           *(f32x4*)(out + co + 4) = f32x4{acc[j][4], acc[j][5], acc[j][6], acc[j][7]};
@@ -317,11 +335,9 @@ __global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ 
     }
     // the slot of plane tn held plane tn - 3, read in this step: write it after a barrier
     __syncthreads();
-    if (tn < g.T) plane_store<TNTH>(ring, g.W, tn, reg);
-    if (t + 1 < g.T) {
+    if (tn < g.T) plane_store<TNTH>(ring, g.W, tn, reg, nvalid);
 #pragma unroll
-      for (int j = 0; j < SEG; ++j) { rv[j][0] = rn[j][0]; rv[j][1] = rn[j][1]; }
-    }
+    for (int j = 0; j < SEG; ++j) { rv[j][0] = rn[j][0]; rv[j][1] = rn[j][1]; }
     __syncthreads();
   }
 }
@@ -344,20 +360,23 @@ __global__ __launch_bounds__(WNTH, 3) void peg_wgrad_tile_kernel(const u16* __re
   // planes two steps ahead (regA = plane t+1, regB = plane t+2), this thread's dout one step
   // ahead (one (row, segment) item per thread: wgrad_ok)
   u32x4 regA[LMAX * TNTH / WNTH], regB[LMAX * TNTH / WNTH];
-  plane_load<WNTH>(xin, g, D, b, h0, c0, 0, regA);
-  plane_store<WNTH>(ring, g.W, 0, regA);
-  if (g.T > 1) plane_load<WNTH>(xin, g, D, b, h0, c0, 1, regA);
+  unsigned va = plane_load<WNTH, false>(xin, g, D, b, h0, c0, 0, regA), vb = ~0u;
+  plane_store<WNTH>(ring, g.W, 0, regA, va);
+  if (g.T > 1) va = plane_load<WNTH, false>(xin, g, D, b, h0, c0, 1, regA);
   const int ns = (g.W + SEGW - 1) / SEGW;
   const int items = HT * ns * 32;
   const int o = threadIdx.x;
   const int s = (o >> 5) % ns, r = (o >> 5) / ns;
   const int h = h0 + r, w0 = s * SEGW;
   const bool act = o < items && h < g.H;
+  unsigned dmask = 0;
+#pragma unroll
+  for (int j = 0; j < SEGW; ++j) dmask |= (unsigned)(act && w0 + j < g.W) << j;
   auto dload = [&](int t, uint32_t (&u)[SEGW]) {
 #pragma unroll
     for (int j = 0; j < SEGW; ++j) {
       u[j] = 0;
-      if (act && w0 + j < g.W)
+      if ((dmask >> j) & 1)
         u[j] = *(const uint32_t*)(dout + (int64_t)canon(g, b, (t * g.H + h) * g.W + w0 + j) * D + c0 + pair * 2);
     }
   };
@@ -366,7 +385,7 @@ __global__ __launch_bounds__(WNTH, 3) void peg_wgrad_tile_kernel(const u16* __re
   __syncthreads();
   for (int t = 0; t < g.T; ++t) {
     const int tn = t + 1;
-    if (tn + 1 < g.T) plane_load<WNTH>(xin, g, D, b, h0, c0, tn + 1, regB);
+    if (tn + 1 < g.T) vb = plane_load<WNTH, false>(xin, g, D, b, h0, c0, tn + 1, regB);
     if (tn < g.T) dload(tn, dn);
     if (act) {
       float dv[SEGW][2];
@@ -404,9 +423,10 @@ __global__ __launch_bounds__(WNTH, 3) void peg_wgrad_tile_kernel(const u16* __re
       }
     }
     __syncthreads();   // slot of plane tn held plane tn - 3, read in this step
-    if (tn < g.T) plane_store<WNTH>(ring, g.W, tn, regA);
+    if (tn < g.T) plane_store<WNTH>(ring, g.W, tn, regA, va);
 #pragma unroll
     for (int m = 0; m < LMAX * TNTH / WNTH; ++m) regA[m] = regB[m];
+    va = vb;
 #pragma unroll
     for (int j = 0; j < SEGW; ++j) du[j] = dn[j];
     __syncthreads();

@@ -6,6 +6,11 @@ import sqlite3
 import sys
 
 
+def short(n):
+    n = n.replace('(anonymous namespace)::', '').replace('void ', '')
+    return n.split('(')[0]
+
+
 def main():
     db = sqlite3.connect(sys.argv[1])
     marker = sys.argv[2] if len(sys.argv) > 2 else 'patch_ln_strip_kernel'
@@ -30,7 +35,15 @@ def main():
                 cl.append([s, e, 1, e - s, n, n])
         for s, e, k, b, a, z in cl:
             print(f'  {1e-6 * (s - t0):7.2f} .. {1e-6 * (e - t0):7.2f} ms  {k:4d} kernels  busy {b / 1e6:6.2f}  '
-                  f'{a.split("(")[0][:38]:38s} .. {z.split("(")[0][:38]}')
+                  f'{short(a)[:38]:38s} .. {short(z)[:38]}')
+        tot = {}
+        for s0, e0, _, n in seq:
+            k = short(n)
+            c, t = tot.get(k, (0, 0))
+            tot[k] = (c + 1, t + e0 - s0)
+        print(f'  top kernels on stream {q} this step:')
+        for k, (c, t) in sorted(tot.items(), key=lambda kv: -kv[1][1])[:25]:
+            print(f'    {t / 1e3:9.1f} us  {c:4d}x  {k[:90]}')
 
 
 if __name__ == '__main__':
