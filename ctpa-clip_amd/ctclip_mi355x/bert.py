@@ -99,6 +99,16 @@ class BertModel(nn.Module):
             if isinstance(m, nn.Linear):
                 nn.init.zeros_(m.bias)
 
+    def param_order(self):
+        """All parameters, each layer's query / key / value weights then biases first and adjacent,
+        so the fused QKV GEMM reads them as one slice of the trainer's arenas (functional.bf_cat)."""
+        first = []
+        for lyr in self.encoder.layer:
+            a = lyr.attention.self
+            first += [a.query.weight, a.key.weight, a.value.weight, a.query.bias, a.key.bias, a.value.bias]
+        ids = {id(p) for p in first}
+        return first + [p for p in self.parameters() if id(p) not in ids]
+
     def forward(self, input_ids, attention_mask=None, join=True, ready=None, **_):
         """Runs on the text stream (streams.py) when there is one, ordered after ``ready`` (an event
         of the calling stream; default: everything queued on it so far) and after the previous

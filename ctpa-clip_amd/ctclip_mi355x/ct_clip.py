@@ -167,10 +167,12 @@ class CTCLIP(nn.Module):
         3D-ViT's temporal stack, spatial stack, the rest of the image tower (patch embed, CPB),
         then BERT (back-propagated last, see encode)."""
         vt = self.visual_transformer
+        order = getattr(self.text_transformer, 'param_order', None)
+        text_first = order() if order is not None else []
         return [('vit_temporal', list(vt.enc_temporal_transformer.parameters())),
                 ('vit_spatial', list(vt.enc_spatial_transformer.parameters())),
                 ('vit_rest', list(vt.parameters())),
-                ('text', list(self.parameters()))]
+                ('text', text_first + list(self.parameters()))]
 
     def _pool_tokens(self, tokens):
         """mean over t + flatten of already-quantised tokens (ct_clip.py:724,740)."""

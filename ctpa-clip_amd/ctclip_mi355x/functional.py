@@ -111,8 +111,53 @@ def pack_ff2(W2):
     return K.pack_rows(W2, W2.shape[0], ff_pad(W2.shape[1]))
 
 
+def shadow_bf16(W):
+    """The bf16 copy of parameter W that the trainer's Adam kernel keeps (trainer.FlatParams), or
+    None when W has none or was changed since it was written."""
+    sh = getattr(W, '_ctclip_bf16', None)
+    if sh is None or W._version != getattr(W, '_ctclip_ver', -1) or W.data_ptr() != getattr(W, '_ctclip_ptr', 0):
+        return None
+    return sh
+
+
 def bf(W):
-    return K.cast_bf16(W.contiguous())
+    """bf16 weight for the MFMA GEMMs: the Adam-maintained shadow when current, else a cast."""
+    sh = shadow_bf16(W)
+    return sh if sh is not None else K.cast_bf16(W.contiguous())
+
+
+def _adjacent(ts, arena_of):
+    """(arena, first offset) when tensors ts are consecutive, in order, in one arena."""
+    flat = getattr(ts[0], '_ctclip_flat', None)
+    if flat is None or any(getattr(t, '_ctclip_flat', None) is not flat for t in ts):
+        return None
+    off = ts[0]._ctclip_off
+    o = off
+    for t in ts:
+        if t._ctclip_off != o:
+            return None
+        o += t.numel()
+    return arena_of(flat), off, o
+
+
+def bf_cat(ws):
+    """bf16 of torch.cat(ws, 0): a view of the shadow arena when the weights are adjacent there
+    (BERT's q / k / v, see bert.BertModel.param_order), else cat + cast."""
+    if all(shadow_bf16(w) is not None for w in ws):
+        a = _adjacent(ws, lambda f: f.bf16)
+        if a is not None:
+            arena, lo, hi = a
+            return arena[lo:hi].view(-1, *ws[0].shape[1:])
+    return K.cast_bf16(torch.cat(ws, 0))
+
+
+def cat_f32(ts):
+    """torch.cat(ts, 0) of f32 parameters: a view of the parameter arena when adjacent there."""
+    a = _adjacent(ts, lambda f: f.data)
+    if a is not None and all(t.data_ptr() == getattr(t, '_ctclip_ptr', 0) for t in ts):
+        arena, lo, hi = a
+        return arena[lo:hi].view(-1, *ts[0].shape[1:])
+    return torch.cat(ts, 0).contiguous()
 
 
 # ----------------------------------------------------------------------------- patch embedding
@@ -557,8 +602,8 @@ class BertLayerFn(torch.autograd.Function):
                 bout, ln2_w, ln2_b):
         Hd = xf.shape[1]
         dh = Hd // heads
-        Wqkv = bf(torch.cat([Wq, Wk, Wv], 0))
-        bqkv = torch.cat([bq, bk, bv], 0).contiguous()
+        Wqkv = bf_cat([Wq, Wk, Wv])
+        bqkv = cat_f32([bq, bk, bv])
         qkv = K.linear(xb, Wqkv, bias=bqkv)
         ctxv, lse = K.attn_fwd(qkv[:, :Hd], qkv[:, Hd:2 * Hd], qkv[:, 2 * Hd:], L=L, H=heads, D=dh, nseq=B,
                                scale=1.0 / math.sqrt(dh), seq=(1, L, 0, 1), kmask=kmask)

@@ -8,6 +8,8 @@ never syncs the host: the clip coefficient stays on the device).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import dist_sync
@@ -16,12 +18,22 @@ from . import kernels as K
 
 
 class FlatParams:
+    """Every trainable parameter as a view of one f32 arena, its .grad a view of one f32 gradient
+    arena, and a bf16 SHADOW arena with the same layout: the Adam kernel writes the bf16 copy of
+    each updated weight as it writes the f32 one, so the forward's GEMMs read bf16 weights
+    (``functional.bf``) without a cast launch per weight per step.  A shadow is trusted only while
+    the parameter's torch version counter and storage are the ones recorded here (an in-place torch
+    update, e.g. load_state_dict, falls back to a fresh cast until the next Adam step re-syncs)."""
+
     def __init__(self, params, device):
         self.params = [p for p in params if p.requires_grad]
         n = sum(p.numel() for p in self.params)
         self.numel = n
         self.data = torch.empty(n, device=device, dtype=torch.float32)
         self.grad = torch.zeros(n, device=device, dtype=torch.float32)
+        # (shadows only on the GPU: the CPU arenas serve the gloo rehearsal tests of the sync logic)
+        gpu = torch.device(device).type == 'cuda' and os.environ.get('CTCLIP_BF16_SHADOW', '1') != '0'
+        self.bf16 = torch.empty(n, device=device, dtype=torch.bfloat16) if gpu else None
         self.views = []
         off = 0
         for p in self.params:
@@ -30,8 +42,24 @@ class FlatParams:
             p.data = self.data[off:off + k].view_as(p)
             g = self.grad[off:off + k].view_as(p)
             p.grad = g
+            if gpu:
+                p._ctclip_bf16 = self.bf16[off:off + k].view_as(p)
+                p._ctclip_off = off
+                p._ctclip_flat = self
             self.views.append((off, k, g))
             off += k
+        if gpu and n:
+            K.cast_bf16(self.data, out=self.bf16)
+            self.sync_shadows(0, n)
+
+    def sync_shadows(self, lo, hi):
+        """Mark the shadows of the parameters in [lo, hi) current (after the kernel that wrote them)."""
+        if self.bf16 is None:
+            return
+        for p, (off, k, _) in zip(self.params, self.views):
+            if lo <= off < hi:
+                p._ctclip_ver = p._version
+                p._ctclip_ptr = p.data_ptr()
 
     def rebind_grads(self, only=None):
         """Make sure every .grad is (still) the arena view; fold stray grads back in."""
@@ -142,7 +170,9 @@ class CTClipTrainer:
     def _adam(self, off, n):
         sl = slice(off, off + n)
         K.adam(self.flat.data[sl], self.flat.grad[sl], self.m[sl], self.v[sl], lr=self.lr, b1=self.betas[0],
-               b2=self.betas[1], eps=self.eps, wd=self.wd, step=self.steps, coef=self.norm)
+               b2=self.betas[1], eps=self.eps, wd=self.wd, step=self.steps, coef=self.norm,
+               p_bf16=self.flat.bf16[sl] if self.flat.bf16 is not None else None)
+        self.flat.sync_shadows(off, off + n)
         self.flat.grad[sl].zero_()
 
     def train_step(self, text, video):

@@ -166,6 +166,25 @@ def test_trainer_step_runs(setup):
     assert not torch.equal(before, p.detach())
     assert p.data_ptr() >= tr.flat.data.data_ptr()
     assert tr.norm[0].item() > 0
+    # the Adam kernel's bf16 shadows (trainer.FlatParams) equal the RNE bf16 of every updated
+    # weight, BERT's q / k / v come out of the shadow arena as one slice, and an in-place torch
+    # update of a weight retires its shadow (the GEMMs then cast afresh)
+    from ctclip_mi355x import functional as Fn
+    for q in tr.flat.params:
+        sh = Fn.shadow_bf16(q)
+        assert sh is not None and torch.equal(sh, q.detach().bfloat16())
+    a = model.text_transformer.encoder.layer[0].attention.self
+    qkv = Fn.bf_cat([a.query.weight, a.key.weight, a.value.weight])
+    assert qkv.data_ptr() == Fn.shadow_bf16(a.query.weight).data_ptr()
+    assert torch.equal(qkv, torch.cat([a.query.weight, a.key.weight, a.value.weight]).detach().bfloat16())
+    assert Fn.cat_f32([a.query.bias, a.key.bias, a.value.bias]).data_ptr() == a.query.bias.data_ptr()
+    with torch.no_grad():
+        p.add_(0.0)
+    assert Fn.shadow_bf16(p) is None
+    assert torch.equal(Fn.bf(p), p.detach().bfloat16())
+    tr.train_step(text, hu.cuda())   # the next Adam step re-syncs it
+    torch.cuda.synchronize()
+    assert Fn.shadow_bf16(p) is not None
 
 
 def test_grad_buckets_final_when_launched(setup):

@@ -13,7 +13,7 @@ def short(n):
 
 def main():
     db = sqlite3.connect(sys.argv[1])
-    marker = sys.argv[2] if len(sys.argv) > 2 else 'patch_ln_strip_kernel'
+    marker = sys.argv[2] if len(sys.argv) > 2 else 'patch_ln_strip'
     gap = float(sys.argv[3]) if len(sys.argv) > 3 else 150.0
     rows = sorted(db.execute('select start, "end", stream_id, name from kernels').fetchall())
     starts = [r[0] for r in rows if marker in r[3]]
