@@ -39,6 +39,10 @@ def main():
     from ctclip_mi355x.preprocess import ct_volume_to_tensor
     scan = torch.randint(-1100, 2000, (512, 512, 300), device='cuda', dtype=torch.int16)
     vol = torch.empty(1, 240, 480, 480, device='cuda')
+    ap, ag, am, av = (torch.rand(23_400_000, device='cuda') for _ in range(4))
+    apb, acoef = torch.empty(23_400_000, device='cuda', dtype=torch.bfloat16), torch.ones(2, device='cuda')
+    sl1024, r512 = torch.randn(1024, 1, 512, device='cuda'), torch.empty(1, 512, device='cuda')
+    sl256, r768 = torch.randn(256, 1, 768, device='cuda'), torch.empty(1, 768, device='cuda')
     cases = [
         ('resample 512x512x300 i16 -> 240x480x480 (f64)',
          lambda: ct_volume_to_tensor(scan, 1.0, -1024.0, 0.7, 1.25, out=vol), scan.numel() * 2 + vol.numel() * 4),
@@ -56,6 +60,12 @@ def main():
         ('l2n_bwd', lambda: K.l2norm_scale_bwd(xb[:, :256], xb[:, 256:], 8, 32, qs, dxb[:, :256]), M * 256 * 6),
         ('cast f32->bf16', lambda: K.cast_bf16(xf), M * D * 6),
         ('colsum bf16', lambda: K.colsum(xb), M * D * 2),
+        ('adam 23.4M (+bf16 copy)', lambda: K.adam(ap, ag, am, av, lr=1e-4, b1=0.9, b2=0.99, eps=1e-8, wd=0.0, step=3,
+                                                  coef=acoef, p_bf16=apb), 23_400_000 * 30),
+        ('adam 23.4M', lambda: K.adam(ap, ag, am, av, lr=1e-4, b1=0.9, b2=0.99, eps=1e-8, wd=0.0, step=3,
+                                      coef=acoef), 23_400_000 * 28),
+        ('reduce 1024 slabs x 512', lambda: K.reduce_slabs(sl1024, r512), 1024 * 512 * 4),
+        ('reduce 256 slabs x 768', lambda: K.reduce_slabs(sl256, r768), 256 * 768 * 4),
     ]
     from ctclip_mi355x import layers
     vol = torch.randint(-1200, 1201, (8, 1, 240, 480, 480), device='cuda', dtype=torch.int32).to(torch.int16)
