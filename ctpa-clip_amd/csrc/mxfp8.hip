@@ -1,0 +1,263 @@
+// MX-fp8 (OCP e4m3 elements, e8m0 scale per 32 consecutive k) GEMM for gfx950 — the
+// configs[3] precision of SURVEY §8(d) ("fp8 attention and MLP GEMMs").  The reference runs these
+// linears in fp32 (ct_clip/attention.py:44-52 FeedForward, :88-181 Attention projections); this
+// path is compared to the build's own bf16 path with a tolerance stated per test.
+//
+// Quantiser (OCP MX v1.0 rule): per row and 32-element k block, X = floor(log2(amax)) - 8
+// (8 = emax of e4m3), element = sat_448(RNE(x * 2^-X)), scale byte = X + 127.  k in [K, Kp) is
+// zero-filled so the GEMM's K only needs to be a multiple of 128.
+//
+// GEMM: C[M,N] = alpha * (A . B^T) (+ bias), A [M][Kp] and B [N][Kp] fp8 K-contiguous with their
+// scale planes [rows][Kp/32].  Tile 128x128x128 (k in elements = bytes), 256 threads = 2x2 waves,
+// each wave a 64x64 block of 4x4 v_mfma_scale_f32_16x16x128_f8f6f4 (2x the bf16 MFMA rate per
+// clock on gfx950).  Operand lane map (tools/mx_probe.hip, found on the GPU with integer data):
+// lane l holds row (l & 15), k = 16g..16g+15 in bytes 0-15 and 64+16g..64+16g+15 in bytes 16-31
+// (g = l>>4), and passes the e8m0 scale of (row, k block g) — block g's 32 k sit in lane groups
+// 2(g&1), 2(g&1)+1 at byte half g>>1, so the scale is NOT that of the lane's own bytes.
+// Register-staged double-buffered LDS (one barrier per k-step), rows padded to 144 B, scales
+// staged beside the tiles; f32 tile staged through LDS for 16-B output rows (element stores for
+// a ragged last column group or an unaligned ldc).
+#include "common.h"
+#include "../../include/ctclip_hip.h"
+
+namespace {
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+constexpr int BM = 128, BN = 128, BK = 128, NTH = 256;
+constexpr int KROW = BK + 16;                      // 144-B rows
+constexpr int TILE = 128 * KROW;                   // 18432 B per operand tile
+constexpr int SCB = 128 * 4;                       // 512 B of scales per operand tile
+constexpr int BUF = 2 * TILE + 2 * SCB;            // A, B, sA, sB
+constexpr int SMEM = 2 * BUF;                      // 75776 B
+constexpr int CS_LD = 132;
+static_assert(BM * CS_LD * 4 <= SMEM, "epilogue staging fits");
+
+__device__ __forceinline__ unsigned e4m3_pair(float a, float b) {
+  a = fminf(fmaxf(a, -448.f), 448.f);
+  b = fminf(fmaxf(b, -448.f), 448.f);
+  return (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false) & 0xffffu;
+}
+
+// one thread per (row, 32-k block)
+__global__ __launch_bounds__(256) void quant_kernel(const void* __restrict__ x, int x_f32, int64_t rows, int64_t K,
+                                                    int64_t ldx, uint8_t* __restrict__ q, int64_t ldq,
+                                                    uint8_t* __restrict__ sc, int64_t nblk) {
+  const int64_t id = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (id >= rows * nblk) return;
+  const int64_t r = id / nblk, b = id - r * nblk, k0 = b * 32;
+  float v[32];
+  if (x_f32) {
+    const float* xr = (const float*)x + r * ldx + k0;
+    if (k0 + 32 <= K && ((ldx | k0) & 3) == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const f32x4 t = ((const f32x4*)xr)[i];
+        v[4 * i] = t[0]; v[4 * i + 1] = t[1]; v[4 * i + 2] = t[2]; v[4 * i + 3] = t[3];
+      }
+    } else {
+      for (int i = 0; i < 32; ++i) v[i] = k0 + i < K ? xr[i] : 0.f;
+    }
+  } else {
+    const u16* xr = (const u16*)x + r * ldx + k0;
+    if (k0 + 32 <= K && ((ldx | k0) & 7) == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) unpack8(((const u32x4*)xr)[i], v + 8 * i);
+    } else {
+      for (int i = 0; i < 32; ++i) v[i] = k0 + i < K ? bf2f(xr[i]) : 0.f;
+    }
+  }
+  float amax = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) amax = fmaxf(amax, fabsf(v[i]));
+  int X = 0;
+  if (amax > 0.f) {
+    const int e = (int)((__float_as_uint(amax) >> 23) & 255);
+    X = (e ? e - 127 : -127) - 8;                 // floor(log2 amax) - emax(e4m3); subnormal amax -> -135
+    X = max(-127, min(127, X));
+  }
+  const float inv = __uint_as_float((unsigned)(127 - X) << 23 & 0x7f800000u);  // 2^-X (X in [-126, 127])
+  const float mul = X == -127 ? 0x1p126f * 2.f : inv;
+  unsigned w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    w[i] = e4m3_pair(v[4 * i] * mul, v[4 * i + 1] * mul) | (e4m3_pair(v[4 * i + 2] * mul, v[4 * i + 3] * mul) << 16);
+  u32x4* qo = (u32x4*)(q + r * ldq + k0);
+  qo[0] = make_uint4(w[0], w[1], w[2], w[3]);
+  qo[1] = make_uint4(w[4], w[5], w[6], w[7]);
+  sc[r * nblk + b] = (uint8_t)(X + 127);
+}
+
+struct P {
+  int64_t M, N, Kp;
+  const uint8_t* A; int64_t lda; const uint8_t* sA;
+  const uint8_t* B; int64_t ldb; const uint8_t* sB;
+  void* C; int64_t ldc; int c_f32;
+  const float* bias; float alpha;
+};
+
+__device__ __forceinline__ void xcd_remap(int& tx, int& ty) {
+  const int gx = gridDim.x, nwg = gridDim.x * gridDim.y;
+  const int orig = blockIdx.y * gx + blockIdx.x;
+  int id = orig;
+  if (nwg >= 16) {
+    const int xcd = orig & 7, qq = nwg >> 3, rr = nwg & 7;
+    id = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);
+  }
+  ty = id / gx;
+  tx = id - ty * gx;
+}
+
+struct Stage {
+  u32x4 a[4], b[4];
+  unsigned s;
+};
+
+__device__ __forceinline__ void gload(Stage& st, const P& p, int64_t m0, int64_t n0, int64_t k0) {
+  const int t = threadIdx.x, kc = (t & 7) * 16;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t r = (t >> 3) + 32 * i;
+    st.a[i] = m0 + r < p.M ? *(const u32x4*)(p.A + (m0 + r) * p.lda + k0 + kc) : make_uint4(0, 0, 0, 0);
+    st.b[i] = n0 + r < p.N ? *(const u32x4*)(p.B + (n0 + r) * p.ldb + k0 + kc) : make_uint4(0, 0, 0, 0);
+  }
+  const int64_t nb = p.Kp >> 5;
+  if (t < 128) st.s = m0 + t < p.M ? *(const unsigned*)(p.sA + (m0 + t) * nb + (k0 >> 5)) : 0x7f7f7f7fu;
+  else st.s = n0 + (t - 128) < p.N ? *(const unsigned*)(p.sB + (n0 + t - 128) * nb + (k0 >> 5)) : 0x7f7f7f7fu;
+}
+
+__device__ __forceinline__ void swrite(char* buf, const Stage& st) {
+  const int t = threadIdx.x, kc = (t & 7) * 16;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (t >> 3) + 32 * i;
+    *(u32x4*)(buf + r * KROW + kc) = st.a[i];
+    *(u32x4*)(buf + TILE + r * KROW + kc) = st.b[i];
+  }
+  *(unsigned*)(buf + 2 * TILE + t * 4) = st.s;     // t < 128: sA row t; else sB row t - 128
+}
+
+__device__ __forceinline__ i32x8 frag(const char* tile, int r0, int lane) {
+  const char* src = tile + (r0 + (lane & 15)) * KROW + 16 * (lane >> 4);
+  const u32x4 lo = *(const u32x4*)src, hi = *(const u32x4*)(src + 64);
+  i32x8 v;
+  v[0] = (int)lo.x; v[1] = (int)lo.y; v[2] = (int)lo.z; v[3] = (int)lo.w;
+  v[4] = (int)hi.x; v[5] = (int)hi.y; v[6] = (int)hi.z; v[7] = (int)hi.w;
+  return v;
+}
+
+__global__ __launch_bounds__(NTH, 2) void mx_gemm_kernel(P p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
+  int tx, ty;
+  xcd_remap(tx, ty);
+  const int64_t m0 = (int64_t)ty * BM, n0 = (int64_t)tx * BN;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (int)(p.Kp / BK);
+  Stage st;
+  if (nk > 0) {
+    gload(st, p, m0, n0, 0);
+    swrite(smem, st);
+  }
+  __syncthreads();
+  const int kb = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * BUF;
+    if (kt + 1 < nk) gload(st, p, m0, n0, (int64_t)(kt + 1) * BK);
+    const uint8_t* sa = (const uint8_t*)(cur + 2 * TILE);
+    const uint8_t* sb = sa + SCB;
+    i32x8 af[4], bfr[4];
+    int sca[4], scb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ra = wr * 64 + i * 16, rb = wc * 64 + i * 16;
+      af[i] = frag(cur, ra, lane);
+      bfr[i] = frag(cur + TILE, rb, lane);
+      sca[i] = sa[(ra + (lane & 15)) * 4 + kb];
+      scb[i] = sb[(rb + (lane & 15)) * 4 + kb];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, sca[i], 0,
+                                                                      scb[j]);
+    if (kt + 1 < nk) swrite(smem + ((kt + 1) & 1) * BUF, st);
+    __syncthreads();
+  }
+
+  float* cs = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        cs[(wr * 64 + i * 16 + (lane >> 4) * 4 + r) * CS_LD + wc * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  const int t = threadIdx.x;
+  const bool vec = (p.ldc & 7) == 0;
+  for (int it = 0; it < (BM * BN / 8) / NTH; ++it) {
+    const int c = t + NTH * it;
+    const int row = c >> 4, cc = (c & 15) * 8;
+    const int64_t gm = m0 + row, gn = n0 + cc;
+    if (gm >= p.M || gn >= p.N) continue;
+    float v[8];
+    const f32x4 lo = *(const f32x4*)(cs + row * CS_LD + cc);
+    const f32x4 hi = *(const f32x4*)(cs + row * CS_LD + cc + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = lo[j] * p.alpha; v[4 + j] = hi[j] * p.alpha; }
+    const int nv = (int)min((int64_t)8, p.N - gn);
+    if (p.bias) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += j < nv ? p.bias[gn + j] : 0.f;
+    }
+    if (vec && nv == 8) {
+      if (p.c_f32) {
+        float* Cf = (float*)p.C + gm * p.ldc + gn;
+        *(f32x4*)Cf = f32x4{v[0], v[1], v[2], v[3]};
+        *(f32x4*)(Cf + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      } else {
+        *(u32x4*)((u16*)p.C + gm * p.ldc + gn) = pack8(v);
+      }
+    } else {
+      for (int j = 0; j < nv; ++j) {
+        if (p.c_f32) ((float*)p.C)[gm * p.ldc + gn + j] = v[j];
+        else ((u16*)p.C)[gm * p.ldc + gn + j] = f2bf(v[j]);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int ctclip_quant_mxfp8(const void* x, int32_t x_f32, int64_t rows, int64_t K, int64_t ldx, void* q,
+                                  int64_t ldq, void* scales, int64_t Kp, void* stream) {
+  CT_REQUIRE(rows >= 0 && K >= 0 && Kp >= K && Kp % 128 == 0 && ldq >= Kp && ldq % 16 == 0 && ldx >= K, CT_ESHAPE);
+  CT_REQUIRE(((uintptr_t)q & 15) == 0, CT_EALIGN);
+  if (rows == 0 || Kp == 0) return 0;
+  const int64_t n = rows * (Kp / 32);
+  hipLaunchKernelGGL(quant_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, x_f32,
+                     rows, K, ldx, (uint8_t*)q, ldq, (uint8_t*)scales, Kp / 32);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_gemm_mxfp8(const ctclip_mx_gemm_args* a, void* stream) {
+  CT_REQUIRE(a->M >= 0 && a->N >= 0 && a->Kp >= 0 && a->Kp % 128 == 0, CT_ESHAPE);
+  CT_REQUIRE(a->lda >= a->Kp && a->ldb >= a->Kp && a->lda % 16 == 0 && a->ldb % 16 == 0, CT_ESHAPE);
+  CT_REQUIRE(a->ldc >= a->N, CT_ESHAPE);
+  CT_REQUIRE(((uintptr_t)a->A & 15) == 0 && ((uintptr_t)a->B & 15) == 0 && ((uintptr_t)a->C & 15) == 0, CT_EALIGN);
+  CT_REQUIRE(((uintptr_t)a->sA & 3) == 0 && ((uintptr_t)a->sB & 3) == 0, CT_EALIGN);
+  if (a->M == 0 || a->N == 0) return 0;
+  P p{a->M, a->N, a->Kp, (const uint8_t*)a->A, a->lda, (const uint8_t*)a->sA, (const uint8_t*)a->B, a->ldb,
+      (const uint8_t*)a->sB, a->C, a->ldc, a->c_f32, a->bias, a->alpha};
+  dim3 grid((unsigned)cdiv(a->N, BN), (unsigned)cdiv(a->M, BM));
+  hipLaunchKernelGGL(mx_gemm_kernel, grid, dim3(NTH), SMEM, (hipStream_t)stream, p);
+  CT_CHECK_LAUNCH();
+  return 0;
+}

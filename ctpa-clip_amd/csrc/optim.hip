@@ -34,23 +34,59 @@ __global__ __launch_bounds__(256) void clip_coef_kernel(const float* __restrict_
   }
 }
 
-__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
-                                                   float* __restrict__ m, float* __restrict__ v, int64_t n, float lr,
-                                                   float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt,
-                                                   const float* __restrict__ coef, u16* __restrict__ pb) {
+__device__ __forceinline__ float adam_one(float& pi, float gi, float& mi, float& vi, float c, float b1, float b2,
+                                          float eps, float wd, float step, float bc2_sqrt) {
+  gi *= c;
+  if (wd != 0.f) gi += wd * pi;
+  mi = b1 * mi + (1.f - b1) * gi;
+  vi = b2 * vi + (1.f - b2) * gi * gi;
+  pi -= step * mi / (sqrtf(vi) / bc2_sqrt + eps);
+  return pi;
+}
+
+// 16-B vector body over [head, head + 4*n4) (all five arenas share one element layout, so one
+// alignment head serves every pointer); block 0 also does the <= 3-element head and the tail.
+// The gradient is zeroed in the same pass (the trainer's zero_grad).
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, int64_t n, int head,
+                                                   float lr, float b1, float b2, float eps, float wd, float bc1,
+                                                   float bc2_sqrt, const float* __restrict__ coef,
+                                                   u16* __restrict__ pb, int zero_grad) {
   const float c = coef ? coef[1] : 1.f;
   const float step = lr / bc1;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float gi = g[i] * c;
-    float pi = p[i];
-    if (wd != 0.f) gi += wd * pi;
-    const float mi = b1 * m[i] + (1.f - b1) * gi;
-    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    pi -= step * mi / (sqrtf(vi) / bc2_sqrt + eps);
-    p[i] = pi;
-    if (pb) pb[i] = f2bf(pi);
+  const int64_t n4 = (n - head) >> 2;
+  f32x4* p4 = (f32x4*)(p + head);
+  f32x4* g4 = (f32x4*)(g + head);
+  f32x4* m4 = (f32x4*)(m + head);
+  f32x4* v4 = (f32x4*)(v + head);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 pi = p4[i], gi = g4[i], mi = m4[i], vi = v4[i];
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float pj = pi[j], mj = mi[j], vj = vi[j];
+      o[j] = adam_one(pj, gi[j], mj, vj, c, b1, b2, eps, wd, step, bc2_sqrt);
+      pi[j] = pj; mi[j] = mj; vi[j] = vj;
+    }
+    p4[i] = pi; m4[i] = mi; v4[i] = vi;
+    if (zero_grad) g4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (pb) {
+      uint2 w;
+      w.x = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
+      w.y = (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16);
+      *(uint2*)(pb + head + 4 * i) = w;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 8) {
+    const int t = threadIdx.x;
+    const int64_t i = t < 4 ? (t < head ? t : -1) : head + 4 * n4 + (t - 4);
+    if (i >= 0 && i < n) {
+      float pj = p[i], mj = m[i], vj = v[i];
+      adam_one(pj, g[i], mj, vj, c, b1, b2, eps, wd, step, bc2_sqrt);
+      p[i] = pj; m[i] = mj; v[i] = vj;
+      if (zero_grad) g[i] = 0.f;
+      if (pb) pb[i] = f2bf(pj);
+    }
   }
 }
 
@@ -64,13 +100,21 @@ extern "C" int ctclip_grad_norm(const float* g, int64_t n, float max_norm, float
   return 0;
 }
 
-extern "C" int ctclip_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
-                           float eps, float wd, int32_t step, const float* coef, void* p_bf16, void* stream) {
+extern "C" int ctclip_adam(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
+                           float eps, float wd, int32_t step, const float* coef, void* p_bf16, int32_t zero_grad,
+                           void* stream) {
   const float bc1 = 1.f - powf(b1, (float)step);
   const float bc2 = sqrtf(1.f - powf(b2, (float)step));
-  const int blocks = (int)std::min<int64_t>(8192, (n + 255) / 256);
-  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, lr, b1, b2, eps, wd,
-                     bc1, bc2, coef, (u16*)p_bf16);
+  if (n <= 0) return 0;
+  // p, g, m, v are slices of arenas with one shared element layout: one alignment head for all
+  const int head = (int)std::min<int64_t>(n, ((16 - ((uintptr_t)p & 15)) & 15) / 4);
+  if (((uintptr_t)g & 15) != ((uintptr_t)p & 15) || ((uintptr_t)m & 15) != ((uintptr_t)p & 15) ||
+      ((uintptr_t)v & 15) != ((uintptr_t)p & 15) || ((uintptr_t)p & 3))
+    return CT_EALIGN;
+  const int64_t n4 = (n - head) / 4;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (n4 + 255) / 256));
+  hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, head, lr, b1, b2,
+                     eps, wd, bc1, bc2, coef, (u16*)p_bf16, zero_grad);
   CT_CHECK_LAUNCH();
   return 0;
 }

@@ -40,6 +40,16 @@ class GemmArgs(ctypes.Structure):
     ]
 
 
+class MxGemmArgs(ctypes.Structure):
+    _fields_ = [
+        ('M', c_i64), ('N', c_i64), ('Kp', c_i64),
+        ('A', c_vp), ('lda', c_i64), ('sA', c_vp),
+        ('B', c_vp), ('ldb', c_i64), ('sB', c_vp),
+        ('C', c_vp), ('ldc', c_i64), ('c_f32', c_i32),
+        ('bias', c_vp), ('alpha', c_f32),
+    ]
+
+
 class AttnArgs(ctypes.Structure):
     _fields_ = [
         ('q', c_vp), ('ldq', c_i64), ('k', c_vp), ('ldk', c_i64), ('v', c_vp), ('ldv', c_i64),
@@ -68,6 +78,8 @@ _SIGS = {
     'ctclip_version': [],
     'ctclip_device_arch': [ctypes.c_char_p, c_i32],
     'ctclip_gemm': [ctypes.POINTER(GemmArgs), c_vp],
+    'ctclip_quant_mxfp8': [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp],
+    'ctclip_gemm_mxfp8': [ctypes.POINTER(MxGemmArgs), c_vp],
     'ctclip_gemm_set_variant': [c_i32],
     'ctclip_gemm_set_stagger': [c_i32],
     'ctclip_gemm_set_persist': [c_i32],
@@ -113,7 +125,7 @@ _SIGS = {
     'ctclip_embed_fwd': [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
     'ctclip_embed_bwd': [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
     'ctclip_grad_norm': [c_vp, c_i64, c_f32, c_vp, c_i32, c_vp, c_vp],
-    'ctclip_adam': [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_i32, c_vp, c_vp, c_vp],
+    'ctclip_adam': [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_i32, c_vp, c_vp, c_i32, c_vp],
 }
 
 

@@ -562,9 +562,9 @@ def weights_epoch():
     return _WEIGHTS_EPOCH[0]
 
 
-def adam(p, g, m, v, *, lr, b1, b2, eps, wd, step, coef=None, p_bf16=None):
+def adam(p, g, m, v, *, lr, b1, b2, eps, wd, step, coef=None, p_bf16=None, zero_grad=False):
     call('ctclip_adam', ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, b1, b2, eps, wd, step, ptr(coef), ptr(p_bf16),
-         stream_ptr())
+         int(zero_grad), stream_ptr())
     _WEIGHTS_EPOCH[0] += 1
 
 
@@ -584,3 +584,31 @@ def colsum_rows_mean(x, B):
         xb = x[b * n:(b + 1) * n]
         sgemm(1, D, n, ones, 0, 1, xb, xb.stride(0), 1, out[b:b + 1], D, 1, alpha=1.0 / n)
     return out
+
+
+# ---------------------------------------------------------------- MX-fp8 (configs[3])
+def quant_mxfp8(x, Kp=None):
+    """x [rows, K] bf16 / f32 -> (q [rows, Kp] uint8 e4m3, scales [rows, Kp/32] uint8 e8m0), the
+    OCP MX rule of csrc/mxfp8.hip; Kp = K rounded up to 128 (zero-filled)."""
+    assert x.dim() == 2 and x.stride(1) == 1 and x.dtype in (torch.bfloat16, torch.float32)
+    rows, Kx = x.shape
+    Kp = Kp or (Kx + 127) // 128 * 128
+    q = torch.empty(rows, Kp, device=x.device, dtype=torch.uint8)
+    s = torch.empty(rows, Kp // 32, device=x.device, dtype=torch.uint8)
+    call('ctclip_quant_mxfp8', ptr(x), int(x.dtype == torch.float32), rows, Kx, x.stride(0), ptr(q), q.stride(0),
+         ptr(s), Kp, stream_ptr())
+    return q, s
+
+
+def gemm_mxfp8(qa, sa, qb, sb, *, bias=None, alpha=1.0, out_f32=False, out=None):
+    """C[M, N] = alpha * dequant(qa) . dequant(qb)^T (+ bias) from quant_mxfp8 operands."""
+    M, Kp = qa.shape
+    N = qb.shape[0]
+    assert qb.shape[1] == Kp and sa.shape == (M, Kp // 32) and sb.shape == (N, Kp // 32)
+    C = out if out is not None else torch.empty(M, N, device=qa.device,
+                                                dtype=torch.float32 if out_f32 else torch.bfloat16)
+    a = _lib.MxGemmArgs(M=M, N=N, Kp=Kp, A=ptr(qa), lda=qa.stride(0), sA=ptr(sa), B=ptr(qb), ldb=qb.stride(0),
+                        sB=ptr(sb), C=ptr(C), ldc=C.stride(0), c_f32=int(C.dtype == torch.float32),
+                        bias=ptr(bias), alpha=float(alpha))
+    call('ctclip_gemm_mxfp8', _lib.ctypes.byref(a), stream_ptr())
+    return C

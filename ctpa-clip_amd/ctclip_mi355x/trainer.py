@@ -171,9 +171,8 @@ class CTClipTrainer:
         sl = slice(off, off + n)
         K.adam(self.flat.data[sl], self.flat.grad[sl], self.m[sl], self.v[sl], lr=self.lr, b1=self.betas[0],
                b2=self.betas[1], eps=self.eps, wd=self.wd, step=self.steps, coef=self.norm,
-               p_bf16=self.flat.bf16[sl] if self.flat.bf16 is not None else None)
+               p_bf16=self.flat.bf16[sl] if self.flat.bf16 is not None else None, zero_grad=True)
         self.flat.sync_shadows(off, off + n)
-        self.flat.grad[sl].zero_()
 
     def train_step(self, text, video):
         """One contrastive step; returns the loss tensor (no host sync)."""

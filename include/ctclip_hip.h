@@ -75,6 +75,26 @@ int ctclip_reduce_slabs_ep(const float* slabs, int64_t nslab, int64_t rows, int6
                            const ctclip_gemm_args* ep, void* stream);
 
 
+/* ---------------------------------------------------------------- MX-fp8 GEMM (configs[3])
+ * SURVEY §8(d) configs[3]: "fp8 attention and MLP GEMMs".  Replaces the fp32 nn.Linear calls of
+ * ct_clip/attention.py:44-52 (FeedForward) and :88-181 (to_q / to_kv / to_out) for that config;
+ * compared to the build's own bf16 path.  OCP MX: e4m3 elements, one e8m0 scale
+ * per 32 consecutive k.
+ * quant: x [rows][K] (bf16, or f32 if x_f32) -> q [rows][Kp] e4m3 (ldq bytes, 16-B aligned),
+ *   scales [rows][Kp/32] (X + 127 with X = floor(log2 amax) - 8); k in [K, Kp) zero; Kp % 128 == 0.
+ * gemm: C[M][N] = alpha * (A . B^T) (+ bias[N]) in bf16 (or f32 if c_f32); A [M][Kp], B [N][Kp]
+ *   e4m3 with their scale planes.  Errors: CT_ESHAPE / CT_EALIGN. */
+typedef struct {
+  int64_t M, N, Kp;
+  const void* A; int64_t lda; const void* sA;   /* lda, ldb in bytes */
+  const void* B; int64_t ldb; const void* sB;
+  void* C; int64_t ldc; int32_t c_f32;
+  const float* bias; float alpha;
+} ctclip_mx_gemm_args;
+int ctclip_quant_mxfp8(const void* x, int32_t x_f32, int64_t rows, int64_t K, int64_t ldx, void* q, int64_t ldq,
+                       void* scales, int64_t Kp, void* stream);
+int ctclip_gemm_mxfp8(const ctclip_mx_gemm_args* a, void* stream);
+
 /* ---------------------------------------------------------------- LayerNorm family
  * ct_clip/attention.py:28-35 (bias-less LayerNorm: gamma, beta = 0 buffer, eps 1e-5),
  * nn.LayerNorm in FeedForward / to_patch_emb (attention.py:47, ctvit.py:171,173), BERT LayerNorms.
@@ -230,10 +250,12 @@ int ctclip_embed_bwd(const int64_t* ids, int64_t B, int32_t L, int32_t Hd, const
 
 /* ---------------------------------------------------------------- optimizer (CTCLIPTrainer.py:347-353)
  * grad norm -> out[0] = norm, out[1] = clip coef (torch clip_grad_norm_ semantics);
- * Adam over a flat arena (optimizer.py:24), grads scaled by coef[1], bf16 copy refreshed. */
+ * Adam over a flat arena (optimizer.py:24), grads scaled by coef[1], bf16 copy refreshed;
+ * zero_grad != 0 also zeroes g in the same pass (the trainer's zero_grad, CTCLIPTrainer.py:353).
+ * p, g, m, v must share one alignment modulo 16 B (slices of arenas with one layout): CT_EALIGN. */
 int ctclip_grad_norm(const float* g, int64_t n, float max_norm, float* part, int32_t nblk, float* out, void* stream);
-int ctclip_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
-                float wd, int32_t step, const float* coef, void* p_bf16, void* stream);
+int ctclip_adam(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
+                float wd, int32_t step, const float* coef, void* p_bf16, int32_t zero_grad, void* stream);
 
 /* ---------------------------------------------------------------- volume preprocessing
  * Replaces the host-side per-sample loader arithmetic:

@@ -338,3 +338,36 @@ def test_adam_and_norm(K):
     K.adam(p, g, m, v, lr=1e-3, b1=0.9, b2=0.99, eps=1e-8, wd=0.0, step=1, coef=out, p_bf16=pb)
     assert rel(p, pr.detach()) < 1e-6
     assert rel(pb, p) < 4e-3
+
+
+@pytest.mark.gpu
+def test_adam_unaligned_slices_and_zero_grad(K):
+    """Arena slices at every 16-B phase and ragged lengths (the vector body's scalar head and
+    tail), the bf16 shadow, the fused zero_grad, and nothing outside the slice touched."""
+    torch.manual_seed(10)
+    N = 4099
+    for off in range(4):
+        for n in (1, 3, 5, 1027, N - 8):
+            p = torch.randn(N, device=dev)
+            g = torch.randn(N, device=dev)
+            m = torch.randn(N, device=dev) * 0.1
+            v = torch.rand(N, device=dev) * 0.1
+            pb = torch.zeros(N, device=dev, dtype=torch.bfloat16)
+            coef = torch.tensor([1.0, 0.37], device=dev)
+            p0, g0, m0, v0 = p.clone(), g.clone(), m.clone(), v.clone()
+            sl = slice(off, off + n)
+            K.adam(p[sl], g[sl], m[sl], v[sl], lr=1e-3, b1=0.9, b2=0.99, eps=1e-8, wd=0.0, step=3, coef=coef,
+                   p_bf16=pb[sl], zero_grad=True)
+            gi = g0[sl] * 0.37
+            mi = 0.9 * m0[sl] + 0.1 * gi
+            vi = 0.99 * v0[sl] + 0.01 * gi * gi
+            bc1, bc2 = 1 - 0.9 ** 3, (1 - 0.99 ** 3) ** 0.5
+            pi = p0[sl] - (1e-3 / bc1) * mi / (vi.sqrt() / bc2 + 1e-8)
+            assert rel(m[sl], mi) < 1e-6 and rel(v[sl], vi) < 1e-6 and rel(p[sl], pi) < 1e-6
+            assert torch.equal(pb[sl], p[sl].to(torch.bfloat16))
+            assert torch.count_nonzero(g[sl]).item() == 0
+            out = torch.ones(N, dtype=torch.bool, device=dev)
+            out[sl] = False
+            assert torch.equal(p[out], p0[out]) and torch.equal(g[out], g0[out])
+            assert torch.equal(m[out], m0[out]) and torch.equal(v[out], v0[out])
+            assert torch.count_nonzero(pb[out].float()).item() == 0
