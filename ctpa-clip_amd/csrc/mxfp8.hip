@@ -24,14 +24,22 @@ namespace {
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
-constexpr int BM = 128, BN = 128, BK = 128, NTH = 256;
+// BM = 128 (wave tile 64x64, 2 workgroups / CU; the default) or 256 (wave tile 128x64: 25 % fewer
+// LDS bytes per flop, 1 workgroup / CU).  Measured (profiles/r01_mx_bench_v2.log): 256 is 12-27 %
+// slower at every model shape — with 4-11 k-steps per tile the exposed first-load latency and
+// epilogue, which a second co-resident workgroup hides, cost more than the LDS reads saved.
+constexpr int BN = 128, BK = 128, NTH = 256;
 constexpr int KROW = BK + 16;                      // 144-B rows
-constexpr int TILE = 128 * KROW;                   // 18432 B per operand tile
-constexpr int SCB = 128 * 4;                       // 512 B of scales per operand tile
-constexpr int BUF = 2 * TILE + 2 * SCB;            // A, B, sA, sB
-constexpr int SMEM = 2 * BUF;                      // 75776 B
 constexpr int CS_LD = 132;
-static_assert(BM * CS_LD * 4 <= SMEM, "epilogue staging fits");
+template <int BM> struct Cfg {
+  static constexpr int TA = BM * KROW, TB = BN * KROW;       // operand tiles
+  static constexpr int SA = BM * 4, SB = BN * 4;              // scale bytes per k-step
+  static constexpr int BUF = TA + TB + SA + SB;
+  static constexpr int SMEM = 2 * BUF;
+  static constexpr int MI = BM / 32;                         // 16-row A fragments per wave
+  static constexpr int NA = BM / 32;                         // 16-B A loads per thread per k-step
+  static_assert(128 * CS_LD * 4 <= SMEM, "epilogue staging fits");
+};
 
 __device__ __forceinline__ unsigned e4m3_pair(float a, float b) {
   a = fminf(fmaxf(a, -448.f), 448.f);
@@ -108,33 +116,49 @@ __device__ __forceinline__ void xcd_remap(int& tx, int& ty) {
   tx = id - ty * gx;
 }
 
+template <int BM>
 struct Stage {
-  u32x4 a[4], b[4];
-  unsigned s;
+  u32x4 a[Cfg<BM>::NA], b[4];
+  unsigned s[BM / 128 + 1];
 };
 
-__device__ __forceinline__ void gload(Stage& st, const P& p, int64_t m0, int64_t n0, int64_t k0) {
+template <int BM>
+__device__ __forceinline__ void gload(Stage<BM>& st, const P& p, int64_t m0, int64_t n0, int64_t k0) {
   const int t = threadIdx.x, kc = (t & 7) * 16;
+#pragma unroll
+  for (int i = 0; i < Cfg<BM>::NA; ++i) {
+    const int64_t r = (t >> 3) + 32 * i;
+    st.a[i] = m0 + r < p.M ? *(const u32x4*)(p.A + (m0 + r) * p.lda + k0 + kc) : make_uint4(0, 0, 0, 0);
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int64_t r = (t >> 3) + 32 * i;
-    st.a[i] = m0 + r < p.M ? *(const u32x4*)(p.A + (m0 + r) * p.lda + k0 + kc) : make_uint4(0, 0, 0, 0);
     st.b[i] = n0 + r < p.N ? *(const u32x4*)(p.B + (n0 + r) * p.ldb + k0 + kc) : make_uint4(0, 0, 0, 0);
   }
+  // scale rows: [0, BM) of A then [0, BN) of B, one u32 (4 k blocks) each
   const int64_t nb = p.Kp >> 5;
-  if (t < 128) st.s = m0 + t < p.M ? *(const unsigned*)(p.sA + (m0 + t) * nb + (k0 >> 5)) : 0x7f7f7f7fu;
-  else st.s = n0 + (t - 128) < p.N ? *(const unsigned*)(p.sB + (n0 + t - 128) * nb + (k0 >> 5)) : 0x7f7f7f7fu;
+#pragma unroll
+  for (int j = 0; j < BM / 128 + 1; ++j) {
+    const int s = t + 256 * j;
+    if (s < BM) st.s[j] = m0 + s < p.M ? *(const unsigned*)(p.sA + (m0 + s) * nb + (k0 >> 5)) : 0x7f7f7f7fu;
+    else if (s < BM + BN)
+      st.s[j] = n0 + (s - BM) < p.N ? *(const unsigned*)(p.sB + (n0 + s - BM) * nb + (k0 >> 5)) : 0x7f7f7f7fu;
+  }
 }
 
-__device__ __forceinline__ void swrite(char* buf, const Stage& st) {
+template <int BM>
+__device__ __forceinline__ void swrite(char* buf, const Stage<BM>& st) {
+  using C = Cfg<BM>;
   const int t = threadIdx.x, kc = (t & 7) * 16;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = (t >> 3) + 32 * i;
-    *(u32x4*)(buf + r * KROW + kc) = st.a[i];
-    *(u32x4*)(buf + TILE + r * KROW + kc) = st.b[i];
+  for (int i = 0; i < C::NA; ++i) *(u32x4*)(buf + ((t >> 3) + 32 * i) * KROW + kc) = st.a[i];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) *(u32x4*)(buf + C::TA + ((t >> 3) + 32 * i) * KROW + kc) = st.b[i];
+#pragma unroll
+  for (int j = 0; j < BM / 128 + 1; ++j) {
+    const int s = t + 256 * j;
+    if (s < BM + BN) *(unsigned*)(buf + C::TA + C::TB + s * 4) = st.s[j];   // sA rows then sB rows
   }
-  *(unsigned*)(buf + 2 * TILE + t * 4) = st.s;     // t < 128: sA row t; else sB row t - 128
 }
 
 __device__ __forceinline__ i32x8 frag(const char* tile, int r0, int lane) {
@@ -146,91 +170,119 @@ __device__ __forceinline__ i32x8 frag(const char* tile, int r0, int lane) {
   return v;
 }
 
-__global__ __launch_bounds__(NTH, 2) void mx_gemm_kernel(P p) {
+template <int BM>
+__global__ __launch_bounds__(NTH, BM == 128 ? 2 : 1) void mx_gemm_kernel(P p) {
+  using C = Cfg<BM>;
+  constexpr int MI = C::MI, WR = BM / 2;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
   int tx, ty;
   xcd_remap(tx, ty);
   const int64_t m0 = (int64_t)ty * BM, n0 = (int64_t)tx * BN;
-  f32x4 acc[4][4];
+  f32x4 acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nk = (int)(p.Kp / BK);
-  Stage st;
+  Stage<BM> st;
   if (nk > 0) {
-    gload(st, p, m0, n0, 0);
-    swrite(smem, st);
+    gload<BM>(st, p, m0, n0, 0);
+    swrite<BM>(smem, st);
   }
   __syncthreads();
   const int kb = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * BUF;
-    if (kt + 1 < nk) gload(st, p, m0, n0, (int64_t)(kt + 1) * BK);
-    const uint8_t* sa = (const uint8_t*)(cur + 2 * TILE);
-    const uint8_t* sb = sa + SCB;
-    i32x8 af[4], bfr[4];
-    int sca[4], scb[4];
+    char* cur = smem + (kt & 1) * C::BUF;
+    if (kt + 1 < nk) gload<BM>(st, p, m0, n0, (int64_t)(kt + 1) * BK);
+    const uint8_t* sa = (const uint8_t*)(cur + C::TA + C::TB);
+    const uint8_t* sb = sa + C::SA;
+    i32x8 bfr[4];
+    int scb[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ra = wr * 64 + i * 16, rb = wc * 64 + i * 16;
-      af[i] = frag(cur, ra, lane);
-      bfr[i] = frag(cur + TILE, rb, lane);
-      sca[i] = sa[(ra + (lane & 15)) * 4 + kb];
-      scb[i] = sb[(rb + (lane & 15)) * 4 + kb];
+    for (int j = 0; j < 4; ++j) {
+      const int rb = wc * 64 + j * 16;
+      bfr[j] = frag(cur + C::TA, rb, lane);
+      scb[j] = sb[(rb + (lane & 15)) * 4 + kb];
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i) {
+      const int ra = wr * WR + i * 16;
+      const i32x8 af = frag(cur, ra, lane);
+      const int sca = sa[(ra + (lane & 15)) * 4 + kb];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfr[j], acc[i][j], 0, 0, 0, sca[i], 0,
-                                                                      scb[j]);
-    if (kt + 1 < nk) swrite(smem + ((kt + 1) & 1) * BUF, st);
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfr[j], acc[i][j], 0, 0, 0, sca, 0, scb[j]);
+    }
+    if (kt + 1 < nk) swrite<BM>(smem + ((kt + 1) & 1) * C::BUF, st);
     __syncthreads();
   }
 
+  // epilogue in 128-row halves: stage f32 through LDS, then 16-B output rows
   float* cs = (float*)smem;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        cs[(wr * 64 + i * 16 + (lane >> 4) * 4 + r) * CS_LD + wc * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
-  __syncthreads();
   const int t = threadIdx.x;
   const bool vec = (p.ldc & 7) == 0;
-  for (int it = 0; it < (BM * BN / 8) / NTH; ++it) {
-    const int c = t + NTH * it;
-    const int row = c >> 4, cc = (c & 15) * 8;
-    const int64_t gm = m0 + row, gn = n0 + cc;
-    if (gm >= p.M || gn >= p.N) continue;
-    float v[8];
-    const f32x4 lo = *(const f32x4*)(cs + row * CS_LD + cc);
-    const f32x4 hi = *(const f32x4*)(cs + row * CS_LD + cc + 4);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { v[j] = lo[j] * p.alpha; v[4 + j] = hi[j] * p.alpha; }
-    const int nv = (int)min((int64_t)8, p.N - gn);
-    if (p.bias) {
+  for (int h = 0; h < BM / 128; ++h) {
+    if (BM == 128 || wr == h) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += j < nv ? p.bias[gn + j] : 0.f;
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            cs[((BM == 128 ? wr * 64 : 0) + i * 16 + (lane >> 4) * 4 + r) * CS_LD + wc * 64 + j * 16 + (lane & 15)] =
+                acc[i][j][r];
     }
-    if (vec && nv == 8) {
-      if (p.c_f32) {
-        float* Cf = (float*)p.C + gm * p.ldc + gn;
-        *(f32x4*)Cf = f32x4{v[0], v[1], v[2], v[3]};
-        *(f32x4*)(Cf + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    __syncthreads();
+    for (int it = 0; it < (128 * BN / 8) / NTH; ++it) {
+      const int c = t + NTH * it;
+      const int row = c >> 4, cc = (c & 15) * 8;
+      const int64_t gm = m0 + h * 128 + row, gn = n0 + cc;
+      if (gm >= p.M || gn >= p.N) continue;
+      float v[8];
+      const f32x4 lo = *(const f32x4*)(cs + row * CS_LD + cc);
+      const f32x4 hi = *(const f32x4*)(cs + row * CS_LD + cc + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { v[j] = lo[j] * p.alpha; v[4 + j] = hi[j] * p.alpha; }
+      const int nv = (int)min((int64_t)8, p.N - gn);
+      if (p.bias) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += j < nv ? p.bias[gn + j] : 0.f;
+      }
+      if (vec && nv == 8) {
+        if (p.c_f32) {
+          float* Cf = (float*)p.C + gm * p.ldc + gn;
+          *(f32x4*)Cf = f32x4{v[0], v[1], v[2], v[3]};
+          *(f32x4*)(Cf + 4) = f32x4{v[4], v[5], v[6], v[7]};
+        } else {
+          *(u32x4*)((u16*)p.C + gm * p.ldc + gn) = pack8(v);
+        }
       } else {
-        *(u32x4*)((u16*)p.C + gm * p.ldc + gn) = pack8(v);
-      }
-    } else {
-      for (int j = 0; j < nv; ++j) {
-        if (p.c_f32) ((float*)p.C)[gm * p.ldc + gn + j] = v[j];
-        else ((u16*)p.C)[gm * p.ldc + gn + j] = f2bf(v[j]);
+        for (int j = 0; j < nv; ++j) {
+          if (p.c_f32) ((float*)p.C)[gm * p.ldc + gn + j] = v[j];
+          else ((u16*)p.C)[gm * p.ldc + gn + j] = f2bf(v[j]);
+        }
       }
     }
+    __syncthreads();
   }
+}
+
+int g_mx_tile = 0;   // 0 = auto, 128 / 256 = forced (diagnostic)
+
+template <int BM>
+int mx_launch(const P& p, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)mx_gemm_kernel<BM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              Cfg<BM>::SMEM);
+    attr = true;
+  }
+  dim3 grid((unsigned)cdiv(p.N, BN), (unsigned)cdiv(p.M, BM));
+  hipLaunchKernelGGL(mx_gemm_kernel<BM>, grid, dim3(NTH), Cfg<BM>::SMEM, s, p);
+  CT_CHECK_LAUNCH();
+  return 0;
 }
 
 }  // namespace
@@ -256,8 +308,12 @@ extern "C" int ctclip_gemm_mxfp8(const ctclip_mx_gemm_args* a, void* stream) {
   if (a->M == 0 || a->N == 0) return 0;
   P p{a->M, a->N, a->Kp, (const uint8_t*)a->A, a->lda, (const uint8_t*)a->sA, (const uint8_t*)a->B, a->ldb,
       (const uint8_t*)a->sB, a->C, a->ldc, a->c_f32, a->bias, a->alpha};
-  dim3 grid((unsigned)cdiv(a->N, BN), (unsigned)cdiv(a->M, BM));
-  hipLaunchKernelGGL(mx_gemm_kernel, grid, dim3(NTH), SMEM, (hipStream_t)stream, p);
-  CT_CHECK_LAUNCH();
-  return 0;
+  const int bm = g_mx_tile ? g_mx_tile : 128;
+  return bm == 256 ? mx_launch<256>(p, (hipStream_t)stream) : mx_launch<128>(p, (hipStream_t)stream);
+}
+
+extern "C" int ctclip_gemm_mxfp8_set_tile(int bm) {
+  const int prev = g_mx_tile;
+  g_mx_tile = (bm == 128 || bm == 256) ? bm : 0;
+  return prev;
 }

@@ -80,6 +80,7 @@ _SIGS = {
     'ctclip_gemm': [ctypes.POINTER(GemmArgs), c_vp],
     'ctclip_quant_mxfp8': [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp],
     'ctclip_gemm_mxfp8': [ctypes.POINTER(MxGemmArgs), c_vp],
+    'ctclip_gemm_mxfp8_set_tile': [c_i32],
     'ctclip_gemm_set_variant': [c_i32],
     'ctclip_gemm_set_stagger': [c_i32],
     'ctclip_gemm_set_persist': [c_i32],

@@ -612,3 +612,8 @@ def gemm_mxfp8(qa, sa, qb, sb, *, bias=None, alpha=1.0, out_f32=False, out=None)
                         bias=ptr(bias), alpha=float(alpha))
     call('ctclip_gemm_mxfp8', _lib.ctypes.byref(a), stream_ptr())
     return C
+
+
+def gemm_mxfp8_set_tile(bm):
+    """diagnostic: force the 128- / 256-row MX tile kernel (0 = auto); returns the previous."""
+    return _lib.lib().ctclip_gemm_mxfp8_set_tile(int(bm))

@@ -94,6 +94,9 @@ typedef struct {
 int ctclip_quant_mxfp8(const void* x, int32_t x_f32, int64_t rows, int64_t K, int64_t ldx, void* q, int64_t ldq,
                        void* scales, int64_t Kp, void* stream);
 int ctclip_gemm_mxfp8(const ctclip_mx_gemm_args* a, void* stream);
+/* diagnostic: force the 128- or 256-row tile kernel (0 = auto); returns the previous setting.
+ * Both compute identical results. */
+int ctclip_gemm_mxfp8_set_tile(int bm);
 
 /* ---------------------------------------------------------------- LayerNorm family
  * ct_clip/attention.py:28-35 (bias-less LayerNorm: gamma, beta = 0 buffer, eps 1e-5),

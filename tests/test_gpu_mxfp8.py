@@ -59,9 +59,31 @@ def test_quant_bit_exact(K, rows, Kx, dtype):
     assert torch.equal(q, qr), (q != qr).sum().item()
 
 
+@pytest.mark.parametrize('tile', [128, 256])
 @pytest.mark.parametrize('M,N,Kx', [(128, 128, 128), (300, 264, 384), (1000, 2730, 512), (257, 512, 1365),
                                     (96, 200, 256)])
-def test_gemm_vs_dequantised_matmul(K, M, N, Kx):
+def test_gemm_vs_dequantised_matmul(K, M, N, Kx, tile):
+    prev = K.gemm_mxfp8_set_tile(tile)
+    try:
+        _check_gemm(K, M, N, Kx)
+    finally:
+        K.gemm_mxfp8_set_tile(prev)
+
+
+def test_gemm_tiles_identical(K):
+    torch.manual_seed(4)
+    a, b = torch.randn(700, 640, device=dev).bfloat16(), torch.randn(392, 640, device=dev).bfloat16()
+    qa, sa = K.quant_mxfp8(a)
+    qb, sb = K.quant_mxfp8(b)
+    outs = []
+    for tile in (128, 256):
+        prev = K.gemm_mxfp8_set_tile(tile)
+        outs.append(K.gemm_mxfp8(qa, sa, qb, sb, out_f32=True))
+        K.gemm_mxfp8_set_tile(prev)
+    assert torch.equal(outs[0], outs[1])
+
+
+def _check_gemm(K, M, N, Kx):
     torch.manual_seed(2)
     a = torch.randn(M, Kx, device=dev).bfloat16()
     b = (torch.randn(N, Kx, device=dev) * 0.05).bfloat16()

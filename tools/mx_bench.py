@@ -35,7 +35,12 @@ def main():
         w.copy_(torch.randn(N, Kx, device='cuda') * Kx ** -0.5)
         qx, sx = K.quant_mxfp8(x)
         qw, sw = K.quant_mxfp8(w)
-        c8 = torch.empty(m, N, device='cuda', dtype=torch.bfloat16)
+        c8 = torch.empty(m, (N + 7) // 8 * 8, device='cuda', dtype=torch.bfloat16)[:, :N]   # aligned ld
+        t8s = []
+        for tile in (128, 256):
+            K.gemm_mxfp8_set_tile(tile)
+            t8s.append(timeit(lambda: K.gemm_mxfp8(qx, sx, qw, sw, out=c8)))
+        K.gemm_mxfp8_set_tile(0)
         t8 = timeit(lambda: K.gemm_mxfp8(qx, sx, qw, sw, out=c8))
         tq = timeit(lambda: K.quant_mxfp8(x))
         # the bf16 kernel needs K, N % 8: it runs on the zero-padded operands (as the model's layers do)
@@ -46,7 +51,8 @@ def main():
         cb = torch.empty(m, n8, device='cuda', dtype=torch.bfloat16)
         tb = timeit(lambda: K.linear(xb, wb, out=cb))
         fl = 2.0 * m * N * Kx
-        print(f'{name:16s} M={m:6d}  mxfp8 {t8 * 1e3:8.1f} us {fl / t8 / 1e9:7.1f} TF/s | quant(x) {tq * 1e3:7.1f} us '
+        print(f'{name:16s} M={m:6d}  mxfp8 {t8 * 1e3:8.1f} us {fl / t8 / 1e9:7.1f} TF/s '
+              f'(tile 128: {fl / t8s[0] / 1e9:6.1f}, 256: {fl / t8s[1] / 1e9:6.1f}) | quant(x) {tq * 1e3:7.1f} us '
               f'| bf16 build {tb * 1e3:8.1f} us {fl / tb / 1e9:7.1f} TF/s', flush=True)
 
 
