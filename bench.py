@@ -184,8 +184,8 @@ def main():
         'dtype': 'bf16',
         'data': 'synthetic: int16 HU volumes 1x240x480x480 (randint -1200..1200) + 128-token reports; '
                 'random-init CT-CLIP base weights',
-        'config': {'workload': 'CT-CLIP base contrastive train step: BERT-base(128 tok) + CTViT(480^2x240, '
-                               'patch 20x20x10, 4+4 layers, VQ 8192) + InfoNCE + bwd + RCCL grad all-reduce + '
+        'config': {'workload': 'CT-CLIP base contrastive train step: BERT-base(128 tok, train-mode dropout '
+                               '0.1) + CTViT(480^2x240, patch 20x20x10, 4+4 layers, VQ 8192) + InfoNCE + bwd + RCCL grad all-reduce + '
                                'clip 0.5 + Adam',
                    'per_gpu_batch': args.batch, 'global_batch': world * args.batch, 'text_len': args.text_len,
                    'parallelism': f'dp{world}', 'infonce_negatives': 'global batch (RCCL all-gather)'},

@@ -54,6 +54,11 @@ struct AP {
   int n_inner;
   int64_t s_outer, s_inner, s_pos;
   int pp;                         // (seq, head) pairs per workgroup
+  // attention-probability dropout (BertSelfAttention.dropout, non-bias kernels only):
+  // keep(s, h, q, k) = hash(seed, index) >= thresh, kept probabilities scaled by 1 / (1 - p)
+  float drop_p, drop_scale;
+  unsigned thresh;
+  uint64_t seed;
 };
 
 constexpr int NW = 8;             // waves per workgroup
@@ -66,6 +71,18 @@ constexpr int SUB = 3;
 
 __device__ __forceinline__ int64_t seq_row(const AP& p, int s, int i) {
   return (int64_t)(s / p.n_inner) * p.s_outer + (int64_t)(s % p.n_inner) * p.s_inner + (int64_t)i * p.s_pos;
+}
+
+// dropout multiplier of P[q][k] for (seq s, head h): 0 or 1 / (1 - p), a pure function of
+// (seed, s, h, q, k) so the backward kernels regenerate the forward's mask (splitmix64 finaliser)
+__device__ __forceinline__ float drop_keep(const AP& p, int s, int h, int q, int k) {
+  uint64_t x = p.seed ^ ((((uint64_t)(s * p.H + h) * p.L + q) * p.L + k) * 0x9E3779B97F4A7C15ull);
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (unsigned)x >= p.thresh ? p.drop_scale : 0.f;
 }
 
 // bias table constants: bin(q, k) = kb[q] + boff - kb[k]
@@ -276,6 +293,14 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
         }
       lsum = lsum * alpha + psum;
       m = mnew;
+      if constexpr (!BIAS) {
+        if (p.drop_p > 0.f) {
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sa[bi][r] *= drop_keep(p, s, h, q, kc + 16 * bi + 4 * g + r);
+        }
+      }
       const bf16x8 pb = pack_perm(sa[0], sa[1]);
 #pragma unroll
       for (int d = 0; d < DB; ++d) {
@@ -385,7 +410,11 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_kernel(AP p) {
         for (int r = 0; r < 4; ++r) {
           float x = sa[bi][r] * sc2 + ma[r];
           if (BIAS) x += ub[cq - kbv[r]];
-          const float ds = fexp2(x - lse2) * (da[bi][r] - dl);   // 0 for masked keys / padded queries
+          float dp = da[bi][r];
+          if constexpr (!BIAS) {
+            if (p.drop_p > 0.f) dp *= drop_keep(p, s, h, q, k0 + r);
+          }
+          const float ds = fexp2(x - lse2) * (dp - dl);   // 0 for masked keys / padded queries
           if (BIAS && p.dbias_u && qv) atomicAdd(&bins[cq - kbv[r]], ds);
           sa[bi][r] = ds * p.scale;
         }
@@ -503,8 +532,12 @@ __global__ __launch_bounds__(W * 64) void attn_bwd_dkv_kernel(AP p) {
           else x = sa[bi][r] * sc2 + kadd;
           if (BIAS && !RUN) x += ub[qbv[r] - ck];
           const float pr = fexp2(x - lv[r]);
-          const float ds = pr * (da[bi][r] - dlv[r]);
-          sa[bi][r] = pr;
+          float keep = 1.f;
+          if constexpr (!BIAS) {
+            if (p.drop_p > 0.f) keep = drop_keep(p, s, h, q0 + r, key);
+          }
+          const float ds = pr * (da[bi][r] * keep - dlv[r]);
+          sa[bi][r] = pr * keep;
           da[bi][r] = ds * p.scale;
         }
       }
@@ -723,6 +756,12 @@ int fill(AP& p, const ctclip_attn_args* a) {
   p.bias_u = a->bias_u; p.dbias_u = a->dbias_u;
   p.kmask = a->kmask;
   p.scale = a->scale;
+  p.drop_p = a->dropout_p;
+  if (!(p.drop_p >= 0.f && p.drop_p < 1.f)) return CT_EINVAL;
+  if (p.drop_p > 0.f && a->bias_u) return CT_EINVAL;            // BERT path only
+  p.drop_scale = p.drop_p > 0.f ? 1.f / (1.f - p.drop_p) : 1.f;
+  p.thresh = (unsigned)std::min(4294967295.0, (double)p.drop_p * 4294967296.0);
+  p.seed = a->dropout_seed;
   p.L = a->L; p.H = a->H; p.nseq = a->nseq; p.M = a->M;
   p.Hg = a->grid_h; p.Wg = a->grid_w;
   p.nbins = (2 * a->grid_h - 1) * (2 * a->grid_w - 1);
@@ -987,7 +1026,7 @@ __global__ __launch_bounds__(SW * 64) void attn_small_bwd_kernel(AP p) {
   }
 }
 
-bool small_ok(const AP& p, int D) { return D == 32 && p.L <= 32 && !p.bias_u && !p.kmask; }
+bool small_ok(const AP& p, int D) { return D == 32 && p.L <= 32 && !p.bias_u && !p.kmask && p.drop_p == 0.f; }
 
 }  // namespace
 

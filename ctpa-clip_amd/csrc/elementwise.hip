@@ -163,3 +163,48 @@ extern "C" int ctclip_gelu_f32(const float* x, float* y, int64_t n, void* stream
   CT_CHECK_LAUNCH();
   return 0;
 }
+
+// Hidden-state dropout of the BERT text tower (transformers BertEmbeddings / BertSelfOutput /
+// BertOutput .dropout, p = hidden_dropout_prob in train mode): y = x * keep(seed, i) / (1 - p)
+// (+ res), element i kept iff its splitmix64 hash >= p * 2^32.  The backward is the same call on
+// the gradient with the same seed (res = null).
+namespace {
+__device__ __forceinline__ float hid_keep(uint64_t seed, int64_t i, unsigned thresh, float scale) {
+  uint64_t x = seed ^ ((uint64_t)i * 0x9E3779B97F4A7C15ull);
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (unsigned)x >= thresh ? scale : 0.f;
+}
+
+__global__ __launch_bounds__(256) void dropout_kernel(const float* __restrict__ x, const float* __restrict__ res,
+                                                      float* __restrict__ yf, u16* __restrict__ yb, int64_t n4,
+                                                      unsigned thresh, float scale, uint64_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    f32x4 v = ((const f32x4*)x)[i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] *= hid_keep(seed, 4 * i + j, thresh, scale);
+    if (res) v += ((const f32x4*)res)[i];
+    if (yf) ((f32x4*)yf)[i] = v;
+    if (yb) {
+      uint2 w;
+      w.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+      w.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+      ((uint2*)yb)[i] = w;
+    }
+  }
+}
+}  // namespace
+
+extern "C" int ctclip_dropout(const float* x, const float* res, float* yf, void* yb, int64_t n, float p,
+                              uint64_t seed, void* stream) {
+  CT_REQUIRE(n % 4 == 0, CT_EALIGN);
+  CT_REQUIRE(p >= 0.f && p < 1.f, CT_EINVAL);
+  const unsigned thresh = (unsigned)std::min(4294967295.0, (double)p * 4294967296.0);
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n / 4)), dim3(256), 0, (hipStream_t)stream, x, res, yf, (u16*)yb,
+                     n / 4, thresh, 1.f / (1.f - p), seed);
+  CT_CHECK_LAUNCH();
+  return 0;
+}

@@ -59,6 +59,7 @@ class AttnArgs(ctypes.Structure):
         ('scale', c_f32), ('L', c_i32), ('H', c_i32), ('D', c_i32), ('nseq', c_i32), ('M', c_i64),
         ('grid_h', c_i32), ('grid_w', c_i32), ('n_inner', c_i32),
         ('s_outer', c_i64), ('s_inner', c_i64), ('s_pos', c_i64),
+        ('dropout_p', c_f32), ('dropout_seed', ctypes.c_uint64),
     ]
 
 
@@ -81,6 +82,7 @@ _SIGS = {
     'ctclip_quant_mxfp8': [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp],
     'ctclip_gemm_mxfp8': [ctypes.POINTER(MxGemmArgs), c_vp],
     'ctclip_gemm_mxfp8_set_tile': [c_i32],
+    'ctclip_dropout': [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, ctypes.c_uint64, c_vp],
     'ctclip_gemm_set_variant': [c_i32],
     'ctclip_gemm_set_stagger': [c_i32],
     'ctclip_gemm_set_persist': [c_i32],

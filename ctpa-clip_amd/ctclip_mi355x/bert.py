@@ -142,11 +142,22 @@ class BertModel(nn.Module):
             attention_mask = torch.ones_like(ids)
         kmask = attention_mask.to(torch.int32).contiguous()
         e = self.embeddings
+        # train-mode dropout (HF BertEmbeddings / BertSelfAttention / BertSelfOutput / BertOutput):
+        # one 64-bit seed per (forward call, layer, site); the masks are hashes of it (no host RNG state
+        # on the step path, the backward regenerates them)
+        ph = float(c.hidden_dropout_prob) if self.training else 0.0
+        pa = float(c.attention_probs_dropout_prob) if self.training else 0.0
+        self._drop_calls = getattr(self, '_drop_calls', 0) + 1
+        base = (torch.initial_seed() * 0x2545F4914F6CDD1D + self._drop_calls * 0x9E3779B97F4A7C15) & (2 ** 64 - 1)
+
+        def seed(layer, site):
+            return (base ^ ((layer * 4 + site + 1) * 0xBF58476D1CE4E5B9)) & (2 ** 64 - 1)
+
         xf, xb = Fn.BertEmbedFn.apply(ids, e.word_embeddings.weight, e.position_embeddings.weight,
                                       e.token_type_embeddings.weight, e.LayerNorm.weight, e.LayerNorm.bias,
-                                      c.layer_norm_eps)
+                                      c.layer_norm_eps, (ph, seed(0, 3)))
         dist_sync.mark_ready(xf, 'text')   # every BERT .grad is final once the embeddings' backward ran
-        for lyr in self.encoder.layer:
+        for li, lyr in enumerate(self.encoder.layer):
             a = lyr.attention
             xf, xb = Fn.BertLayerFn.apply(
                 xf, xb, kmask, B, L, c.num_attention_heads, c.layer_norm_eps,
@@ -154,5 +165,6 @@ class BertModel(nn.Module):
                 a.self.value.weight, a.self.value.bias, a.output.dense.weight, a.output.dense.bias,
                 a.output.LayerNorm.weight, a.output.LayerNorm.bias, lyr.intermediate.dense.weight,
                 lyr.intermediate.dense.bias, lyr.output.dense.weight, lyr.output.dense.bias,
-                lyr.output.LayerNorm.weight, lyr.output.LayerNorm.bias)
+                lyr.output.LayerNorm.weight, lyr.output.LayerNorm.bias,
+                (ph, pa, seed(li + 1, 0), seed(li + 1, 1), seed(li + 1, 2)))
         return (xf.view(B, L, c.hidden_size), None)

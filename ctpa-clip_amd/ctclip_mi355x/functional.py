@@ -573,9 +573,14 @@ class BertEmbedFn(torch.autograd.Function):
     """BertEmbeddings: word + position + token_type(0), LayerNorm(eps 1e-12)."""
 
     @staticmethod
-    def forward(ctx, ids, word, pos, typ, ln_w, ln_b, eps):
+    def forward(ctx, ids, word, pos, typ, ln_w, ln_b, eps, drop=(0.0, 0)):
         x = K.embed_fwd(ids, word, pos, typ[0])
-        yb, yf, mean, rstd = K.layernorm_fwd(x, ln_w, ln_b, eps, out_bf16=True, out_f32=True)
+        if drop[0] > 0:
+            _, yf, mean, rstd = K.layernorm_fwd(x, ln_w, ln_b, eps, out_bf16=False, out_f32=True)
+            yf, yb = K.dropout(yf, drop[0], drop[1], out_f32=True, out_bf16=True)
+        else:
+            yb, yf, mean, rstd = K.layernorm_fwd(x, ln_w, ln_b, eps, out_bf16=True, out_f32=True)
+        ctx.drop = drop
         ctx.save_for_backward(ids, x, mean, rstd, ln_w)
         ctx.params = (word, pos, typ, ln_w, ln_b)
         ctx.mark_non_differentiable(yb)
@@ -585,12 +590,15 @@ class BertEmbedFn(torch.autograd.Function):
     def backward(ctx, dyf, _):
         ids, x, mean, rstd, ln_w = ctx.saved_tensors
         word, pos, typ, _, ln_b = ctx.params
-        dx, _, _, _ = K.layernorm_bwd(dyf.contiguous(), x, mean, rstd, ln_w, dx_bf16=False,
+        dyf = dyf.contiguous()
+        if ctx.drop[0] > 0:
+            dyf = K.dropout(dyf, ctx.drop[0], ctx.drop[1])[0]
+        dx, _, _, _ = K.layernorm_bwd(dyf, x, mean, rstd, ln_w, dx_bf16=False,
                                       dgamma_out=gsink(ln_w), dbeta_out=gsink(ln_b))
         dtyp = gsink(typ)
         # scatter-add straight into the parameters' .grad
         K.embed_bwd(ids, dx, gsink(word), gsink(pos), dtyp[0] if dtyp is not None else None)
-        return None, None, None, None, None, None, None
+        return None, None, None, None, None, None, None, None
 
 
 class BertLayerFn(torch.autograd.Function):
@@ -599,27 +607,35 @@ class BertLayerFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xf, xb, kmask, B, L, heads, eps, Wq, bq, Wk, bk, Wv, bv, Wo, bo, ln1_w, ln1_b, Wi, bi, Wout,
-                bout, ln2_w, ln2_b):
+                bout, ln2_w, ln2_b, drop=(0.0, 0.0, 0, 0, 0)):
+        ph, pa, s_attn, s_out1, s_out2 = drop
         Hd = xf.shape[1]
         dh = Hd // heads
         Wqkv = bf_cat([Wq, Wk, Wv])
         bqkv = cat_f32([bq, bk, bv])
         qkv = K.linear(xb, Wqkv, bias=bqkv)
         ctxv, lse = K.attn_fwd(qkv[:, :Hd], qkv[:, Hd:2 * Hd], qkv[:, 2 * Hd:], L=L, H=heads, D=dh, nseq=B,
-                               scale=1.0 / math.sqrt(dh), seq=(1, L, 0, 1), kmask=kmask)
+                               scale=1.0 / math.sqrt(dh), seq=(1, L, 0, 1), kmask=kmask, dropout=(pa, s_attn))
         Wo_b = bf(Wo)
-        a = K.linear(ctxv, Wo_b, bias=bo, residual=xf, out_dtype=F32)
+        if ph > 0:       # LN(dropout(dense(ctx)) + x): the residual leaves the GEMM epilogue
+            a = K.dropout(K.linear(ctxv, Wo_b, bias=bo, out_dtype=F32), ph, s_out1, res=xf)[0]
+        else:
+            a = K.linear(ctxv, Wo_b, bias=bo, residual=xf, out_dtype=F32)
         x1b, x1f, m1, r1 = K.layernorm_fwd(a, ln1_w, ln1_b, eps, out_bf16=True, out_f32=True)
         Wi_b = bf(Wi)
         hpre = torch.empty(xf.shape[0], Wi.shape[0], device=xf.device, dtype=BF16)
         hact = K.linear(x1b, Wi_b, bias=bi, act=K.ACT_GELU, out2=hpre)
         Wout_b = bf(Wout)
-        b2 = K.linear(hact, Wout_b, bias=bout, residual=x1f, out_dtype=F32)
+        if ph > 0:
+            b2 = K.dropout(K.linear(hact, Wout_b, bias=bout, out_dtype=F32), ph, s_out2, res=x1f)[0]
+        else:
+            b2 = K.linear(hact, Wout_b, bias=bout, residual=x1f, out_dtype=F32)
         x2b, x2f, m2, r2 = K.layernorm_fwd(b2, ln2_w, ln2_b, eps, out_bf16=True, out_f32=True)
         ctx.save_for_backward(xb, kmask, qkv, ctxv, lse, a, m1, r1, x1b, hpre, hact, b2, m2, r2, Wqkv, Wo_b, Wi_b,
                               Wout_b, ln1_w, ln2_w)
         ctx.params = (Wq, bq, Wk, bk, Wv, bv, Wo, bo, ln1_w, ln1_b, Wi, bi, Wout, bout, ln2_w, ln2_b)
         ctx.dims = (B, L, heads, dh)
+        ctx.drop = drop
         ctx.mark_non_differentiable(x2b)
         return x2f, x2b
 
@@ -629,6 +645,7 @@ class BertLayerFn(torch.autograd.Function):
          ln2_w) = ctx.saved_tensors
         Wq, bq, Wk, bk, Wv, bv, Wo, bo, _, ln1_b, Wi, bi, Wout, bout, _, ln2_b = ctx.params
         B, L, heads, dh = ctx.dims
+        ph, pa, s_attn, s_out1, s_out2 = ctx.drop
         Hd = heads * dh
 
         def wgrad(dy, x, W, b):          # dW += dy^T x, db += colsum(dy), into the parameters' .grad
@@ -640,6 +657,8 @@ class BertLayerFn(torch.autograd.Function):
         # LN2 + FF out
         db2f, db2b, _, _ = K.layernorm_bwd(dx2f.contiguous(), b2, m2, r2, ln2_w, dgamma_out=gsink(ln2_w),
                                            dbeta_out=gsink(ln2_b))
+        if ph > 0:       # gradient through the output dropout (the residual path bypasses it)
+            db2b = K.dropout(db2f, ph, s_out2, out_f32=False, out_bf16=True)[1]
         dhact = K.matmul_nn(db2b, Wout_b)
         wgrad(db2b, hact, Wout, bout)
         dhpre = K.gelu_bwd(dhact, hpre)
@@ -647,13 +666,15 @@ class BertLayerFn(torch.autograd.Function):
         wgrad(dhpre, x1b, Wi, bi)
         # LN1 + attention out
         daf, dab, _, _ = K.layernorm_bwd(dx1, a, m1, r1, ln1_w, dgamma_out=gsink(ln1_w), dbeta_out=gsink(ln1_b))
+        if ph > 0:
+            dab = K.dropout(daf, ph, s_out1, out_f32=False, out_bf16=True)[1]
         dctx = K.matmul_nn(dab, Wo_b)
         wgrad(dab, ctxv, Wo, bo)
         dqkv = torch.empty_like(qkv)
         K.attn_bwd(qkv[:, :Hd], qkv[:, Hd:2 * Hd], qkv[:, 2 * Hd:], ctxv, lse, dctx, dqkv[:, :Hd],
                    dqkv[:, Hd:2 * Hd], dqkv[:, 2 * Hd:], L=L, H=heads, D=dh, nseq=B, scale=1.0 / math.sqrt(dh),
-                   seq=(1, L, 0, 1), kmask=kmask)
+                   seq=(1, L, 0, 1), kmask=kmask, dropout=(pa, s_attn))
         dx = K.matmul_nn(dqkv, Wqkv, residual=daf, out_dtype=F32)
         for i, (W, b) in enumerate(((Wq, bq), (Wk, bk), (Wv, bv))):
             wgrad(dqkv[:, i * Hd:(i + 1) * Hd], xb, W, b)
-        return (dx, None, None, None, None, None, None) + (None,) * 16
+        return (dx, None, None, None, None, None, None) + (None,) * 17

@@ -371,7 +371,7 @@ def peg_bwd(doutb, doutf, xb, B, T, H, W, weight, mode):
 
 # ----------------------------------------------------------------------------- attention
 def _attn_args(q, k, v, o, *, L, H, D, nseq, M, scale, seq, bias_u=None, grid=(0, 0), kmask=None, lse=None,
-               dout=None, dq=None, dk=None, dv=None, delta=None, dbias_u=None):
+               dout=None, dq=None, dk=None, dv=None, delta=None, dbias_u=None, dropout=(0.0, 0)):
     a = _lib.AttnArgs()
     a.q, a.ldq = ptr(q), q.stride(0)
     a.k, a.ldk = ptr(k), k.stride(0)
@@ -386,26 +386,28 @@ def _attn_args(q, k, v, o, *, L, H, D, nseq, M, scale, seq, bias_u=None, grid=(0
     a.scale, a.L, a.H, a.D, a.nseq, a.M = scale, L, H, D, nseq, M
     a.grid_h, a.grid_w = grid
     a.n_inner, a.s_outer, a.s_inner, a.s_pos = seq
+    a.dropout_p, a.dropout_seed = float(dropout[0]), int(dropout[1]) & (2 ** 64 - 1)
     return a
 
 
-def attn_fwd(q, k, v, *, L, H, D, nseq, scale, seq, bias_u=None, grid=(0, 0), kmask=None):
+def attn_fwd(q, k, v, *, L, H, D, nseq, scale, seq, bias_u=None, grid=(0, 0), kmask=None, dropout=(0.0, 0)):
     """q/k/v: 2D views [M, ...] whose head h occupies columns h*D:(h+1)*D.  Returns (o [M, H*D], lse [H, M])."""
     M = q.shape[0]
     o = torch.empty(M, H * D, device=q.device, dtype=BF16)
     lse = torch.empty(H, M, device=q.device, dtype=F32)
     a = _attn_args(q, k, v, o, L=L, H=H, D=D, nseq=nseq, M=M, scale=scale, seq=seq, bias_u=bias_u, grid=grid,
-                   kmask=kmask, lse=lse)
+                   kmask=kmask, lse=lse, dropout=dropout)
     call('ctclip_attn_fwd', _lib.ctypes.byref(a), stream_ptr())
     return o, lse
 
 
 def attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, *, L, H, D, nseq, scale, seq, bias_u=None, dbias_u=None,
-             grid=(0, 0), kmask=None):
+             grid=(0, 0), kmask=None, dropout=(0.0, 0)):
     M = q.shape[0]
     delta = torch.empty(H, M, device=q.device, dtype=F32)
     a = _attn_args(q, k, v, o, L=L, H=H, D=D, nseq=nseq, M=M, scale=scale, seq=seq, bias_u=bias_u, grid=grid,
-                   kmask=kmask, lse=lse, dout=dout, dq=dq, dk=dk, dv=dv, delta=delta, dbias_u=dbias_u)
+                   kmask=kmask, lse=lse, dout=dout, dq=dq, dk=dk, dv=dv, delta=delta, dbias_u=dbias_u,
+                   dropout=dropout)
     call('ctclip_attn_bwd', _lib.ctypes.byref(a), stream_ptr())
 
 
@@ -617,3 +619,13 @@ def gemm_mxfp8(qa, sa, qb, sb, *, bias=None, alpha=1.0, out_f32=False, out=None)
 def gemm_mxfp8_set_tile(bm):
     """diagnostic: force the 128- / 256-row MX tile kernel (0 = auto); returns the previous."""
     return _lib.lib().ctclip_gemm_mxfp8_set_tile(int(bm))
+
+
+def dropout(x, p, seed, *, res=None, out_f32=True, out_bf16=False):
+    """BERT hidden dropout: (x * keep / (1 - p) (+ res)) as (f32 or None, bf16 or None)."""
+    assert x.dtype == F32 and x.is_contiguous() and (res is None or (res.dtype == F32 and res.is_contiguous()))
+    yf = torch.empty_like(x) if out_f32 else None
+    yb = torch.empty(x.shape, device=x.device, dtype=BF16) if out_bf16 else None
+    call('ctclip_dropout', ptr(x), ptr(res), ptr(yf), ptr(yb), x.numel(), float(p), int(seed) & (2 ** 64 - 1),
+         stream_ptr())
+    return yf, yb

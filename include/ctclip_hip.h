@@ -134,6 +134,11 @@ int ctclip_pack_rows(const float* src, int64_t ld_src, const int32_t* map, int64
 int ctclip_unpack_rows(const float* src, int64_t ld_src, const int32_t* map, int64_t rows_src, int32_t cols,
                        float* dst, int64_t ld_dst, int32_t accumulate, void* stream);
 int ctclip_gelu_f32(const float* x, float* y, int64_t n, void* stream);
+/* BERT hidden dropout (BertEmbeddings / BertSelfOutput / BertOutput, train mode):
+ * y = x * keep / (1 - p) (+ res) into yf (f32) and / or yb (bf16); keep = hash(seed, i) >= p * 2^32.
+ * The backward is the same call on dy with the same seed.  n % 4 == 0. */
+int ctclip_dropout(const float* x, const float* res, float* yf, void* yb, int64_t n, float p, uint64_t seed,
+                   void* stream);
 int ctclip_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
 int ctclip_add_f32(const float* a, const float* b, float* y, void* y_bf16, int64_t n, void* stream);
 
@@ -197,6 +202,11 @@ typedef struct {
   int32_t grid_h, grid_w;
   int32_t n_inner;
   int64_t s_outer, s_inner, s_pos;
+  /* attention-probability dropout (transformers BertSelfAttention.dropout, train mode): P[q][k]
+   * kept iff hash(dropout_seed, seq, head, q, k) >= p * 2^32, kept entries scaled by 1/(1-p);
+   * the backward regenerates the mask from the same seed.  0 = off; bias_u != null: CT_EINVAL. */
+  float dropout_p;
+  uint64_t dropout_seed;
 } ctclip_attn_args;
 int ctclip_attn_fwd(const ctclip_attn_args* a, void* stream);
 int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream);

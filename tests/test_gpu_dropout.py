@@ -1,0 +1,127 @@
+"""BERT train-mode dropout (transformers BertEmbeddings / BertSelfAttention / BertSelfOutput /
+BertOutput, p = 0.1 in the reference's train step, ct_clip/ct_clip.py:685-686): the hidden-state
+kernel (ctclip_dropout) and the attention-probability dropout inside the fused attention kernels,
+against torch references that regenerate the same hash mask (splitmix64 finaliser of
+seed ^ index * golden ratio, kept iff the low 32 bits >= p * 2^32)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+dev = 'cuda'
+GOLD, C1, C2 = 0x9E3779B97F4A7C15, 0xff51afd7ed558ccd, 0xc4ceb9fe1a85ec53
+
+
+def s64(c):
+    c &= 2 ** 64 - 1
+    return c - 2 ** 64 if c >= 2 ** 63 else c
+
+
+def keep_mask(idx, seed, p):
+    """idx int64 tensor -> bool keep mask (uint64 arithmetic emulated in wrapping int64)."""
+    x = torch.bitwise_xor(idx * s64(GOLD), torch.full_like(idx, s64(seed)))
+    for c in (C1, C2):
+        x = x ^ ((x >> 33) & ((1 << 31) - 1))
+        x = x * s64(c)
+    x = x ^ ((x >> 33) & ((1 << 31) - 1))
+    thresh = int(min(4294967295.0, float(np.float32(p)) * 4294967296.0))
+    return (x & 0xffffffff) >= thresh
+
+
+@pytest.fixture(scope='module')
+def K():
+    from ctclip_mi355x import kernels
+    return kernels
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def test_hidden_dropout(K):
+    torch.manual_seed(0)
+    n = 1024 * 768
+    x = torch.randn(1024, 768, device=dev)
+    r = torch.randn(1024, 768, device=dev)
+    p, seed = 0.1, 0x1234_5678_9abc_def0
+    yf, yb = K.dropout(x, p, seed, res=r, out_bf16=True)
+    keep = keep_mask(torch.arange(n, device=dev), seed, p).view(1024, 768)
+    scale = np.float32(1.0) / (np.float32(1.0) - np.float32(p))
+    ref = torch.where(keep, x * float(scale), torch.zeros_like(x)) + r
+    assert torch.equal(yf, ref)
+    assert torch.equal(yb, ref.bfloat16())
+    assert abs(keep.float().mean().item() - (1 - p)) < 3e-3
+    # backward = same call on the gradient: same mask
+    g, _ = K.dropout(torch.ones_like(x), p, seed)
+    assert torch.equal(g != 0, keep)
+    # a different seed gives a different mask
+    g2, _ = K.dropout(torch.ones_like(x), p, seed + 1)
+    assert (g2 != g).float().mean().item() > 0.1
+
+
+def test_attention_prob_dropout_fwd_bwd(K):
+    """BERT shape (L = 128, 12 heads x 64, ragged key mask): O, dQ, dK, dV against torch autograd
+    on softmax(QK^T/8 + mask) * keep / (1 - p) . V with the regenerated mask (bf16 tolerance)."""
+    torch.manual_seed(1)
+    B, L, H, D = 2, 128, 12, 64
+    p, seed = 0.1, 987654321
+    qkv = torch.randn(B * L, 3 * H * D, device=dev).bfloat16()
+    lens = [128, 77]
+    kmask = torch.zeros(B, L, dtype=torch.int32, device=dev)
+    for b, n in enumerate(lens):
+        kmask[b, :n] = 1
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    scale = 1.0 / math.sqrt(D)
+    o, lse = K.attn_fwd(q, k, v, L=L, H=H, D=D, nseq=B, scale=scale, seq=(1, L, 0, 1), kmask=kmask,
+                        dropout=(p, seed))
+    dout = torch.randn(B * L, H * D, device=dev).bfloat16()
+    dq, dk, dv = (torch.empty(B * L, H * D, device=dev, dtype=torch.bfloat16) for _ in range(3))
+    K.attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, L=L, H=H, D=D, nseq=B, scale=scale, seq=(1, L, 0, 1),
+               kmask=kmask, dropout=(p, seed))
+    # torch reference
+    qr, kr, vr = (t.float().view(B, L, H, D).transpose(1, 2).requires_grad_(True) for t in (q, k, v))
+    s = qr @ kr.transpose(-1, -2) * scale
+    s = s.masked_fill(kmask[:, None, None, :] == 0, float('-inf'))
+    P = torch.softmax(s, -1)
+    idx = (((torch.arange(B, device=dev)[:, None, None, None] * H + torch.arange(H, device=dev)[None, :, None, None])
+            * L + torch.arange(L, device=dev)[None, None, :, None]) * L + torch.arange(L, device=dev)[None, None, None, :])
+    keep = keep_mask(idx, seed, p)
+    dscale = float(np.float32(1.0) / (np.float32(1.0) - np.float32(p)))
+    O = (P * keep * dscale) @ vr
+    O.backward(dout.float().view(B, L, H, D).transpose(1, 2))
+    Oref = O.detach().transpose(1, 2).reshape(B * L, H * D)
+    assert rel(o, Oref) < 1e-2
+    for got, ref in ((dq, qr.grad), (dk, kr.grad), (dv, vr.grad)):
+        assert rel(got, ref.transpose(1, 2).reshape(B * L, H * D)) < 2e-2
+    # p = 0 path unchanged
+    o0, _ = K.attn_fwd(q, k, v, L=L, H=H, D=D, nseq=B, scale=scale, seq=(1, L, 0, 1), kmask=kmask)
+    O0 = (P.detach() @ vr.detach()).transpose(1, 2).reshape(B * L, H * D)
+    assert rel(o0, O0) < 1e-2 and rel(o, o0) > 0.05
+
+
+def test_bert_train_step_with_dropout(K):
+    """Whole BERT layer stack in train mode with p = 0.1: finite, differs from eval, masks
+    regenerated consistently (two forwards with the same call counter give the same output)."""
+    from ctclip_mi355x.bert import BertModel, BertConfig
+    torch.manual_seed(2)
+    m = BertModel(BertConfig(vocab_size=1000, hidden_size=768, num_hidden_layers=2, num_attention_heads=12,
+                             intermediate_size=3072, max_position_embeddings=128)).cuda()
+    ids = torch.randint(5, 1000, (2, 64), device=dev)
+    mask = torch.ones_like(ids)
+    m.eval()
+    with torch.no_grad():
+        ye = m(ids, mask)[0].clone()
+    m.train()
+    m._drop_calls = 10
+    y1 = m(ids, mask)[0]
+    m._drop_calls = 10
+    y2 = m(ids, mask)[0]
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    assert torch.isfinite(y1).all() and rel(y1, ye) > 0.05
+    y1[:, 0].float().square().sum().backward()
+    g = m.encoder.layer[0].attention.self.query.weight.grad
+    assert g is not None and torch.isfinite(g).all() and g.abs().sum().item() > 0

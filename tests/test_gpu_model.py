@@ -33,7 +33,8 @@ def build(cfg):
                temporal_depth=v.temporal_depth, dim_head=v.dim_head, heads=v.heads)
     bert = BertConfig(vocab_size=b.vocab_size, hidden_size=b.hidden, num_hidden_layers=b.layers,
                       num_attention_heads=b.heads, intermediate_size=b.intermediate,
-                      max_position_embeddings=b.max_position)
+                      max_position_embeddings=b.max_position,
+                      hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)   # parity runs: SURVEY §8(c)
     m = build_ctclip(vit, bert, cfg.dim_latent)
     m.load_state_dict(W.make_state_dict(cfg), strict=True)
     return set_finetune_trainable(m).cuda()
