@@ -1,7 +1,8 @@
 """Benchmark: CT-CLIP contrastive train step on MI355X (BASELINE.json metric: CT-report pairs/s).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
-    (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL)
+    (N > 1: one rank per GPU over RCCL -- under torch.distributed.run, or, when started without a
+    launcher, bench.py starts torch.distributed.run --nproc-per-node N itself as a child process)
 
 A step = CTCLIP forward (BERT-base text tower on 128-token reports + CTViT base image tower on
 int16-HU 240x480x480 volumes + projections + InfoNCE over the all-gathered global batch) ->
@@ -97,11 +98,35 @@ def cpu_baseline(batch):
                       f'fp32 eager oracle on CPU ({cpu_name}); {dt:.1f} s'}
 
 
+def launch_ranks(args):
+    """``--gpus N`` (N > 1) without a torch.distributed launcher around us: start N ranks with
+    torch.distributed.run (one process per GPU) as a CHILD process, before this process touches
+    the GPU, and exit with its status."""
+    import socket
+    import subprocess
+    ndev = torch.cuda.device_count()          # does not initialise the GPU
+    if args.dist_backend == 'nccl' and ndev < args.gpus:
+        sys.exit(f'bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs for RCCL, found {ndev} '
+                 f'(--dist-backend gloo rehearses N ranks on fewer GPUs)')
+    with socket.socket() as s_:
+        s_.bind(('127.0.0.1', 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.gpus}',
+           '--master-addr', '127.0.0.1', f'--master-port={port}', os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    sys.exit(subprocess.run(cmd, env=env).returncode)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        launch_ranks(args)
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        sys.exit(f'bench.py: WORLD_SIZE {world} != --gpus {args.gpus}')
     dev = torch.device('cuda', local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
     if world > 1:
@@ -109,6 +134,8 @@ def main():
             dist.init_process_group('nccl', device_id=dev)
         else:
             dist.init_process_group('gloo')
+        if dist.get_world_size() != args.gpus:
+            sys.exit(f'bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}')
 
     from ctclip_mi355x.models import build_ctclip, set_finetune_trainable
     from ctclip_mi355x.trainer import CTClipTrainer
@@ -193,6 +220,8 @@ def main():
     }
     if in_sync is not None:
         result['ranks_in_sync'] = in_sync
+        result['dist'] = {'backend': dist.get_backend(), 'world_size': dist.get_world_size(),
+                          'devices_visible': torch.cuda.device_count()}
     if args.dist_backend != 'nccl':
         result['note'] = f'{args.dist_backend} rehearsal: {world} ranks on {torch.cuda.device_count()} GPU(s)'
     if ff1:

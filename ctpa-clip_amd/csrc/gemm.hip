@@ -185,18 +185,24 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
     // argmax over this tile's columns per row: write (value, index) pairs per (row, tile)
     // C = float2 [M][ntiles]; columns >= N excluded.
     // one (value, index) per (row, 64-column group), first-max tie-break (torch.argmax semantics)
+    // optional C2 (f32 [M][ldc2]): the group's second-best score, so the f32 re-score knows
+    // when a non-winner of the group can still be the f32 argmax (vq.hip)
     const int row = t >> 1, half = t & 1;
     const int ncol = (int)min((int64_t)BN, p.N - n0);
-    float best = -INFINITY;
+    float best = -INFINITY, second = -INFINITY;
     int bi = 0x7fffffff;
     for (int c = half * 64; c < half * 64 + 64; ++c) {
       const float v = cs[row * CS_LD + c];
-      if (c < ncol && v > best) { best = v; bi = c; }
+      if (c < ncol) {
+        if (v > best) { second = best; best = v; bi = c; }
+        else if (v > second) second = v;
+      }
     }
     const int64_t gm = m0 + row;
     if (gm < p.M && half * 64 < ncol) {
       float2* out = (float2*)p.C + bidx * p.sC;
       out[gm * p.ldc + tx * 2 + half] = make_float2(best, __int_as_float((int)(n0 + bi)));
+      if (p.C2) ((float*)p.C2)[bidx * p.sC2 + gm * p.ldc2 + tx * 2 + half] = second;
     }
     return;
   }

@@ -136,21 +136,28 @@ __device__ __forceinline__ void epilogue(const P& p, f32x4 (&acc)[8][4], char* s
     if (p.act == 3) {
       // argmax over this wave's 64 columns: 2 lanes per row (32 columns each), (value, index)
       // per (row, 64-col group), first-max tie-break
+      // (+ the group's second-best score into the optional f32 C2, see gemm.hip)
       const int row = lane >> 1, hc = lane & 1;
       const int64_t gm = rbase + row;
-      float best = -INFINITY;
+      float best = -INFINITY, second = -INFINITY;
       int bi = 0x7fffffff;
       const int ncol = (int)max((int64_t)0, min((int64_t)64, p.N - wcol0));
       for (int c = hc * 32; c < hc * 32 + 32; ++c) {
         const float v = cs[row * EP_LD + c];
-        if (c < ncol && v > best) { best = v; bi = c; }
+        if (c < ncol) {
+          if (v > best) { second = best; best = v; bi = c; }
+          else if (v > second) second = v;
+        }
       }
       const float ob = __shfl_xor(best, 1, 64);
+      const float os = __shfl_xor(second, 1, 64);
       const int oi = __shfl_xor(bi, 1, 64);
-      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+      if (ob > best || (ob == best && oi < bi)) { second = fmaxf(best, os); best = ob; bi = oi; }
+      else second = fmaxf(second, ob);
       if (hc == 0 && gm < p.M && ncol > 0) {
         float2* out = (float2*)p.C + bidx * p.sC;
         out[gm * p.ldc + (wcol0 >> 6)] = make_float2(best, __int_as_float((int)(wcol0 + bi)));
+        if (p.C2) ((float*)p.C2)[bidx * p.sC2 + gm * p.ldc2 + (wcol0 >> 6)] = second;
       }
     } else if (p.act == 2) {
       // GEGLU pairs of 32 columns: [x | gate] -> 32 outputs; h (C) keeps both halves
@@ -481,24 +488,30 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
     if constexpr (MODE == 3) {
       // argmax over the wave's 64 columns of row gm (first-max tie-break): 16 values per lane,
       // then across the 4 lanes g = 0..3 that hold the same row
-      float best = -INFINITY;
+      float best = -INFINITY, second = -INFINITY;
       int bi = 0x7fffffff;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = 16 * j + 4 * g + r;
-          if (wcol0 + c < p.N && (v[j][r] > best || (v[j][r] == best && c < bi))) { best = v[j][r]; bi = c; }
+          if (wcol0 + c < p.N) {
+            if (v[j][r] > best || (v[j][r] == best && c < bi)) { second = best; best = v[j][r]; bi = c; }
+            else second = fmaxf(second, v[j][r]);
+          }
         }
 #pragma unroll
       for (int o = 16; o <= 32; o <<= 1) {
         const float ob = __shfl_xor(best, o, 64);
+        const float os = __shfl_xor(second, o, 64);
         const int oi = __shfl_xor(bi, o, 64);
-        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+        if (ob > best || (ob == best && oi < bi)) { second = fmaxf(best, os); best = ob; bi = oi; }
+        else second = fmaxf(second, ob);
       }
       if (g == 0 && rok && wcol0 < p.N) {
         float2* out = (float2*)p.C + bidx * p.sC;
         out[gm * p.ldc + (wcol0 >> 6)] = make_float2(best, __int_as_float((int)(wcol0 + bi)));
+        if (p.C2) ((float*)p.C2)[bidx * p.sC2 + gm * p.ldc2 + (wcol0 >> 6)] = second;
       }
       continue;
     }

@@ -1,56 +1,100 @@
 // Cosine-similarity vector quantiser (vector_quantize_pytorch==1.1.2, used at
 // ct_clip/ctvit.py:187,421-427) and the image pooling of CTCLIP.forward (ct_clip.py:724,740).
 //
-// The distance matmul l2norm(x) . codebook^T runs as a bf16 MFMA GEMM whose epilogue keeps
-// the per-(row, 128-code tile) argmax (gemm.hip act=3).  vq_select then re-scores, in f32
-// against the f32 codebook, every tile winner within `margin` of the best bf16 score, so the
-// chosen index is the exact f32 argmax whenever the true winner's bf16 score is within the
-// margin (bf16 operand rounding moves a unit-vector cosine by ~1e-4; margin default 2e-2).
+// The distance matmul l2norm(x) . codebook^T runs as a bf16 MFMA GEMM whose epilogue keeps,
+// per (row, 64-code group), the bf16 argmax and the group's second-best bf16 score (gemm.hip
+// act=3 with C2).  vq_select then re-scores in f32, against the f32 codebook and the f32
+// tokens, every code whose bf16 score can be within `margin` of the best: each group winner
+// within the margin, and ALL codes of a group whose second-best is within it too.  Every
+// bf16 score is within 2^-7 of the f32 cosine (bf16 x, its l2norm and the codebook each round
+// at 2^-9 relative; Cauchy-Schwarz on unit vectors), so the true f32 winner's bf16 score is
+// >= best - 2^-6 and margin 2e-2 > 2^-6 makes the result the exact f32 argmax (first index on
+// f32 ties), independent of the bf16 rounding.
 #include "common.h"
 #include "../../include/ctclip_hip.h"
 
 namespace {
 
-// one wave per row; D % 8 == 0, D <= 512 handled as 8 floats per lane (+ loop for larger)
-__global__ __launch_bounds__(256) void vq_select_kernel(const float2* __restrict__ cand, int ntiles,
+// one wave per row; the row's f32 l2norm lives in a wave-private LDS strip (D floats) so the
+// full-group re-score can run one code per lane
+__global__ __launch_bounds__(256) void vq_select_kernel(const float2* __restrict__ cand,
+                                                        const float* __restrict__ cand2, int ntiles,
                                                         const float* __restrict__ x, int64_t rows, int D,
-                                                        const float* __restrict__ cb, float margin,
+                                                        const float* __restrict__ cb, int C, float margin,
                                                         int32_t* __restrict__ idx_out, float* __restrict__ xn_out) {
+  extern __shared__ float xs_all[];
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
+  float* xs = xs_all + (threadIdx.x >> 6) * D;
   const float* xr = x + row * D;
   // f32 l2norm of x (F.normalize, eps 1e-12)
   float ss = 0.f;
   for (int c = lane; c < D; c += 64) ss += xr[c] * xr[c];
   ss = warp_sum(ss);
   const float inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
-  // best bf16 score over tiles
+  for (int c = lane; c < D; c += 64) {
+    const float v = xr[c] * inv;
+    xs[c] = v;
+    if (xn_out) xn_out[row * D + c] = v;
+  }
+  // best bf16 score over groups
   float best = -INFINITY;
   for (int t = lane; t < ntiles; t += 64) best = fmaxf(best, cand[row * ntiles + t].x);
   best = warp_max(best);
+  const float thr = best - margin;
   float bv = -INFINITY;
   int bi = 0x7fffffff;
   for (int t0 = 0; t0 < ntiles; t0 += 64) {
     const int t = t0 + lane;
-    bool take = false;
+    bool take = false, full = false;
     float2 c = make_float2(-INFINITY, 0.f);
-    if (t < ntiles) { c = cand[row * ntiles + t]; take = c.x >= best - margin; }
+    if (t < ntiles) {
+      c = cand[row * ntiles + t];
+      take = c.x >= thr;
+      full = take && cand2 && cand2[row * ntiles + t] >= thr;
+    }
     unsigned long long mask = __ballot(take);
+    const unsigned long long fmask = __ballot(full);
     while (mask) {
       const int src = __ffsll((long long)mask) - 1;
       mask &= mask - 1;
-      const int ci = __float_as_int(__shfl(c.y, src, 64));
-      const float* cr = cb + (int64_t)ci * D;
-      float d = 0.f;
-      for (int k = lane; k < D; k += 64) d += xr[k] * inv * cr[k];
-      d = warp_sum(d);
-      if (d > bv || (d == bv && ci < bi)) { bv = d; bi = ci; }
+      if ((fmask >> src) & 1ull) {
+        // several codes of this group are within the margin: score all of them, one per lane
+        const int ci = (t0 + src) * 64 + lane;
+        float d = -INFINITY;
+        if (ci < C) {
+          const float* cr = cb + (int64_t)ci * D;
+          d = 0.f;
+          for (int k = 0; k < D; k += 4) {
+            const f32x4 w = *(const f32x4*)(cr + k);
+            const f32x4 xv = *(const f32x4*)(xs + k);
+            d += xv[0] * w[0];
+            d += xv[1] * w[1];
+            d += xv[2] * w[2];
+            d += xv[3] * w[3];
+          }
+        }
+        float dv = d;
+        int di = ci < C ? ci : 0x7fffffff;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+          const float ov = __shfl_xor(dv, o, 64);
+          const int oi = __shfl_xor(di, o, 64);
+          if (ov > dv || (ov == dv && oi < di)) { dv = ov; di = oi; }
+        }
+        if (dv > bv || (dv == bv && di < bi)) { bv = dv; bi = di; }
+      } else {
+        const int ci = __float_as_int(__shfl(c.y, src, 64));
+        const float* cr = cb + (int64_t)ci * D;
+        float d = 0.f;
+        for (int k = lane; k < D; k += 64) d += xs[k] * cr[k];
+        d = warp_sum(d);
+        if (d > bv || (d == bv && ci < bi)) { bv = d; bi = ci; }
+      }
     }
   }
   if (lane == 0) idx_out[row] = bi;
-  if (xn_out)
-    for (int c = lane; c < D; c += 64) xn_out[row * D + c] = xr[c] * inv;
 }
 
 // pooled[b][hw][d] = (1/T) sum_t cb[idx[b][t*HW + hw]][d]
@@ -160,11 +204,13 @@ inline int gridn(int64_t n) { return (int)std::min<int64_t>(8192, std::max<int64
 
 }  // namespace
 
-extern "C" int ctclip_vq_select(const float* cand, int32_t ntiles, const float* x, int64_t rows, int32_t D,
-                                const float* codebook, float margin, int32_t* idx, float* xn_out, void* stream) {
+extern "C" int ctclip_vq_select(const float* cand, const float* cand2, int32_t ntiles, const float* x, int64_t rows,
+                                int32_t D, const float* codebook, int32_t C, float margin, int32_t* idx,
+                                float* xn_out, void* stream) {
   if (rows == 0) return 0;
-  hipLaunchKernelGGL(vq_select_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, (hipStream_t)stream, (const float2*)cand,
-                     ntiles, x, rows, D, codebook, margin, idx, xn_out);
+  CT_REQUIRE(D % 4 == 0 && D <= 4096 && aligned16(codebook) && ntiles == (C + 63) / 64, CT_EINVAL);
+  hipLaunchKernelGGL(vq_select_kernel, dim3(cdiv(rows, 4)), dim3(256), 4 * D * sizeof(float), (hipStream_t)stream,
+                     (const float2*)cand, cand2, ntiles, x, rows, D, codebook, C, margin, idx, xn_out);
   CT_CHECK_LAUNCH();
   return 0;
 }

@@ -113,7 +113,7 @@ _SIGS = {
     'ctclip_peg_wgrad_slabs': [c_i64, c_i32, c_i32, c_i32, c_i32],
     'ctclip_attn_fwd': [ctypes.POINTER(AttnArgs), c_vp],
     'ctclip_attn_bwd': [ctypes.POINTER(AttnArgs), c_vp],
-    'ctclip_vq_select': [c_vp, c_i32, c_vp, c_i64, c_i32, c_vp, c_f32, c_vp, c_vp, c_vp],
+    'ctclip_vq_select': [c_vp, c_vp, c_i32, c_vp, c_i64, c_i32, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp],
     'ctclip_vq_pool': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
     'ctclip_vq_pool_bwd': [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
     'ctclip_vq_gather': [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp],

@@ -13,6 +13,7 @@ from pathlib import Path
 import torch
 from torch import nn
 
+from . import dist_sync
 from . import functional as Fn
 from . import streams
 
@@ -66,6 +67,7 @@ class CTCLIP(nn.Module):
         self._wvis = (None, None)
         self.defer_text_backward = False     # set by CTClipTrainer (see encode)
         self._deferred_text = None
+        self._t_gather = None
 
     # ------------------------------------------------------------------ checkpoint
     def load(self, path):
@@ -100,6 +102,9 @@ class CTCLIP(nn.Module):
         ts = streams.text_stream(dev)
         with torch.cuda.stream(ts) if ts is not None else _nullctx():
             t_raw = Fn.TextProjFn.apply(enc_text[:, 0, :].contiguous(), self.to_text_latent.weight)
+            # N > 1: the text latents' all-gather goes out from the text stream now, beside the
+            # 3D-ViT forward still running on the main stream (SURVEY 8(e) overlap)
+            self._t_gather = dist_sync.start_gather(t_raw) if dist_sync.world_rank()[0] > 1 else None
         streams.join_text(dev)
         if ts is not None:
             t_raw.record_stream(torch.cuda.current_stream(dev))
@@ -141,7 +146,8 @@ class CTCLIP(nn.Module):
         if not return_loss:
             from . import kernels as K
             return K.clip_scores(t_raw.contiguous(), i_raw.contiguous(), self.temperature.detach().reshape(1))
-        return Fn.ClipLossFn.apply(t_raw, i_raw, self.temperature)
+        tg, self._t_gather = self._t_gather, None
+        return Fn.ClipLossFn.apply(t_raw, i_raw, self.temperature, None, tg)
 
     def backward_deferred_text(self):
         """Back-propagate the text tower whose graph ``encode`` detached (defer_text_backward).

@@ -100,9 +100,10 @@ class CTViT(nn.Module):
         return self._offs[key]
 
     # ------------------------------------------------------------------ encoder
-    def encode_tokens(self, video):
+    def encode_tokens(self, video, trace=None):
         """Patch-embed + spatial + temporal transformers.  video: (B, C, F, H, W) float in [-1, 1]
-        or int16 HU (normalised in-kernel).  Returns (z f32 [M, D], z bf16, geometry)."""
+        or int16 HU (normalised in-kernel).  Returns (z f32 [M, D], z bf16, geometry); ``trace``
+        (a dict, tests) receives the f32 token rows after patch-embed / spatial / temporal stacks."""
         if video.ndim == 4:
             video = video.unsqueeze(2)
         assert video.ndim == 5
@@ -118,6 +119,8 @@ class CTViT(nn.Module):
                                        pe[3].bias, self.temporal_patch_size, self.patch_size[0], is_hu,
                                        self._offsets(video.shape, video.device))
         dist_sync.mark_ready(xf, 'vit_rest')   # with the CPB node below: the rest of the image tower
+        if trace is not None:
+            trace['patch_emb'] = xf
         hg, wg = self.patch_height_width
         T = F // self.temporal_patch_size
         g_sp = Fn.Geo(B, T, hg, wg, self.heads, self.dim_head, 0)
@@ -126,6 +129,8 @@ class CTViT(nn.Module):
         dist_sync.mark_ready(bias_u, 'vit_rest')
         xf, xb = self.enc_spatial_transformer.run(xf, xb, g_sp, bias_u)   # ctvit.py:319
         zf, zb = self.enc_temporal_transformer.run(xf, xb, g_tm)         # ctvit.py:327
+        if trace is not None:
+            trace['spatial_out'], trace['temporal_out'] = xf, zf
         return zf, zb, g_sp
 
     def encode_pooled(self, video):

@@ -5,7 +5,8 @@ an all-reduce of every gradient bucket, and — through the loss — negatives d
 local batch.  Here the step has exactly three exchanges, each one collective:
 
   1. ``gather_latents``: all-gather of the raw [B, 512] text / image latents so InfoNCE sees the
-     GLOBAL batch as negatives (every rank then computes the same global loss; ``local_rows``
+     GLOBAL batch as negatives (the text latents' gather is issued on the text stream as soon as
+     BERT finishes, beside the 3D-ViT forward: ``start_gather``) (every rank then computes the same global loss; ``local_rows``
      keeps the gradient rows of this rank's pairs);
   2. ``sum_codebook_stats``: SUM of the VQ EMA statistics (per-code counts and token sums) so every
      rank applies the same codebook update (vector_quantize_pytorch's EMA with a synced codebook);
@@ -29,11 +30,43 @@ def world_rank():
     return 1, 0
 
 
-def gather_latents(t_raw: torch.Tensor, i_raw: torch.Tensor):
-    """[B, Dl] x 2 on each rank -> ([world*B, Dl], [world*B, Dl]) in rank order."""
+def start_gather(x: torch.Tensor):
+    """Asynchronous all-gather of this rank's [B, Dl] rows -> handle for ``finish_gather``.  RCCL
+    orders it after the work already queued on the CURRENT stream only, so issuing it inside the
+    producing stream's context (the text stream, streams.py) lets it run while the other stream
+    keeps computing -- the side-stream latent exchange of SURVEY 8(e).  World 1: no collective."""
+    world, _ = world_rank()
+    x = x.detach().contiguous()
+    if world == 1:
+        return x, None
+    B = x.shape[0]
+    out = torch.empty(world * B, *x.shape[1:], device=x.device, dtype=x.dtype)
+    if dist.get_backend() == 'gloo':
+        work = dist.all_gather(list(out.view(world, B, *x.shape[1:]).unbind(0)), x, async_op=True)
+    else:
+        work = dist.all_gather_into_tensor(out, x, async_op=True)
+    return out, work
+
+
+def finish_gather(handle) -> torch.Tensor:
+    """The gathered [world*B, Dl] tensor, with the current stream ordered after the collective."""
+    out, work = handle
+    if work is not None:
+        work.wait()
+        if out.is_cuda:
+            out.record_stream(torch.cuda.current_stream(out.device))
+    return out
+
+
+def gather_latents(t_raw: torch.Tensor, i_raw: torch.Tensor, t_handle=None):
+    """[B, Dl] x 2 on each rank -> ([world*B, Dl], [world*B, Dl]) in rank order.  ``t_handle``:
+    the text latents' gather already started by ``start_gather`` (CTCLIP.encode)."""
     world, _ = world_rank()
     if world == 1:
         return t_raw.contiguous(), i_raw.contiguous()
+    if t_handle is not None:
+        ih = start_gather(i_raw)
+        return finish_gather(t_handle), finish_gather(ih)
     B, Dl = t_raw.shape
     both = torch.cat([t_raw, i_raw], 0).contiguous()
     gathered = torch.empty(world * 2 * B, Dl, device=both.device, dtype=both.dtype)

@@ -420,13 +420,8 @@ class VQPoolFn(torch.autograd.Function):
         C = embed.shape[-2]
         cb = embed.view(C, D)
         streams.join_aux(zf.device)     # the previous step's EMA update of the codebook
-        cb_b = state.codebook_bf16(cb)
-        ones = state.ones(D, zf.device)
-        xn_b = K.l2norm_scale_fwd(zb, 1, D, ones)
-        nt = (C + 63) // 64          # one (score, index) candidate per 64-code group
-        cand = torch.empty(zf.shape[0], nt, 2, device=zf.device, dtype=F32)
-        K.gemm_raw(zf.shape[0], C, D, xn_b, D, True, cb_b, D, True, cand, nt, act=K.ACT_ARGMAX)
-        idx, xn = K.vq_select(cand, zf, cb, want_xn=training)
+        idx, xn = vq_assign(zf, zb, cb, state, want_xn=training)
+        cb_b = state.codebook_bf16(cb)   # the mirror vq_assign scored against (cached)
         HW = geo.Hg * geo.Wg
         pooled, pooled_b = K.vq_pool(idx, cb, geo.B, geo.T, HW)
         tokens = K.vq_gather(idx, cb) if want_tokens else torch.empty(0, device=zf.device)
@@ -465,6 +460,22 @@ class VQPoolFn(torch.autograd.Function):
         if dtokens is not None and dtokens.numel():
             dz = dtokens.contiguous() if dz is None else dz + dtokens
         return dz, None, None, None, None, None, None, None, None
+
+
+def vq_assign(zf, zb, cb, state, want_xn=False):
+    """Cosine-codebook assignment (vector_quantize_pytorch cosine sim + argmax, ct_clip/ctvit.py:427):
+    bf16 MFMA distance GEMM over l2norm(zb) with a per-64-code-group (best, index, second-best)
+    epilogue, then the f32 re-score of every code within the bf16 error margin (vq.hip) -> the
+    exact f32 argmax of l2norm(zf) . cb^T.  Returns (idx int32 [M], l2norm(zf) f32 or None)."""
+    D = zf.shape[1]
+    C = cb.shape[0]
+    cb_b = state.codebook_bf16(cb)
+    xn_b = K.l2norm_scale_fwd(zb, 1, D, state.ones(D, zf.device))
+    nt = (C + 63) // 64
+    cand = torch.empty(zf.shape[0], nt, 2, device=zf.device, dtype=F32)
+    cand2 = torch.empty(zf.shape[0], nt, device=zf.device, dtype=F32)
+    K.gemm_raw(zf.shape[0], C, D, xn_b, D, True, cb_b, D, True, cand, nt, C2=cand2, ldc2=nt, act=K.ACT_ARGMAX)
+    return K.vq_select(cand, zf, cb, want_xn=want_xn, cand2=cand2)
 
 
 class VQState:
@@ -549,9 +560,9 @@ class ClipLossFn(torch.autograd.Function):
     same global loss and back-propagates its own rows (gradients are then SUM-reduced)."""
 
     @staticmethod
-    def forward(ctx, t_raw, i_raw, log_temp, impl=None):
+    def forward(ctx, t_raw, i_raw, log_temp, impl=None, t_gather=None):
         B = t_raw.shape[0]
-        tg, ig = dist_sync.gather_latents(t_raw, i_raw)
+        tg, ig = dist_sync.gather_latents(t_raw, i_raw, t_gather)
         # impl: the fused HIP loss (default); tests substitute a CPU restatement to exercise
         # the exchange logic under gloo
         loss, dt, di, dlt = (impl or K.clip_loss)(tg, ig, log_temp.reshape(1).contiguous())[:4]
@@ -565,7 +576,7 @@ class ClipLossFn(torch.autograd.Function):
         s = dloss.reshape(1)
         # log-temperature gradient: every rank holds the full global value -> scaled by 1/world so
         # the SUM all-reduce reproduces it once.
-        return dt * s, di * s, (dlt * s * ctx.scale).reshape(()), None
+        return dt * s, di * s, (dlt * s * ctx.scale).reshape(()), None, None
 
 
 # ----------------------------------------------------------------------------- BERT

@@ -412,12 +412,14 @@ def attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, *, L, H, D, nseq, scale, seq, bi
 
 
 # ----------------------------------------------------------------------------- VQ
-def vq_select(cand, x, codebook_f32, margin=2e-2, want_xn=True):
+def vq_select(cand, x, codebook_f32, margin=2e-2, want_xn=True, cand2=None):
+    """Exact f32 cosine argmax from the bf16 GEMM's per-group candidates (vq.hip); cand2 = the
+    groups' second-best scores (None: group winners only)."""
     rows, D = x.shape
     idx = torch.empty(rows, device=x.device, dtype=torch.int32)
     xn = torch.empty(rows, D, device=x.device, dtype=F32) if want_xn else None
-    call('ctclip_vq_select', ptr(cand), cand.shape[1], ptr(x), rows, D, ptr(codebook_f32), margin, ptr(idx), ptr(xn),
-         stream_ptr())
+    call('ctclip_vq_select', ptr(cand), ptr(cand2), cand.shape[1], ptr(x), rows, D, ptr(codebook_f32),
+         codebook_f32.shape[0], margin, ptr(idx), ptr(xn), stream_ptr())
     return idx, xn
 
 

@@ -213,10 +213,14 @@ int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream);
 
 /* ---------------------------------------------------------------- vector quantiser
  * vector_quantize_pytorch==1.1.2 cosine codebook (ct_clip/ctvit.py:187,421-427).
- * cand = float2[rows][ntiles] (score, index) from ctclip_gemm(act=3) over l2norm(x).codebook_bf16^T;
- * select re-scores in f32 every candidate within `margin` of the best -> exact f32 argmax. */
-int ctclip_vq_select(const float* cand, int32_t ntiles, const float* x, int64_t rows, int32_t D,
-                     const float* codebook, float margin, int32_t* idx, float* xn_out, void* stream);
+ * cand = float2[rows][ntiles] (score, index) and cand2 = float[rows][ntiles] (second-best score) of
+ * each 64-code group, from ctclip_gemm(act=3, C2 = cand2) over l2norm(x).codebook_bf16^T;
+ * ntiles = ceil(C / 64).  select re-scores in f32 (f32 x, f32 codebook [C][D]) every code whose bf16
+ * score can lie within `margin` of the best -- group winners, and whole groups whose second-best is
+ * within it -> the exact f32 argmax (first index on ties) for margin >= 2^-6 (bf16 scoring error
+ * bound, see vq.hip).  cand2 = NULL re-scores group winners only.  D % 4 == 0, D <= 4096. */
+int ctclip_vq_select(const float* cand, const float* cand2, int32_t ntiles, const float* x, int64_t rows, int32_t D,
+                     const float* codebook, int32_t C, float margin, int32_t* idx, float* xn_out, void* stream);
 /* pooled[b][hw][:] = mean_t codebook[idx[b][t*HW+hw]]   (ct_clip/ct_clip.py:724,740) */
 int ctclip_vq_pool(const int32_t* idx, const float* codebook, int64_t B, int32_t T, int32_t HW, int32_t D,
                    float* out, void* out_bf16, void* stream);

@@ -414,6 +414,36 @@ def zero_shot(sd, ids, mask, video, cfg: ClipConfig, force_ind=None):
     return probs, scores
 
 
+# ----------------------------------------------------------------------------- VQA vision features
+VFE_FALLBACK_DIM = 512
+# parity config of the extractor: base widths on a reduced 160 x 160 x 40 volume (4 x 8 x 8 tokens)
+VFE_VIT = ViTConfig(image_size=160, frames=40, spatial_depth=4, temporal_depth=1)
+
+
+def vision_features(sd, p, video, cfg: ViTConfig, proj, position_bias=False, trace=None):
+    """``VisionFeatureExtractor.forward`` (``ctpa_report/vqa_meditron.py:91-123``) on its intended
+    path.  As shipped, the reference's call ``enc_spatial_transformer(spatial_input)`` (``:107``)
+    omits ``video_shape``, PEG's assert (``ct_clip/attention.py:65``) raises and the forward returns
+    ``torch.randn`` (``:125-127``); the one repair restated here is passing
+    ``video_shape = (b, t, h, w)``.  No ``attn_bias`` (the reference call passes none;
+    ``position_bias=True`` adds the CPB bias of ``CTViT.encode``, ``ctvit.py:317``).  Then the mean
+    over every token (``adaptive_avg_pool3d(..., (1, 1, 1))``, ``:114-117``, over the token grid)
+    and ``feature_projector`` = Linear + LayerNorm + GELU(erf) (``:42-46``).
+    ``proj`` holds the ``feature_projector.*`` tensors; returns (b, feature_dim)."""
+    tokens = patch_embed(sd, p, video, cfg)                         # (b, t, h, w, d)
+    b, t, h, w, d = tokens.shape
+    x = tokens.reshape(b * t, h * w, d)                             # vqa_meditron.py:134-141
+    bias = cpb_forward(sd, p + 'spatial_rel_pos_bias.', h, w, cfg.cpb_layers) if position_bias else None
+    x = transformer_forward(sd, p + 'enc_spatial_transformer.', x, cfg.spatial_depth, cfg.heads,
+                            cfg.dim_head, (b, t, h, w), bias)
+    pooled = x.reshape(b, t * h * w, d).mean(dim=1)
+    if trace is not None:
+        trace.update(patch_emb=tokens, spatial_out=x.reshape(b, t, h, w, d), pooled=pooled)
+    y = F.linear(pooled, proj['feature_projector.0.weight'], proj['feature_projector.0.bias'])
+    y = F.layer_norm(y, y.shape[-1:], proj['feature_projector.1.weight'], proj['feature_projector.1.bias'], 1e-5)
+    return F.gelu(y)
+
+
 # ----------------------------------------------------------------------------- weights recipe
 def trainable_prefixes():
     """``ct_clip/fine_tuning_ctclip.py:6-14``: only visual_transformer and text_transformer

@@ -183,3 +183,17 @@ def make_text(batch, length, vocab, seed=4321, ragged=False):
         ids[b, n:] = 0
         mask[b, n:] = 0
     return ids, mask
+
+
+def make_projector(input_dim=512, feature_dim=512, seed=0):
+    """VisionFeatureExtractor.feature_projector (ctpa_report/vqa_meditron.py:42-46):
+    Linear(input_dim, feature_dim) + LayerNorm(feature_dim) (+ GELU), name-seeded like the rest."""
+    keys = OrderedDict([('feature_projector.0.weight', ('lin', (feature_dim, input_dim))),
+                        ('feature_projector.0.bias', ('bias', (feature_dim,))),
+                        ('feature_projector.1.weight', ('ln_w', (feature_dim,))),
+                        ('feature_projector.1.bias', ('ln_b', (feature_dim,)))])
+    sd = OrderedDict()
+    for key, (kind, shape) in keys.items():
+        g = torch.Generator().manual_seed((zlib.crc32(key.encode()) ^ seed) & 0x7FFFFFFF)
+        sd[key] = _make(kind, shape, g).to(torch.float32).contiguous()
+    return sd

@@ -30,6 +30,7 @@ import transformers  # noqa: E402  (must import before the torchvision stub)
 from transformers import BertModel, BertConfig as HFBertConfig  # noqa: E402
 import torch  # noqa: E402
 import torch.nn as nn  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
 from safetensors.torch import save_file  # noqa: E402
 
 from oracle import ctclip_oracle as O  # noqa: E402
@@ -267,14 +268,57 @@ def run_recon(V, C):
     print('recon loss', float(loss), 'grads', sum(k.startswith('grad.') for k in out), '->', path)
 
 
+def run_vfe(V, C):
+    """VisionFeatureExtractor fixture (configs[4], ctpa_report/vqa_meditron.py:26-131): base widths
+    on a reduced volume (160 x 160 x 40 -> 4 x 8 x 8 tokens, 4 spatial layers).  The reference's own
+    modules run the extractor's forward (:91-123) with the one repair it needs -- video_shape for
+    the spatial transformer, whose absence makes PEG raise and the forward return torch.randn --
+    and no attn_bias, as its call has none.  vqa_meditron.py itself cannot be imported offline (it
+    loads the CT-CLIP_v2.pt checkpoint at import through ct_clip.pretrained_model and needs peft),
+    so its projector -- nn.Sequential(Linear, LayerNorm, GELU) (:42-46) -- is built here as torch
+    modules with the oracle/weights.make_projector recipe."""
+    vit_cfg = O.VFE_VIT
+    cfg = O.ClipConfig(vit=vit_cfg, bert=O.TINY.bert, dim_latent=512)
+    clip = build_reference(cfg, V, C)
+    sd = W.make_state_dict(cfg)
+    clip.load_state_dict(sd, strict=True)
+    vt = clip.visual_transformer
+    vt.eval()
+    proj = W.make_projector(512, 512)
+    fp = nn.Sequential(nn.Linear(512, 512), nn.LayerNorm(512), nn.GELU())
+    fp.load_state_dict({k[len('feature_projector.'):]: v for k, v in proj.items()}, strict=True)
+    hu = W.make_hu(2, vit_cfg, seed=31)
+    x = O.normalize_hu(hu)
+    with torch.no_grad():
+        pe = vt.to_patch_emb(x)                                    # vqa_meditron.py:101
+        b, t, h, w, d = pe.shape
+        si = pe.reshape(-1, h * w, d)                              # its local rearrange, :134-141
+        sf = vt.enc_spatial_transformer(si, video_shape=(b, t, h, w))   # :107 + video_shape
+        pooled = F.adaptive_avg_pool3d(sf.reshape(b, t, h, w, d).permute(0, 4, 1, 2, 3), (1, 1, 1)).reshape(b, d)
+        feats = fp(pooled)                                         # :120
+    # input: W.make_hu(2, vit, seed=31), regenerated by the tests
+    out = {'out.patch_emb': pe, 'out.spatial_out': sf.reshape(b, t, h, w, d), 'out.pooled': pooled,
+           'out.features': feats}
+    path = os.path.join(HERE, 'golden_vfe.safetensors')
+    save_file({k: v.contiguous() for k, v in out.items()}, path,
+              metadata={'generator': 'tests/golden/make_golden.py --vfe',
+                        'reference': 'sharonct/CTPA-CLIP @ 2025-06-20 (ctpa_report/vqa_meditron.py:91-123, '
+                                     'ct_clip/ctvit.py:169-174, ct_clip/attention.py:280-333)'})
+    print('vfe features', feats.shape, float(feats.abs().mean()), '->', path)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--base', action='store_true', help='also write the base-config B=2 fixture')
     ap.add_argument('--zero-shot', action='store_true', help='only write the zero-shot fixture')
     ap.add_argument('--recon', action='store_true', help='only write the reconstruction fixture')
+    ap.add_argument('--vfe', action='store_true', help='only write the VisionFeatureExtractor fixture')
     args = ap.parse_args()
     torch.set_num_threads(os.cpu_count())
     A, V, C = import_reference()
+    if args.vfe:
+        run_vfe(V, C)
+        return
     if args.zero_shot:
         run_zero_shot(V, C)
         return

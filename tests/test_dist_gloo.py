@@ -100,6 +100,20 @@ def _worker(rank, port, out_dir):
         assert torch.equal(bins, ref_bins)
         torch.testing.assert_close(esum, ref_esum)
 
+        # the text latents' gather started early (CTCLIP.encode, text stream) gives the same step
+        wt.grad = None
+        wi.grad = None
+        lt.grad = None
+        t_loc = xt[rows] @ wt
+        h = dist_sync.start_gather(t_loc)
+        loss2 = ClipLossFn.apply(t_loc, xi[rows] @ wi, lt, oracle_clip_loss, h)
+        loss2.backward()
+        assert torch.equal(loss2.detach(), loss.detach())
+        for prm in (wt, wi, lt):
+            dist.all_reduce(prm.grad)
+        torch.testing.assert_close(wt.grad, gwt, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(lt.grad, glt, rtol=1e-5, atol=1e-6)
+
         # gathered latents arrive in rank order
         tg, ig = dist_sync.gather_latents(torch.full((B, DL), float(rank)), torch.full((B, DL), 10.0 + rank))
         assert torch.equal(tg[:, 0], torch.arange(WORLD).repeat_interleave(B).float())

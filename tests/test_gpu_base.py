@@ -1,0 +1,236 @@
+"""configs[1] at full size on the GPU: the base CT-CLIP (480x480x240 volumes -> 24^3 tokens, 4+4
+ViT layers, VQ 8192, BERT-base at 128 tokens) against the reference's OWN base-config output,
+tests/golden/golden_base_b2.safetensors (tests/golden/make_golden.py --base ran
+ct_clip/ct_clip.py:614-901 and ct_clip/ctvit.py:377-436 on these inputs and weights).
+
+* stage checks: patch-embed / spatial / temporal head rows and per-volume token sums, CPB rows;
+* the SURVEY 8(c) vector-quantiser contract, split in two:
+  - the VQ op itself (bf16 MFMA candidates + f32 re-score, vq.hip) on the oracle's own f32
+    pre-VQ tokens must return the oracle's argmax everywhere except f32-level ties (top-2 cosine
+    margin < 1e-6);
+  - end to end, every index the free-running HIP path picks differently from the reference must
+    be explained by that token's own pre-VQ error: the oracle's score gap between its winner and
+    the HIP choice is at most 2 * |l2norm(z_hip) - l2norm(z_oracle)| (both scores move by at most
+    that much, Cauchy-Schwarz with unit codes).  Counts above / below the 1e-6 margin are printed;
+* loss free-running against the fixture, logits / loss with the oracle forced onto the HIP indices
+  (< 1e-3, the north-star bf16 tolerance); latents and free-running logits reported with their
+  measured bounds;
+* B = 8 (the bench workload) through train_step: finite, loss ~ ln 8 at init, weights move.
+The oracle (fp32 CPU) runs the B = 2 forward here; it is pinned to the same fixture by
+tests/test_oracle_golden.py::test_base_b2_matches_reference."""
+import math
+import os
+import types
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import ctclip_oracle as O
+from oracle import weights as W
+
+pytestmark = pytest.mark.gpu
+
+CFG = O.BASE
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.fixture(scope='module')
+def base():
+    from safetensors.torch import load_file
+    from test_gpu_model import build
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    g = load_file(os.path.join(HERE, 'golden', 'golden_base_b2.safetensors'))
+    sd = W.make_state_dict(CFG)
+    model = build(CFG)
+    hu = W.make_hu(2, CFG.vit)
+    ids, mask = W.make_text(2, 128, CFG.bert.vocab_size)
+    trace = {}
+    with torch.no_grad():
+        ref = O.ctclip_forward(sd, ids, mask, O.normalize_hu(hu), CFG, training=False, trace=trace)
+    text = types.SimpleNamespace(input_ids=ids.cuda(), attention_mask=mask.cuda())
+    return dict(g=g, sd=sd, model=model, hu=hu, ids=ids, mask=mask, text=text, ref=ref, trace=trace)
+
+
+def test_oracle_full_size_matches_fixture(base):
+    """The checker itself at full size: the oracle's indices / latents / loss vs the reference's."""
+    g, ref = base['g'], base['ref']
+    mism = (ref['indices'].reshape(-1).to(torch.int32) != g['out.vq_indices'].reshape(-1)).sum().item()
+    print('oracle vs reference VQ index mismatches:', mism, 'of', g['out.vq_indices'].numel())
+    assert mism <= 3
+    assert (ref['text_latents'] - g['out.text_latents']).abs().max().item() < 1e-4
+    assert abs(ref['loss'].item() - g['out.loss'].item()) < 1e-4
+
+
+def test_stages_full_size(base):
+    g, model = base['g'], base['model']
+    vt = model.visual_transformer
+    model.eval()
+    tr = {}
+    with torch.no_grad():
+        zf, zb, geo = vt.encode_tokens(base['hu'].cuda(), trace=tr)
+        cpb = vt.spatial_rel_pos_bias.dense(24, 24)
+    torch.cuda.synchronize()
+    D = CFG.vit.dim
+    pe, sp = tr['patch_emb'], tr['spatial_out']
+    # temporal head rows are in the reference's '(b h w) t d' order: row r = (hw = r // 24, t = r % 24)
+    r = torch.arange(256)
+    trow = (r % 24) * 576 + r // 24
+    checks = {
+        'patch_emb_head': (pe[:256], g['out.patch_emb_head'], 1e-2),
+        'patch_emb_sum': (pe.view(2, -1, D).double().sum(1), g['out.patch_emb_sum'], 1e-2),
+        'spatial_out_head': (sp[:256], g['out.spatial_out_head'], 2e-2),
+        'temporal_out_head': (zf[trow.cuda()], g['out.temporal_out_head'], 3e-2),
+        'temporal_out_sum': (zf.view(2, -1, D).double().sum(1), g['out.temporal_out_sum'], 3e-2),
+        'cpb_rows': (cpb[:, :4, :], g['out.cpb_rows'], 1e-5),
+    }
+    bad = []
+    for k, (a, b, tol) in checks.items():
+        e = rel(a, b)
+        print(f'{k}: rel err {e:.3e} (tol {tol})')
+        if not e < tol:
+            bad.append((k, e))
+    assert not bad, bad
+    # the patch / token index maps are exact: the f32 [-1, 1] video takes the int16 path bit-for-bit
+    with torch.no_grad():
+        tr2 = {}
+        vt.encode_tokens(O.normalize_hu(base['hu']).cuda(), trace=tr2)
+    assert torch.equal(tr2['patch_emb'], pe)
+    base['zf'], base['zb'] = zf, zb
+    model.train()
+
+
+def _oracle_tokens(base):
+    t = base['trace']['temporal_out']                  # (b, t, h, w, d) = canonical HIP row order
+    return t.reshape(-1, CFG.vit.dim).contiguous()
+
+
+def test_vq_op_exact_on_oracle_tokens(base):
+    """SURVEY 8(c) for the quantiser op: same f32 tokens in -> the oracle's argmax out, except
+    f32 ties (top-2 margin < 1e-6)."""
+    from ctclip_mi355x import functional as Fn
+    from ctclip_mi355x import kernels as K
+    vt = base['model'].visual_transformer
+    zo = _oracle_tokens(base)
+    cb = vt.vq._codebook.embed.view(-1, CFG.vit.dim)
+    with torch.no_grad():
+        zf = zo.cuda()
+        idx, _ = Fn.vq_assign(zf, K.cast_bf16(zf), cb, vt.vq.state)
+    torch.cuda.synchronize()
+    so = F.normalize(zo, dim=-1) @ base['sd']['visual_transformer.vq._codebook.embed'][0].t()
+    top2 = so.topk(2, dim=1)
+    oi = top2.indices[:, 0]
+    margin = top2.values[:, 0] - top2.values[:, 1]
+    diff = idx.cpu().long() != oi
+    print(f'VQ op on oracle tokens: {diff.sum().item()} mismatches of {diff.numel()}; '
+          f'{(margin < 1e-6).sum().item()} oracle rows with top-2 margin < 1e-6; '
+          f'min margin {margin.min().item():.3e}')
+    assert (diff & (margin >= 1e-6)).sum().item() == 0
+
+
+def test_vq_free_running_contract(base):
+    """End to end: every HIP index that differs from the reference's is a near-tie explained by
+    that token's measured pre-VQ error (see module docstring)."""
+    g, sd = base['g'], base['sd']
+    if 'zf' not in base:
+        pytest.skip('needs test_stages_full_size')
+    from ctclip_mi355x import functional as Fn
+    vt = base['model'].visual_transformer
+    cb = vt.vq._codebook.embed.view(-1, CFG.vit.dim)
+    with torch.no_grad():
+        idx, _ = Fn.vq_assign(base['zf'], base['zb'], cb, vt.vq.state)
+    idx = idx.cpu().long()
+    gi = g['out.vq_indices'].reshape(-1).long()
+    diff = (idx != gi).nonzero().flatten()
+    zo = _oracle_tokens(base)
+    xo = F.normalize(zo[diff], dim=-1)
+    xh = F.normalize(base['zf'][diff.cuda()].cpu(), dim=-1)
+    E = sd['visual_transformer.vq._codebook.embed'][0]
+    so = xo @ E.t()
+    gap = so.gather(1, gi[diff][:, None]).squeeze(1) - so.gather(1, idx[diff][:, None]).squeeze(1)
+    bound = 2 * (xh - xo).norm(dim=1)
+    tok_err = (F.normalize(base['zf'].cpu(), dim=-1) - F.normalize(zo, dim=-1)).norm(dim=1)
+    n = gi.numel()
+    print(f'free-running VQ: {diff.numel()} of {n} indices differ ({100 * diff.numel() / n:.2f} %); '
+          f'oracle margin < 1e-6: {(gap < 1e-6).sum().item()}, above: {(gap >= 1e-6).sum().item()}; '
+          f'max gap {gap.max().item() if diff.numel() else 0:.3e}; '
+          f'pre-VQ |dxn| median {tok_err.median().item():.3e} max {tok_err.max().item():.3e}')
+    unexplained = (gap > bound + 1e-6).sum().item()
+    assert unexplained == 0, unexplained
+    assert diff.numel() < 0.05 * n
+
+
+def test_latents_and_loss_full_size(base):
+    g, sd, model, text = base['g'], base['sd'], base['model'], base['text']
+    model.eval()
+    with torch.no_grad():
+        _, _, t_raw, i_raw = model.encode(text, base['hu'].cuda())
+        idx = model.visual_transformer.vq.state.last_indices.cpu()
+        loss = model(text, base['hu'].cuda(), return_loss=True)
+    torch.cuda.synchronize()
+    tl, il = F.normalize(t_raw, dim=-1).cpu(), F.normalize(i_raw, dim=-1).cpu()
+    e = math.e            # temperature.exp() at init (ct_clip.py:568,796)
+    logits = tl @ il.t() * e
+    g_logits = g['out.text_latents'] @ g['out.image_latents'].t() * e
+    dt = (tl - g['out.text_latents']).abs().max().item()
+    di = (il - g['out.image_latents']).abs().max().item()
+    dlog = (logits - g_logits).abs().max().item()
+    dl = abs(loss.item() - g['out.loss'].item())
+    print(f'free-running vs reference fixture: text latents {dt:.2e}, image latents {di:.2e}, logits {dlog:.2e}, '
+          f'loss {loss.item():.6f} vs {g["out.loss"].item():.6f} (|d| {dl:.2e})')
+    # text latents: 12 bf16 BERT-base layers (1.4e-3 measured); the loss stays within the north-star
+    # 1e-3 free-running (6.2e-4 measured); the image latents / logits carry the ~2 % near-tie VQ
+    # flips (2.5e-2 / 5.3e-2 measured): a flipped token swaps in a different codebook row, so the
+    # free-running logits cannot meet 1e-3 from bf16 pre-VQ tokens (1e-2 relative) -- they do once
+    # the indices agree (forced, below)
+    assert dt < 2.5e-3
+    assert dl < 1e-3
+    assert di < 0.1 and dlog < 0.15
+    with torch.no_grad():
+        forced = O.ctclip_forward(sd, base['ids'], base['mask'], O.normalize_hu(base['hu']), CFG,
+                                  training=False, force_ind=idx)
+    fi = (il - forced['image_latents']).abs().max().item()
+    f_logits = forced['text_latents'] @ forced['image_latents'].t() * e
+    flog = (logits - f_logits).abs().max().item()
+    fl = abs(loss.item() - forced['loss'].item())
+    print(f'oracle forced onto the HIP indices: image latents {fi:.2e}, logits {flog:.2e}, loss |d| {fl:.2e}')
+    assert fi < 1e-3
+    assert fl < 1e-3
+    # logits = e * text . image: the text side carries BERT-base's bf16-weight rounding (1.4e-3 on
+    # the latents; tools/bert_precision.py attributes ~70 % of it to the bf16 weights)
+    assert flog < 1.5e-3
+    model.train()
+
+
+def test_train_step_batch8_full_size(base):
+    """configs[1] itself (B = 8): one full train step -- finite loss near ln 8 at init, finite
+    non-zero gradient norm, parameters of both towers updated."""
+    from ctclip_mi355x.trainer import CTClipTrainer
+    model = base['model']
+    for k in ('zf', 'zb'):
+        base.pop(k, None)
+    dev = torch.device('cuda')
+    gen = torch.Generator(device=dev).manual_seed(1234)
+    hu = torch.randint(-1200, 1201, (8, 1, 240, 480, 480), generator=gen, device=dev,
+                       dtype=torch.int32).to(torch.int16)
+    ids = torch.randint(5, CFG.bert.vocab_size, (8, 128), generator=gen, device=dev)
+    ids[:, 0], ids[:, -1] = 2, 3
+    text = types.SimpleNamespace(input_ids=ids, attention_mask=torch.ones_like(ids))
+    model.train()
+    tr = CTClipTrainer(model)
+    p_img = model.visual_transformer.enc_temporal_transformer.layers[3][3][1].weight
+    p_txt = model.text_transformer.encoder.layer[11].output.dense.weight
+    b_img, b_txt = p_img.detach().clone(), p_txt.detach().clone()
+    loss = tr.train_step(text, hu)
+    torch.cuda.synchronize()
+    print(f'B=8 full-size train step: loss {loss.item():.5f} (ln 8 = {math.log(8):.5f}), '
+          f'grad norm {tr.norm[0].item():.4e}')
+    assert torch.isfinite(loss) and abs(loss.item() - math.log(8)) < 0.1
+    assert math.isfinite(tr.norm[0].item()) and tr.norm[0].item() > 0
+    assert not torch.equal(b_img, p_img.detach()) and not torch.equal(b_txt, p_txt.detach())
+    assert model.visual_transformer.vq.state.last_indices.numel() == 8 * 24 ** 3

@@ -145,3 +145,23 @@ def test_recon_matches_reference():
             _close(v.grad, g['grad.' + k], 2e-4)
             n += 1
     assert n >= 40, n
+
+
+def test_vision_features_match_reference():
+    """VisionFeatureExtractor (configs[4], ctpa_report/vqa_meditron.py:91-123): the oracle's
+    vision_features against the reference's own to_patch_emb / enc_spatial_transformer (with the
+    video_shape repair) + pooling + projector (golden_vfe, tests/golden/make_golden.py --vfe)."""
+    from safetensors.torch import load_file
+    import os
+    g = load_file(os.path.join(os.path.dirname(__file__), 'golden', 'golden_vfe.safetensors'))
+    vit = O.VFE_VIT
+    sd = W.make_state_dict(O.ClipConfig(vit=vit, bert=O.TINY.bert, dim_latent=512))
+    trace = {}
+    with torch.no_grad():
+        f = O.vision_features(sd, 'visual_transformer.', O.normalize_hu(W.make_hu(2, vit, seed=31)), vit,
+                              W.make_projector(), trace=trace)
+    _close(trace['patch_emb'], g['out.patch_emb'], 1e-5)
+    _close(trace['spatial_out'], g['out.spatial_out'], 1e-5)
+    _close(trace['pooled'], g['out.pooled'], 1e-5)
+    _close(f, g['out.features'], 1e-5)
+    assert f.shape == (2, 512)
