@@ -2,8 +2,10 @@
 (the reference's text tower, ct_clip/pretrained_model.py:9, called at ct_clip/ct_clip.py:685-686).
 
 ``forward(input_ids, attention_mask)`` returns a tuple whose [0] is last_hidden_state, like
-the HF model output indexed by the reference (``text_embeddings[0]``).  Dropout is not
-applied.  The pooler's parameters are kept for checkpoint
+the HF model output indexed by the reference (``text_embeddings[0]``).  In train mode HF's
+dropout (p = 0.1) is applied at its four sites -- embeddings, attention probabilities (inside
+the fused attention kernels), attention output and FF output -- with hash masks regenerated in
+the backward.  The pooler's parameters are kept for checkpoint
 compatibility; the pooler output is unused by CT-CLIP and is not computed.
 """
 from __future__ import annotations

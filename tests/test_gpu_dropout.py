@@ -125,3 +125,68 @@ def test_bert_train_step_with_dropout(K):
     y1[:, 0].float().square().sum().backward()
     g = m.encoder.layer[0].attention.self.query.weight.grad
     assert g is not None and torch.isfinite(g).all() and g.abs().sum().item() > 0
+
+
+def test_bert_layer_dropout_grads_match_torch(K):
+    """BertLayerFn with all three in-layer dropout sites on (attention probabilities, attention
+    output, FF output; p = 0.1): output, dx and every weight / bias / LN gradient against torch
+    autograd in fp32 on the same masked graph, masks regenerated from the per-site seeds
+    (transformers BertLayer, the reference's text tower, ct_clip/ct_clip.py:685-686)."""
+    from ctclip_mi355x import functional as Fn
+    torch.manual_seed(3)
+    B, L, H, D, I = 2, 64, 12, 64, 3072
+    Hd = H * D
+    p, s_attn, s_out1, s_out2 = 0.1, 0x1111_2222_3333_4444, 0x5555_6666_7777_8888, 0x0123_4567_89ab_cdef
+    eps = 1e-12
+
+    def prm(*shape, scale=0.03):
+        return torch.nn.Parameter((torch.randn(*shape, device=dev) * scale).bfloat16().float())
+
+    Wq, Wk, Wv, Wo = prm(Hd, Hd), prm(Hd, Hd), prm(Hd, Hd), prm(Hd, Hd)
+    bq, bk, bv, bo = prm(Hd), prm(Hd), prm(Hd), prm(Hd)
+    Wi, bi, Wout, bout = prm(I, Hd), prm(I), prm(Hd, I), prm(Hd)
+    ln1_w, ln1_b = torch.nn.Parameter(1 + 0.1 * torch.randn(Hd, device=dev)), prm(Hd)
+    ln2_w, ln2_b = torch.nn.Parameter(1 + 0.1 * torch.randn(Hd, device=dev)), prm(Hd)
+    params = [Wq, bq, Wk, bk, Wv, bv, Wo, bo, ln1_w, ln1_b, Wi, bi, Wout, bout, ln2_w, ln2_b]
+    x = torch.randn(B * L, Hd, device=dev).bfloat16().float().requires_grad_(True)
+    lens = [64, 41]
+    kmask = torch.zeros(B, L, dtype=torch.int32, device=dev)
+    for b, n in enumerate(lens):
+        kmask[b, :n] = 1
+    R = torch.randn(B * L, Hd, device=dev)
+
+    yf, _ = Fn.BertLayerFn.apply(x, x.detach().bfloat16(), kmask, B, L, H, eps, *params,
+                                 (p, p, s_attn, s_out1, s_out2))
+    (yf * R).sum().backward()
+    got = [x.grad.clone()] + [q.grad.clone() for q in params]
+    for t in [x] + params:
+        t.grad = None
+
+    # torch fp32 reference on the same masks
+    dscale = float(np.float32(1.0) / (np.float32(1.0) - np.float32(p)))
+    n_h = torch.arange(B * L * Hd, device=dev)
+    keep1 = keep_mask(n_h, s_out1, p).view(B * L, Hd)
+    keep2 = keep_mask(n_h, s_out2, p).view(B * L, Hd)
+    idx = (((torch.arange(B, device=dev)[:, None, None, None] * H + torch.arange(H, device=dev)[None, :, None, None])
+            * L + torch.arange(L, device=dev)[None, None, :, None]) * L + torch.arange(L, device=dev)[None, None, None, :])
+    keepa = keep_mask(idx, s_attn, p)
+    heads = lambda t: t.view(B, L, H, D).transpose(1, 2)  # noqa: E731
+    q, k, v = heads(x @ Wq.t() + bq), heads(x @ Wk.t() + bk), heads(x @ Wv.t() + bv)
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(D)
+    s = s.masked_fill(kmask[:, None, None, :] == 0, float('-inf'))
+    P = torch.softmax(s, -1) * keepa * dscale
+    ctxv = (P @ v).transpose(1, 2).reshape(B * L, Hd)
+    a = (ctxv @ Wo.t() + bo) * keep1 * dscale + x
+    x1 = torch.nn.functional.layer_norm(a, (Hd,), ln1_w, ln1_b, eps)
+    h = torch.nn.functional.gelu(x1 @ Wi.t() + bi)
+    b2 = (h @ Wout.t() + bout) * keep2 * dscale + x1
+    y = torch.nn.functional.layer_norm(b2, (Hd,), ln2_w, ln2_b, eps)
+    (y * R).sum().backward()
+    ref = [x.grad] + [q.grad for q in params]
+    assert rel(yf, y.detach()) < 2e-2
+    names = ['x', 'Wq', 'bq', 'Wk', 'bk', 'Wv', 'bv', 'Wo', 'bo', 'ln1_w', 'ln1_b', 'Wi', 'bi', 'Wout', 'bout',
+             'ln2_w', 'ln2_b']
+    errs = {n: rel(g_, r_) for n, g_, r_ in zip(names, got, ref)}
+    print('BertLayerFn dropout grads rel err: ' + ', '.join(f'{n} {e:.1e}' for n, e in errs.items()))
+    for n, e in errs.items():
+        assert e < 5e-2, (n, e)
