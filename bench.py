@@ -228,17 +228,22 @@ def main():
         tflops = ff1['flops'] / (ff1['avg_ms'] * 1e-3) / 1e12
         M = args.batch * 24 * 24 * 24
         algo_bytes = 2 * (M * 512 + 2816 * 512 + M * (2816 + 1408))   # A + W1 + h + GEGLU(h), bf16
-        traffic, traffic_src = None, None
-        pmc = os.path.join(REPO, 'profiles', 'r01_ff1_pmc.json')
+        # counter record of the SAME kernel (tools/pmc_gemm.sh ff1 -> tools/pmc_gemm_json.py): used only
+        # when its kernel name matches the one reported here
+        traffic, traffic_src, mfma_busy = None, None, None
+        pmc = os.path.join(REPO, 'profiles', 'r02_pmc_ff1.json')
         if args.batch == 8 and os.path.exists(pmc):
             rec = json.load(open(pmc))
-            traffic = round(rec['traffic_bytes_per_launch'] / 1e9, 4)
-            traffic_src = 'profiles/r01_ff1_pmc.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, GB per launch)'
+            if any('gemm8p_kernel<true, true, 2>' in k for k in rec.get('kernel', [])):
+                traffic = round(rec['traffic_bytes_per_launch'] / 1e9, 4)
+                mfma_busy = round(rec['mfma_busy'], 4)
+                traffic_src = ('profiles/r02_pmc_ff1.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch; '
+                               'mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / SIMD-cycles)')
         result['roofline'] = {
             'kernel': 'g256::gemm8p_kernel<true,true,2> FF1 (LN-out x W1^T, GEGLU epilogue)',
             'bound': 'mfma', 'achieved': round(tflops, 1), 'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
             'frac': round(tflops / PEAK_BF16_TFLOPS, 4), 'traffic': traffic, 'traffic_unit': 'GB',
-            'traffic_source': traffic_src, 'algorithmic_bytes': algo_bytes,
+            'traffic_source': traffic_src, 'mfma_busy': mfma_busy, 'algorithmic_bytes': algo_bytes,
             'hbm_frac': round(algo_bytes / (ff1['avg_ms'] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
             'avg_launch_ms': round(ff1['avg_ms'], 4), 'flops_per_launch': ff1['flops'],
             'launches': ff1['launches']}

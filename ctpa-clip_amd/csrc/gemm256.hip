@@ -448,6 +448,19 @@ __device__ __forceinline__ u32x4 pair_swap(const float* x4, const float* y4) {
 }
 __device__ __forceinline__ int pair_coff(int g) { return ((g & 1) ? 16 : 0) + ((g & 2) ? 8 : 0); }
 
+// 16-B epilogue store; CTCLIP_EPI_SC1 (A/B build): write-through sc1, which drops the line from
+// the XCD's L2 instead of keeping it (MI355X_MICROARCH.md, store flavours), so the output stream
+// does not evict the operand panels that the XCD's other tiles re-read
+__device__ __forceinline__ void st16(void* p, u32x4 d) {
+#ifdef CTCLIP_EPI_SC1
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const v4u dv = {d.x, d.y, d.z, d.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(dv) : "memory");
+#else
+  *(u32x4*)p = d;
+#endif
+}
+
 // store one row's 4 j-blocks x 4 cols as bf16; rowp = row base at the wave's first column c0
 __device__ __forceinline__ void store_row_bf16(u16* rowp, const float (&v)[4][4], int g, bool ok, int64_t c0,
                                                int64_t N) {
@@ -455,7 +468,7 @@ __device__ __forceinline__ void store_row_bf16(u16* rowp, const float (&v)[4][4]
   for (int jp = 0; jp < 2; ++jp) {
     const u32x4 d = pair_swap(v[2 * jp], v[2 * jp + 1]);
     const int coff = 32 * jp + pair_coff(g);
-    if (ok && c0 + coff < N) *(u32x4*)(rowp + coff) = d;
+    if (ok && c0 + coff < N) st16(rowp + coff, d);
   }
 }
 
@@ -534,7 +547,7 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
           gg[j][r] = gelu_erf(gb) * xb;
         }
       const u32x4 d = pair_swap(gg[0], gg[1]);
-      if (rok && wcol0 < p.N) *(u32x4*)(p.C2 + bidx * p.sC2 + gm * p.ldc2 + (wcol0 >> 1) + pair_coff(g)) = d;
+      if (rok && wcol0 < p.N) st16(p.C2 + bidx * p.sC2 + gm * p.ldc2 + (wcol0 >> 1) + pair_coff(g), d);
       continue;
     }
     if constexpr (MODE != 0) continue;
@@ -657,8 +670,8 @@ __device__ __forceinline__ void epilogue_geglu_bwd(const P& p, f32x4 (&acc)[8][4
       const int64_t t = t0 + jp;
       if (gm < p.M && t * 32 < p.N) {
         u16* dp = db + gm * p.ldc + t * 64 + co;
-        *(u32x4*)dp = pack8(ox);
-        *(u32x4*)(dp + 32) = pack8(og);
+        st16(dp, pack8(ox));
+        st16(dp + 32, pack8(og));
       }
     }
   }
@@ -697,6 +710,20 @@ __device__ __forceinline__ Tile tile_at(const P& p, int lin, int gx, int gy, int
   t.nk = (kend > t.kbeg && !(p.debug & 2)) ? (int)((kend - t.kbeg) / p8::BKK) : 0;
   return t;
 }
+
+#ifdef CTCLIP_GEMM_STAMPS
+// diagnostic build only (tools/gemm_stamps.py): per (workgroup, tile) s_memtime stamps of thread 0
+// (0 tile start, 1 after the first K-tile, 2 after the second, 3 after the last MFMA + barrier,
+// 4 after the epilogue's stores are issued) and the tile start in s_memrealtime (5, chip-wide)
+__device__ unsigned long long g_stamps[256][32][6];
+#define STAMP(k, v)                                                                        \
+  do {                                                                                     \
+    const unsigned long long t_ = (v);                                                     \
+    if (threadIdx.x == 0 && tcount < 32) g_stamps[blockIdx.x][tcount][k] = t_;             \
+  } while (0)
+#else
+#define STAMP(k, v) do { } while (0)
+#endif
 
 template <bool AK, bool BKC, int EP>
 __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
@@ -790,11 +817,16 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
   stage(A0, 1); stage(B0, 1);
   wait_ahead(T.nk > 1);
 
+  int tcount = 0;
+  (void)tcount;
   while (true) {
     const int nk = T.nk;
+    STAMP(0, __builtin_amdgcn_s_memtime());
+    STAMP(5, __builtin_amdgcn_s_memrealtime());
     bar();
     if (wr == 1) bar();   // the stagger: waves 4-7 run one barrier behind
     for (int i = 0; 2 * i < nk; ++i) {
+      if (i == 1) STAMP(2, __builtin_amdgcn_s_memtime());
       const int te = 2 * i, to = 2 * i + 1;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -823,6 +855,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
     }
     if (wr == 0) bar();   // balance the stagger barrier
     __syncthreads();      // every wave's last fragment reads done before LDS is refilled / reused
+    STAMP(3, __builtin_amdgcn_s_memtime());
     lin += lstride;
     const bool more = lin < ntiles;
     if (more) {
@@ -845,6 +878,8 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
       // staging in buffer O and beyond (the next tile's tile 0 is landing in E)
       epilogue(p, acc, smem + TILEB, w, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
     }
+    STAMP(4, __builtin_amdgcn_s_memtime());
+    ++tcount;
     if (!more) break;
     T = tile_at(p, lin, gx, gy, ntiles);
 #pragma unroll
@@ -996,3 +1031,15 @@ extern "C" int ctclip_gemm_set_variant(int v) {
   if (v == 1 || v == 2 || v == 8) g256::g_variant = v;
   return old;
 }
+
+#ifdef CTCLIP_GEMM_STAMPS
+// diagnostic: copy the stamp buffer (256 x 32 x 6 u64) to host memory (and clear it)
+extern "C" int ctclip_gemm_stamps(void* host, int clear) {
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g256::g_stamps), sizeof(g256::g_stamps), 0, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && clear) {
+    static unsigned long long zero[256 * 32 * 6];
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g256::g_stamps), zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+  }
+  return (int)e;
+}
+#endif

@@ -189,4 +189,8 @@ def test_bert_layer_dropout_grads_match_torch(K):
     errs = {n: rel(g_, r_) for n, g_, r_ in zip(names, got, ref)}
     print('BertLayerFn dropout grads rel err: ' + ', '.join(f'{n} {e:.1e}' for n, e in errs.items()))
     for n, e in errs.items():
+        if n == 'bk':    # exactly 0 in exact arithmetic (softmax is shift-invariant per query row)
+            continue
         assert e < 5e-2, (n, e)
+    # the key bias gradient: both sides are rounding noise around 0, far below the query bias's
+    assert got[names.index("bk")].norm() < 3e-2 * got[names.index("bq")].norm()

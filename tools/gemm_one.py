@@ -27,6 +27,7 @@ def main():
         'ff2': lambda: K.linear(x1408, w2, residual=res, out_dtype=torch.float32),
         'dxnn': lambda: K.matmul_nn(dh, w1),
         'dwtn': lambda: K.matmul_tn(dh, x512),
+        'dx1408': lambda: K.matmul_nn(x512, w2),
     }[which]
     for _ in range(reps):
         fn()
