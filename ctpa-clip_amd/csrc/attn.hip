@@ -710,6 +710,207 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_bias_kernel(AP p, int nfc) {
   }
 }
 
+// ------------------------------------------ backward dQ, biased, base spatial shape (L = LF = 576)
+// attn_bwd_dq_bias_kernel specialised to a full 24 x 24 grid (r02), same grid, LDS tables,
+// bias-gradient binning and results (up to the summation order of the dQ parts):
+//  * the NEXT frame's K / V land in a second LDS buffer by LDS-DMA (global_load_lds, 9 x 1 KB per
+//    wave) while this frame computes: one counted wait + one barrier per frame, no staging
+//    registers (the generic kernel waits on every frame's staging: 67 % of its wave cycles
+//    parked in s_waitcnt / s_barrier, r02 PMC).  The images are unpadded 64-B rows with the 16-B
+//    chunk XOR (row >> 1) & 3 (conflict-free for the ds_read_b128 row fragments and the
+//    ds_read_b64_tr_b16 transposed ones: searched over the gfx950 lane groups);
+//  * 8 waves = 4 query sub-blocks x 2 key halves of NC / 2 = 9 chunks, as the generic kernel, but
+//    straight-line chunk code (254 VGPRs, no spills; 12 waves x 3 parts spill at the 168 cap);
+//  * the dQ exchange of the key parts reuses the finished frame's buffer; the bias bins reuse
+//    buffer 0 after the last frame.
+constexpr int DQD_W = 8, DQD_NT = DQD_W * 64, DQD_KP = 2;
+__device__ __forceinline__ int kv_swz(int row) { return (row >> 1) & 3; }
+__device__ __forceinline__ bf16x8 rowfrag_sw(const char* img, int r0, int lane) {
+  const int row = r0 + (lane & 15);
+  return *(const bf16x8*)(img + row * 64 + (((lane >> 4) ^ kv_swz(row)) << 4));
+}
+__device__ __forceinline__ bf16x8 trfrag_sw(const char* img, int r0, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  const int row = r0 + 4 * g + q, colb = 2 * c0 + 8 * pp;
+  const char* a1 = img + row * 64 + (((colb >> 4) ^ kv_swz(row)) << 4) + (colb & 15);
+  const char* a2 = a1 + 16 * 64;   // row + 16: same swizzle
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a1));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a2));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int LF>
+__global__ __launch_bounds__(DQD_NT) void attn_bwd_dq_bias_dma_kernel(AP p, int nfc) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int D = 32, DB = 2, L = LF, NC = L / 32, KP = DQD_KP, NCP = NC / KP, NTH = DQD_NT;
+  constexpr int IMG = L * 64, BUF = 2 * IMG, NG = BUF / 1024 / DQD_W;   // glds per wave per frame
+  static_assert(L % 64 == 0 && NC % KP == 0 && (BUF / 1024) % DQD_W == 0 && (IMG / 1024) % NG == 0,
+                "full-shape specialisation");
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h = blockIdx.x, qg = blockIdx.y, fc = blockIdx.z;
+  const int qsub = w & 3, kpart = w >> 2;
+  const int c_begin = kpart * NCP;
+  float* ub = (float*)(smem + 2 * BUF);
+  const int nb4 = (p.nbins + 3) & ~3;
+  int* kb = (int*)(ub + nb4);
+  for (int i = tid; i < p.nbins; i += NTH) ub[i] = p.bias_u[(int64_t)h * p.nbins + i] * LOG2E;
+  for (int i = tid; i < L; i += NTH) kb[i] = kb_of(p, i);
+  const int g = lane >> 4, li = lane & 15;
+  const int q = qg * 64 + qsub * 16 + li;   // < L: L % 64 == 0
+  const float sc2 = p.scale * LOG2E;
+  f32x4 acc[NCP][2];
+#pragma unroll
+  for (int c = 0; c < NCP; ++c) { acc[c][0] = f32x4{0.f, 0.f, 0.f, 0.f}; acc[c][1] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+  const int f0 = (int)((int64_t)p.nseq * fc / nfc), f1 = (int)((int64_t)p.nseq * (fc + 1) / nfc);
+  // LDS-DMA map: instruction j of wave w fills bytes [(w NG + j) KB, +1 KB) of a buffer, lane l the
+  // 16 B at + 16 l: image (K below IMG, V above; wave-uniform), row, swizzled chunk
+  auto stage_frame = [&](int s, int b) {
+    const int64_t fb = (int64_t)s * p.s_outer;   // spatial: row(s, i) = s * s_outer + i (host-checked)
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+      const int pos = (w * NG + j) * 1024 + lane * 16;
+      const bool isv = pos >= IMG;
+      const int pi = isv ? pos - IMG : pos, row = pi >> 6, ch = ((pi >> 4) & 3) ^ kv_swz(row);
+      const u16* src = isv ? p.v + (fb + row) * p.ldv : p.k + (fb + row) * p.ldk;
+      glds16_asm(src + h * D + ch * 8, smem + b * BUF + (w * NG + j) * 1024);   // (common.h)
+    }
+  };
+  // per-query operands of one frame (registers, loaded one frame ahead)
+  bf16x8 qf = zero8(), df = zero8(), of = zero8();
+  float lse2 = 0.f;
+  auto load_q = [&](int s) {
+    const int64_t qrow = (int64_t)s * p.s_outer + q;
+    qf = gload8(p.q + qrow * p.ldq + h * D + 8 * g);
+    df = gload8(p.dout + qrow * p.lddo + h * D + 8 * g);
+    of = gload8(p.o + qrow * p.ldo + h * D + 8 * g);
+    lse2 = p.lse[(int64_t)h * p.M + qrow];   // scaled after the frame's wait: a use here would
+  };                                          // make the compiler drain the DMA queue (vmcnt(0))
+  if (f0 < f1) {
+    load_q(f0);
+    stage_frame(f0, 0);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();   // tables (frame f0's DMA may still be in flight)
+  __builtin_amdgcn_sched_barrier(0);
+  const int cq = kb[q] + boff(p);
+  for (int s = f0; s < f1; ++s) {
+    const int b = (s - f0) & 1;
+    const char* Kimg = smem + b * BUF;
+    const char* Vimg = Kimg + IMG;
+    // frame s landed (this wave's DMA), published by the barrier; the other buffer's last readers
+    // (frame s - 1) all passed the previous frame's exchange barriers
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // consume this frame's per-query registers BEFORE the next frame's loads are issued: hipcc
+    // waits vmcnt(0) at the first use of an ordinary load result while LDS-DMA is outstanding
+    bf16x8 qc = qf, dc = df;
+    float l2 = lse2 * LOG2E;
+    float dl = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dl += (float)df[j] * (float)of[j];
+    dl += __shfl_xor(dl, 16, 64);
+    dl += __shfl_xor(dl, 32, 64);
+    {
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      v4u qv = __builtin_bit_cast(v4u, qc), dv = __builtin_bit_cast(v4u, dc);
+      asm volatile("" : "+v"(qv), "+v"(dv), "+v"(l2), "+v"(dl));
+      qc = __builtin_bit_cast(bf16x8, qv);
+      dc = __builtin_bit_cast(bf16x8, dv);
+    }
+    const int64_t qrow = (int64_t)s * p.s_outer + q;
+    if (g == 0 && kpart == 0) p.delta[(int64_t)h * p.M + qrow] = dl;
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + 1 < f1) {
+      load_q(s + 1);
+      stage_frame(s + 1, b ^ 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 dq[DB];
+#pragma unroll
+    for (int d = 0; d < DB; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ci = 0; ci < NCP; ++ci) {
+      const int kc = (c_begin + ci) * 32;
+      f32x4 sa[2], da[2];
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi) {
+        sa[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Kimg, kc + 16 * bi, lane), qc,
+                                                         f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        da[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Vimg, kc + 16 * bi, lane), dc,
+                                                         f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      }
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi) {
+        const int k0 = kc + 16 * bi + 4 * g;
+        const float* up = ub + (cq - kb[k0] - 3);   // up[3 - r] = ub[bin(q, k0 + r)] (RUN)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = sa[bi][r] * sc2 + up[3 - r];
+          const float ds = fexp2(x - l2) * (da[bi][r] - dl);
+          acc[ci][bi][r] += ds;
+          sa[bi][r] = ds * p.scale;
+        }
+      }
+      const bf16x8 dsb = pack_perm(sa[0], sa[1]);
+#pragma unroll
+      for (int d = 0; d < DB; ++d)
+        dq[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag_sw(Kimg, kc, d * 16, lane), dsb, dq[d], 0, 0, 0);
+    }
+    // combine the key parts of this frame's dQ through the finished buffer (after every wave's
+    // last K / V read of it); part 0 sums and stores
+    float* xch = (float*)(smem + b * BUF);   // [KP - 1][4 sub-blocks][64 lanes][8]
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kpart > 0) {
+#pragma unroll
+      for (int d = 0; d < DB; ++d)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xch[(((kpart - 1) * 4 + qsub) * 64 + lane) * 8 + d * 4 + r] = dq[d][r];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (kpart == 0) {
+#pragma unroll
+      for (int d = 0; d < DB; ++d) {
+        f32x4 v = dq[d];
+#pragma unroll
+        for (int pp = 0; pp < KP - 1; ++pp)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += xch[((pp * 4 + qsub) * 64 + lane) * 8 + d * 4 + r];
+        uint2 pk;
+        pk.x = pack2(v[0], v[1]);
+        pk.y = pack2(v[2], v[3]);
+        *(uint2*)(p.dq + qrow * p.lddq + h * D + d * 16 + 4 * g) = pk;
+      }
+    }
+  }
+  // bin the frame-summed dS once (bins in buffer 0: every wave is past its last read of it)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  float* bins = (float*)smem;
+  for (int i = tid; i < p.nbins; i += NTH) bins[i] = 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int ci = 0; ci < NCP; ++ci)
+#pragma unroll
+    for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = (c_begin + ci) * 32 + 16 * bi + 4 * g + r;
+        atomicAdd(&bins[cq - kb[key]], acc[ci][bi][r]);
+      }
+  __syncthreads();
+  for (int i = tid; i < p.nbins; i += NTH) {
+    const float v = bins[i];
+    if (v != 0.f) atomicAdd(&p.dbias_u[(int64_t)h * p.nbins + i], v);
+  }
+}
+
 bool s_attr = false;
 
 template <int D, bool BIAS>
@@ -731,6 +932,8 @@ void set_attrs() {
                             160 * 1024);
   (void)hipFuncSetAttribute((const void*)attn_bwd_dq_bias_kernel<9, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dq_bias_dma_kernel<576>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<32, true, 12, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<32, true, 12, true>,
@@ -1091,7 +1294,13 @@ extern "C" int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream) {
     const size_t lds = (size_t)2 * Lp * RSb + 2 * (size_t)((p.nbins + 3) & ~3) * 4 + 2 * (size_t)Lp * 4 +
                        4 * 64 * 8 * 4;
     if (lds > 160 * 1024) return CT_ESHAPE;
-    if (run_ok(p)) hipLaunchKernelGGL((attn_bwd_dq_bias_kernel<9, true>), dim3(p.H, nqg, nfc), dim3(NT), lds, st, p, nfc);
+    static int dma_ok = -1;   // CTCLIP_ATTN_DQ_DMA=0: the generic kernel (A/B)
+    if (dma_ok < 0) { const char* e = getenv("CTCLIP_ATTN_DQ_DMA"); dma_ok = e ? atoi(e) != 0 : 1; }
+    const size_t lds_dma = (size_t)2 * 2 * 576 * 64 + (size_t)((p.nbins + 3) & ~3) * 4 + 576 * 4;
+    if (dma_ok && run_ok(p) && p.L == 576 && p.s_pos == 1 && p.n_inner == 1 && p.nbins * 4 <= 2 * 576 * 64 &&
+        lds_dma <= 160 * 1024)
+      hipLaunchKernelGGL((attn_bwd_dq_bias_dma_kernel<576>), dim3(p.H, nqg, nfc), dim3(DQD_NT), lds_dma, st, p, nfc);
+    else if (run_ok(p)) hipLaunchKernelGGL((attn_bwd_dq_bias_kernel<9, true>), dim3(p.H, nqg, nfc), dim3(NT), lds, st, p, nfc);
     else hipLaunchKernelGGL((attn_bwd_dq_bias_kernel<9>), dim3(p.H, nqg, nfc), dim3(NT), lds, st, p, nfc);
     launch_dkv<32>(p, grid, lds2, st);
     CT_CHECK_LAUNCH();

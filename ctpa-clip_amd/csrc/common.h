@@ -14,6 +14,29 @@ typedef uint4 u32x4;
 
 #define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
+// ds_read_b64_tr_b16 through inline asm, for kernels that keep LDS-DMA (global_load_lds) in
+// flight across fragment reads: hipcc (ROCm 7.2) puts an s_waitcnt vmcnt(0) in front of every
+// intrinsic ds_read_tr while any LDS-DMA is outstanding (it cannot prove they do not alias),
+// which drains the load pipeline each phase.  The asm form is invisible to that check AND to the
+// compiler's lgkmcnt tracking: the caller must wait (s_waitcnt lgkmcnt) before using the result.
+// 16-B LDS-DMA (global_load_lds_dwordx4) through inline asm: wave-uniform LDS base in M0, lane l
+// lands at base + 16 l.  Invisible to hipcc's LDS-DMA tracking, so the compiler no longer drains
+// the queue (vmcnt(0)) before LDS reads it cannot prove disjoint (every ds_read_b64_tr_b16 of an
+// MN-contiguous operand); the kernel's own counted vmcnt waits order the DMA and the reads.  The
+// compiler's waits for its own loads stay safe: unseen younger ops only make them stricter.
+__device__ __forceinline__ void glds16_asm(const void* g, const void* lds) {
+  const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)(size_t)LDS_PTR(char, lds));
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
+}
+
+template <int OFF>
+__device__ __forceinline__ s16x4 ds_read_tr16_b64_asm(const void* p) {
+  s16x4 r;
+  const unsigned a = (unsigned)(size_t)LDS_PTR(char, p);
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+  return r;
+}
+
 #define CT_CHECK_LAUNCH()                                  \
   do {                                                     \
     hipError_t _e = hipGetLastError();                     \

@@ -12,7 +12,7 @@ def main():
     sub = sys.argv[2] if len(sys.argv) > 2 else 'gemm256_kernel'
     vals = defaultdict(list)
     durs = []
-    for f in sorted(glob.glob(os.path.join(root, 'p*', 'p_counter_collection.csv'))):
+    for f in sorted(glob.glob(os.path.join(root, 'p*', '**', '*counter_collection.csv'), recursive=True)):
         for r in csv.DictReader(open(f)):
             if sub in r['Kernel_Name']:
                 vals[r['Counter_Name']].append(float(r['Counter_Value']))
