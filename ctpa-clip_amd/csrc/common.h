@@ -24,9 +24,20 @@ typedef uint4 u32x4;
 // the queue (vmcnt(0)) before LDS reads it cannot prove disjoint (every ds_read_b64_tr_b16 of an
 // MN-contiguous operand); the kernel's own counted vmcnt waits order the DMA and the reads.  The
 // compiler's waits for its own loads stay safe: unseen younger ops only make them stricter.
+// M0 is a reserved register: it is saved and restored around the DMA, with the one wait state a
+// SALU write of M0 needs before an LDS-DMA reads it.
 __device__ __forceinline__ void glds16_asm(const void* g, const void* lds) {
   const unsigned l = __builtin_amdgcn_readfirstlane((unsigned)(size_t)LDS_PTR(char, lds));
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
+  unsigned saved;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(saved)
+      : "v"(g), "s"(l)
+      : "memory");
 }
 
 template <int OFF>

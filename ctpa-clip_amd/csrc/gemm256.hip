@@ -409,15 +409,36 @@ __device__ __forceinline__ int frag_base(int r0, int lane) {
     return k1 * 256 + (((r0 >> 4) ^ mn_swz(k1)) << 5) + pp * 8;
   }
 }
+// ds_read_b64_tr_b16 at LDS byte address a + off through inline asm (off folds to one immediate
+// once the phase loops are unrolled).  hipcc (ROCm 7.2) puts s_waitcnt vmcnt(0) in front of every
+// ds_read_tr INTRINSIC while any global_load_lds is outstanding (it cannot prove they do not
+// alias): 60-140 per MN-operand kernel, each draining the glds ring.  The asm form escapes that
+// check and the compiler's lgkmcnt tracking: every fragment is consumed after compute_phase()'s
+// explicit s_waitcnt lgkmcnt(0).
+__device__ __forceinline__ s16x4 tr_asm(unsigned a, int off) {
+  s16x4 r;
+  switch (off) {
+#define CT_TR(o) \
+  case o: asm volatile("ds_read_b64_tr_b16 %0, %1 offset:" #o : "=v"(r) : "v"(a)); break;
+    CT_TR(0) CT_TR(1024) CT_TR(8192) CT_TR(9216) CT_TR(16384) CT_TR(17408) CT_TR(24576) CT_TR(25600)
+    CT_TR(32768) CT_TR(33792) CT_TR(40960) CT_TR(41984) CT_TR(49152) CT_TR(50176) CT_TR(57344) CT_TR(58368)
+#undef CT_TR
+    default: asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a + off)); break;
+  }
+  return r;
+}
+
+// buf: base of the 64 KB buffer; which: half-tile index (A0 A1 B0 B1)
 template <bool KC>
-__device__ __forceinline__ bf16x8 hfrag(const char* half, int base, int blk, int s) {
+__device__ __forceinline__ bf16x8 hfrag(const char* buf, int which, int base, int blk, int s) {
   if constexpr (KC) {
     // chunk s*4 + c ^ sw = (c ^ sw) ^ (s*4): the k-substep flips bit 6 of the byte offset
-    return *(const bf16x8*)(half + ((base + blk * 2048) ^ (s << 6)));
+    return *(const bf16x8*)(buf + which * HALF + ((base + blk * 2048) ^ (s << 6)));
   } else {
-    const char* p0 = half + (base ^ (blk << 5)) + s * 8192;
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, p0));
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, p0 + 1024));
+    const unsigned a = (unsigned)(size_t)LDS_PTR(char, buf) + (unsigned)(base ^ (blk << 5));
+    const int off = which * HALF + s * 8192;
+    s16x4 lo = tr_asm(a, off);
+    s16x4 hi = tr_asm(a, off + 1024);
     typedef short s16x8 __attribute__((ext_vector_type(8)));
     s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     return __builtin_bit_cast(bf16x8, v);
@@ -765,23 +786,22 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
   auto load_frags = [&](int buf, int q) {
     const char* base = smem + buf * TILEB;
     if (q == 0 || q == 2) {
-      const char* ah = base + (q == 0 ? A0 : A1) * HALF;
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int ii = 0; ii < 4; ++ii) a[ii][s] = hfrag<AK>(ah, abase, ii, s);
+        for (int ii = 0; ii < 4; ++ii) a[ii][s] = hfrag<AK>(base, q == 0 ? A0 : A1, abase, ii, s);
     }
     if (q == 0) {
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) b0[jj][s] = hfrag<BKC>(base + B0 * HALF, bbase, jj, s);
+        for (int jj = 0; jj < 2; ++jj) b0[jj][s] = hfrag<BKC>(base, B0, bbase, jj, s);
     }
     if (q == 1) {
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) b1[jj][s] = hfrag<BKC>(base + B1 * HALF, bbase, jj, s);
+        for (int jj = 0; jj < 2; ++jj) b1[jj][s] = hfrag<BKC>(base, B1, bbase, jj, s);
     }
   };
   // compute segment: quadrant q = (mi, ni) in order (0,0) (0,1) (1,1) (1,0)
