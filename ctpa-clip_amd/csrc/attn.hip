@@ -911,6 +911,138 @@ __global__ __launch_bounds__(DQD_NT) void attn_bwd_dq_bias_dma_kernel(AP p, int 
   }
 }
 
+// --------------------------------------------- backward dK dV, biased, base spatial shape (L = LF)
+// attn_bwd_dkv_kernel<32, true, 12, true> made persistent over frames (r02): 32 workgroups per
+// head walk frames s = blockIdx.x / H, + gridDim.x / H, ... with their head's bias table loaded
+// once, and the NEXT frame's Q / dO rows (6 x 16 B per thread) and lse / delta are loaded into
+// registers while this frame computes, then written to the LDS images behind one barrier (the
+// per-pair kernel pays every (frame, head) pair's staging latency with nothing to overlap it:
+// 1 workgroup per CU).  Each wave's K / V fragments of its next key block are loaded one block
+// ahead.  The Q / dO images are unpadded 64-B rows with the dQ kernel's chunk swizzle (the
+// padded 80-B rows conflict under gfx950's ds_read_b128 lane groups: 35 % of the per-pair
+// kernel's LDS cycles, r02 PMC).  Same arithmetic and results as the per-pair kernel.
+constexpr int DKP_W = 12, DKP_NT = DKP_W * 64;
+template <int LF>
+__global__ __launch_bounds__(DKP_NT) void attn_bwd_dkv_persist_kernel(AP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int D = 32, DB = 2, RS = 64, W = DKP_W, NTH = DKP_NT, L = LF, CH = D / 8;
+  constexpr int NLD = 2 * L * CH / NTH, RPU = NTH / CH, NKB = L / 16;
+  static_assert((2 * L * CH) % NTH == 0 && L % 32 == 0 && L % 16 == 0 && (W * 64 / CH) % 16 == 0, "shape");
+  const int tid = threadIdx.x, lane = tid & 63, wi = tid >> 6;
+  const int h = blockIdx.x % p.H, wg = blockIdx.x / p.H, nwg = gridDim.x / p.H;
+  char* Qimg = smem;
+  char* Dimg = smem + L * RS;
+  float* ls = (float*)(smem + 2 * L * RS);
+  float* dls = ls + L;
+  float* ub = dls + L;
+  const int nb4 = (p.nbins + 3) & ~3;
+  int* kb = (int*)(ub + nb4);
+  for (int i = tid; i < p.nbins; i += NTH) ub[i] = p.bias_u[(int64_t)h * p.nbins + i] * LOG2E;
+  for (int i = tid; i < L; i += NTH) kb[i] = kb_of(p, i);
+  const int g = lane >> 4, li = lane & 15;
+  const float sc2 = p.scale * LOG2E;
+  // staging map: chunk u of a thread is row R = tid / CH + RPU u of the stacked [Q; dO] image
+  // (dO when R >= L: wave-uniform as 64 / CH rows per wave divide L), 16-B column tid % CH
+  const int r0 = tid / CH, c0 = tid % CH;
+  const int64_t offq = (int64_t)r0 * p.ldq + h * D + c0 * 8, offd = (int64_t)r0 * p.lddo + h * D + c0 * 8;
+  u32x4 st[NLD];
+  float lsv = 0.f, dlv = 0.f;   // this thread's lse / delta row (tid < L)
+#define CT_DKV_LOAD(S_)                                                                          \
+  do {                                                                                           \
+    const int64_t fb_ = (int64_t)(S_) * p.s_outer;   /* row(s, i) = s * s_outer + i (host-checked) */ \
+    _Pragma("unroll") for (int u = 0; u < NLD; ++u) {                                            \
+      const bool isq = u * RPU + (wi * 64) / CH < L;                                             \
+      const u16* src_ = isq ? p.q + (fb_ + u * RPU) * p.ldq + offq : p.dout + (fb_ + u * RPU - L) * p.lddo + offd; \
+      st[u] = *(const u32x4*)src_;                                                               \
+    }                                                                                            \
+    if (tid < L) {                                                                               \
+      lsv = p.lse[(int64_t)h * p.M + fb_ + tid];                                                 \
+      dlv = p.delta[(int64_t)h * p.M + fb_ + tid];                                               \
+    }                                                                                            \
+  } while (0)
+  int s = wg;
+  if (s < p.nseq) CT_DKV_LOAD(s);
+  for (; s < p.nseq; s += nwg) {
+    __syncthreads();   // previous frame's LDS reads done (and, first time, the tables written)
+#pragma unroll
+    for (int u = 0; u < NLD; ++u) {
+      const bool isq = u * RPU + (wi * 64) / CH < L;
+      char* dst = isq ? Qimg + (u * RPU) * RS : Dimg + (u * RPU - L) * RS;
+      *(u32x4*)(dst + r0 * RS + ((c0 ^ kv_swz(u * RPU + r0)) << 4)) = st[u];   // R = u RPU + r0, same swizzle for the dO part (L % 8 == 0)
+    }
+    if (tid < L) {
+      ls[tid] = lsv * LOG2E;
+      dls[tid] = dlv;
+    }
+    __syncthreads();
+    if (s + nwg < p.nseq) CT_DKV_LOAD(s + nwg);   // in flight under this frame's key blocks
+    const int64_t fb = (int64_t)s * p.s_outer;
+    // K / V fragments one key block ahead
+    bf16x8 kf = zero8(), vf = zero8();
+    {
+      const int64_t krow = fb + wi * 16 + li;
+      kf = gload8(p.k + krow * p.ldk + h * D + 8 * g);
+      vf = gload8(p.v + krow * p.ldv + h * D + 8 * g);
+    }
+    for (int kbk = wi; kbk < NKB; kbk += W) {
+      const bf16x8 kc = kf, vc = vf;
+      if (kbk + W < NKB) {
+        const int64_t krow = fb + (kbk + W) * 16 + li;
+        kf = gload8(p.k + krow * p.ldk + h * D + 8 * g);
+        vf = gload8(p.v + krow * p.ldv + h * D + 8 * g);
+      }
+      const int key = kbk * 16 + li;
+      const int ck = kb[key] - boff(p);   // bin(q, key) = kb[q] - ck
+      f32x4 dk[DB], dv[DB];
+#pragma unroll
+      for (int d = 0; d < DB; ++d) { dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[d] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+      for (int qc = 0; qc < L; qc += 32) {
+        f32x4 sa[2], da[2];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi) {
+          sa[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Qimg, qc + 16 * bi, lane), kc,
+                                                           f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          da[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Dimg, qc + 16 * bi, lane), vc,
+                                                           f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        }
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi) {
+          const int q0 = qc + 16 * bi + 4 * g;
+          const f32x4 lv = *(const f32x4*)(ls + q0);
+          const f32x4 dlq = *(const f32x4*)(dls + q0);
+          const float* up = ub + (kb[q0] - ck);   // up[r] = ub[bin(q0 + r, key)]
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float x = sa[bi][r] * sc2 + up[r];
+            const float pr = fexp2(x - lv[r]);
+            const float ds = pr * (da[bi][r] - dlq[r]);
+            sa[bi][r] = pr;
+            da[bi][r] = ds * p.scale;
+          }
+        }
+        const bf16x8 pa = pack_perm(sa[0], sa[1]);
+        const bf16x8 dsa = pack_perm(da[0], da[1]);
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+          dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, trfrag_sw(Dimg, qc, d * 16, lane), dv[d], 0, 0, 0);
+          dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsa, trfrag_sw(Qimg, qc, d * 16, lane), dk[d], 0, 0, 0);
+        }
+      }
+      // C[key][d]: rows = keys kbk*16 + 4g + r, col = d*16 + li
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = fb + kbk * 16 + 4 * g + r;
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+          p.dk[row * p.lddk + h * D + d * 16 + li] = f2bf(dk[d][r]);
+          p.dv[row * p.lddv + h * D + d * 16 + li] = f2bf(dv[d][r]);
+        }
+      }
+    }
+  }
+}
+#undef CT_DKV_LOAD
+
 bool s_attr = false;
 
 template <int D, bool BIAS>
@@ -933,6 +1065,8 @@ void set_attrs() {
   (void)hipFuncSetAttribute((const void*)attn_bwd_dq_bias_kernel<9, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             160 * 1024);
   (void)hipFuncSetAttribute((const void*)attn_bwd_dq_bias_dma_kernel<576>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_persist_kernel<576>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<32, true, 12, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1009,6 +1143,17 @@ void launch_dq(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
 template <int D>
 void launch_dkv(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
   if constexpr (D == 32) {
+    static int persist = -1;   // CTCLIP_ATTN_DKV_PERSIST=0: the per-pair kernel (A/B)
+    if (persist < 0) { const char* e = getenv("CTCLIP_ATTN_DKV_PERSIST"); persist = e ? atoi(e) != 0 : 1; }
+    if (persist && run_ok(p) && p.L == 576 && p.s_pos == 1 && p.n_inner == 1 && p.pp == 1 && !p.kmask &&
+        p.nseq >= 2 && 256 % p.H == 0) {
+      const size_t lds_p = (size_t)2 * 576 * 64 + 2 * 576 * 4 + (size_t)((p.nbins + 3) & ~3) * 4 + 576 * 4;
+      if (lds_p <= 160 * 1024) {
+        const int per_head = std::min(p.nseq, 256 / p.H);
+        hipLaunchKernelGGL((attn_bwd_dkv_persist_kernel<576>), dim3(per_head * p.H), dim3(DKP_NT), lds_p, st, p);
+        return;
+      }
+    }
     if (run_ok(p)) {
       hipLaunchKernelGGL((attn_bwd_dkv_kernel<D, true, 12, true>), grid, dim3(12 * 64), lds, st, p);
       return;

@@ -978,7 +978,10 @@ int tile_rows() { return variant() == 2 ? 2 : 1; }
 template <bool AK, bool BKC>
 int launch8_ep(const P& p, int batch, hipStream_t st) {
   if (p.act == 4) return launch8<AK, BKC, 4>(p, batch, st);
-  const bool tr = !p.c_f32 && p.split_k <= 1 && p.act != 3 && !p.R;
+  // CTCLIP_GEMM_TR_F32=1 (A/B): f32 / residual outputs through the transposed (LDS-free) epilogue too
+  static int tr_f32 = -1;
+  if (tr_f32 < 0) { const char* e = getenv("CTCLIP_GEMM_TR_F32"); tr_f32 = e ? atoi(e) != 0 : 0; }
+  const bool tr = (tr_f32 || (!p.c_f32 && !p.R)) && p.split_k <= 1 && p.act != 3;
   if (!tr) return launch8<AK, BKC, -1>(p, batch, st);
   if (p.act == 2) return launch8<AK, BKC, 2>(p, batch, st);
   return launch8<AK, BKC, 0>(p, batch, st);
