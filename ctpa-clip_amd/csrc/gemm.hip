@@ -517,6 +517,54 @@ extern "C" int ctclip_reduce_slabs_ep(const float* slabs, int64_t nslab, int64_t
   return 0;
 }
 
+// batched skinny reductions: blockIdx.y = job, blockIdx.x = 64 float4 columns; 16 slab lanes
+// strided as reduce_slabs_skinny_kernel (same order of additions)
+constexpr int MULTI_JOBS = 32;
+struct MultiJobs {
+  ctclip_slab_job j[MULTI_JOBS];
+};
+__global__ __launch_bounds__(1024) void reduce_slabs_multi_kernel(MultiJobs jobs) {
+  __shared__ f32x4 red[16][64];
+  const ctclip_slab_job jb = jobs.j[blockIdx.y];
+  const int c4 = threadIdx.x & 63, lane = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + c4;
+  if ((int64_t)blockIdx.x * 64 >= jb.cols / 4) return;   // uniform: this job has fewer columns
+  const bool valid = e < jb.cols / 4;
+  const int64_t c = valid ? e * 4 : 0;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (valid) {
+#pragma unroll 4
+    for (int64_t z = lane; z < jb.nslab; z += 16) acc += *(const f32x4*)(jb.slabs + z * jb.cols + c);
+  }
+  red[lane][c4] = acc;
+  __syncthreads();
+  if (lane == 0 && valid) {
+    for (int k = 1; k < 16; ++k) acc += red[k][c4];
+    float* o = jb.out + c;
+    if (jb.accumulate) acc += *(const f32x4*)o;
+    *(f32x4*)o = acc;
+  }
+}
+
+extern "C" int ctclip_reduce_slabs_multi(const ctclip_slab_job* jobs, int32_t njobs, void* stream) {
+  for (int32_t j0 = 0; j0 < njobs; j0 += MULTI_JOBS) {
+    MultiJobs mj{};
+    const int n = std::min<int32_t>(MULTI_JOBS, njobs - j0);
+    int64_t maxc = 0;
+    for (int i = 0; i < n; ++i) {
+      const ctclip_slab_job& jb = jobs[j0 + i];
+      CT_REQUIRE(jb.cols % 4 == 0 && aligned16(jb.slabs) && aligned16(jb.out), CT_EALIGN);
+      mj.j[i] = jb;
+      maxc = std::max(maxc, jb.cols);
+    }
+    if (maxc == 0) continue;
+    hipLaunchKernelGGL(reduce_slabs_multi_kernel, dim3((unsigned)cdiv(maxc / 4, 64), n), dim3(1024), 0,
+                       (hipStream_t)stream, mj);
+    CT_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
 extern "C" int ctclip_reduce_slabs(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,
                                    void* out, int64_t ldo, int32_t out_f32, int32_t accumulate, void* stream) {
   if (rows == 0 || cols == 0) return 0;

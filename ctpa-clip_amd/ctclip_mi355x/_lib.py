@@ -22,6 +22,11 @@ c_f32 = ctypes.c_float
 c_vp = ctypes.c_void_p
 
 
+class SlabJob(ctypes.Structure):
+    _fields_ = [('slabs', c_vp), ('nslab', c_i64), ('cols', c_i64), ('out', c_vp), ('accumulate', c_i32),
+                ('pad', c_i32)]
+
+
 class GemmArgs(ctypes.Structure):
     _fields_ = [
         ('M', c_i64), ('N', c_i64), ('K', c_i64),
@@ -88,6 +93,7 @@ _SIGS = {
     'ctclip_gemm_set_persist': [c_i32],
     'ctclip_reduce_slabs_ep': [c_vp, c_i64, c_i64, c_i64, c_i64, ctypes.POINTER(GemmArgs), c_vp],
     'ctclip_reduce_slabs': [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp],
+    'ctclip_reduce_slabs_multi': [ctypes.POINTER(SlabJob), c_i32, c_vp],
     'ctclip_layernorm_fwd': [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_f32, c_vp, c_i64, c_vp, c_i64,
                              c_vp, c_vp, c_vp],
     'ctclip_layernorm_bwd': [c_vp, c_i32, c_i64, c_vp, c_i32, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_i64,

@@ -23,6 +23,8 @@ from __future__ import annotations
 import torch
 import torch.distributed as dist
 
+from . import kernels as K
+
 
 def world_rank():
     if dist.is_available() and dist.is_initialized():
@@ -157,6 +159,14 @@ class BucketedGradSync:
         for t, off, n in self.buckets:
             if t in self.launched:
                 continue
+            # queued parameter-gradient reductions into this bucket (kernels.reduce_param_partials)
+            # land before it is read; one queued on another stream is waited for by this one
+            if K._DEFERRED:
+                lo = self.grad[off:off + n].data_ptr()
+                cur = torch.cuda.current_stream()
+                for st in K.flush_reductions(lo, lo + 4 * n):
+                    if st != cur:
+                        cur.wait_stream(st)
             if self.before_launch is not None:
                 self.before_launch(t)
             self.launched.append(t)

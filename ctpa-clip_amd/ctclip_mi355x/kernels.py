@@ -2,6 +2,8 @@
 torch's current HIP stream and returns torch tensors allocated by the caching allocator."""
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -176,6 +178,71 @@ def reduce_slabs(slabs, out, accumulate=False):
     return out
 
 
+# ------------------------------------------------- deferred parameter-gradient reductions
+# The LN / l2norm / bias backward kernels leave per-block partials [nb][D] of a parameter
+# gradient; each used to be summed into .grad by its own ~10 us launch (72 per step on the image
+# tower's stream).  Inside a backward pass they are queued per stream instead and summed by ONE
+# batched launch (ctclip_reduce_slabs_multi, bit-identical to the single reduction) when the pass
+# ends (autograd callback), or earlier when a gradient bucket's all-reduce is about to read them
+# (dist_sync.BucketedGradSync).  CTCLIP_DEFER_REDUCE=0 restores the immediate launches.
+DEFER_REDUCE = os.environ.get('CTCLIP_DEFER_REDUCE', '1') != '0'
+_DEFERRED = {}        # stream id -> (stream, [(slabs, out, accumulate), ...])
+_CB_QUEUED = [False]
+
+
+def _in_backward():
+    try:
+        return torch._C._current_graph_task_id() != -1
+    except AttributeError:
+        return False
+
+
+def flush_reductions(lo=None, hi=None):
+    """Launch the queued reductions (each on the stream that queued it), all of them or only those
+    whose output lies in the byte range [lo, hi) (a gradient bucket); returns the streams used."""
+    used = []
+    for k in list(_DEFERRED):
+        st, jobs = _DEFERRED[k]
+        if lo is None:
+            take, keep = jobs, []
+        else:
+            take = [j for j in jobs if lo <= j[1].data_ptr() < hi]
+            keep = [j for j in jobs if not (lo <= j[1].data_ptr() < hi)]
+        if keep:
+            _DEFERRED[k] = (st, keep)
+        else:
+            del _DEFERRED[k]
+        if not take:
+            continue
+        arr = (_lib.SlabJob * len(take))()
+        for i, (sl, out, acc) in enumerate(take):
+            arr[i].slabs, arr[i].nslab, arr[i].cols = sl.data_ptr(), sl.shape[0], sl.shape[-1]
+            arr[i].out, arr[i].accumulate = out.data_ptr(), int(acc)
+        call('ctclip_reduce_slabs_multi', arr, len(take), st.cuda_stream)
+        # the partial buffers were allocated on `st`; freeing them after this launch is ordered
+        used.append(st)
+    return used
+
+
+def _end_of_backward():
+    _CB_QUEUED[0] = False
+    flush_reductions()
+
+
+def reduce_param_partials(part, out, accumulate):
+    """out[D] (+)= sum of part[nb][D]: deferred inside a backward pass (see above)."""
+    nb, D = part.shape[0], part.shape[-1]
+    if (DEFER_REDUCE and nb >= 16 and out.dtype == F32 and out.is_contiguous() and part.is_contiguous()
+            and D % 4 == 0 and _in_backward()):
+        st = torch.cuda.current_stream(part.device)
+        _DEFERRED.setdefault(st.cuda_stream, (st, []))[1].append((part, out.view(-1), accumulate))
+        if not _CB_QUEUED[0]:
+            torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
+            _CB_QUEUED[0] = True
+        return out
+    return reduce_slabs(part.view(nb, 1, D), out.view(1, D), accumulate=accumulate)
+
+
 # ----------------------------------------------------------------------------- reductions
 def nblocks_for(rows, cap=1024):
     return int(max(1, min(cap, (rows + 63) // 64)))
@@ -190,7 +257,10 @@ def colsum(x, out=None, accumulate=False):
     if out is None:
         out = torch.zeros(cols, device=x.device, dtype=F32) if accumulate else torch.empty(cols, device=x.device,
                                                                                            dtype=F32)
-    reduce_slabs(part.view(nb, 1, cols), out.view(1, cols), accumulate=accumulate)
+    if accumulate:
+        reduce_param_partials(part, out, accumulate)
+    else:
+        reduce_slabs(part.view(nb, 1, cols), out.view(1, cols), accumulate=accumulate)
     return out
 
 
@@ -219,12 +289,18 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, *, dres=None, want_beta=True, dx_f32
     call('ctclip_layernorm_bwd', ptr(dy), int(dy.dtype == F32), dy.stride(0), ptr(x), int(x.dtype == F32),
          x.stride(0), ptr(mean), ptr(rstd), ptr(gamma), rows, D, ptr(dres),
          dres.stride(0) if dres is not None else 0, ptr(dxf), D, ptr(dxb), D, ptr(pg), ptr(pb), nb, stream_ptr())
-    dg = dgamma_out if dgamma_out is not None else torch.empty(D, device=x.device, dtype=F32)
-    reduce_slabs(pg.view(nb, 1, D), dg.view(1, D), accumulate=dgamma_out is not None)
+    if dgamma_out is not None:      # a parameter's .grad: possibly deferred (reduce_param_partials)
+        dg = reduce_param_partials(pg, dgamma_out, True)
+    else:
+        dg = torch.empty(D, device=x.device, dtype=F32)
+        reduce_slabs(pg.view(nb, 1, D), dg.view(1, D))
     db = None
     if want_beta:
-        db = dbeta_out if dbeta_out is not None else torch.empty(D, device=x.device, dtype=F32)
-        reduce_slabs(pb.view(nb, 1, D), db.view(1, D), accumulate=dbeta_out is not None)
+        if dbeta_out is not None:
+            db = reduce_param_partials(pb, dbeta_out, True)
+        else:
+            db = torch.empty(D, device=x.device, dtype=F32)
+            reduce_slabs(pb.view(nb, 1, D), db.view(1, D))
     return dxf, dxb, dg, db
 
 
@@ -247,8 +323,10 @@ def l2norm_scale_bwd(x, dy, H, D, scale, out, ds_out=None):
     part = torch.empty(nb, D, device=x.device, dtype=F32)
     call('ctclip_l2norm_scale_bwd', ptr(x), x.stride(0), ptr(dy), dy.stride(0), rows, H, D, ptr(scale), ptr(out),
          out.stride(0), ptr(part), nb, stream_ptr())
-    ds = ds_out if ds_out is not None else torch.empty(D, device=x.device, dtype=F32)
-    reduce_slabs(part.view(nb, 1, D), ds.view(1, D), accumulate=ds_out is not None)
+    if ds_out is not None:
+        return reduce_param_partials(part, ds_out, True)
+    ds = torch.empty(D, device=x.device, dtype=F32)
+    reduce_slabs(part.view(nb, 1, D), ds.view(1, D))
     return ds
 
 

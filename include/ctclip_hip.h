@@ -69,6 +69,17 @@ int ctclip_gemm_set_persist(int on);
 /* sum f32 slabs [s][rows][ld] -> out (f32 or bf16), optional accumulate into f32 out */
 int ctclip_reduce_slabs(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,
                         void* out, int64_t ldo, int32_t out_f32, int32_t accumulate, void* stream);
+/* batched [nslab][1][cols] -> [1][cols] f32 reductions (parameter-gradient partials of the LN /
+ * l2norm / bias backward kernels), many jobs per launch: the host defers them to the end of the
+ * backward pass or the gradient bucket's all-reduce (kernels.py) instead of one launch each.
+ * Same summation order as ctclip_reduce_slabs' skinny path (bit-identical results). */
+typedef struct {
+  const float* slabs;  /* [nslab][cols] */
+  int64_t nslab, cols; /* cols % 4 == 0 */
+  float* out;          /* [cols] */
+  int32_t accumulate, pad;
+} ctclip_slab_job;
+int ctclip_reduce_slabs_multi(const ctclip_slab_job* jobs, int32_t njobs, void* stream);
 /* split-K combine with the GEMM epilogue of `ep` (C, ldc, c_f32, C2, ldc2, bias, R, ldr, r_f32,
  * act in {0, 1}, accumulate; M/N/K/A/B ignored): C = epilogue(sum_z slabs[z][rows][ld]) */
 int ctclip_reduce_slabs_ep(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,

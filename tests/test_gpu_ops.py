@@ -389,3 +389,27 @@ def test_adam_unaligned_slices_and_zero_grad(K):
             assert torch.equal(p[out], p0[out]) and torch.equal(g[out], g0[out])
             assert torch.equal(m[out], m0[out]) and torch.equal(v[out], v0[out])
             assert torch.count_nonzero(pb[out].float()).item() == 0
+
+
+def test_reduce_slabs_multi_bit_identical(K):
+    """Batched parameter-gradient reductions (kernels.reduce_param_partials, one launch for many
+    jobs, 32+ jobs split over launches): bit-identical to one ctclip_reduce_slabs per job."""
+    from ctclip_mi355x import _lib
+    torch.manual_seed(7)
+    jobs, refs = [], []
+    for i in range(40):
+        nb, D = (1024, 512) if i % 3 == 0 else ((2048, 32) if i % 3 == 1 else (64, 768))
+        part = torch.randn(nb, D, device='cuda')
+        out = torch.randn(D, device='cuda')
+        ref = out.clone()
+        K.reduce_slabs(part.view(nb, 1, D), ref.view(1, D), accumulate=bool(i % 2))
+        jobs.append((part, out, bool(i % 2)))
+        refs.append(ref)
+    arr = (_lib.SlabJob * len(jobs))()
+    for i, (part, out, acc) in enumerate(jobs):
+        arr[i].slabs, arr[i].nslab, arr[i].cols = part.data_ptr(), part.shape[0], part.shape[1]
+        arr[i].out, arr[i].accumulate = out.data_ptr(), int(acc)
+    assert _lib.lib().ctclip_reduce_slabs_multi(arr, len(jobs), torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    for (_, out, _), ref in zip(jobs, refs):
+        assert torch.equal(out, ref)
