@@ -116,11 +116,15 @@ __device__ __forceinline__ void xcd_remap(int& tx, int& ty) {
 // Shared epilogue: wave (wr, wc) owns output rows m0 + wr*128 + [0,128), cols n0 + wc*64 + [0,64);
 // acc[i][j] is the 16x16 block (i, j) of that region in the MFMA 16x16 C layout.  Stages each
 // 32-row quarter through a wave-private LDS region (8.7 KB per wave) and writes 16-B row chunks.
+// LM (compile time, one kernel instantiation each so only that path's registers are allocated):
+// -1 = general (bias / residual / GELU / f32 or bf16 / accumulate / shadow; GEGLU), -3 = argmax,
+// -5 = split-K slabs
+template <int LM = -1>
 __device__ __forceinline__ void epilogue(const P& p, f32x4 (&acc)[8][4], char* smem, int w, int wr, int wc, int lane,
                                          int64_t m0, int64_t n0, int split, int bidx) {
   float* cs = (float*)(smem + w * (32 * EP_LD * 4));   // 8.7 KB per wave, 8 waves = 70 KB
   const int64_t wrow0 = m0 + wr * 128, wcol0 = n0 + wc * 64;
-  const bool slab = p.split_k > 1;
+  const bool slab = LM == -5 || (LM == -1 && p.split_k > 1);
 #pragma unroll
   for (int quarter = 0; quarter < 4; ++quarter) {
 #pragma unroll
@@ -133,7 +137,7 @@ __device__ __forceinline__ void epilogue(const P& p, f32x4 (&acc)[8][4], char* s
     // wave-private region: no block barrier needed, only LDS write->read ordering in the wave
     __builtin_amdgcn_s_waitcnt(0xC07F);
     const int64_t rbase = wrow0 + quarter * 32;
-    if (p.act == 3) {
+    if (LM == -3 || (LM == -1 && p.act == 3)) {   // (LM -2 never takes the argmax / GEGLU paths)
       // argmax over this wave's 64 columns: 2 lanes per row (32 columns each), (value, index)
       // per (row, 64-col group), first-max tie-break
       // (+ the group's second-best score into the optional f32 C2, see gemm.hip)
@@ -159,7 +163,7 @@ __device__ __forceinline__ void epilogue(const P& p, f32x4 (&acc)[8][4], char* s
         out[gm * p.ldc + (wcol0 >> 6)] = make_float2(best, __int_as_float((int)(wcol0 + bi)));
         if (p.C2) ((float*)p.C2)[bidx * p.sC2 + gm * p.ldc2 + (wcol0 >> 6)] = second;
       }
-    } else if (p.act == 2) {
+    } else if (LM == -1 && p.act == 2) {
       // GEGLU pairs of 32 columns: [x | gate] -> 32 outputs; h (C) keeps both halves
       for (int it = 0; it < 4; ++it) {
         const int c = lane + 64 * it;          // 256 chunks of 8 = 32 rows x 8
@@ -186,10 +190,124 @@ __device__ __forceinline__ void epilogue(const P& p, f32x4 (&acc)[8][4], char* s
         *(u32x4*)(p.C2 + bidx * p.sC2 + gm * p.ldc2 + (wcol0 >> 1) + cc) = pack8(v);
       }
     } else {
+      // Every load this quarter's stores depend on (the residual, else the accumulate target)
+      // is issued first.  With the previous quarter's stores still pending, the compiler can
+      // only wait for a load with vmcnt(0) (read and write events retire out of order), so a
+      // load interleaved with the stores costs a full store round trip each: 4+ per quarter
+      // before (r02 ISA), one now.  The column gn = wcol0 + (lane & 7) * 8 is the same in all
+      // four row chunks, so the bias is loaded once.
+      const int64_t gn = wcol0 + (lane & 7) * 8;
+      const int cc = (lane & 7) * 8;
+      const bool pre_acc = LM == -1 && !p.R && p.accumulate;
+      if constexpr (LM == -2) {
+        // residual mode: C (f32) = alpha acc + bias + R (f32), bf16 shadow into C2 when given
+        // unconditional loads (rows / columns clamped into the matrix, results of clamped
+        // chunks unused): a load under a branch must complete before its phi copy, which put a
+        // vmcnt(0) behind every pair
+        f32x4 ra[4], rb[4];
+        const int64_t gnc = min(gn, p.N - 8);
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          const int64_t gm = min(rbase + ((lane + 64 * it) >> 3), p.M - 1);
+          const float* Rp = (const float*)p.R + bidx * p.sR + gm * p.ldr + gnc;
+          ra[it] = *(const f32x4*)Rp;
+          rb[it] = *(const f32x4*)(Rp + 4);
+        }
+        f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
+        if (p.bias) {
+          b0 = *(const f32x4*)(p.bias + gnc);
+          b1 = *(const f32x4*)(p.bias + gnc + 4);
+        }
+        // wave-uniform: the wave's 32 x 64 quarter lies inside the matrix (every tile of the
+        // 3D-ViT's residual GEMMs), so the stores run without per-lane branches -- a divergent
+        // branch around each store group made the compiler drain vmcnt at every block boundary
+        const bool full = rbase + 32 <= p.M && wcol0 + 64 <= p.N;
+        auto row_out = [&](int it) {
+          const int row = (lane + 64 * it) >> 3;
+          const int64_t gm = rbase + row;
+          const f32x4 lo = *(const f32x4*)(cs + row * EP_LD + cc);
+          const f32x4 hi = *(const f32x4*)(cs + row * EP_LD + cc + 4);
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[j] = lo[j] * p.alpha + b0[j] + ra[it][j];
+            v[4 + j] = hi[j] * p.alpha + b1[j] + rb[it][j];
+          }
+          float* Cf = (float*)p.C + bidx * p.sC + gm * p.ldc + gn;
+          *(f32x4*)Cf = f32x4{v[0], v[1], v[2], v[3]};
+          *(f32x4*)(Cf + 4) = f32x4{v[4], v[5], v[6], v[7]};
+          if (p.C2) *(u32x4*)(p.C2 + bidx * p.sC2 + gm * p.ldc2 + gn) = pack8(v);
+        };
+        if (full) {
+          // phase by phase (all LDS reads, all math, all stores), so the four chunks' store
+          // operands occupy distinct registers and no store waits for an earlier one to drain
+          f32x4 lo[4], hi[4];
+#pragma unroll
+          for (int it = 0; it < 4; ++it) {
+            const int row = (lane + 64 * it) >> 3;
+            lo[it] = *(const f32x4*)(cs + row * EP_LD + cc);
+            hi[it] = *(const f32x4*)(cs + row * EP_LD + cc + 4);
+          }
+#pragma unroll
+          for (int it = 0; it < 4; ++it)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              lo[it][j] = lo[it][j] * p.alpha + b0[j] + ra[it][j];
+              hi[it][j] = hi[it][j] * p.alpha + b1[j] + rb[it][j];
+            }
+#pragma unroll
+          for (int it = 0; it < 4; ++it) {
+            float* Cf = (float*)p.C + bidx * p.sC + (rbase + ((lane + 64 * it) >> 3)) * p.ldc + gn;
+            *(f32x4*)Cf = lo[it];
+            *(f32x4*)(Cf + 4) = hi[it];
+          }
+          if (p.C2) {
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+              const float v[8] = {lo[it][0], lo[it][1], lo[it][2], lo[it][3], hi[it][0], hi[it][1], hi[it][2], hi[it][3]};
+              *(u32x4*)(p.C2 + bidx * p.sC2 + (rbase + ((lane + 64 * it) >> 3)) * p.ldc2 + gn) = pack8(v);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int it = 0; it < 4; ++it)
+            if (rbase + ((lane + 64 * it) >> 3) < p.M && gn < p.N) row_out(it);
+        }
+      } else {
+      f32x4 ra[4], rb[4];
+#pragma unroll
       for (int it = 0; it < 4; ++it) {
-        const int c = lane + 64 * it;
-        const int row = c >> 3, cc = (c & 7) * 8;
-        const int64_t gm = rbase + row, gn = wcol0 + cc;
+        const int row = (lane + 64 * it) >> 3;
+        const int64_t gm = rbase + row;
+        ra[it] = rb[it] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (slab || gm >= p.M || gn >= p.N) continue;
+        if (LM == -1 && p.R) {
+          if (p.r_f32) {
+            const float* Rp = (const float*)p.R + bidx * p.sR + gm * p.ldr + gn;
+            ra[it] = *(const f32x4*)Rp;
+            rb[it] = *(const f32x4*)(Rp + 4);
+          } else {
+            ra[it] = __builtin_bit_cast(f32x4, *(const u32x4*)((const u16*)p.R + bidx * p.sR + gm * p.ldr + gn));
+          }
+        } else if (pre_acc) {
+          if (p.c_f32) {
+            const float* Cf = (const float*)p.C + bidx * p.sC + gm * p.ldc + gn;
+            ra[it] = *(const f32x4*)Cf;
+            rb[it] = *(const f32x4*)(Cf + 4);
+          } else {
+            ra[it] = __builtin_bit_cast(f32x4, *(const u32x4*)((const u16*)p.C + bidx * p.sC + gm * p.ldc + gn));
+          }
+        }
+      }
+      f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
+      if (p.bias && !slab && gn < p.N) {
+        b0 = *(const f32x4*)(p.bias + gn);
+        b1 = *(const f32x4*)(p.bias + gn + 4);
+      }
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int row = (lane + 64 * it) >> 3;
+        const int64_t gm = rbase + row;
         if (gm >= p.M || gn >= p.N) continue;
         float v[8];
         const f32x4 lo = *(const f32x4*)(cs + row * EP_LD + cc);
@@ -202,20 +320,15 @@ __device__ __forceinline__ void epilogue(const P& p, f32x4 (&acc)[8][4], char* s
           *(f32x4*)(Cf + 4) = f32x4{v[4], v[5], v[6], v[7]};
           continue;
         }
-        if (p.bias) {
-          const f32x4 b0 = *(const f32x4*)(p.bias + gn), b1 = *(const f32x4*)(p.bias + gn + 4);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) { v[j] += b0[j]; v[4 + j] += b1[j]; }
-        }
+        for (int j = 0; j < 4; ++j) { v[j] += b0[j]; v[4 + j] += b1[j]; }
         if (p.R) {
           if (p.r_f32) {
-            const float* Rp = (const float*)p.R + bidx * p.sR + gm * p.ldr + gn;
-            const f32x4 a = *(const f32x4*)Rp, b = *(const f32x4*)(Rp + 4);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) { v[j] += a[j]; v[4 + j] += b[j]; }
+            for (int j = 0; j < 4; ++j) { v[j] += ra[it][j]; v[4 + j] += rb[it][j]; }
           } else {
             float rr[8];
-            unpack8(*(const u32x4*)((const u16*)p.R + bidx * p.sR + gm * p.ldr + gn), rr);
+            unpack8(__builtin_bit_cast(u32x4, ra[it]), rr);
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] += rr[j];
           }
@@ -228,7 +341,8 @@ __device__ __forceinline__ void epilogue(const P& p, f32x4 (&acc)[8][4], char* s
         if (p.c_f32) {
           float* Cf = (float*)p.C + bidx * p.sC + gm * p.ldc + gn;
           if (p.accumulate) {
-            const f32x4 a = *(const f32x4*)Cf, b = *(const f32x4*)(Cf + 4);
+            const f32x4 a = pre_acc ? ra[it] : *(const f32x4*)Cf;
+            const f32x4 b = pre_acc ? rb[it] : *(const f32x4*)(Cf + 4);
 #pragma unroll
             for (int j = 0; j < 4; ++j) { v[j] += a[j]; v[4 + j] += b[j]; }
           }
@@ -238,13 +352,14 @@ __device__ __forceinline__ void epilogue(const P& p, f32x4 (&acc)[8][4], char* s
           u16* Cb = (u16*)p.C + bidx * p.sC + gm * p.ldc + gn;
           if (p.accumulate) {
             float rr[8];
-            unpack8(*(const u32x4*)Cb, rr);
+            unpack8(pre_acc ? __builtin_bit_cast(u32x4, ra[it]) : *(const u32x4*)Cb, rr);
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[j] += rr[j];
           }
           *(u32x4*)Cb = pack8(v);
         }
         if (p.C2 && p.act == 0) *(u32x4*)(p.C2 + bidx * p.sC2 + gm * p.ldc2 + gn) = pack8(v);
+      }
       }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);   // reads of this half done before it is overwritten
@@ -896,7 +1011,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
       epilogue_t<0>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
     } else {
       // staging in buffer O and beyond (the next tile's tile 0 is landing in E)
-      epilogue(p, acc, smem + TILEB, w, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
+      epilogue<EP == -2 || EP == -3 || EP == -5 ? EP : -1>(p, acc, smem + TILEB, w, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
     }
     STAMP(4, __builtin_amdgcn_s_memtime());
     ++tcount;
@@ -982,7 +1097,12 @@ int launch8_ep(const P& p, int batch, hipStream_t st) {
   static int tr_f32 = -1;
   if (tr_f32 < 0) { const char* e = getenv("CTCLIP_GEMM_TR_F32"); tr_f32 = e ? atoi(e) != 0 : 0; }
   const bool tr = (tr_f32 || (!p.c_f32 && !p.R)) && p.split_k <= 1 && p.act != 3;
-  if (!tr) return launch8<AK, BKC, -1>(p, batch, st);
+  if (!tr) {
+    if (p.act == 3) return launch8<AK, BKC, -3>(p, batch, st);
+    if (p.split_k > 1) return launch8<AK, BKC, -5>(p, batch, st);   // slabs: alpha only
+    if (p.R && p.r_f32 && p.c_f32 && p.act == 0 && !p.accumulate) return launch8<AK, BKC, -2>(p, batch, st);
+    return launch8<AK, BKC, -1>(p, batch, st);
+  }
   if (p.act == 2) return launch8<AK, BKC, 2>(p, batch, st);
   return launch8<AK, BKC, 0>(p, batch, st);
 }

@@ -60,6 +60,26 @@ def test_nt_bias_residual(K, M, N, Kd):
     assert torch.equal(outs[8], outs[1])
 
 
+@pytest.mark.parametrize('M,N,Kd,ak', [(110592 // 8, 512, 256, True), (5000, 768, 512, True), (9000, 512, 512, False)])
+def test_residual_f32_with_bf16_shadow(K, M, N, Kd, ak):
+    """The residual epilogue (f32 out = acc + R, bf16 shadow in C2; gemm256.hip LM -2): full and
+    ragged tiles, both A layouts; the shadow is the f32 output rounded to bf16, bit for bit."""
+    torch.manual_seed(1)
+    x = torch.randn(M, Kd, device='cuda').bfloat16()
+    w = torch.randn(N, Kd, device='cuda').bfloat16()
+    r = torch.randn(M, N, device='cuda')
+    out = torch.empty(M, N, device='cuda')
+    sh = torch.empty(M, N, device='cuda', dtype=torch.bfloat16)
+    if ak:
+        K.linear(x, w, residual=r, out_dtype=torch.float32, out=out, out2=sh)
+    else:
+        xt = x.t().contiguous()      # A stored M-contiguous (the dW-style layout)
+        K._gemm_raw(M, N, Kd, xt, M, False, w, Kd, True, out, N, R=r, ldr=N, C2=sh, ldc2=N)
+    ref = x.float() @ w.float().t() + r
+    assert _rel(out, ref) < 1e-5
+    assert torch.equal(sh, out.bfloat16())
+
+
 @pytest.mark.parametrize('ak,bk', [(True, False), (False, True), (False, False)])
 def test_layouts(K, ak, bk):
     torch.manual_seed(1)

@@ -31,12 +31,20 @@ def main():
     w1, w2, wq, wkv = r(2816, 512), r(512, 1408), r(256, 512), r(512, 512)
     g = torch.empty(M, 1408, device='cuda', dtype=torch.bfloat16)
     res = torch.randn(M, 512, device='cuda')
+    x256, wo = r(M, 256), r(512, 256)
+    xo = torch.empty(M, 512, device='cuda', dtype=torch.bfloat16)
     dh = r(M, 2816)
     cases = [
         ('FF1 NT+GEGLU  110592x2816x512', lambda: K.linear(x512, w1, act=K.ACT_GEGLU, out2=g), 2 * M * 2816 * 512),
         ('FF1 NT plain  110592x2816x512', lambda: K.linear(x512, w1, out=dh), 2 * M * 2816 * 512),
         ('FF2 NT+res32  110592x512x1408', lambda: K.linear(x1408, w2, residual=res, out_dtype=torch.float32),
          2 * M * 512 * 1408),
+        ('FF2 NT+res32+C2 110592x512x1408', lambda: K.linear(x1408, w2, residual=res, out_dtype=torch.float32,
+                                                             out2=xo), 2 * M * 512 * 1408),
+        ('Wo  NT+res32+C2 110592x512x256', lambda: K.linear(x256, wo, residual=res, out_dtype=torch.float32,
+                                                            out2=xo), 2 * M * 512 * 256),
+        ('dX  NN+res32  110592x512x512', lambda: K.matmul_nn(x512, wkv, residual=res, out_dtype=torch.float32),
+         2 * M * 512 * 512),
         ('Q   NT        110592x256x512', lambda: K.linear(x512, wq), 2 * M * 256 * 512),
         ('KV  NT        110592x512x512', lambda: K.linear(x512, wkv), 2 * M * 512 * 512),
         ('dX  NN        110592x512x2816', lambda: K.matmul_nn(dh, w1), 2 * M * 512 * 2816),
@@ -50,7 +58,10 @@ def main():
     ]
     from ctclip_mi355x import _lib
     variants = [v for v in os.environ.get('GEMM_VARIANTS', '8,1').split(',')]
+    only = [o for o in os.environ.get('GEMM_ONLY', '').split(',') if o]
     for name, fn, fl in cases:
+        if only and not any(o in name for o in only):
+            continue
         row = []
         for v in variants:   # '8' or '8s<stagger>', 'n' suffix = not persistent
             vv, _, st = v.rstrip('n').partition('s')
