@@ -835,7 +835,20 @@ __device__ __forceinline__ Tile tile_at(const P& p, int lin, int gx, int gy, int
     const int xcd = lin & 7, q = ntiles >> 3, r = ntiles & 7;
     id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (lin >> 3);
   }
-  const int gxy = gx * gy, z = id / gxy, rem = id - z * gxy, ty = rem / gx, tx = rem - ty * gx;
+  const int gxy = gx * gy, z = id / gxy, rem = id - z * gxy;
+  int ty, tx;
+  if (gx >= 16) {
+    // wide N (the VQ distance GEMM: 32 codebook tiles = 8 MB): groups of 8 tile rows walked
+    // column by column, so an XCD's ~32 concurrent tiles touch 8 A panels + 4 B panels (3 MB,
+    // L2-resident) instead of 1 A panel + the whole codebook streamed through its 4 MB L2
+    constexpr int GM = 8;
+    const int grp = rem / (GM * gx), y0 = grp * GM, gsz = min(gy - y0, GM), r = rem - grp * GM * gx;
+    ty = y0 + r % gsz;
+    tx = r / gsz;
+  } else {
+    ty = rem / gx;
+    tx = rem - ty * gx;
+  }
   Tile t;
   t.split = z % p.split_k;
   t.bidx = z / p.split_k;
@@ -1009,6 +1022,8 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
       epilogue_geglu_bwd(p, acc, wr, wc, lane, T.m0, T.n0, T.bidx);
     } else if constexpr (EP == 0) {
       epilogue_t<0>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
+    } else if constexpr (EP == 3) {
+      epilogue_t<3>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
     } else {
       // staging in buffer O and beyond (the next tile's tile 0 is landing in E)
       epilogue<EP == -2 || EP == -3 || EP == -5 ? EP : -1>(p, acc, smem + TILEB, w, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
@@ -1098,6 +1113,11 @@ int launch8_ep(const P& p, int batch, hipStream_t st) {
   if (tr_f32 < 0) { const char* e = getenv("CTCLIP_GEMM_TR_F32"); tr_f32 = e ? atoi(e) != 0 : 0; }
   const bool tr = (tr_f32 || (!p.c_f32 && !p.R)) && p.split_k <= 1 && p.act != 3;
   if (!tr) {
+    // the argmax through the transposed (LDS-free) epilogue: VQ distance GEMM 1.73 -> 1.56 ms (r02);
+    // CTCLIP_GEMM_ARGMAX_TR=0: the LDS-staged one (A/B)
+    static int am_tr = -1;
+    if (am_tr < 0) { const char* e = getenv("CTCLIP_GEMM_ARGMAX_TR"); am_tr = e ? atoi(e) != 0 : 1; }
+    if (p.act == 3 && am_tr && p.split_k <= 1) return launch8<AK, BKC, 3>(p, batch, st);
     if (p.act == 3) return launch8<AK, BKC, -3>(p, batch, st);
     if (p.split_k > 1) return launch8<AK, BKC, -5>(p, batch, st);   // slabs: alpha only
     if (p.R && p.r_f32 && p.c_f32 && p.act == 0 && !p.accumulate) return launch8<AK, BKC, -2>(p, batch, st);

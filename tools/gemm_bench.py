@@ -33,6 +33,9 @@ def main():
     res = torch.randn(M, 512, device='cuda')
     x256, wo = r(M, 256), r(512, 256)
     xo = torch.empty(M, 512, device='cuda', dtype=torch.bfloat16)
+    cb = r(8192, 512)
+    cand = torch.empty(M, 128, 2, device='cuda')
+    cand2 = torch.empty(M, 128, device='cuda')
     dh = r(M, 2816)
     cases = [
         ('FF1 NT+GEGLU  110592x2816x512', lambda: K.linear(x512, w1, act=K.ACT_GEGLU, out2=g), 2 * M * 2816 * 512),
@@ -45,6 +48,8 @@ def main():
                                                             out2=xo), 2 * M * 512 * 256),
         ('dX  NN+res32  110592x512x512', lambda: K.matmul_nn(x512, wkv, residual=res, out_dtype=torch.float32),
          2 * M * 512 * 512),
+        ('VQ  NT argmax 110592x8192x512', lambda: K.gemm_raw(M, 8192, 512, x512, 512, True, cb, 512, True, cand, 128,
+                                                          C2=cand2, ldc2=128, act=K.ACT_ARGMAX), 2 * M * 8192 * 512),
         ('Q   NT        110592x256x512', lambda: K.linear(x512, wq), 2 * M * 256 * 512),
         ('KV  NT        110592x512x512', lambda: K.linear(x512, wkv), 2 * M * 512 * 512),
         ('dX  NN        110592x512x2816', lambda: K.matmul_nn(dh, w1), 2 * M * 512 * 2816),
