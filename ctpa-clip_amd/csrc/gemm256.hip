@@ -42,6 +42,7 @@ struct P {
   int64_t sA, sB, sC, sC2, sR;
   int64_t kper;
   int debug;     // diagnostic knob (CTCLIP_G256_DEBUG): 1 = skip the epilogue, 2 = skip the main loop
+  int group_gx;  // grouped (8-row) tile walk when the N tile count >= this (CTCLIP_GEMM_GROUP_GX, default 8)
   int stagger;   // start delay (s_sleep units of 64 cycles) for the second co-resident workgroup
   int gz;        // batch * split_k (8-phase tile count = ceil(N/256) * ceil(M/256) * gz)
   int persist;   // 8-phase: persistent workgroups (one per CU) walking the tile sequence
@@ -837,7 +838,7 @@ __device__ __forceinline__ Tile tile_at(const P& p, int lin, int gx, int gy, int
   }
   const int gxy = gx * gy, z = id / gxy, rem = id - z * gxy;
   int ty, tx;
-  if (gx >= 16) {
+  if (gx >= p.group_gx) {
     // wide N (the VQ distance GEMM: 32 codebook tiles = 8 MB): groups of 8 tile rows walked
     // column by column, so an XCD's ~32 concurrent tiles touch 8 A panels + 4 B panels (3 MB,
     // L2-resident) instead of 1 A panel + the whole codebook streamed through its 4 MB L2
@@ -1166,6 +1167,9 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   // 8-phase default: stagger only the GEGLU GEMM, whose epilogue (h + g stores + erf) is long
   // enough that desynchronised CUs pay off (r01 sweep: 0.52 -> 0.48 ms at B = 8; neutral to
   // slightly negative on the plain / residual epilogues)
+  static int ggx = -1;
+  if (ggx < 0) { const char* e = getenv("CTCLIP_GEMM_GROUP_GX"); ggx = e ? atoi(e) : 8; }   // r02: FF1 (11 tiles) -2%, VQ (32) -17%; N <= 6 tiles: neutral to +4% (not grouped)
+  p.group_gx = ggx;
   p.stagger = variant() == 8 ? (g_stagger8 >= 0 ? g_stagger8 : (a->act == 2 ? 4 : 0)) : (tile_rows() == 1 ? stag : 0);
   hipStream_t st = (hipStream_t)stream;
   if (variant() == 8 || a->act == 4)
