@@ -229,12 +229,27 @@ __device__ __forceinline__ void plane_store(char* ring, int W, int tp, const u32
 }
 
 // forward (TR = 0) or input-gradient (TR = 1); grid (B * ceil(H/HT), D/64), TNTH threads
-template <int TR>
+// GK > 0: the geometry is the compile-time cube T = H = W = GK with index map MD (the 3D-ViT's
+// 24^3 token grid in both transformers), so every division of the plane / row index maps is by
+// a constant (the runtime form spends most of its issue slots on integer divisions)
+template <int GK, int MD>
+__device__ __forceinline__ void fix_geo(Geo& g) {
+  if constexpr (GK > 0) {
+    g.T = GK;
+    g.H = GK;
+    g.W = GK;
+    g.thw = GK * GK * GK;
+    g.mode = MD;
+  }
+}
+
+template <int TR, int GK = 0, int MD = 0>
 __global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ xin, int D,
                                                         const float* __restrict__ w, const float* __restrict__ bias,
                                                         const float* __restrict__ res, Geo g,
                                                         float* __restrict__ out, u16* __restrict__ outb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  fix_geo<GK, MD>(g);
   const int nht = (g.H + HT - 1) / HT;
   const int b = blockIdx.x / nht, h0 = (blockIdx.x - b * nht) * HT, c0 = blockIdx.y * 64;
   const int pb = plane_bytes(g.W);
@@ -345,10 +360,12 @@ __global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ 
 // weight/bias gradient: grid (B * ceil(H/HT), D/64), WNTH threads; thread = (row, w-segment of
 // SEGW, channel pair); part[blockIdx.x][c][28] (27 taps in (kt,kh,kw) order, then bias).
 // Channel pairs keep the 27 x 2 accumulators + windows under 128 VGPRs (4 waves/SIMD).
+template <int GK = 0, int MD = 0>
 __global__ __launch_bounds__(WNTH, 3) void peg_wgrad_tile_kernel(const u16* __restrict__ dout,
                                                               const u16* __restrict__ xin, int D, Geo g,
                                                               float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  fix_geo<GK, MD>(g);
   const int nht = (g.H + HT - 1) / HT;
   const int b = blockIdx.x / nht, h0 = (blockIdx.x - b * nht) * HT, c0 = blockIdx.y * 64;
   const int pb = plane_bytes(g.W);
@@ -464,11 +481,33 @@ bool s_tile_attr = false;
 void tile_attrs() {
   if (s_tile_attr) return;
   // up to W = 30: 4 x 4 x 32 x 128 B + weights = 72 KB
-  (void)hipFuncSetAttribute((const void*)peg_tile_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-  (void)hipFuncSetAttribute((const void*)peg_tile_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-  (void)hipFuncSetAttribute((const void*)peg_wgrad_tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            80 * 1024);
+  const void* ks[] = {(const void*)peg_tile_kernel<0>,         (const void*)peg_tile_kernel<1>,
+                      (const void*)peg_tile_kernel<0, 24, 0>,  (const void*)peg_tile_kernel<0, 24, 1>,
+                      (const void*)peg_tile_kernel<1, 24, 0>,  (const void*)peg_tile_kernel<1, 24, 1>,
+                      (const void*)peg_wgrad_tile_kernel<>,    (const void*)peg_wgrad_tile_kernel<24, 0>,
+                      (const void*)peg_wgrad_tile_kernel<24, 1>};
+  for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
   s_tile_attr = true;
+}
+
+// the compile-time 24^3 instantiations (CTCLIP_PEG_FIXED=0: the runtime-geometry kernels, A/B)
+bool fixed24(const Geo& g) {
+  static int on = -1;
+  if (on < 0) { const char* e = getenv("CTCLIP_PEG_FIXED"); on = e ? atoi(e) != 0 : 1; }
+  return on && g.T == 24 && g.H == 24 && g.W == 24 && (g.mode == 0 || g.mode == 1);
+}
+
+template <int TR>
+void launch_tile(dim3 grid, size_t smem, hipStream_t st, const u16* x, int D, const float* w, const float* bias,
+                 const float* res, const Geo& g, float* out, u16* outb) {
+  if (fixed24(g)) {
+    if (g.mode == 0)
+      hipLaunchKernelGGL((peg_tile_kernel<TR, 24, 0>), grid, dim3(TNTH), smem, st, x, D, w, bias, res, g, out, outb);
+    else
+      hipLaunchKernelGGL((peg_tile_kernel<TR, 24, 1>), grid, dim3(TNTH), smem, st, x, D, w, bias, res, g, out, outb);
+    return;
+  }
+  hipLaunchKernelGGL((peg_tile_kernel<TR>), grid, dim3(TNTH), smem, st, x, D, w, bias, res, g, out, outb);
 }
 
 }  // namespace
@@ -488,8 +527,8 @@ extern "C" int ctclip_peg_fwd(const void* x_bf16, const float* x_f32, int64_t B,
   if (tiled_ok(W, D)) {
     tile_attrs();
     dim3 grid(B * ((H + HT - 1) / HT), D / 64);
-    hipLaunchKernelGGL(peg_tile_kernel<0>, grid, dim3(TNTH), tile_smem(W), (hipStream_t)stream, (const u16*)x_bf16,
-                       D, weight, bias, x_f32, g, out_f32, (u16*)out_bf16);
+    launch_tile<0>(grid, tile_smem(W), (hipStream_t)stream, (const u16*)x_bf16, D, weight, bias, x_f32, g, out_f32,
+                   (u16*)out_bf16);
   } else {
     dim3 grid(cdiv(ntok, 32), cdiv(D, 64));
     hipLaunchKernelGGL(peg_kernel<0>, grid, dim3(256), 0, (hipStream_t)stream, (const u16*)x_bf16, ntok, D, weight,
@@ -510,8 +549,8 @@ extern "C" int ctclip_peg_bwd_data(const void* dout_bf16, const float* dout_f32,
   if (tiled_ok(W, D)) {
     tile_attrs();
     dim3 grid(B * ((H + HT - 1) / HT), D / 64);
-    hipLaunchKernelGGL(peg_tile_kernel<1>, grid, dim3(TNTH), tile_smem(W), (hipStream_t)stream,
-                       (const u16*)dout_bf16, D, weight, (const float*)nullptr, dout_f32, g, dx_f32, (u16*)dx_bf16);
+    launch_tile<1>(grid, tile_smem(W), (hipStream_t)stream, (const u16*)dout_bf16, D, weight, (const float*)nullptr,
+                   dout_f32, g, dx_f32, (u16*)dx_bf16);
   } else {
     dim3 grid(cdiv(ntok, 32), cdiv(D, 64));
     hipLaunchKernelGGL(peg_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, (const u16*)dout_bf16, ntok, D,
@@ -531,8 +570,16 @@ extern "C" int ctclip_peg_bwd_weight(const void* dout_bf16, const void* x_bf16, 
   if (tiled_ok(W, D)) {
     tile_attrs();
     dim3 grid(nblk, D / 64);
-    hipLaunchKernelGGL(peg_wgrad_tile_kernel, grid, dim3(WNTH), wgrad_smem(W), (hipStream_t)stream, (const u16*)dout_bf16,
-                       (const u16*)x_bf16, D, g, part);
+    const hipStream_t st = (hipStream_t)stream;
+    if (fixed24(g) && g.mode == 0)
+      hipLaunchKernelGGL((peg_wgrad_tile_kernel<24, 0>), grid, dim3(WNTH), wgrad_smem(W), st, (const u16*)dout_bf16,
+                         (const u16*)x_bf16, D, g, part);
+    else if (fixed24(g))
+      hipLaunchKernelGGL((peg_wgrad_tile_kernel<24, 1>), grid, dim3(WNTH), wgrad_smem(W), st, (const u16*)dout_bf16,
+                         (const u16*)x_bf16, D, g, part);
+    else
+      hipLaunchKernelGGL((peg_wgrad_tile_kernel<>), grid, dim3(WNTH), wgrad_smem(W), st, (const u16*)dout_bf16,
+                         (const u16*)x_bf16, D, g, part);
   } else {
     const int64_t per = (ntok + nblk - 1) / nblk;
     dim3 grid(nblk, cdiv(D, 64));

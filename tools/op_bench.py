@@ -52,6 +52,7 @@ def main():
         ('peg_fwd mode0', lambda: K.peg_fwd(xb, xf, 8, 24, 24, 24, w, pb, 0), M * D * (2 + 4 + 4 + 2)),
         ('peg_fwd mode1', lambda: K.peg_fwd(xb, xf, 8, 24, 24, 24, w, pb, 1), M * D * (2 + 4 + 4 + 2)),
         ('peg_bwd (data+w)', lambda: K.peg_bwd(xb, xf, xb, 8, 24, 24, 24, w, 0), M * D * (2 + 4 + 4 + 2 + 4)),
+        ('peg_bwd mode1 (data+w)', lambda: K.peg_bwd(xb, xf, xb, 8, 24, 24, 24, w, 1), M * D * (2 + 4 + 4 + 2 + 4)),
         ('peg_bwd data only', lambda: K.call('ctclip_peg_bwd_data', K.ptr(xb), K.ptr(xf), 8, 24, 24, 24, D,
                                              K.ptr(w), 0, K.ptr(dxf), K.ptr(dxb), K.stream_ptr()),
          M * D * (2 + 4 + 4 + 2)),
@@ -71,7 +72,10 @@ def main():
     vol = torch.randint(-1200, 1201, (8, 1, 240, 480, 480), device='cuda', dtype=torch.int32).to(torch.int16)
     offs = layers.patch_offsets(1, 10, 20, 20, 480, 480).cuda()
     cases.append(('patch_ln int16->bf16', lambda: K.patch_ln(vol, True, 10, 20, offs), vol.numel() * 4))
+    only = [o for o in os.environ.get('OP_ONLY', '').split(',') if o]
     for name, fn, nbytes in cases:
+        if only and not any(o in name for o in only):
+            continue
         ms = timeit(fn)
         print(f'{name:24s} {ms * 1e3:9.1f} us  {nbytes / ms / 1e9:7.2f} TB/s (algorithmic bytes)', flush=True)
 
