@@ -37,7 +37,10 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--batch', type=int, default=8, help='volume/report pairs per GPU (configs[1]: 8)')
+    ap.add_argument('--batch', type=int, default=None,
+                    help='volume/report pairs per GPU (configs[1]: 8; configs[3] with --fp8: 16)')
+    ap.add_argument('--fp8', action='store_true',
+                    help='configs[3]: the 3D-ViT forward linears as MX-fp8 GEMMs (default batch 16 per GPU)')
     ap.add_argument('--text-len', type=int, default=128)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-batch', type=int, default=2)
@@ -120,6 +123,8 @@ def launch_ranks(args):
 
 def main():
     args = parse()
+    if args.batch is None:
+        args.batch = 16 if args.fp8 else 8
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
         launch_ranks(args)
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -141,6 +146,9 @@ def main():
     from ctclip_mi355x.trainer import CTClipTrainer
     from ctclip_mi355x import kernels as K
 
+    if args.fp8:
+        from ctclip_mi355x import functional as Fn
+        Fn.set_vit_fp8(True)
     torch.manual_seed(0)   # identical random-init weights on every rank
     model = set_finetune_trainable(build_ctclip()).to(dev)
     model.train()
@@ -208,14 +216,16 @@ def main():
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
-        'dtype': 'bf16',
+        'dtype': 'mx-fp8 e4m3 (3D-ViT forward linears) + bf16' if args.fp8 else 'bf16',
         'data': 'synthetic: int16 HU volumes 1x240x480x480 (randint -1200..1200) + 128-token reports; '
                 'random-init CT-CLIP base weights',
         'config': {'workload': 'CT-CLIP base contrastive train step: BERT-base(128 tok, train-mode dropout '
                                '0.1) + CTViT(480^2x240, patch 20x20x10, 4+4 layers, VQ 8192) + InfoNCE + bwd + RCCL grad all-reduce + '
                                'clip 0.5 + Adam',
                    'per_gpu_batch': args.batch, 'global_batch': world * args.batch, 'text_len': args.text_len,
-                   'parallelism': f'dp{world}', 'infonce_negatives': 'global batch (RCCL all-gather)'},
+                   'parallelism': f'dp{world}', 'infonce_negatives': 'global batch (RCCL all-gather)',
+                   **({'precision': 'configs[3]: Q / KV / attn-out / FF1+GEGLU / FF2 forward GEMMs MX-fp8 '
+                                    '(e4m3, e8m0 per 32 k), backward bf16'} if args.fp8 else {})},
         'loss': round(loss_v, 5),
     }
     if in_sync is not None:

@@ -7,7 +7,8 @@
 // (8 = emax of e4m3), element = sat_448(RNE(x * 2^-X)), scale byte = X + 127.  k in [K, Kp) is
 // zero-filled so the GEMM's K only needs to be a multiple of 128.
 //
-// GEMM: C[M,N] = alpha * (A . B^T) (+ bias), A [M][Kp] and B [N][Kp] fp8 K-contiguous with their
+// GEMM: C[M,N] = alpha * (A . B^T) (+ bias) (+ f32 residual, bf16 copy; or the GEGLU epilogue of
+// the 8-phase bf16 kernel), A [M][Kp] and B [N][Kp] fp8 K-contiguous with their
 // scale planes [rows][Kp/32].  Tile 128x128x128 (k in elements = bytes), 256 threads = 2x2 waves,
 // each wave a 64x64 block of 4x4 v_mfma_scale_f32_16x16x128_f8f6f4 (2x the bf16 MFMA rate per
 // clock on gfx950).  Operand lane map (tools/mx_probe.hip, found on the GPU with integer data):
@@ -102,6 +103,9 @@ struct P {
   const uint8_t* B; int64_t ldb; const uint8_t* sB;
   void* C; int64_t ldc; int c_f32;
   const float* bias; float alpha;
+  const float* R; int64_t ldr;     // f32 residual added after bias (or null)
+  u16* C2; int64_t ldc2;           // act 0: bf16 copy of C; act 2: the GEGLU output g
+  int act;                         // 0 none, 2 GEGLU over 32-column [x | gate] pairs (bf16 C = h)
 };
 
 __device__ __forceinline__ void xcd_remap(int& tx, int& ty) {
@@ -250,6 +254,27 @@ __global__ __launch_bounds__(NTH, BM == 128 ? 2 : 1) void mx_gemm_kernel(P p) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += j < nv ? p.bias[gn + j] : 0.f;
       }
+      if (p.act == 2) {
+        // GEGLU (the 8-phase kernel's rule): h keeps both halves (bf16), g = gelu(gate) x from the
+        // bf16-rounded x and gate; chunks in the x half of a 64-column group write g's 8 columns
+        *(u32x4*)((u16*)p.C + gm * p.ldc + gn) = pack8(v);
+        if ((cc & 63) < 32) {
+          const f32x4 glo = *(const f32x4*)(cs + row * CS_LD + cc + 32);
+          const f32x4 ghi = *(const f32x4*)(cs + row * CS_LD + cc + 36);
+          const float gt[8] = {glo[0], glo[1], glo[2], glo[3], ghi[0], ghi[1], ghi[2], ghi[3]};
+          float gg[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) gg[j] = gelu_erf(bf2f(f2bf(gt[j] * p.alpha))) * bf2f(f2bf(v[j]));
+          *(u32x4*)(p.C2 + gm * p.ldc2 + (gn >> 6) * 32 + (gn & 63)) = pack8(gg);
+        }
+        continue;
+      }
+      if (p.R) {
+        const float* Rp = p.R + gm * p.ldr + gn;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] += j < nv ? Rp[j] : 0.f;
+      }
+      if (p.C2 && vec && nv == 8) *(u32x4*)(p.C2 + gm * p.ldc2 + gn) = pack8(v);
       if (vec && nv == 8) {
         if (p.c_f32) {
           float* Cf = (float*)p.C + gm * p.ldc + gn;
@@ -306,8 +331,12 @@ extern "C" int ctclip_gemm_mxfp8(const ctclip_mx_gemm_args* a, void* stream) {
   CT_REQUIRE(((uintptr_t)a->A & 15) == 0 && ((uintptr_t)a->B & 15) == 0 && ((uintptr_t)a->C & 15) == 0, CT_EALIGN);
   CT_REQUIRE(((uintptr_t)a->sA & 3) == 0 && ((uintptr_t)a->sB & 3) == 0, CT_EALIGN);
   if (a->M == 0 || a->N == 0) return 0;
+  CT_REQUIRE(a->act == 0 || a->act == 2, CT_EINVAL);
+  if (a->act == 2) CT_REQUIRE(a->C2 && !a->c_f32 && !a->R && !a->bias && a->N % 64 == 0 && a->ldc % 8 == 0 && a->ldc2 % 8 == 0, CT_ESHAPE);
+  if (a->C2 || a->R) CT_REQUIRE(a->ldc % 8 == 0 && a->N % 8 == 0, CT_ESHAPE);
+  if (a->C2) CT_REQUIRE(((uintptr_t)a->C2 & 15) == 0 && a->ldc2 % 8 == 0, CT_EALIGN);
   P p{a->M, a->N, a->Kp, (const uint8_t*)a->A, a->lda, (const uint8_t*)a->sA, (const uint8_t*)a->B, a->ldb,
-      (const uint8_t*)a->sB, a->C, a->ldc, a->c_f32, a->bias, a->alpha};
+      (const uint8_t*)a->sB, a->C, a->ldc, a->c_f32, a->bias, a->alpha, a->R, a->ldr, (u16*)a->C2, a->ldc2, a->act};
   const int bm = g_mx_tile ? g_mx_tile : 128;
   return bm == 256 ? mx_launch<256>(p, (hipStream_t)stream) : mx_launch<128>(p, (hipStream_t)stream);
 }

@@ -52,6 +52,9 @@ class MxGemmArgs(ctypes.Structure):
         ('B', c_vp), ('ldb', c_i64), ('sB', c_vp),
         ('C', c_vp), ('ldc', c_i64), ('c_f32', c_i32),
         ('bias', c_vp), ('alpha', c_f32),
+        ('R', c_vp), ('ldr', c_i64),
+        ('C2', c_vp), ('ldc2', c_i64),
+        ('act', c_i32),
     ]
 
 

@@ -140,6 +140,43 @@ def _adjacent(ts, arena_of):
     return arena_of(flat), off, o
 
 
+# ----------------------------------------------------------------------------- MX-fp8 (configs[3])
+# The 3D-ViT's five forward linears (Q, KV, attention out, FF1 + GEGLU, FF2) run as MX-fp8 GEMMs
+# (csrc/mxfp8.hip: e4m3 elements, one e8m0 scale per 32 k) when enabled: activations quantised per
+# call, weights once per optimizer update.  The backward stays bf16 on the same saved bf16
+# activations and weights.  SURVEY 8(c): compared to the build's own bf16 path, tolerance per test.
+_FP8 = {'on': False}
+_FP8_W = {}
+
+
+def set_vit_fp8(on):
+    """Switch the 3D-ViT forward linears to MX-fp8 (True) or bf16 (False); returns the previous."""
+    old = _FP8['on']
+    _FP8['on'] = bool(on)
+    return old
+
+
+def vit_fp8():
+    return _FP8['on']
+
+
+def fp8_weight(key, Wb):
+    """(q, scales) of the bf16 weight Wb, re-quantised when the optimizer has moved the weights."""
+    ep = K.weights_epoch()
+    e = _FP8_W.get(key)
+    if e is None or e[0] != ep or e[1] != Wb.data_ptr():
+        e = (ep, Wb.data_ptr()) + K.quant_mxfp8(Wb)
+        _FP8_W[key] = e
+    return e[2], e[3]
+
+
+def fp8_linear(x, key, Wb, **kw):
+    """x[M, K] (bf16) @ Wb[N, K]^T through the MX-fp8 GEMM (epilogue keywords of gemm_mxfp8)."""
+    qa, sa = K.quant_mxfp8(x)
+    qb, sb = fp8_weight(key, Wb)
+    return K.gemm_mxfp8(qa, sa, qb, sb, **kw)
+
+
 def bf_cat(ws):
     """bf16 of torch.cat(ws, 0): a view of the shadow arena when the weights are adjacent there
     (BERT's q / k / v, see bert.BertModel.param_order), else cat + cast."""
@@ -304,8 +341,13 @@ class ViTLayerFn(torch.autograd.Function):
         x1f, x1b = K.peg_fwd(xb, xf, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, peg_b, geo.mode)
         xn, _, m1, r1 = K.layernorm_fwd(x1f, norm_g, None, 1e-5)
         Wq_b, Wkv_b, Wo_b = bf(Wq), bf(Wkv), bf(Wo)
-        q = K.linear(xn, Wq_b)
-        kv = K.linear(x1b, Wkv_b)
+        fp8 = vit_fp8()
+        if fp8:
+            q = fp8_linear(xn, (id(Wq), 'q'), Wq_b)
+            kv = fp8_linear(x1b, (id(Wkv), 'kv'), Wkv_b)
+        else:
+            q = K.linear(xn, Wq_b)
+            kv = K.linear(x1b, Wkv_b)
         qn = K.l2norm_scale_fwd(q, H, dh, q_scale)
         kn = K.l2norm_scale_fwd(kv[:, :inner], H, dh, k_scale)
         L, nseq, seq = geo.seq()
@@ -313,15 +355,22 @@ class ViTLayerFn(torch.autograd.Function):
         o, lse = K.attn_fwd(qn, kn, kv[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
                             bias_u=bias_u if use_bias else None, grid=(geo.Hg, geo.Wg) if use_bias else (0, 0))
         x2b = torch.empty_like(xb)
-        x2f = K.linear(o, Wo_b, residual=x1f, out_dtype=F32, out2=x2b)
+        if fp8:
+            x2f = fp8_linear(o, (id(Wo), 'o'), Wo_b, residual=x1f, out_f32=True, out2=x2b)
+        else:
+            x2f = K.linear(o, Wo_b, residual=x1f, out_dtype=F32, out2=x2b)
         xn2, _, m2, r2 = K.layernorm_fwd(x2f, ff_w, ff_b, 1e-5)
         W1p, W2p = pack_ff1(W1), pack_ff2(W2)
         g = torch.empty(xf.shape[0], W2p.shape[1], device=xf.device, dtype=BF16)
-        # tagged for bench.py's live roofline: algorithmic flops exclude the zero padding rows
-        h = K.linear(xn2, W1p, act=K.ACT_GEGLU, out2=g, tag='ff1',
-                     flops=2.0 * xf.shape[0] * W1.shape[0] * W1.shape[1])
         x3b = torch.empty_like(xb)
-        x3f = K.linear(g, W2p, residual=x2f, out_dtype=F32, out2=x3b)
+        if fp8:
+            h = fp8_linear(xn2, (id(W1), 'ff1'), W1p, act=K.ACT_GEGLU, out2=g)
+            x3f = fp8_linear(g, (id(W2), 'ff2'), W2p, residual=x2f, out_f32=True, out2=x3b)
+        else:
+            # tagged for bench.py's live roofline: algorithmic flops exclude the zero padding rows
+            h = K.linear(xn2, W1p, act=K.ACT_GEGLU, out2=g, tag='ff1',
+                         flops=2.0 * xf.shape[0] * W1.shape[0] * W1.shape[1])
+            x3f = K.linear(g, W2p, residual=x2f, out_dtype=F32, out2=x3b)
         ctx.geo = geo
         ctx.use_bias = use_bias
         ctx.params = (peg_w, peg_b, norm_g, q_scale, k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1, W2)

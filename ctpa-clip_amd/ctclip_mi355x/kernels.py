@@ -682,16 +682,23 @@ def quant_mxfp8(x, Kp=None):
     return q, s
 
 
-def gemm_mxfp8(qa, sa, qb, sb, *, bias=None, alpha=1.0, out_f32=False, out=None):
-    """C[M, N] = alpha * dequant(qa) . dequant(qb)^T (+ bias) from quant_mxfp8 operands."""
+def gemm_mxfp8(qa, sa, qb, sb, *, bias=None, alpha=1.0, out_f32=False, out=None, residual=None, out2=None,
+               act=ACT_NONE):
+    """C[M, N] = alpha * dequant(qa) . dequant(qb)^T (+ bias) (+ f32 residual) from quant_mxfp8
+    operands; out2: bf16 copy of C, or with act=ACT_GEGLU the GEGLU output g [M, N/2] (C = h)."""
     M, Kp = qa.shape
     N = qb.shape[0]
     assert qb.shape[1] == Kp and sa.shape == (M, Kp // 32) and sb.shape == (N, Kp // 32)
+    assert act in (ACT_NONE, ACT_GEGLU)
     C = out if out is not None else torch.empty(M, N, device=qa.device,
                                                 dtype=torch.float32 if out_f32 else torch.bfloat16)
+    if residual is not None:
+        assert residual.dtype == torch.float32 and residual.shape == (M, N) and residual.stride(1) == 1
     a = _lib.MxGemmArgs(M=M, N=N, Kp=Kp, A=ptr(qa), lda=qa.stride(0), sA=ptr(sa), B=ptr(qb), ldb=qb.stride(0),
                         sB=ptr(sb), C=ptr(C), ldc=C.stride(0), c_f32=int(C.dtype == torch.float32),
-                        bias=ptr(bias), alpha=float(alpha))
+                        bias=ptr(bias), alpha=float(alpha), R=ptr(residual),
+                        ldr=residual.stride(0) if residual is not None else 0, C2=ptr(out2),
+                        ldc2=out2.stride(0) if out2 is not None else 0, act=int(act))
     call('ctclip_gemm_mxfp8', _lib.ctypes.byref(a), stream_ptr())
     return C
 

@@ -93,14 +93,18 @@ int ctclip_reduce_slabs_ep(const float* slabs, int64_t nslab, int64_t rows, int6
  * per 32 consecutive k.
  * quant: x [rows][K] (bf16, or f32 if x_f32) -> q [rows][Kp] e4m3 (ldq bytes, 16-B aligned),
  *   scales [rows][Kp/32] (X + 127 with X = floor(log2 amax) - 8); k in [K, Kp) zero; Kp % 128 == 0.
- * gemm: C[M][N] = alpha * (A . B^T) (+ bias[N]) in bf16 (or f32 if c_f32); A [M][Kp], B [N][Kp]
- *   e4m3 with their scale planes.  Errors: CT_ESHAPE / CT_EALIGN. */
+ * gemm: C[M][N] = alpha * (A . B^T) (+ bias[N]) (+ R) in bf16 (or f32 if c_f32), optional bf16
+ *   copy C2; or act 2: GEGLU (C = h bf16, C2 = g [M][N/2]); A [M][Kp], B [N][Kp] e4m3 with their
+ *   scale planes.  Errors: CT_ESHAPE / CT_EALIGN / CT_EINVAL. */
 typedef struct {
   int64_t M, N, Kp;
   const void* A; int64_t lda; const void* sA;   /* lda, ldb in bytes */
   const void* B; int64_t ldb; const void* sB;
   void* C; int64_t ldc; int32_t c_f32;
   const float* bias; float alpha;
+  const float* R; int64_t ldr;   /* f32 residual added after the bias (or NULL) */
+  void* C2; int64_t ldc2;        /* act 0: bf16 copy of C (or NULL); act 2: GEGLU output g (bf16) */
+  int32_t act;                   /* 0 none; 2 GEGLU over 32-column [x | gate] pairs, C = h (bf16) */
 } ctclip_mx_gemm_args;
 int ctclip_quant_mxfp8(const void* x, int32_t x_f32, int64_t rows, int64_t K, int64_t ldx, void* q, int64_t ldq,
                        void* scales, int64_t Kp, void* stream);
