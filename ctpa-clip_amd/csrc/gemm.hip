@@ -461,12 +461,26 @@ extern "C" int ctclip_gemm(const ctclip_gemm_args* a, void* stream) {
   }
   if (a->act == 2) CT_REQUIRE(a->N % 64 == 0 && a->ldc2 % 8 == 0, CT_ESHAPE);
   if (a->act == 4) CT_REQUIRE(a->N % 32 == 0 && a->R && !a->r_f32 && !a->c_f32 && a->split_k <= 1, CT_EINVAL);
+  if (a->act == 5)
+    CT_REQUIRE(a->C2 && a->bias && aligned16(a->bias) && !a->R && !a->c_f32 && !a->accumulate && split == 1 &&
+                   (a->batch <= 1) && a->N % 64 == 0 && a->n2 > 0 && a->n2 % 64 == 0 && a->n2 <= a->N,
+               CT_EINVAL);
   {
     const int b = a->batch > 0 ? a->batch : 1;
     const int64_t tiles256 = ((a->M + 255) / 256) * ((a->N + 255) / 256) * split * b;
     if (a->K % 64 == 0 && a->M >= 256 && a->N >= 256 && tiles256 >= 160 && (split == 1 || (a->K / split) >= 512) &&
         (!a->bias || aligned16(a->bias)))
       return ctclip_gemm256(a, split, b, stream);
+  }
+  if (a->act == 5) {
+    // small shapes: the plain GEMM, then the stand-alone l2norm kernel (same rule)
+    ctclip_gemm_args g = *a;
+    g.act = 0;
+    g.bias = nullptr;
+    g.C2 = nullptr;
+    const int rc = ctclip_gemm(&g, stream);
+    if (rc) return rc;
+    return ctclip_l2norm_scale_fwd(a->C, a->ldc, a->M, a->n2 / 32, 32, a->bias, a->C2, a->ldc2, stream);
   }
   if (!s_smem_set) {
     (void)hipFuncSetAttribute((const void*)gemm_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);

@@ -40,6 +40,7 @@ struct P {
   const void* R; int64_t ldr; int r_f32;
   float alpha; int act; int accumulate; int split_k;
   int64_t sA, sB, sC, sC2, sR;
+  int n2;        // act 5: columns of C2 (the per-head l2norm of C)
   int64_t kper;
   int debug;     // diagnostic knob (CTCLIP_G256_DEBUG): 1 = skip the epilogue, 2 = skip the main loop
   int group_gx;  // grouped (8-row) tile walk when the N tile count >= this (CTCLIP_GEMM_GROUP_GX, default 8)
@@ -622,7 +623,7 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (p.bias && p.split_k <= 1 && p.act != 3 && cl + 16 * j < p.N) b = *(const f32x4*)(p.bias + cl + 16 * j);
+    if (p.bias && p.split_k <= 1 && p.act != 3 && p.act != 5 && cl + 16 * j < p.N) b = *(const f32x4*)(p.bias + cl + 16 * j);
 #pragma unroll
     for (int r = 0; r < 4; ++r) bias[j][r] = b[r];
   }
@@ -662,6 +663,39 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
         float2* out = (float2*)p.C + bidx * p.sC;
         out[gm * p.ldc + (wcol0 >> 6)] = make_float2(best, __int_as_float((int)(wcol0 + bi)));
         if (p.C2) ((float*)p.C2)[bidx * p.sC2 + gm * p.ldc2 + (wcol0 >> 6)] = second;
+      }
+      continue;
+    }
+    if constexpr (MODE == 6) {
+      // C = bf16 result; C2 = its l2norm over each 32-column head (the wave's 64 columns are two
+      // heads: blocks 0-1 and 2-3; a head's 32 values sit in the 4 lanes g of row m) times the
+      // head-dim scale p.bias[c % 32], from the bf16-rounded values as ctclip_l2norm_scale_fwd
+      float qb[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) qb[j][r] = bf2f(f2bf(v[j][r]));
+      store_row_bf16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N);
+      if (wcol0 < p.n2) {
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s0 += qb[0][r] * qb[0][r] + qb[1][r] * qb[1][r];
+          s1 += qb[2][r] * qb[2][r] + qb[3][r] * qb[3][r];
+        }
+        s0 += __shfl_xor(s0, 16, 64);
+        s1 += __shfl_xor(s1, 16, 64);
+        s0 += __shfl_xor(s0, 32, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        const float inv0 = 1.f / fmaxf(sqrtf(s0), 1e-12f), inv1 = 1.f / fmaxf(sqrtf(s1), 1e-12f);
+        float o[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x4 sc = *(const f32x4*)(p.bias + 16 * (j & 1) + 4 * g);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[j][r] = qb[j][r] * (j < 2 ? inv0 : inv1) * sc[r];
+        }
+        store_row_bf16(p.C2 + bidx * p.sC2 + gm * p.ldc2 + wcol0, o, g, rok, wcol0, p.n2);
       }
       continue;
     }
@@ -1025,6 +1059,8 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
       epilogue_t<0>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
     } else if constexpr (EP == 3) {
       epilogue_t<3>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
+    } else if constexpr (EP == 6) {
+      epilogue_t<6>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
     } else {
       // staging in buffer O and beyond (the next tile's tile 0 is landing in E)
       epilogue<EP == -2 || EP == -3 || EP == -5 ? EP : -1>(p, acc, smem + TILEB, w, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
@@ -1109,6 +1145,7 @@ int tile_rows() { return variant() == 2 ? 2 : 1; }
 template <bool AK, bool BKC>
 int launch8_ep(const P& p, int batch, hipStream_t st) {
   if (p.act == 4) return launch8<AK, BKC, 4>(p, batch, st);
+  if (p.act == 5) return launch8<AK, BKC, 6>(p, batch, st);
   // CTCLIP_GEMM_TR_F32=1 (A/B): f32 / residual outputs through the transposed (LDS-free) epilogue too
   static int tr_f32 = -1;
   if (tr_f32 < 0) { const char* e = getenv("CTCLIP_GEMM_TR_F32"); tr_f32 = e ? atoi(e) != 0 : 0; }
@@ -1148,7 +1185,8 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   p.R = a->R; p.ldr = a->ldr; p.r_f32 = a->r_f32;
   p.alpha = a->alpha; p.act = a->act; p.accumulate = a->accumulate; p.split_k = split;
   p.sA = a->sA; p.sB = a->sB; p.sC = a->sC; p.sC2 = a->sC2; p.sR = a->sR;
-  const int kstep = (variant() == 8 || a->act == 4) ? p8::BKK : BK;
+  p.n2 = a->n2;
+  const int kstep = (variant() == 8 || a->act == 4 || a->act == 5) ? p8::BKK : BK;
   p.kper = (a->K / kstep + split - 1) / split * kstep;
   static int dbg = -1, stag = 0;
   if (dbg < 0) {
@@ -1172,7 +1210,7 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   p.group_gx = ggx;
   p.stagger = variant() == 8 ? (g_stagger8 >= 0 ? g_stagger8 : (a->act == 2 ? 4 : 0)) : (tile_rows() == 1 ? stag : 0);
   hipStream_t st = (hipStream_t)stream;
-  if (variant() == 8 || a->act == 4)
+  if (variant() == 8 || a->act == 4 || a->act == 5)
     return a->a_kcontig ? launch8_any<true>(p, a->b_kcontig, batch, st) : launch8_any<false>(p, a->b_kcontig, batch, st);
   if (tile_rows() == 2) return launch_any<2>(p, a->a_kcontig, a->b_kcontig, batch, st);
   return launch_any<1>(p, a->a_kcontig, a->b_kcontig, batch, st);

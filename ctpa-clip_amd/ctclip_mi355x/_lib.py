@@ -42,6 +42,7 @@ class GemmArgs(ctypes.Structure):
         ('split_k', c_i32),
         ('batch', c_i32),
         ('sA', c_i64), ('sB', c_i64), ('sC', c_i64), ('sC2', c_i64), ('sR', c_i64),
+        ('n2', c_i32),
     ]
 
 

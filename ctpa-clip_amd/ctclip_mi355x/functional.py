@@ -10,6 +10,7 @@ by index arithmetic instead of transposing).
 from __future__ import annotations
 
 import math
+import os
 import weakref
 from dataclasses import dataclass
 
@@ -146,6 +147,7 @@ def _adjacent(ts, arena_of):
 # call, weights once per optimizer update.  The backward stays bf16 on the same saved bf16
 # activations and weights.  SURVEY 8(c): compared to the build's own bf16 path, tolerance per test.
 _FP8 = {'on': False}
+_L2N_FUSED = os.environ.get('CTCLIP_L2N_FUSED', '1') != '0'   # A/B switch of the act-5 projections
 _FP8_W = {}
 
 
@@ -345,11 +347,19 @@ class ViTLayerFn(torch.autograd.Function):
         if fp8:
             q = fp8_linear(xn, (id(Wq), 'q'), Wq_b)
             kv = fp8_linear(x1b, (id(Wkv), 'kv'), Wkv_b)
+            qn = K.l2norm_scale_fwd(q, H, dh, q_scale)
+            kn = K.l2norm_scale_fwd(kv[:, :inner], H, dh, k_scale)
+        elif _L2N_FUSED and dh == 32 and inner % 64 == 0:
+            # l2norm(q) * q_scale, l2norm(k) * k_scale fused into the projections' epilogues (act 5)
+            qn = torch.empty(xf.shape[0], inner, device=xf.device, dtype=BF16)
+            kn = torch.empty(xf.shape[0], inner, device=xf.device, dtype=BF16)
+            q = K.linear(xn, Wq_b, out2=qn, l2n_scale=q_scale.detach(), l2n_cols=inner)
+            kv = K.linear(x1b, Wkv_b, out2=kn, l2n_scale=k_scale.detach(), l2n_cols=inner)
         else:
             q = K.linear(xn, Wq_b)
             kv = K.linear(x1b, Wkv_b)
-        qn = K.l2norm_scale_fwd(q, H, dh, q_scale)
-        kn = K.l2norm_scale_fwd(kv[:, :inner], H, dh, k_scale)
+            qn = K.l2norm_scale_fwd(q, H, dh, q_scale)
+            kn = K.l2norm_scale_fwd(kv[:, :inner], H, dh, k_scale)
         L, nseq, seq = geo.seq()
         use_bias = bias_u is not None
         o, lse = K.attn_fwd(qn, kn, kv[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,

@@ -12,7 +12,7 @@ from ._lib import GemmArgs, call, ptr, stream_ptr
 BF16 = torch.bfloat16
 F32 = torch.float32
 
-ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_ARGMAX, ACT_GEGLU_BWD = 0, 1, 2, 3, 4
+ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_ARGMAX, ACT_GEGLU_BWD, ACT_L2N = 0, 1, 2, 3, 4, 5
 
 
 def _chk(t, name, dtype=None):
@@ -59,18 +59,18 @@ TIMER = KernelTimer()
 
 def gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, *, C2=None, ldc2=0, bias=None,
              R=None, ldr=0, alpha=1.0, act=ACT_NONE, accumulate=False, split_k=1, batch=1,
-             sA=0, sB=0, sC=0, sC2=0, sR=0, tag=None, flops=None):
+             sA=0, sB=0, sC=0, sC2=0, sR=0, tag=None, flops=None, n2=0):
     end = TIMER(tag, flops if flops is not None else 2.0 * M * N * K * batch) if tag else None
     _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, C2=C2, ldc2=ldc2, bias=bias, R=R, ldr=ldr,
               alpha=alpha, act=act, accumulate=accumulate, split_k=split_k, batch=batch, sA=sA, sB=sB, sC=sC,
-              sC2=sC2, sR=sR)
+              sC2=sC2, sR=sR, n2=n2)
     if end is not None:
         end.record()
 
 
 def _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, *, C2=None, ldc2=0, bias=None,
               R=None, ldr=0, alpha=1.0, act=ACT_NONE, accumulate=False, split_k=1, batch=1,
-              sA=0, sB=0, sC=0, sC2=0, sR=0):
+              sA=0, sB=0, sC=0, sC2=0, sR=0, n2=0):
     s = _auto_split(M, N, K, act, split_k, batch, accumulate, C)
     if s > 1:
         # skinny GEMM (text tower, M = B * L tokens): split K into f32 slabs over ~4x more
@@ -95,6 +95,7 @@ def _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, *, C2=None,
     a.R, a.ldr, a.r_f32 = ptr(R), ldr, int(R is not None and R.dtype == F32)
     a.alpha, a.act, a.accumulate, a.split_k, a.batch = alpha, act, int(accumulate), split_k, batch
     a.sA, a.sB, a.sC, a.sC2, a.sR = sA, sB, sC, sC2, sR
+    a.n2 = n2
     call('ctclip_gemm', _lib.ctypes.byref(a), stream_ptr())
 
 
@@ -109,17 +110,22 @@ def _auto_split(M, N, K, act, split_k, batch, accumulate, C):
 
 
 def linear(x, w, *, bias=None, residual=None, out=None, out_dtype=BF16, act=ACT_NONE, out2=None, alpha=1.0,
-           accumulate=False, tag=None, flops=None):
-    """y[M,N] = x[M,K] @ w[N,K]^T (+bias) (+residual); x, w bf16 row-major."""
+           accumulate=False, tag=None, flops=None, l2n_scale=None, l2n_cols=0):
+    """y[M,N] = x[M,K] @ w[N,K]^T (+bias) (+residual); x, w bf16 row-major.  l2n_scale (the [32]
+    head-dim scale): out2[:, :l2n_cols] = per 32-column head l2norm(y) * scale, fused (act 5)."""
     M, K = x.shape
     N = w.shape[0]
     assert w.shape[1] == K and x.stride(1) == 1 and w.stride(1) == 1
     if out is None:
         out = torch.empty(M, N, device=x.device, dtype=out_dtype)
+    if l2n_scale is not None:
+        assert bias is None and residual is None and out2 is not None and l2n_scale.numel() == 32
+        assert l2n_scale.dtype == torch.float32 and l2n_scale.is_contiguous()
+        act, bias = ACT_L2N, l2n_scale
     gemm_raw(M, N, K, x, x.stride(0), True, w, w.stride(0), True, out, out.stride(0),
              C2=out2, ldc2=out2.stride(0) if out2 is not None else 0, bias=bias, R=residual,
              ldr=residual.stride(0) if residual is not None else 0, alpha=alpha, act=act, accumulate=accumulate,
-             tag=tag, flops=flops)
+             tag=tag, flops=flops, n2=l2n_cols)
     return out
 
 

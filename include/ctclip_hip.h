@@ -38,7 +38,10 @@ int ctclip_device_arch(char* buf, int n); /* writes gcnArchName of the current d
  *   b_kcontig = 1: B[n*ldb + k]   (nn.Linear weight);  0: B[k*ldb + n]  (K x N)
  *   act: 0 none, 1 gelu(erf), 2 geglu (tile-interleaved pairs), 3 argmax,
  *        4 geglu backward: acc = dg (N = g-space columns, N % 32 == 0), R = h (bf16, the
- *          act-2 pre-activation), C = dh (bf16, h's layout) — replaces dg + geglu_bwd
+ *          act-2 pre-activation), C = dh (bf16, h's layout) — replaces dg + geglu_bwd,
+ *        5 l2norm: C = bf16 result (N % 64 == 0), C2[:, :n2] = per 32-column head
+ *          l2norm(C) * bias[c % 32] (Attention's l2norm(q) * q_scale, attention.py:152-154;
+ *          bias = the [32] scale) — replaces a GEMM + ctclip_l2norm_scale_fwd
  *   split_k > 1: C is an f32 slab array [split_k][M][ldc] of partial sums (no epilogue).
  */
 typedef struct {
@@ -55,6 +58,7 @@ typedef struct {
   int32_t split_k;
   int32_t batch;
   int64_t sA, sB, sC, sC2, sR;      /* batch strides in elements */
+  int32_t n2;                       /* act 5: normalised columns (multiple of 64, <= N) */
 } ctclip_gemm_args;
 int ctclip_gemm(const ctclip_gemm_args* a, void* stream);
 /* diagnostic: large-tile kernel variant (8 = 8-phase 256x256x64 default, 1 = 128x256x32,
