@@ -668,8 +668,10 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
     }
     if constexpr (MODE == 6) {
       // C = bf16 result; C2 = its l2norm over each 32-column head (the wave's 64 columns are two
-      // heads: blocks 0-1 and 2-3; a head's 32 values sit in the 4 lanes g of row m) times the
-      // head-dim scale p.bias[c % 32], from the bf16-rounded values as ctclip_l2norm_scale_fwd
+      // heads) times the head-dim scale p.bias[c % 32], bit-identical to ctclip_l2norm_scale_fwd:
+      // the permlane16 pair swap leaves each lane 8 consecutive columns (a chunk: offset
+      // pair_coff(g)), summed in that kernel's order, then combined chunk 0+1, 2+3 (lanes g ^ 2)
+      // and the two pairs (g ^ 1), as its xor-1 / xor-2 shuffles over the 4 lanes of a head
       float qb[4][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -677,25 +679,30 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
         for (int r = 0; r < 4; ++r) qb[j][r] = bf2f(f2bf(v[j][r]));
       store_row_bf16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N);
       if (wcol0 < p.n2) {
-        float s0 = 0.f, s1 = 0.f;
+        const int d0 = pair_coff(g);
+        const f32x4 s0v = *(const f32x4*)(p.bias + d0), s1v = *(const f32x4*)(p.bias + d0 + 4);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          s0 += qb[0][r] * qb[0][r] + qb[1][r] * qb[1][r];
-          s1 += qb[2][r] * qb[2][r] + qb[3][r] * qb[3][r];
+        for (int jp = 0; jp < 2; ++jp) {
+          float c8[8];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(qb[2 * jp][k]),
+                                                            __float_as_uint(qb[2 * jp + 1][k]), false, false);
+            c8[k] = __uint_as_float(r[0]);
+            c8[4 + k] = __uint_as_float(r[1]);
+          }
+          float ss = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) ss += c8[e] * c8[e];
+          ss += __shfl_xor(ss, 32, 64);
+          ss += __shfl_xor(ss, 16, 64);
+          const float inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
+          float o8[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { o8[e] = c8[e] * inv * s0v[e]; o8[4 + e] = c8[4 + e] * inv * s1v[e]; }
+          const int64_t c0 = wcol0 + 32 * jp + d0;
+          if (rok && c0 < p.n2) st16(p.C2 + bidx * p.sC2 + gm * p.ldc2 + c0, pack8(o8));
         }
-        s0 += __shfl_xor(s0, 16, 64);
-        s1 += __shfl_xor(s1, 16, 64);
-        s0 += __shfl_xor(s0, 32, 64);
-        s1 += __shfl_xor(s1, 32, 64);
-        const float inv0 = 1.f / fmaxf(sqrtf(s0), 1e-12f), inv1 = 1.f / fmaxf(sqrtf(s1), 1e-12f);
-        float o[4][4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const f32x4 sc = *(const f32x4*)(p.bias + 16 * (j & 1) + 4 * g);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) o[j][r] = qb[j][r] * (j < 2 ? inv0 : inv1) * sc[r];
-        }
-        store_row_bf16(p.C2 + bidx * p.sC2 + gm * p.ldc2 + wcol0, o, g, rok, wcol0, p.n2);
       }
       continue;
     }

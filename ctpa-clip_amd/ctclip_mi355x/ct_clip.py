@@ -79,8 +79,17 @@ class CTCLIP(nn.Module):
 
     # ------------------------------------------------------------------ helpers
     def _visual_weight_bf16(self, W):
+        """bf16 to_visual_latent weight (151 M parameters): the Adam-kept shadow when W trains,
+        else a cast cached until W changes.  Frozen in the fine-tune configuration
+        (fine_tuning_ctclip.py:6-14), so it is cast once, not every step (0.23 ms per recast)."""
         from . import kernels as K
-        key = (W.data_ptr(), W._version, K.weights_epoch())
+        from . import functional as Fn
+        sh = Fn.shadow_bf16(W)
+        if sh is not None:
+            return sh
+        # only an optimizer arena member is written behind torch's version counter (raw pointers)
+        in_arena = getattr(W, '_ctclip_flat', None) is not None
+        key = (W.data_ptr(), W._version, K.weights_epoch() if in_arena else -1)
         if self._wvis[0] != key:
             self._wvis = (key, K.cast_bf16(W.detach().contiguous()))
         return self._wvis[1]
