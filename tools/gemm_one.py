@@ -1,5 +1,5 @@
 """Run one GEMM shape of the step repeatedly (for rocprofv3 counter passes).
-usage: python tools/gemm_one.py {ff1,ff1plain,ff2,dxnn,dwtn} [reps]"""
+usage: python tools/gemm_one.py {ff1,ff1plain,ff2,dxnn,dwtn,dx1408,geglubwd,dwq} [reps]"""
 import os
 import sys
 
@@ -28,6 +28,8 @@ def main():
         'dxnn': lambda: K.matmul_nn(dh, w1),
         'dwtn': lambda: K.matmul_tn(dh, x512),
         'dx1408': lambda: K.matmul_nn(x512, w2),
+        'geglubwd': lambda: K.matmul_nn_geglu_bwd(x512, w2, dh),
+        'dwq': lambda: K.matmul_tn(x512[:, :256], x512),
     }[which]
     for _ in range(reps):
         fn()

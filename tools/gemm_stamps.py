@@ -28,6 +28,8 @@ def main():
         'ff1': lambda: K.linear(x512, w1, act=K.ACT_GEGLU, out2=g),
         'ff1plain': lambda: K.linear(x512, w1, out=dh),
         'dx1408': lambda: K.matmul_nn(x512, w2),
+        'geglubwd': lambda: K.matmul_nn_geglu_bwd(x512, w2, dh),
+        'dwq': lambda: K.matmul_tn(x512[:, :256], x512),
     }
     L = _lib.lib()
     L.ctclip_gemm_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -53,6 +55,8 @@ def main():
         a = np.array(rows, dtype=np.float64)
         first = a[a[:, 6] == 0]
         later = a[a[:, 6] > 0]
+        if len(later) == 0:   # one tile per workgroup (split-K dW): report the first tiles
+            later = first
         print(f'== {name}: {len(a)} tiles; median cycles per tile part (later tiles / first):')
         for k, lab in enumerate(['K-tiles 0-1', 'K-tiles 2..', 'epilogue issue', 'wait before next tile']):
             print(f'   {lab:34s} {np.median(later[:, k]):9.0f}  p90 {np.percentile(later[:, k], 90):9.0f}'
