@@ -1088,6 +1088,10 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
   }
 }
 
+// persistent grid cap (workgroups; default 256 = one per CU): lets two GEMMs on two streams share
+// the chip (ctclip_gemm_set_grid_cap)
+static int g_grid_cap = 0;
+
 template <bool AK, bool BKC, int EP>
 int launch8(const P& p, int batch, hipStream_t st) {
   static bool attr = false;
@@ -1098,7 +1102,8 @@ int launch8(const P& p, int batch, hipStream_t st) {
   }
   const int64_t ntiles = cdiv(p.N, p8::BNN) * cdiv(p.M, p8::BM) * (int64_t)p.gz;
   if (p.persist) {
-    dim3 grid((unsigned)(ntiles < 256 ? ntiles : 256));
+    const int64_t cap = g_grid_cap > 0 && g_grid_cap < 256 ? g_grid_cap : 256;
+    dim3 grid((unsigned)(ntiles < cap ? ntiles : cap));
     hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP>), grid, dim3(p8::NTH), p8::SMEM_P, st, p);
   } else {
     dim3 grid(cdiv(p.N, p8::BNN), cdiv(p.M, p8::BM), batch * p.split_k);
@@ -1227,6 +1232,14 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
 extern "C" int ctclip_gemm_set_stagger(int v) {
   const int old = g256::g_stagger8;
   g256::g_stagger8 = v;
+  return old;
+}
+
+// 8-phase persistent grid cap for the launches that follow (0 = one workgroup per CU); returns the
+// previous value.  Used to split the chip between two concurrent GEMMs on two streams.
+extern "C" int ctclip_gemm_set_grid_cap(int v) {
+  const int old = g256::g_grid_cap;
+  g256::g_grid_cap = v > 0 ? v : 0;
   return old;
 }
 

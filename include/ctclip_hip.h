@@ -69,6 +69,9 @@ int ctclip_gemm_set_stagger(int units);
 /* diagnostic: 8-phase kernel as persistent workgroups walking the tile sequence (1, default) or
  * one workgroup per tile (0); returns the previous setting.  Results are identical. */
 int ctclip_gemm_set_persist(int on);
+/* 8-phase persistent grid cap (workgroups) for the launches that follow; 0 = one per CU (default).
+ * Two GEMMs on two streams, each capped, share the chip.  Returns the previous cap. */
+int ctclip_gemm_set_grid_cap(int workgroups);
 
 /* sum f32 slabs [s][rows][ld] -> out (f32 or bf16), optional accumulate into f32 out */
 int ctclip_reduce_slabs(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,
