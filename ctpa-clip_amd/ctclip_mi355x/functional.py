@@ -36,6 +36,22 @@ def gsink(p):
     return p.grad
 
 
+def gsink_cat(ps):
+    """One gradient sink for parameters ``ps`` that sit consecutively, in order, in the trainer's
+    arena (BERT's q / k / v weights, and their biases: bert.BertModel.param_order): a view of the
+    gradient arena covering all of them, so one weight-gradient GEMM and one column sum serve the
+    fused QKV projection.  None when they are not adjacent there or a .grad was rebound."""
+    if not all(p.requires_grad for p in ps):
+        return None
+    a = _adjacent(ps, lambda f: f.grad)
+    if a is None:
+        return None
+    arena, lo, hi = a
+    if any(p.grad is None or p.grad.data_ptr() != arena[p._ctclip_off:].data_ptr() for p in ps):
+        return None
+    return arena[lo:hi].view(-1, *ps[0].shape[1:])
+
+
 _SHADOW = {}
 
 
@@ -148,6 +164,7 @@ def _adjacent(ts, arena_of):
 # activations and weights.  SURVEY 8(c): compared to the build's own bf16 path, tolerance per test.
 _FP8 = {'on': False}
 _L2N_FUSED = os.environ.get('CTCLIP_L2N_FUSED', '1') != '0'   # A/B switch of the act-5 projections
+_QKV_WGRAD = os.environ.get('CTCLIP_QKV_WGRAD', '1') != '0'   # A/B switch of BERT's merged q/k/v wgrad
 _FP8_W = {}
 
 
@@ -745,6 +762,13 @@ class BertLayerFn(torch.autograd.Function):
                    dqkv[:, Hd:2 * Hd], dqkv[:, 2 * Hd:], L=L, H=heads, D=dh, nseq=B, scale=1.0 / math.sqrt(dh),
                    seq=(1, L, 0, 1), kmask=kmask, dropout=(pa, s_attn))
         dx = K.matmul_nn(dqkv, Wqkv, residual=daf, out_dtype=F32)
-        for i, (W, b) in enumerate(((Wq, bq), (Wk, bk), (Wv, bv))):
-            wgrad(dqkv[:, i * Hd:(i + 1) * Hd], xb, W, b)
+        gW, gB = (gsink_cat([Wq, Wk, Wv]), gsink_cat([bq, bk, bv])) if _QKV_WGRAD else (None, None)
+        if gW is not None and gB is not None:
+            # q / k / v gradients adjacent in the arena: one [3 Hd, Hd] weight-gradient GEMM (108
+            # tiles instead of 3 x 36) and one column sum, same per-element arithmetic
+            K.matmul_tn(dqkv, xb, out=gW, accumulate=True)
+            K.colsum(dqkv, out=gB, accumulate=True)
+        else:
+            for i, (W, b) in enumerate(((Wq, bq), (Wk, bk), (Wv, bv))):
+                wgrad(dqkv[:, i * Hd:(i + 1) * Hd], xb, W, b)
         return (dx, None, None, None, None, None, None) + (None,) * 17

@@ -251,7 +251,16 @@ def reduce_param_partials(part, out, accumulate):
 
 # ----------------------------------------------------------------------------- reductions
 def nblocks_for(rows, cap=1024):
-    return int(max(1, min(cap, (rows + 63) // 64)))
+    """Workgroups of the LayerNorm backward (4 waves each; a wave walks its rows one at a time):
+    >= 64 rows per workgroup on long inputs (the 3D-ViT's 110,592 tokens: the parameter-gradient
+    partial slabs stay small), but one row per wave on short ones (BERT's 1,024 tokens: 256
+    workgroups instead of 16, whose waves walked 16 rows one memory latency after another)."""
+    if not _LNB_WIDE:
+        return int(max(1, min(cap, (rows + 63) // 64)))
+    return int(max(1, min(cap, max((rows + 63) // 64, min(256, (rows + 3) // 4)))))
+
+
+_LNB_WIDE = os.environ.get('CTCLIP_LNB_WIDE', '1') != '0'   # A/B switch of nblocks_for's short-input rule
 
 
 def colsum(x, out=None, accumulate=False):
