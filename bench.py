@@ -177,7 +177,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    K.TIMER.start(['ff1'])
+    K.TIMER.start(['ff1', 'dw'])
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = trainer.train_step(text, hu)
@@ -200,6 +200,7 @@ def main():
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         in_sync = bool(lo.item() == hi.item())
     ff1 = K.TIMER.summary('ff1')
+    dw = K.TIMER.summary('dw')
     vit_ms = sum(s.elapsed_time(e) for s, e in vit_events) / max(1, len(vit_events))
     loss_v = float(loss.item())
 
@@ -257,6 +258,26 @@ def main():
             'hbm_frac': round(algo_bytes / (ff1['avg_ms'] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
             'avg_launch_ms': round(ff1['avg_ms'], 4), 'flops_per_launch': ff1['flops'],
             'launches': ff1['launches']}
+    if dw:
+        # the kernel with the largest share of the step's time (rocprof): the split-K weight-gradient
+        # GEMM, 41 launches per step of five shapes (3D-ViT Q / KV / attention-out / FF1 / FF2 dW per
+        # layer + the patch-embed dW); achieved = their algorithmic flops / their summed durations
+        tf = dw['total_flops'] / (dw['total_ms'] * 1e-3) / 1e12
+        busy = None
+        pmc = os.path.join(REPO, 'profiles', 'r02_pmc_dwtn.json')
+        if args.batch == 8 and os.path.exists(pmc):
+            rec = json.load(open(pmc))
+            if any('gemm8p_kernel<false, false, -5>' in k for k in rec.get('kernel', [])):
+                busy = round(rec['mfma_busy'], 4)
+        result['roofline_dominant'] = {
+            'kernel': 'g256::gemm8p_kernel<false,false,-5> split-K weight-gradient GEMMs (all launches of a step)',
+            'bound': 'mfma', 'achieved': round(tf, 1), 'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
+            'frac': round(tf / PEAK_BF16_TFLOPS, 4), 'traffic': None,
+            'mfma_busy_ff1_shape': busy,
+            'mfma_busy_source': 'profiles/r02_pmc_dwtn.json (the 2816x512x110592 launch)' if busy else None,
+            'avg_launch_ms': round(dw['total_ms'] / dw['launches'], 4),
+            'launches_per_step': round(dw['launches'] / args.steps, 2),
+            'flops_per_step': round(dw['total_flops'] / args.steps)}
     if vit_ms > 0:
         vit_tf = VIT_FWD_GFLOP_PER_VOL * args.batch / (vit_ms * 1e-3) / 1e3
         result['vit_forward'] = {'ms': round(vit_ms, 3), 'achieved_tflops': round(vit_tf, 1),

@@ -242,7 +242,7 @@ class PatchEmbedFn(torch.autograd.Function):
         xhat, y1, mean, rstd, ln1_w, ln1_b, W, ln2_w = ctx.saved_tensors
         take_shadow(dyf)
         _, dy1b, dg2, db2 = K.layernorm_bwd(dyf.contiguous(), y1, mean, rstd, ln2_w, dx_f32=False)
-        G = K.matmul_tn(dy1b, xhat)                                     # [D, pd] f32
+        G = K.matmul_tn(dy1b, xhat, tag='dw')                           # [D, pd] f32
         cs = K.colsum(dy1b)                                             # d bias
         # straight into .grad (gsink), so the node's parameters are final when it returns
         # (dist_sync buckets fire on the node's post-hook, before any AccumulateGrad would run)
@@ -421,16 +421,17 @@ class ViTLayerFn(torch.autograd.Function):
             dx3b = K.cast_bf16(dx3f)
         # feed-forward (weight gradients accumulate straight into the parameters' .grad)
         dh_ = K.matmul_nn_geglu_bwd(dx3b, W2p, h)      # dg = dx3 . W2 and the GEGLU backward, fused
-        dW2p = K.matmul_tn(dx3b, g)
+        M_ = dx3b.shape[0]
+        dW2p = K.matmul_tn(dx3b, g, tag='dw', flops=2.0 * M_ * W2.shape[0] * W2.shape[1])
         dxn2 = K.matmul_nn(dh_, W1p)
-        dW1p = K.matmul_tn(dh_, xn2)
+        dW1p = K.matmul_tn(dh_, xn2, tag='dw', flops=2.0 * M_ * W1.shape[0] * W1.shape[1])
         dx2f, dx2b, _, _ = K.layernorm_bwd(dxn2, x2b, m2, r2, ff_w, dres=dx3f, dgamma_out=gsink(ff_w),
                                            dbeta_out=gsink(ff_b))
         K.unpack_rows(dW1p, gsink(W1), rowmap=ff1_rowmap(W1.shape[0] // 2, dev), accumulate=True)
         K.unpack_rows(dW2p, gsink(W2), cols=W2.shape[1], accumulate=True)
         # attention
         do = K.matmul_nn(dx2b, Wo_b)
-        K.matmul_tn(dx2b, o, out=gsink(Wo), accumulate=True)
+        K.matmul_tn(dx2b, o, out=gsink(Wo), accumulate=True, tag='dw')
         dqn = torch.empty_like(qn)
         dkn = torch.empty_like(kn)
         dkv = torch.empty_like(kv)
@@ -443,8 +444,8 @@ class ViTLayerFn(torch.autograd.Function):
         K.l2norm_scale_bwd(q, dqn, H, dh, q_scale, dq, ds_out=gsink(q_scale))
         K.l2norm_scale_bwd(kv[:, :inner], dkn, H, dh, k_scale, dkv[:, :inner], ds_out=gsink(k_scale))
         dxn = K.matmul_nn(dq, Wq_b)
-        K.matmul_tn(dq, xn, out=gsink(Wq), accumulate=True)
-        K.matmul_tn(dkv, x1b, out=gsink(Wkv), accumulate=True)
+        K.matmul_tn(dq, xn, out=gsink(Wq), accumulate=True, tag='dw')
+        K.matmul_tn(dkv, x1b, out=gsink(Wkv), accumulate=True, tag='dw')
         dx1kv = K.matmul_nn(dkv, Wkv_b, residual=dx2f, out_dtype=F32)
         dx1f, dx1b, _, _ = K.layernorm_bwd(dxn, x1b, m1, r1, norm_g, dres=dx1kv, want_beta=False,
                                            dgamma_out=gsink(norm_g))

@@ -51,7 +51,8 @@ class KernelTimer:
         if not ev:
             return None
         ms = [s.elapsed_time(e) for s, e, _ in ev]
-        return dict(launches=len(ev), avg_ms=sum(ms) / len(ms), flops=ev[0][2])
+        return dict(launches=len(ev), avg_ms=sum(ms) / len(ms), flops=ev[0][2], total_ms=sum(ms),
+                    total_flops=sum(f for _, _, f in ev))
 
 
 TIMER = KernelTimer()
@@ -148,8 +149,9 @@ def split_for(m_rows, tiles):
     return max(1, s)
 
 
-def matmul_tn(dy, x, *, out=None, accumulate=False, split_k=None, alpha=1.0):
-    """dW[N,K] (f32) = dy[M,N]^T @ x[M,K]; reduction over the M tokens (split-K slabs)."""
+def matmul_tn(dy, x, *, out=None, accumulate=False, split_k=None, alpha=1.0, tag=None, flops=None):
+    """dW[N,K] (f32) = dy[M,N]^T @ x[M,K]; reduction over the M tokens (split-K slabs).
+    tag / flops: KernelTimer bracketing of the GEMM launch (not the slab reduction)."""
     M, N = dy.shape
     K = x.shape[1]
     assert x.shape[0] == M
@@ -169,10 +171,11 @@ def matmul_tn(dy, x, *, out=None, accumulate=False, split_k=None, alpha=1.0):
         s = split_for(M, ((N + 127) // 128) * ((K + 127) // 128))
     if s <= 1:
         gemm_raw(N, K, M, dy, dy.stride(0), False, x, x.stride(0), False, out, out.stride(0),
-                 accumulate=accumulate, alpha=alpha)
+                 accumulate=accumulate, alpha=alpha, tag=tag, flops=flops)
         return out
     slabs = torch.empty(s, N, K, device=dy.device, dtype=F32)
-    gemm_raw(N, K, M, dy, dy.stride(0), False, x, x.stride(0), False, slabs, K, split_k=s, alpha=alpha)
+    gemm_raw(N, K, M, dy, dy.stride(0), False, x, x.stride(0), False, slabs, K, split_k=s, alpha=alpha, tag=tag,
+             flops=flops)
     reduce_slabs(slabs, out, accumulate=accumulate)
     return out
 

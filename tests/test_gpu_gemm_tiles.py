@@ -19,7 +19,8 @@ def _rel(a, b):
 
 def _variants(K, fn):
     """Outputs of the 8-phase kernel (persistent, key 8) and the 128x256x32 kernel (key 1); the
-    8-phase kernel with one workgroup per tile must match the persistent one bit for bit."""
+    8-phase kernel with one workgroup per tile, and persistent on a grid capped at 92 workgroups,
+    must match the persistent one bit for bit."""
     from ctclip_mi355x import _lib
     outs = {}
     lib = _lib.lib()
@@ -31,14 +32,20 @@ def _variants(K, fn):
             outs[v] = snap(fn())
             torch.cuda.synchronize()
         lib.ctclip_gemm_set_variant(8)
+        lib.ctclip_gemm_set_grid_cap(92)      # persistent walk on a capped grid (two-stream sharing)
+        capped = snap(fn())
+        torch.cuda.synchronize()
+        lib.ctclip_gemm_set_grid_cap(0)
         lib.ctclip_gemm_set_persist(0)
         single = snap(fn())
         torch.cuda.synchronize()
     finally:
+        lib.ctclip_gemm_set_grid_cap(0)
         lib.ctclip_gemm_set_variant(prev)
         lib.ctclip_gemm_set_persist(prev_p if prev_p >= 0 else 1)
     if torch.is_tensor(single):
         assert torch.equal(single, outs[8]), 'persistent 8-phase GEMM differs from one workgroup per tile'
+        assert torch.equal(capped, outs[8]), 'persistent 8-phase GEMM on a capped grid differs'
     return outs
 
 
