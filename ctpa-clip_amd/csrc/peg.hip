@@ -181,7 +181,14 @@ __global__ __launch_bounds__(192) void peg_wgrad_kernel(const u16* __restrict__ 
 // three read in step t, so one barrier per step suffices.
 // W <= 24 (one item per thread); 3 ring slots + weights = 47 KB -> 3 workgroups per CU, so the
 // base grid (8 x 12 x 8 = 768 workgroups) is resident in one round
-constexpr int HT = 2, SEG = 3, SEGW = 6, TNTH = 128, WNTH = 256, LMAX = 8, NSLOT = 3;
+#ifndef CTCLIP_PEG_SEG
+#define CTCLIP_PEG_SEG 3
+#endif
+// SEG w positions per conv thread; TNTH = one (row, segment, chunk) item per thread on the 24-wide
+// grid; PLANE_CH = 16-B chunks a plane (HT + 2 rows x W + 2 columns x 8 chunks) may hold
+constexpr int HT = 2, SEG = CTCLIP_PEG_SEG, SEGW = 6, TNTH = HT * ((24 + SEG - 1) / SEG) * 8, WNTH = 256,
+              PLANE_CH = 1024, NSLOT = 3;
+template <int NT> constexpr int nld() { return (PLANE_CH + NT - 1) / NT; }   // plane loads per thread
 
 __host__ __device__ inline int plane_bytes(int W) { return (HT + 2) * (W + 2) * 128; }
 
@@ -195,11 +202,11 @@ __host__ __device__ inline int plane_bytes(int W) { return (HT + 2) * (W + 2) * 
 // 107 -> 126 us there, while the conv kernels gain 174 -> 156 us)
 template <int NT, bool BF = true>
 __device__ __forceinline__ unsigned plane_load(const u16* __restrict__ x, const Geo& g, int D, int b, int h0, int c0,
-                                               int tp, u32x4 (&reg)[LMAX * TNTH / NT]) {
+                                               int tp, u32x4 (&reg)[nld<NT>()]) {
   const int nl = (HT + 2) * (g.W + 2) * 8;
   unsigned valid = BF ? 0u : ~0u;
 #pragma unroll
-  for (int m = 0; m < LMAX * TNTH / NT; ++m) {
+  for (int m = 0; m < nld<NT>(); ++m) {
     const int i = threadIdx.x + m * NT;
     const int k = i & 7, cw = (i >> 3) % (g.W + 2), hr = (i >> 3) / (g.W + 2);
     const int h = h0 - 1 + hr, w = cw - 1;
@@ -217,12 +224,12 @@ __device__ __forceinline__ unsigned plane_load(const u16* __restrict__ x, const 
 }
 
 template <int NT>
-__device__ __forceinline__ void plane_store(char* ring, int W, int tp, const u32x4 (&reg)[LMAX * TNTH / NT],
+__device__ __forceinline__ void plane_store(char* ring, int W, int tp, const u32x4 (&reg)[nld<NT>()],
                                             unsigned valid) {
   const int nl = (HT + 2) * (W + 2) * 8;
   char* dst = ring + (tp % NSLOT) * plane_bytes(W);
 #pragma unroll
-  for (int m = 0; m < LMAX * TNTH / NT; ++m) {
+  for (int m = 0; m < nld<NT>(); ++m) {
     const int i = threadIdx.x + m * NT;
     if (i < nl) *(u32x4*)(dst + i * 16) = ((valid >> m) & 1) ? reg[m] : u32x4{0u, 0u, 0u, 0u};
   }
@@ -262,7 +269,7 @@ __global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ 
   }
   if (threadIdx.x < 64) bs[threadIdx.x] = bias ? bias[c0 + threadIdx.x] : 0.f;
   const int lead = TR ? 2 : 0;
-  u32x4 reg[LMAX];   // LMAX * TNTH / TNTH
+  u32x4 reg[nld<TNTH>()];
   unsigned rvalid = 0;
   for (int tp = 0; tp <= lead && tp < g.T; ++tp) {
     rvalid = plane_load<TNTH>(xin, g, D, b, h0, c0, tp, reg);
@@ -376,7 +383,7 @@ __global__ __launch_bounds__(WNTH, 3) void peg_wgrad_tile_kernel(const u16* __re
   for (int i = 0; i < 27; ++i) acc[i][0] = acc[i][1] = 0.f;
   // planes two steps ahead (regA = plane t+1, regB = plane t+2), this thread's dout one step
   // ahead (one (row, segment) item per thread: wgrad_ok)
-  u32x4 regA[LMAX * TNTH / WNTH], regB[LMAX * TNTH / WNTH];
+  u32x4 regA[nld<WNTH>()], regB[nld<WNTH>()];
   unsigned va = plane_load<WNTH, false>(xin, g, D, b, h0, c0, 0, regA), vb = ~0u;
   plane_store<WNTH>(ring, g.W, 0, regA, va);
   if (g.T > 1) va = plane_load<WNTH, false>(xin, g, D, b, h0, c0, 1, regA);
@@ -442,7 +449,7 @@ __global__ __launch_bounds__(WNTH, 3) void peg_wgrad_tile_kernel(const u16* __re
     __syncthreads();   // slot of plane tn held plane tn - 3, read in this step
     if (tn < g.T) plane_store<WNTH>(ring, g.W, tn, regA, va);
 #pragma unroll
-    for (int m = 0; m < LMAX * TNTH / WNTH; ++m) regA[m] = regB[m];
+    for (int m = 0; m < nld<WNTH>(); ++m) regA[m] = regB[m];
     va = vb;
 #pragma unroll
     for (int j = 0; j < SEGW; ++j) du[j] = dn[j];
@@ -470,7 +477,7 @@ __global__ __launch_bounds__(WNTH, 3) void peg_wgrad_tile_kernel(const u16* __re
 }
 
 bool tiled_ok(int W, int D) {
-  return D % 64 == 0 && HT * ((W + SEG - 1) / SEG) * 8 <= TNTH && (HT + 2) * (W + 2) * 8 <= LMAX * TNTH &&
+  return D % 64 == 0 && HT * ((W + SEG - 1) / SEG) * 8 <= TNTH && (HT + 2) * (W + 2) * 8 <= PLANE_CH &&
          HT * ((W + SEGW - 1) / SEGW) * 32 <= WNTH;   // wgrad: one item per thread
 }
 
