@@ -586,6 +586,24 @@ __device__ __forceinline__ u32x4 pair_swap(const float* x4, const float* y4) {
 }
 __device__ __forceinline__ int pair_coff(int g) { return ((g & 1) ? 16 : 0) + ((g & 2) ? 8 : 0); }
 
+// value of lane ^ 16 / lane ^ 32 through v_permlane16_swap / v_permlane32_swap (VALU) instead of
+// ds_bpermute (the LDS crossbar, ~100+ cycles each in the argmax / l2norm epilogues).  Swapping x
+// with itself leaves (even rows / low half in [0], odd rows / high half in [1]) exchanged copies.
+__device__ __forceinline__ unsigned xor16_u(unsigned x, int lane) {
+  const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  return (lane & 16) ? r[0] : r[1];
+}
+__device__ __forceinline__ unsigned xor32_u(unsigned x, int lane) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return (lane & 32) ? r[0] : r[1];
+}
+template <int O> __device__ __forceinline__ float xorf(float x, int lane) {
+  return __uint_as_float(O == 16 ? xor16_u(__float_as_uint(x), lane) : xor32_u(__float_as_uint(x), lane));
+}
+template <int O> __device__ __forceinline__ int xori(int x, int lane) {
+  return (int)(O == 16 ? xor16_u((unsigned)x, lane) : xor32_u((unsigned)x, lane));
+}
+
 // 16-B epilogue store; CTCLIP_EPI_SC1 (A/B build): write-through sc1, which drops the line from
 // the XCD's L2 instead of keeping it (MI355X_MICROARCH.md, store flavours), so the output stream
 // does not evict the operand panels that the XCD's other tiles re-read
@@ -613,6 +631,13 @@ __device__ __forceinline__ void store_row_bf16(u16* rowp, const float (&v)[4][4]
 // MODE (compile time, so each variant's row loop stays small enough to unroll fully and the
 // accumulator never leaves registers): 0 = general (bias / residual / GELU / f32 or bf16 /
 // accumulate / shadow), 2 = GEGLU, 3 = argmax, 4 = GEGLU backward, 5 = split-K slab.
+#ifndef CTCLIP_GEMM_PERMLANE
+#define CTCLIP_GEMM_PERMLANE 0
+#endif
+// A/B build switch of the xor16 / xor32 exchanges: permlane swaps measured 2 % slower than
+// ds_bpermute on the VQ argmax GEMM (1.193 vs 1.171-1.176 ms, profiles/r02aw_*), so off
+constexpr bool GEMM_PERMLANE = CTCLIP_GEMM_PERMLANE;
+
 template <int MODE>
 __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int wr, int wc, int lane, int64_t m0,
                                            int64_t n0, int split, int bidx) {
@@ -639,6 +664,10 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
     if constexpr (MODE == 3) {
       // argmax over the wave's 64 columns of row gm (first-max tie-break): 16 values per lane,
       // then across the 4 lanes g = 0..3 that hold the same row
+      // branch-free (selects): the if / else form compiled to exec-mask branches per element and
+      // made this epilogue as long as the tile's whole main loop (r02 stamps: 31.5 k cycles).  A
+      // lane scans its columns in increasing order, so the in-lane tie-break (first max) is a
+      // strict >; columns past N read as -inf and never win (bi stays 0x7fffffff when all are)
       float best = -INFINITY, second = -INFINITY;
       int bi = 0x7fffffff;
 #pragma unroll
@@ -646,18 +675,25 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = 16 * j + 4 * g + r;
-          if (wcol0 + c < p.N) {
-            if (v[j][r] > best || (v[j][r] == best && c < bi)) { second = best; best = v[j][r]; bi = c; }
-            else second = fmaxf(second, v[j][r]);
-          }
+          const float x = wcol0 + c < p.N ? v[j][r] : -INFINITY;
+          const bool gt = x > best;
+          second = gt ? best : fmaxf(second, x);
+          bi = gt ? c : bi;
+          best = gt ? x : best;
         }
+      auto merge = [&](float ob, float os, int oi) {
+        const bool take = ob > best || (ob == best && oi < bi);
+        second = take ? fmaxf(best, os) : fmaxf(second, ob);
+        bi = take ? oi : bi;
+        best = take ? ob : best;
+      };
+      if (GEMM_PERMLANE) {
+        { const float ob = xorf<16>(best, lane), os = xorf<16>(second, lane); merge(ob, os, xori<16>(bi, lane)); }
+        { const float ob = xorf<32>(best, lane), os = xorf<32>(second, lane); merge(ob, os, xori<32>(bi, lane)); }
+      } else {
 #pragma unroll
-      for (int o = 16; o <= 32; o <<= 1) {
-        const float ob = __shfl_xor(best, o, 64);
-        const float os = __shfl_xor(second, o, 64);
-        const int oi = __shfl_xor(bi, o, 64);
-        if (ob > best || (ob == best && oi < bi)) { second = fmaxf(best, os); best = ob; bi = oi; }
-        else second = fmaxf(second, ob);
+        for (int o = 16; o <= 32; o <<= 1)
+          merge(__shfl_xor(best, o, 64), __shfl_xor(second, o, 64), __shfl_xor(bi, o, 64));
       }
       if (g == 0 && rok && wcol0 < p.N) {
         float2* out = (float2*)p.C + bidx * p.sC;
@@ -694,8 +730,13 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
           float ss = 0.f;
 #pragma unroll
           for (int e = 0; e < 8; ++e) ss += c8[e] * c8[e];
-          ss += __shfl_xor(ss, 32, 64);
-          ss += __shfl_xor(ss, 16, 64);
+          if (GEMM_PERMLANE) {
+            ss += xorf<32>(ss, lane);
+            ss += xorf<16>(ss, lane);
+          } else {
+            ss += __shfl_xor(ss, 32, 64);
+            ss += __shfl_xor(ss, 16, 64);
+          }
           const float inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
           float o8[8];
 #pragma unroll

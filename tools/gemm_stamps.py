@@ -24,12 +24,17 @@ def main():
     w1, w2 = r(2816, 512), r(512, 1408)
     g = torch.empty(M, 1408, device='cuda', dtype=torch.bfloat16)
     dh = torch.empty(M, 2816, device='cuda', dtype=torch.bfloat16)
+    cb = r(8192, 512)
+    cand = torch.empty(M, 128, 2, device='cuda')
+    cand2 = torch.empty(M, 128, device='cuda')
     shapes = {
         'ff1': lambda: K.linear(x512, w1, act=K.ACT_GEGLU, out2=g),
         'ff1plain': lambda: K.linear(x512, w1, out=dh),
         'dx1408': lambda: K.matmul_nn(x512, w2),
         'geglubwd': lambda: K.matmul_nn_geglu_bwd(x512, w2, dh),
         'dwq': lambda: K.matmul_tn(x512[:, :256], x512),
+        'vq': lambda: K.gemm_raw(M, 8192, 512, x512, 512, True, cb, 512, True, cand, 128, C2=cand2, ldc2=128,
+                                 act=K.ACT_ARGMAX),
     }
     L = _lib.lib()
     L.ctclip_gemm_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
