@@ -724,6 +724,13 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_bias_kernel(AP p, int nfc) {
 //  * the dQ exchange of the key parts reuses the finished frame's buffer; the bias bins reuse
 //    buffer 0 after the last frame.
 constexpr int DQD_W = 8, DQD_NT = DQD_W * 64, DQD_KP = 2;
+// bias-gradient binning of the dQ kernel: 1 = diagonal sums over an LDS image of the block's
+// frame-summed dS (no LDS float atomics); 0 = LDS atomics per (query, key) (A/B build switch).
+// Measured (profiles/r02ba_attn_bin_ab.log): spatial backward 837 -> 807 us per layer; without
+// any binning it would be 692 us -- the remainder is the 1,008 workgroups x 2,209 global atomics
+#ifndef CTCLIP_ATTN_DIAG_BIN
+#define CTCLIP_ATTN_DIAG_BIN 1
+#endif
 __device__ __forceinline__ int kv_swz(int row) { return (row >> 1) & 3; }
 __device__ __forceinline__ bf16x8 rowfrag_sw(const char* img, int r0, int lane) {
   const int row = r0 + (lane & 15);
@@ -892,9 +899,39 @@ __global__ __launch_bounds__(DQD_NT) void attn_bwd_dq_bias_dma_kernel(AP p, int 
   // bin the frame-summed dS once (bins in buffer 0: every wave is past its last read of it)
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
+#if CTCLIP_ATTN_DIAG_BIN
+  // without LDS float atomics: the block's 64 x L frame-summed dS go to LDS (both K / V buffers,
+  // free now: 64 x 576 x 4 B = 147,456 B = 2 BUF), then each thread sums whole bins along their
+  // diagonals, bin (dh, dw) = sum over the 64 queries q of dS[q][q - (dh, dw)], in a fixed order
+  {
+    static_assert(64 * L * 4 <= 2 * BUF, "dS block fits the two frame buffers");
+    float* S = (float*)smem;
+    const int ql = qsub * 16 + li;
+#pragma unroll
+    for (int ci = 0; ci < NCP; ++ci)
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) S[ql * L + (c_begin + ci) * 32 + 16 * bi + 4 * g + r] = acc[ci][bi][r];
+    __syncthreads();
+    const int Wg = p.Wg, Hg = p.Hg, W2 = 2 * Wg - 1, q0 = qg * 64;
+    for (int b = tid; b < p.nbins; b += NTH) {
+      const int dh = b / W2 - (Hg - 1), dw = b % W2 - (Wg - 1);
+      float sum = 0.f;
+      int qh = q0 / Wg, qw = q0 - (q0 / Wg) * Wg;
+      for (int j = 0; j < 64; ++j) {
+        const int kh = qh - dh, kw = qw - dw;
+        if (kh >= 0 && kh < Hg && kw >= 0 && kw < Wg) sum += S[j * L + kh * Wg + kw];
+        if (++qw == Wg) { qw = 0; ++qh; }
+      }
+      if (sum != 0.f) atomicAdd(&p.dbias_u[(int64_t)h * p.nbins + b], sum);
+    }
+  }
+#else
   float* bins = (float*)smem;
   for (int i = tid; i < p.nbins; i += NTH) bins[i] = 0.f;
   __syncthreads();
+#ifndef CTCLIP_ATTN_NO_BIN   // diagnostic build only: skip the binning (wrong bias gradient) to time it
 #pragma unroll
   for (int ci = 0; ci < NCP; ++ci)
 #pragma unroll
@@ -904,11 +941,15 @@ __global__ __launch_bounds__(DQD_NT) void attn_bwd_dq_bias_dma_kernel(AP p, int 
         const int key = (c_begin + ci) * 32 + 16 * bi + 4 * g + r;
         atomicAdd(&bins[cq - kb[key]], acc[ci][bi][r]);
       }
+#else
+  if (acc[0][0][0] == 12345.f) bins[0] = 1.f;   // keep acc live
+#endif
   __syncthreads();
   for (int i = tid; i < p.nbins; i += NTH) {
     const float v = bins[i];
     if (v != 0.f) atomicAdd(&p.dbias_u[(int64_t)h * p.nbins + i], v);
   }
+#endif
 }
 
 // --------------------------------------------- backward dK dV, biased, base spatial shape (L = LF)
