@@ -46,6 +46,7 @@ struct AP {
   float* delta;                   // [H][M]
   const float* bias_u;            // [H][nbins] or null
   float* dbias_u;                 // [H][nbins] (accumulated with atomics) or null
+  float* dbias_ws;                // spatial dQ kernel: [workgroups per head][H][nbins] partial bins, or null
   const int32_t* kmask;           // [nseq][L] 1 = keep, or null
   float scale;
   int L, H, nseq;
@@ -924,7 +925,8 @@ __global__ __launch_bounds__(DQD_NT) void attn_bwd_dq_bias_dma_kernel(AP p, int 
         if (kh >= 0 && kh < Hg && kw >= 0 && kw < Wg) sum += S[j * L + kh * Wg + kw];
         if (++qw == Wg) { qw = 0; ++qh; }
       }
-      if (sum != 0.f) atomicAdd(&p.dbias_u[(int64_t)h * p.nbins + b], sum);
+      if (p.dbias_ws) p.dbias_ws[((int64_t)(qg * nfc + fc) * p.H + h) * p.nbins + b] = sum;
+      else if (sum != 0.f) atomicAdd(&p.dbias_u[(int64_t)h * p.nbins + b], sum);
     }
   }
 #else
@@ -1132,6 +1134,7 @@ int fill(AP& p, const ctclip_attn_args* a) {
   p.dv = (u16*)a->dv; p.lddv = a->lddv;
   p.lse = a->lse; p.delta = a->delta;
   p.bias_u = a->bias_u; p.dbias_u = a->dbias_u;
+  p.dbias_ws = a->dbias_ws;
   p.kmask = a->kmask;
   p.scale = a->scale;
   p.drop_p = a->dropout_p;
@@ -1442,6 +1445,48 @@ extern "C" int ctclip_attn_fwd(const ctclip_attn_args* a, void* stream) {
   return 0;
 }
 
+// launch plan of the frame-inner dQ + bias-gradient kernels (shared with the workspace query)
+struct DqPlan {
+  int nqg = 0, nfc = 0;
+  bool dma = false;
+  size_t lds = 0, lds_dma = 0;
+};
+bool dq_plan(const AP& p, int D, DqPlan& pl) {
+  const int Lp = (p.L + 31) & ~31, nc = Lp / 32;
+  if (!(D == 32 && p.bias_u && p.dbias_u && !p.kmask && (nc + 1) / 2 <= 9)) return false;
+  const size_t RSb = D * 2 + 16;
+  pl.nqg = cdiv(p.L, 64);
+  // frame chunks: at least two workgroups per CU, then (up to twice that) the count whose last
+  // dispatch round is fullest -- 72 x 14 = 1,008 workgroups = 3.94 rounds of 256 at the base
+  // shape (measured: nfc 8 / 14 / 28 -> spatial backward 1,109 / 1,074 / 1,242 us)
+  const int per = p.H * pl.nqg;
+  const int lo = std::max(1, std::min(p.nseq, (2 * 256 + per - 1) / per));
+  pl.nfc = lo;
+  double best = 0.0;
+  for (int f = lo; f <= std::min(p.nseq, 2 * lo); ++f) {
+    const long wgs = (long)per * f, rounds = (wgs + 255) / 256;
+    const double eff = (double)wgs / (double)(rounds * 256);
+    if (eff > best + 1e-3) { best = eff; pl.nfc = f; }
+  }
+  pl.lds = (size_t)2 * Lp * RSb + 2 * (size_t)((p.nbins + 3) & ~3) * 4 + 2 * (size_t)Lp * 4 + 4 * 64 * 8 * 4;
+  static int dma_ok = -1;   // CTCLIP_ATTN_DQ_DMA=0: the generic kernel (A/B)
+  if (dma_ok < 0) { const char* e = getenv("CTCLIP_ATTN_DQ_DMA"); dma_ok = e ? atoi(e) != 0 : 1; }
+  pl.lds_dma = (size_t)2 * 2 * 576 * 64 + (size_t)((p.nbins + 3) & ~3) * 4 + 576 * 4;
+  pl.dma = dma_ok && run_ok(p) && p.L == 576 && p.s_pos == 1 && p.n_inner == 1 && p.nbins * 4 <= 2 * 576 * 64 &&
+           pl.lds_dma <= 160 * 1024;
+  return true;
+}
+
+// floats of the optional bias-gradient workspace (ctclip_attn_args.dbias_ws) for this shape;
+// 0 when the shape bins with atomics (no frame-inner dQ kernel / not the LDS-DMA one)
+extern "C" int ctclip_attn_bwd_ws_floats(const ctclip_attn_args* a) {
+  AP p;
+  if (fill(p, a)) return 0;
+  DqPlan pl;
+  if (!CTCLIP_ATTN_DIAG_BIN || !dq_plan(p, a->D, pl) || !pl.dma || (p.H * p.nbins) % 4) return 0;
+  return pl.nqg * pl.nfc * p.H * p.nbins;
+}
+
 extern "C" int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream) {
   AP p;
   int rc = fill(p, a);
@@ -1461,33 +1506,25 @@ extern "C" int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream) {
     CT_CHECK_LAUNCH();
     return 0;
   }
-  const int nc = Lp / 32;
-  if (a->D == 32 && p.bias_u && p.dbias_u && !p.kmask && (nc + 1) / 2 <= 9) {
+  DqPlan pl;
+  if (dq_plan(p, a->D, pl)) {
     // frame-inner dQ + bias-gradient kernel (see attn_bwd_dq_bias_kernel)
-    const int nqg = cdiv(p.L, 64);
-    // frame chunks: at least two workgroups per CU, then (up to twice that) the count whose last
-    // dispatch round is fullest -- 72 x 14 = 1,008 workgroups = 3.94 rounds of 256 at the base
-    // shape (measured: nfc 8 / 14 / 28 -> spatial backward 1,109 / 1,074 / 1,242 us)
-    const int per = p.H * nqg;
-    const int lo = std::max(1, std::min(p.nseq, (2 * 256 + per - 1) / per));
-    int nfc = lo;
-    double best = 0.0;
-    for (int f = lo; f <= std::min(p.nseq, 2 * lo); ++f) {
-      const long wgs = (long)per * f, rounds = (wgs + 255) / 256;
-      const double eff = (double)wgs / (double)(rounds * 256);
-      if (eff > best + 1e-3) { best = eff; nfc = f; }
+    const int nqg = pl.nqg, nfc = pl.nfc;
+    if (pl.lds > 160 * 1024) return CT_ESHAPE;
+    const bool slab = CTCLIP_ATTN_DIAG_BIN && pl.dma && p.dbias_ws && (p.H * p.nbins) % 4 == 0 &&
+                      a->dbias_ws_floats >= (int64_t)nqg * nfc * p.H * p.nbins;
+    if (!slab) p.dbias_ws = nullptr;
+    if (pl.dma)
+      hipLaunchKernelGGL((attn_bwd_dq_bias_dma_kernel<576>), dim3(p.H, nqg, nfc), dim3(DQD_NT), pl.lds_dma, st, p, nfc);
+    else if (run_ok(p)) hipLaunchKernelGGL((attn_bwd_dq_bias_kernel<9, true>), dim3(p.H, nqg, nfc), dim3(NT), pl.lds, st, p, nfc);
+    else hipLaunchKernelGGL((attn_bwd_dq_bias_kernel<9>), dim3(p.H, nqg, nfc), dim3(NT), pl.lds, st, p, nfc);
+    CT_CHECK_LAUNCH();
+    if (slab) {   // deterministic sum of the workgroups' partial bins into dbias_u
+      // [H][nbins] summed as one row of H * nbins floats (nbins = 2,209 is odd; the product is not)
+      const int64_t n = (int64_t)p.H * p.nbins;
+      const int r = ctclip_reduce_slabs(p.dbias_ws, (int64_t)nqg * nfc, 1, n, n, p.dbias_u, n, 1, 1, stream);
+      if (r) return r;
     }
-    const size_t lds = (size_t)2 * Lp * RSb + 2 * (size_t)((p.nbins + 3) & ~3) * 4 + 2 * (size_t)Lp * 4 +
-                       4 * 64 * 8 * 4;
-    if (lds > 160 * 1024) return CT_ESHAPE;
-    static int dma_ok = -1;   // CTCLIP_ATTN_DQ_DMA=0: the generic kernel (A/B)
-    if (dma_ok < 0) { const char* e = getenv("CTCLIP_ATTN_DQ_DMA"); dma_ok = e ? atoi(e) != 0 : 1; }
-    const size_t lds_dma = (size_t)2 * 2 * 576 * 64 + (size_t)((p.nbins + 3) & ~3) * 4 + 576 * 4;
-    if (dma_ok && run_ok(p) && p.L == 576 && p.s_pos == 1 && p.n_inner == 1 && p.nbins * 4 <= 2 * 576 * 64 &&
-        lds_dma <= 160 * 1024)
-      hipLaunchKernelGGL((attn_bwd_dq_bias_dma_kernel<576>), dim3(p.H, nqg, nfc), dim3(DQD_NT), lds_dma, st, p, nfc);
-    else if (run_ok(p)) hipLaunchKernelGGL((attn_bwd_dq_bias_kernel<9, true>), dim3(p.H, nqg, nfc), dim3(NT), lds, st, p, nfc);
-    else hipLaunchKernelGGL((attn_bwd_dq_bias_kernel<9>), dim3(p.H, nqg, nfc), dim3(NT), lds, st, p, nfc);
     launch_dkv<32>(p, grid, lds2, st);
     CT_CHECK_LAUNCH();
     return 0;

@@ -69,6 +69,7 @@ class AttnArgs(ctypes.Structure):
         ('grid_h', c_i32), ('grid_w', c_i32), ('n_inner', c_i32),
         ('s_outer', c_i64), ('s_inner', c_i64), ('s_pos', c_i64),
         ('dropout_p', c_f32), ('dropout_seed', ctypes.c_uint64),
+        ('dbias_ws', c_vp), ('dbias_ws_floats', c_i64),
     ]
 
 
@@ -124,6 +125,7 @@ _SIGS = {
     'ctclip_peg_wgrad_slabs': [c_i64, c_i32, c_i32, c_i32, c_i32],
     'ctclip_attn_fwd': [ctypes.POINTER(AttnArgs), c_vp],
     'ctclip_attn_bwd': [ctypes.POINTER(AttnArgs), c_vp],
+    'ctclip_attn_bwd_ws_floats': [ctypes.POINTER(AttnArgs)],
     'ctclip_vq_select': [c_vp, c_vp, c_i32, c_vp, c_i64, c_i32, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp],
     'ctclip_vq_pool': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
     'ctclip_vq_pool_bwd': [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],

@@ -504,7 +504,19 @@ def attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, *, L, H, D, nseq, scale, seq, bi
     a = _attn_args(q, k, v, o, L=L, H=H, D=D, nseq=nseq, M=M, scale=scale, seq=seq, bias_u=bias_u, grid=grid,
                    kmask=kmask, lse=lse, dout=dout, dq=dq, dk=dk, dv=dv, delta=delta, dbias_u=dbias_u,
                    dropout=dropout)
+    ws = None
+    if dbias_u is not None and _ATTN_BIAS_WS:
+        # per-workgroup partial bins + one deterministic reduction instead of global float atomics
+        n = _lib.lib().ctclip_attn_bwd_ws_floats(_lib.ctypes.byref(a))
+        if n > 0:
+            ws = torch.empty(n, device=q.device, dtype=F32)
+            a.dbias_ws, a.dbias_ws_floats = ptr(ws), n
     call('ctclip_attn_bwd', _lib.ctypes.byref(a), stream_ptr())
+
+
+# the bias-gradient workspace (deterministic slab reduction) measured no faster than the atomics
+# (spatial backward 822 vs 810 us, profiles/r02bc_attn_ws_ab.log): opt-in via CTCLIP_ATTN_BIAS_WS=1
+_ATTN_BIAS_WS = os.environ.get('CTCLIP_ATTN_BIAS_WS', '0') != '0'
 
 
 # ----------------------------------------------------------------------------- VQ

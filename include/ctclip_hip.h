@@ -229,9 +229,15 @@ typedef struct {
    * the backward regenerates the mask from the same seed.  0 = off; bias_u != null: CT_EINVAL. */
   float dropout_p;
   uint64_t dropout_seed;
+  /* bwd, optional: caller-provided workspace for the bias gradient's per-workgroup partial bins,
+   * summed into dbias_u by one deterministic reduction instead of global float atomics; NULL =
+   * atomics.  Its size in floats is ctclip_attn_bwd_ws_floats(a) (0: this shape does not use it). */
+  float* dbias_ws;
+  int64_t dbias_ws_floats;
 } ctclip_attn_args;
 int ctclip_attn_fwd(const ctclip_attn_args* a, void* stream);
 int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream);
+int ctclip_attn_bwd_ws_floats(const ctclip_attn_args* a);
 
 /* ---------------------------------------------------------------- vector quantiser
  * vector_quantize_pytorch==1.1.2 cosine codebook (ct_clip/ctvit.py:187,421-427).
