@@ -264,6 +264,7 @@ def nblocks_for(rows, cap=1024):
 
 
 _LNB_WIDE = os.environ.get('CTCLIP_LNB_WIDE', '1') != '0'   # A/B switch of nblocks_for's short-input rule
+_LNB_CAP = int(os.environ.get('CTCLIP_LNB_CAP', '1024'))      # LayerNorm-backward workgroup cap (A/B)
 
 
 def colsum(x, out=None, accumulate=False):
@@ -299,7 +300,7 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, *, dres=None, want_beta=True, dx_f32
     """Returns (dx_f32, dx_bf16, dgamma, dbeta).  dgamma_out / dbeta_out: accumulate the
     parameter gradients into these f32 tensors instead of returning fresh ones."""
     rows, D = x.shape
-    nb = nblocks_for(rows, 1024)
+    nb = nblocks_for(rows, _LNB_CAP)
     dxf = torch.empty(rows, D, device=x.device, dtype=F32) if dx_f32 else None
     dxb = torch.empty(rows, D, device=x.device, dtype=BF16) if dx_bf16 else None
     pg = torch.empty(nb, D, device=x.device, dtype=F32)
