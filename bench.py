@@ -62,9 +62,12 @@ def synthetic_inputs(B, L, rank, device, frames=240, size=480, vocab=30522):
     return hu, types.SimpleNamespace(input_ids=ids, attention_mask=mask)
 
 
-def cpu_baseline(batch):
+def cpu_baseline(batch, runs=3):
     """The oracle (fp32 eager CPU restatement of the reference, pinned by tests/golden) timed on
-    this host: one full contrastive step (fwd + bwd + Adam) at batch `batch`, base config."""
+    this host, per SURVEY 8(d) / BASELINE.md: one full contrastive step (fwd + bwd + clip + Adam) at
+    batch `batch`, base config, all host threads; one untimed warm-up step, then the MEDIAN of
+    `runs` timed steps."""
+    import statistics
     from oracle import ctclip_oracle as O
     from oracle import weights as W
     threads = os.cpu_count() or 1
@@ -81,13 +84,23 @@ def cpu_baseline(batch):
     opt = torch.optim.Adam(params, lr=1.25e-6, betas=(0.9, 0.99), eps=1e-8)
     ids, mask = W.make_text(batch, 128, cfg.bert.vocab_size)
     video = O.normalize_hu(W.make_hu(batch, cfg.vit))
-    t0 = time.perf_counter()
-    out = O.ctclip_forward(sd, ids, mask, video, cfg, training=True)
-    out['loss'].backward()
-    torch.nn.utils.clip_grad_norm_(params, 0.5)
-    opt.step()
-    opt.zero_grad()
-    dt = time.perf_counter() - t0
+
+    def step():
+        t0 = time.perf_counter()
+        out = O.ctclip_forward(sd, ids, mask, video, cfg, training=True)
+        out['loss'].backward()
+        torch.nn.utils.clip_grad_norm_(params, 0.5)
+        opt.step()
+        opt.zero_grad()
+        return time.perf_counter() - t0
+
+    warm = step()
+    print(f'cpu_baseline: warm-up step {warm:.1f} s', file=sys.stderr, flush=True)
+    times = []
+    for i in range(runs):
+        times.append(step())
+        print(f'cpu_baseline: step {i + 1}/{runs} {times[-1]:.1f} s', file=sys.stderr, flush=True)
+    dt = statistics.median(times)
     cpu_name = ''
     try:
         for line in open('/proc/cpuinfo'):
@@ -96,9 +109,12 @@ def cpu_baseline(batch):
                 break
     except OSError:
         pass
-    return {'value': batch / dt, 'unit': 'pairs/s', 'cores': threads, 'kind': 'port',
-            'sample': f'1 contrastive step (fwd+bwd+clip+Adam), base config, batch {batch}, 128-token text, '
-                      f'fp32 eager oracle on CPU ({cpu_name}); {dt:.1f} s'}
+    return {'value': round(batch / dt, 4), 'unit': 'pairs/s', 'cores': threads, 'kind': 'port',
+            'sample': f'contrastive step (fwd+bwd+clip+Adam), base config, batch {batch}, 128-token text, fp32 '
+                      f'eager oracle on CPU ({cpu_name}, {threads} threads of {os.cpu_count()} logical CPUs): '
+                      f'1 warm-up ({warm:.1f} s) then median of {runs} steps '
+                      f'({", ".join(f"{t:.1f}" for t in times)} s)',
+            'step_s_median': round(dt, 3), 'step_s_runs': [round(t, 3) for t in times]}
 
 
 def launch_ranks(args):

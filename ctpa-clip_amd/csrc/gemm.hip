@@ -561,6 +561,10 @@ __global__ __launch_bounds__(1024) void reduce_slabs_multi_kernel(MultiJobs jobs
 }
 
 extern "C" int ctclip_reduce_slabs_multi(const ctclip_slab_job* jobs, int32_t njobs, void* stream) {
+  // the jobs of one call run concurrently, each read-add-writing its output: outputs must be
+  // distinct (the caller splits a shared output over successive calls, kernels.flush_reductions)
+  for (int32_t i = 0; i < njobs; ++i)
+    for (int32_t k = 0; k < i; ++k) CT_REQUIRE(jobs[i].out != jobs[k].out, CT_EINVAL);
   for (int32_t j0 = 0; j0 < njobs; j0 += MULTI_JOBS) {
     MultiJobs mj{};
     const int n = std::min<int32_t>(MULTI_JOBS, njobs - j0);

@@ -97,9 +97,11 @@ class CTCLIP(nn.Module):
     def _project(self, W, Wb, pooled, pooled_b):
         return Fn.ImageProjFn.apply(pooled, pooled_b, W, Wb)
 
-    def encode(self, text, image):
+    def encode(self, text, image, gather=False):
         """Text + image towers and raw latents: (enc_text (B,L,768), pooled (B, h*w*d),
-        text_raw (B, dl), image_raw (B, dl))."""
+        text_raw (B, dl), image_raw (B, dl)).  ``gather``: the caller will compute the global-batch
+        loss, so under torch.distributed the text latents' all-gather starts here (every rank makes
+        the same call); other callers (scores, encodings) issue no collective."""
         # The host queues the image tower first (its ~16 ms of GPU work keep this stream busy while
         # the host queues BERT's many small launches), BERT on the text stream (streams.py) ordered
         # only after an event taken before the image tower, so the two run side by side.
@@ -113,7 +115,7 @@ class CTCLIP(nn.Module):
             t_raw = Fn.TextProjFn.apply(enc_text[:, 0, :].contiguous(), self.to_text_latent.weight)
             # N > 1: the text latents' all-gather goes out from the text stream now, beside the
             # 3D-ViT forward still running on the main stream (SURVEY 8(e) overlap)
-            self._t_gather = dist_sync.start_gather(t_raw) if dist_sync.world_rank()[0] > 1 else None
+            self._t_gather = dist_sync.start_gather(t_raw) if gather and dist_sync.world_rank()[0] > 1 else None
         streams.join_text(dev)
         if ts is not None:
             t_raw.record_stream(torch.cuda.current_stream(dev))
@@ -149,7 +151,8 @@ class CTCLIP(nn.Module):
             W = self.to_visual_latent.weight
             i_raw = self._project(W, self._visual_weight_bf16(W), pooled, pooled_b)
             return l2norm(t_raw), l2norm(i_raw), tokens
-        enc_text, pooled, t_raw, i_raw = self.encode(text, image)
+        self._t_gather = None
+        enc_text, pooled, t_raw, i_raw = self.encode(text, image, gather=return_loss and not return_encodings)
         if return_encodings:
             return enc_text, pooled
         if not return_loss:

@@ -165,7 +165,6 @@ def _adjacent(ts, arena_of):
 _FP8 = {'on': False}
 _L2N_FUSED = os.environ.get('CTCLIP_L2N_FUSED', '1') != '0'   # A/B switch of the act-5 projections
 _QKV_WGRAD = os.environ.get('CTCLIP_QKV_WGRAD', '1') != '0'   # A/B switch of BERT's merged q/k/v wgrad
-_FP8_W = {}
 
 
 def set_vit_fp8(on):
@@ -179,20 +178,25 @@ def vit_fp8():
     return _FP8['on']
 
 
-def fp8_weight(key, Wb):
-    """(q, scales) of the bf16 weight Wb, re-quantised when the optimizer has moved the weights."""
-    ep = K.weights_epoch()
-    e = _FP8_W.get(key)
-    if e is None or e[0] != ep or e[1] != Wb.data_ptr():
-        e = (ep, Wb.data_ptr()) + K.quant_mxfp8(Wb)
-        _FP8_W[key] = e
-    return e[2], e[3]
+def fp8_weight(W, tag, Wb):
+    """(q, scales) of the bf16 weight image Wb of parameter W, cached ON the parameter and
+    re-quantised whenever the master changed: an optimizer update (weights_epoch; Adam writes the
+    arena through raw pointers), an in-place copy / load_state_dict (W._version) or a re-bound
+    storage (data_ptr).  Dies with the parameter (no module-level cache keeping dead models alive)."""
+    key = (K.weights_epoch(), W._version, W.data_ptr())
+    cache = W.__dict__.setdefault('_ctclip_fp8', {})
+    e = cache.get(tag)
+    if e is None or e[0] != key:
+        e = (key,) + K.quant_mxfp8(Wb)
+        cache[tag] = e
+    return e[1], e[2]
 
 
-def fp8_linear(x, key, Wb, **kw):
-    """x[M, K] (bf16) @ Wb[N, K]^T through the MX-fp8 GEMM (epilogue keywords of gemm_mxfp8)."""
+def fp8_linear(x, W, tag, Wb, **kw):
+    """x[M, K] (bf16) @ Wb[N, K]^T through the MX-fp8 GEMM (epilogue keywords of gemm_mxfp8);
+    Wb is the bf16 (packed) image of parameter W."""
     qa, sa = K.quant_mxfp8(x)
-    qb, sb = fp8_weight(key, Wb)
+    qb, sb = fp8_weight(W, tag, Wb)
     return K.gemm_mxfp8(qa, sa, qb, sb, **kw)
 
 
@@ -362,8 +366,8 @@ class ViTLayerFn(torch.autograd.Function):
         Wq_b, Wkv_b, Wo_b = bf(Wq), bf(Wkv), bf(Wo)
         fp8 = vit_fp8()
         if fp8:
-            q = fp8_linear(xn, (id(Wq), 'q'), Wq_b)
-            kv = fp8_linear(x1b, (id(Wkv), 'kv'), Wkv_b)
+            q = fp8_linear(xn, Wq, 'q', Wq_b)
+            kv = fp8_linear(x1b, Wkv, 'kv', Wkv_b)
             qn = K.l2norm_scale_fwd(q, H, dh, q_scale)
             kn = K.l2norm_scale_fwd(kv[:, :inner], H, dh, k_scale)
         elif _L2N_FUSED and dh == 32 and inner % 64 == 0:
@@ -383,7 +387,7 @@ class ViTLayerFn(torch.autograd.Function):
                             bias_u=bias_u if use_bias else None, grid=(geo.Hg, geo.Wg) if use_bias else (0, 0))
         x2b = torch.empty_like(xb)
         if fp8:
-            x2f = fp8_linear(o, (id(Wo), 'o'), Wo_b, residual=x1f, out_f32=True, out2=x2b)
+            x2f = fp8_linear(o, Wo, 'o', Wo_b, residual=x1f, out_f32=True, out2=x2b)
         else:
             x2f = K.linear(o, Wo_b, residual=x1f, out_dtype=F32, out2=x2b)
         xn2, _, m2, r2 = K.layernorm_fwd(x2f, ff_w, ff_b, 1e-5)
@@ -391,8 +395,8 @@ class ViTLayerFn(torch.autograd.Function):
         g = torch.empty(xf.shape[0], W2p.shape[1], device=xf.device, dtype=BF16)
         x3b = torch.empty_like(xb)
         if fp8:
-            h = fp8_linear(xn2, (id(W1), 'ff1'), W1p, act=K.ACT_GEGLU, out2=g)
-            x3f = fp8_linear(g, (id(W2), 'ff2'), W2p, residual=x2f, out_f32=True, out2=x3b)
+            h = fp8_linear(xn2, W1, 'ff1', W1p, act=K.ACT_GEGLU, out2=g)
+            x3f = fp8_linear(g, W2, 'ff2', W2p, residual=x2f, out_f32=True, out2=x3b)
         else:
             # tagged for bench.py's live roofline: algorithmic flops exclude the zero padding rows
             h = K.linear(xn2, W1p, act=K.ACT_GEGLU, out2=g, tag='ff1',

@@ -196,14 +196,26 @@ def reduce_slabs(slabs, out, accumulate=False):
 # (dist_sync.BucketedGradSync).  CTCLIP_DEFER_REDUCE=0 restores the immediate launches.
 DEFER_REDUCE = os.environ.get('CTCLIP_DEFER_REDUCE', '1') != '0'
 _DEFERRED = {}        # stream id -> (stream, [(slabs, out, accumulate), ...])
-_CB_QUEUED = [False]
+_CB_QUEUED = [None]   # graph task id whose end-of-pass callback is queued (None: none)
+
+
+def _graph_task():
+    try:
+        return torch._C._current_graph_task_id()
+    except AttributeError:
+        return -1
 
 
 def _in_backward():
-    try:
-        return torch._C._current_graph_task_id() != -1
-    except AttributeError:
-        return False
+    return _graph_task() != -1
+
+
+def discard_deferred():
+    """Drop every queued reduction and forget the queued callback: the exception path of a
+    backward pass (trainer.forward_backward) -- a pass that raised never runs its callback, and
+    its partial sums must not land in the next pass's gradients."""
+    _DEFERRED.clear()
+    _CB_QUEUED[0] = None
 
 
 def flush_reductions(lo=None, hi=None):
@@ -223,18 +235,27 @@ def flush_reductions(lo=None, hi=None):
             del _DEFERRED[k]
         if not take:
             continue
-        arr = (_lib.SlabJob * len(take))()
-        for i, (sl, out, acc) in enumerate(take):
-            arr[i].slabs, arr[i].nslab, arr[i].cols = sl.data_ptr(), sl.shape[0], sl.shape[-1]
-            arr[i].out, arr[i].accumulate = out.data_ptr(), int(acc)
-        call('ctclip_reduce_slabs_multi', arr, len(take), st.cuda_stream)
+        # the jobs of one launch run concurrently and each read-add-writes its output: jobs that
+        # share an output (a parameter used twice in one pass) go to successive launches, in
+        # queue order, so no update is lost
+        while take:
+            seen, batch, rest = set(), [], []
+            for j in take:
+                (rest if j[1].data_ptr() in seen else batch).append(j)
+                seen.add(j[1].data_ptr())
+            arr = (_lib.SlabJob * len(batch))()
+            for i, (sl, out, acc) in enumerate(batch):
+                arr[i].slabs, arr[i].nslab, arr[i].cols = sl.data_ptr(), sl.shape[0], sl.shape[-1]
+                arr[i].out, arr[i].accumulate = out.data_ptr(), int(acc)
+            call('ctclip_reduce_slabs_multi', arr, len(batch), st.cuda_stream)
+            take = rest
         # the partial buffers were allocated on `st`; freeing them after this launch is ordered
         used.append(st)
     return used
 
 
 def _end_of_backward():
-    _CB_QUEUED[0] = False
+    _CB_QUEUED[0] = None
     flush_reductions()
 
 
@@ -245,9 +266,10 @@ def reduce_param_partials(part, out, accumulate):
             and D % 4 == 0 and _in_backward()):
         st = torch.cuda.current_stream(part.device)
         _DEFERRED.setdefault(st.cuda_stream, (st, []))[1].append((part, out.view(-1), accumulate))
-        if not _CB_QUEUED[0]:
+        task = _graph_task()
+        if _CB_QUEUED[0] != task:      # a new pass (or one whose predecessor raised before its end)
             torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
-            _CB_QUEUED[0] = True
+            _CB_QUEUED[0] = task
         return out
     return reduce_slabs(part.view(nb, 1, D), out.view(1, D), accumulate=accumulate)
 

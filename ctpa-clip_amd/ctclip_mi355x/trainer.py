@@ -135,6 +135,7 @@ class CTClipTrainer:
                 self.model.backward_deferred_text()   # then BERT (text stream), beside the ViT tail
         except BaseException:
             dist_sync.disarm()
+            K.discard_deferred()
             raise
         finally:
             if defer:

@@ -224,3 +224,77 @@ def test_two_rank_bucketed_overlap(tmp_path):
     BucketedGradSync) reproduce the single-process global-batch gradient."""
     mp.spawn(_bucket_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
     assert all((tmp_path / f'ok{r}').exists() for r in range(WORLD))
+
+
+# ------------------------------------------------------------------ eval calls issue no collective
+class _StubVision(torch.nn.Module):
+    def encode_pooled(self, image):
+        return image, image
+
+
+class _StubText(torch.nn.Module):
+    def forward(self, input_ids, attention_mask=None, join=True, ready=None):
+        return (input_ids[:, None, :].float(),)
+
+
+def _eval_worker(rank, port, out_dir):
+    """CTCLIP.forward(return_loss=False / return_encodings=True) on ONE rank must not start the
+    latents' all-gather: the other rank never matches it, so the next collective
+    would pair with it.  Here rank 0 scores alone, then both ranks all-reduce and compute the
+    global loss; both must be exact."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=WORLD)
+    try:
+        import types
+        from ctclip_mi355x import ct_clip as C
+        from ctclip_mi355x import functional as Fn
+        from ctclip_mi355x import kernels as K
+
+        class _TP(torch.autograd.Function):   # f32 Linear on the CLS row (TextProjFn's math)
+            @staticmethod
+            def forward(ctx, cls, W):
+                ctx.save_for_backward(cls, W)
+                return cls @ W.t()
+
+            @staticmethod
+            def backward(ctx, g):
+                cls, W = ctx.saved_tensors
+                return g @ W, g.t() @ cls
+
+        Fn.TextProjFn = _TP
+        K.clip_scores = lambda t, i, lt: (torch.nn.functional.normalize(t, dim=-1)
+                                          * torch.nn.functional.normalize(i, dim=-1)).sum(-1) * lt.exp()
+        xt, xi, _, _ = _problem()
+        torch.manual_seed(5)              # same projection weights on both ranks
+        model = C.CTCLIP(image_encoder=_StubVision(), text_encoder=_StubText(), dim_text=DIN, dim_image=DIN,
+                         dim_latent=DL)
+        model._project = lambda W, Wb, pooled, pooled_b: pooled @ W.t()
+        model._visual_weight_bf16 = lambda W: W
+        rows = slice(rank * B, (rank + 1) * B)
+        text = types.SimpleNamespace(input_ids=xt[rows], attention_mask=torch.ones(B, DIN))
+        if rank == 0:
+            with torch.no_grad():
+                s = model(text, xi[rows], return_loss=False)
+                enc = model(text, xi[rows], return_encodings=True)
+            assert s.shape == (B,) and enc[1].shape == (B, DIN)
+            assert model._t_gather is None
+        probe = torch.full((4,), float(rank + 1))
+        dist.all_reduce(probe)
+        assert torch.equal(probe, torch.full((4,), 3.0)), probe
+        # the loss path still gathers: the global InfoNCE over both ranks' pairs
+        orig = Fn.ClipLossFn.apply
+        C.Fn.ClipLossFn = types.SimpleNamespace(apply=lambda t, i, lt, impl, tg: orig(t, i, lt, oracle_clip_loss, tg))
+        loss = model(text, xi[rows], return_loss=True)
+        with torch.no_grad():
+            t = torch.nn.functional.normalize(xt @ model.to_text_latent.weight.t(), dim=-1)
+            i = torch.nn.functional.normalize(xi @ model.to_visual_latent.weight.t(), dim=-1)
+            ref = O.infonce(t, i, model.temperature)
+        assert torch.allclose(loss.detach(), ref, rtol=1e-6, atol=1e-6), (loss.item(), ref.item())
+        open(os.path.join(out_dir, f'ok{rank}'), 'w').close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_eval_call_issues_no_collective(tmp_path):
+    mp.spawn(_eval_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    assert all((tmp_path / f'ok{r}').exists() for r in range(WORLD))

@@ -198,3 +198,23 @@ def test_vit_fp8_forward_vs_bf16(K):
         assert torch.isfinite(loss) and not torch.equal(before, p.detach())
     finally:
         Fn.set_vit_fp8(old)
+
+
+def test_fp8_weight_cache_follows_reload(K):
+    """The quantised-weight cache lives on the parameter and is keyed on its version: a weight
+    reload (in-place copy_, as load_state_dict does) between two fp8 forwards must re-quantise
+    (a module-level cache keyed by id() served stale weights)."""
+    from ctclip_mi355x import functional as Fn
+    torch.manual_seed(3)
+    W = torch.nn.Parameter((torch.randn(256, 512, device=dev) * 0.05))
+    x = torch.randn(300, 512, device=dev).bfloat16()
+    y0 = Fn.fp8_linear(x, W, 'probe', K.cast_bf16(W.detach()))
+    with torch.no_grad():
+        W.copy_(torch.randn(256, 512, device=dev) * 0.05)
+    y1 = Fn.fp8_linear(x, W, 'probe', K.cast_bf16(W.detach()))
+    ref = x.float() @ W.detach().t()
+    assert rel(y1, ref) < 6e-2 and rel(y0, ref) > 0.5
+    # unchanged weights: served from the cache (same quantised tensor object)
+    q1 = W._ctclip_fp8['probe'][1]
+    Fn.fp8_linear(x, W, 'probe', K.cast_bf16(W.detach()))
+    assert W._ctclip_fp8['probe'][1] is q1

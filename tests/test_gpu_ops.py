@@ -413,3 +413,26 @@ def test_reduce_slabs_multi_bit_identical(K):
     torch.cuda.synchronize()
     for (_, out, _), ref in zip(jobs, refs):
         assert torch.equal(out, ref)
+
+
+def test_deferred_reductions_shared_output(K):
+    """Two queued reductions into the SAME output (a parameter used twice in one pass):
+    flush_reductions splits them over successive launches so neither update is lost, and the C-ABI
+    refuses one call holding both."""
+    from ctclip_mi355x import _lib
+    torch.manual_seed(9)
+    out = torch.randn(512, device='cuda')
+    p1, p2 = torch.randn(64, 512, device='cuda'), torch.randn(96, 512, device='cuda')
+    ref = out.clone()
+    K.reduce_slabs(p1.view(64, 1, 512), ref.view(1, 512), accumulate=True)
+    K.reduce_slabs(p2.view(96, 1, 512), ref.view(1, 512), accumulate=True)
+    st = torch.cuda.current_stream()
+    K._DEFERRED[st.cuda_stream] = (st, [(p1, out, True), (p2, out, True)])
+    K.flush_reductions()
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    arr = (_lib.SlabJob * 2)()
+    for i, p in enumerate((p1, p2)):
+        arr[i].slabs, arr[i].nslab, arr[i].cols = p.data_ptr(), p.shape[0], 512
+        arr[i].out, arr[i].accumulate = out.data_ptr(), 1
+    assert _lib.lib().ctclip_reduce_slabs_multi(arr, 2, st.cuda_stream) == 1001
