@@ -84,6 +84,16 @@ __global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restr
     y[i] = f2bf(x[i]);
 }
 
+__global__ __launch_bounds__(256) void cast_split_kernel(const float* __restrict__ x, u16* __restrict__ hi,
+                                                         u16* __restrict__ lo, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    const u16 h = f2bf(v);
+    hi[i] = h;
+    lo[i] = f2bf(v - bf2f(h));
+  }
+}
+
 // y = a + b (f32) with optional bf16 shadow; n % 4 == 0
 __global__ __launch_bounds__(256) void add_f32_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                       float* __restrict__ y, u16* __restrict__ yb, int64_t n4) {
@@ -139,6 +149,12 @@ extern "C" int ctclip_unpack_rows(const float* src, int64_t ld_src, const int32_
 
 extern "C" int ctclip_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream) {
   hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, (u16*)y, n);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_cast_f32_bf16_split(const float* x, void* hi, void* lo, int64_t n, void* stream) {
+  hipLaunchKernelGGL(cast_split_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, (u16*)hi, (u16*)lo, n);
   CT_CHECK_LAUNCH();
   return 0;
 }

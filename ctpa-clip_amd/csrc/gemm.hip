@@ -28,6 +28,7 @@ struct P {
   int64_t M, N, K;
   const u16* A; int64_t lda;
   const u16* B; int64_t ldb;
+  const u16* B2;                 // optional second B (the bf16 "lo" residual of an f32 weight)
   void* C; int64_t ldc; int c_f32;
   u16* C2; int64_t ldc2;
   const float* bias;
@@ -135,7 +136,11 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   u32x4 ra[4], rb[4];
-  const int nk = kend > kbeg ? (int)((kend - kbeg + BKT - 1) / BKT) : 0;
+  // with B2 the K range is walked twice into the same accumulators: A.B^T then A.B2^T
+  // (hi / lo split weights: W = hi + lo to ~16 mantissa bits, two MFMA passes, one f32 sum)
+  const int nk1 = kend > kbeg ? (int)((kend - kbeg + BKT - 1) / BKT) : 0;
+  const int nk = p.B2 ? 2 * nk1 : nk1;
+  const u16* B2 = p.B2 ? p.B2 + bidx * p.sB : nullptr;
   if (nk > 0) {
     gload<AK>(ra, A, p.lda, p.M, kend, m0, kbeg);
     gload<BK>(rb, B, p.ldb, p.N, kend, n0, kbeg);
@@ -146,8 +151,9 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
-      gload<AK>(ra, A, p.lda, p.M, kend, m0, kbeg + (int64_t)(kt + 1) * BKT);
-      gload<BK>(rb, B, p.ldb, p.N, kend, n0, kbeg + (int64_t)(kt + 1) * BKT);
+      const int kn = kt + 1 < nk1 ? kt + 1 : kt + 1 - nk1;
+      gload<AK>(ra, A, p.lda, p.M, kend, m0, kbeg + (int64_t)kn * BKT);
+      gload<BK>(rb, kt + 1 < nk1 ? B : B2, p.ldb, p.N, kend, n0, kbeg + (int64_t)kn * BKT);
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -465,7 +471,8 @@ extern "C" int ctclip_gemm(const ctclip_gemm_args* a, void* stream) {
     CT_REQUIRE(a->C2 && a->bias && aligned16(a->bias) && !a->R && !a->c_f32 && !a->accumulate && split == 1 &&
                    (a->batch <= 1) && a->N % 64 == 0 && a->n2 > 0 && a->n2 % 64 == 0 && a->n2 <= a->N,
                CT_EINVAL);
-  {
+  if (a->B2) CT_REQUIRE(aligned16(a->B2) && a->act != 3, CT_EINVAL);
+  if (!a->B2) {
     const int b = a->batch > 0 ? a->batch : 1;
     const int64_t tiles256 = ((a->M + 255) / 256) * ((a->N + 255) / 256) * split * b;
     if (a->K % 64 == 0 && a->M >= 256 && a->N >= 256 && tiles256 >= 160 && (split == 1 || (a->K / split) >= 512) &&
@@ -493,6 +500,7 @@ extern "C" int ctclip_gemm(const ctclip_gemm_args* a, void* stream) {
   p.M = a->M; p.N = a->N; p.K = a->K;
   p.A = (const u16*)a->A; p.lda = a->lda;
   p.B = (const u16*)a->B; p.ldb = a->ldb;
+  p.B2 = (const u16*)a->B2;
   p.C = a->C; p.ldc = a->ldc; p.c_f32 = a->c_f32;
   p.C2 = (u16*)a->C2; p.ldc2 = a->ldc2;
   p.bias = a->bias;

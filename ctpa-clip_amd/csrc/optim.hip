@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
                                                    float* __restrict__ m, float* __restrict__ v, int64_t n, int head,
                                                    float lr, float b1, float b2, float eps, float wd, float bc1,
                                                    float bc2_sqrt, const float* __restrict__ coef,
-                                                   u16* __restrict__ pb, int zero_grad) {
+                                                   u16* __restrict__ pb, u16* __restrict__ pbl, int zero_grad) {
   const float c = coef ? coef[1] : 1.f;
   const float step = lr / bc1;
   const int64_t n4 = (n - head) >> 2;
@@ -71,10 +71,18 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
     p4[i] = pi; m4[i] = mi; v4[i] = vi;
     if (zero_grad) g4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (pb) {
+      u16 h[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) h[j] = f2bf(o[j]);
       uint2 w;
-      w.x = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
-      w.y = (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16);
+      w.x = (unsigned)h[0] | ((unsigned)h[1] << 16);
+      w.y = (unsigned)h[2] | ((unsigned)h[3] << 16);
       *(uint2*)(pb + head + 4 * i) = w;
+      if (pbl) {          // lo = bf16(p - hi): the text tower's split weights (gemm.hip B2)
+        w.x = (unsigned)f2bf(o[0] - bf2f(h[0])) | ((unsigned)f2bf(o[1] - bf2f(h[1])) << 16);
+        w.y = (unsigned)f2bf(o[2] - bf2f(h[2])) | ((unsigned)f2bf(o[3] - bf2f(h[3])) << 16);
+        *(uint2*)(pbl + head + 4 * i) = w;
+      }
     }
   }
   if (blockIdx.x == 0 && threadIdx.x < 8) {
@@ -86,6 +94,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
       p[i] = pj; m[i] = mj; v[i] = vj;
       if (zero_grad) g[i] = 0.f;
       if (pb) pb[i] = f2bf(pj);
+      if (pb && pbl) pbl[i] = f2bf(pj - bf2f(f2bf(pj)));
     }
   }
 }
@@ -101,8 +110,8 @@ extern "C" int ctclip_grad_norm(const float* g, int64_t n, float max_norm, float
 }
 
 extern "C" int ctclip_adam(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
-                           float eps, float wd, int32_t step, const float* coef, void* p_bf16, int32_t zero_grad,
-                           void* stream) {
+                           float eps, float wd, int32_t step, const float* coef, void* p_bf16, void* p_bf16_lo,
+                           int32_t zero_grad, void* stream) {
   const float bc1 = 1.f - powf(b1, (float)step);
   const float bc2 = sqrtf(1.f - powf(b2, (float)step));
   if (n <= 0) return 0;
@@ -114,7 +123,7 @@ extern "C" int ctclip_adam(float* p, float* g, float* m, float* v, int64_t n, fl
   const int64_t n4 = (n - head) / 4;
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (n4 + 255) / 256));
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, head, lr, b1, b2,
-                     eps, wd, bc1, bc2, coef, (u16*)p_bf16, zero_grad);
+                     eps, wd, bc1, bc2, coef, (u16*)p_bf16, (u16*)p_bf16_lo, zero_grad);
   CT_CHECK_LAUNCH();
   return 0;
 }

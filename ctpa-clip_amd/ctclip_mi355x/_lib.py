@@ -43,6 +43,7 @@ class GemmArgs(ctypes.Structure):
         ('batch', c_i32),
         ('sA', c_i64), ('sB', c_i64), ('sC', c_i64), ('sC2', c_i64), ('sR', c_i64),
         ('n2', c_i32),
+        ('B2', c_vp),
     ]
 
 
@@ -113,6 +114,7 @@ _SIGS = {
     'ctclip_unpack_rows': [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp],
     'ctclip_gelu_f32': [c_vp, c_vp, c_i64, c_vp],
     'ctclip_cast_f32_bf16': [c_vp, c_vp, c_i64, c_vp],
+    'ctclip_cast_f32_bf16_split': [c_vp, c_vp, c_vp, c_i64, c_vp],
     'ctclip_add_f32': [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
     'ctclip_patch_ln': [c_vp, c_i32, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp, c_i64,
                         c_vp],
@@ -126,6 +128,12 @@ _SIGS = {
     'ctclip_attn_fwd': [ctypes.POINTER(AttnArgs), c_vp],
     'ctclip_attn_bwd': [ctypes.POINTER(AttnArgs), c_vp],
     'ctclip_attn_bwd_ws_floats': [ctypes.POINTER(AttnArgs)],
+    'ctclip_attn_fwd_f32': [ctypes.POINTER(AttnArgs), c_vp],
+    'ctclip_patch_ln_f32': [c_vp, c_i32, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp,
+                            c_vp, c_vp, c_i64, c_vp],
+    'ctclip_peg_fwd_f32': [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp],
+    'ctclip_l2norm_scale_fwd_f32': [c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp],
+    'ctclip_geglu_f32': [c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
     'ctclip_vq_select': [c_vp, c_vp, c_i32, c_vp, c_i64, c_i32, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp],
     'ctclip_vq_pool': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
     'ctclip_vq_pool_bwd': [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
@@ -141,7 +149,8 @@ _SIGS = {
     'ctclip_embed_fwd': [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
     'ctclip_embed_bwd': [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
     'ctclip_grad_norm': [c_vp, c_i64, c_f32, c_vp, c_i32, c_vp, c_vp],
-    'ctclip_adam': [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_i32, c_vp, c_vp, c_i32, c_vp],
+    'ctclip_adam': [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_i32, c_vp, c_vp, c_vp, c_i32,
+                    c_vp],
 }
 
 

@@ -101,6 +101,43 @@ class BertModel(nn.Module):
             if isinstance(m, nn.Linear):
                 nn.init.zeros_(m.bias)
 
+    bucket_layers = 3     # encoder layers per gradient all-reduce bucket (grad_buckets)
+
+    def _layer_params(self, li):
+        lyr = self.encoder.layer[li]
+        a = lyr.attention.self
+        first = [a.query.weight, a.key.weight, a.value.weight, a.query.bias, a.key.bias, a.value.bias]
+        ids = {id(p) for p in first}
+        return first + [p for p in lyr.parameters() if id(p) not in ids]
+
+    def _bucket_groups(self):
+        """[(lo, hi)] layer ranges, top of the stack first (the order the backward finalises them)."""
+        n, k = len(self.encoder.layer), max(1, int(self.bucket_layers))
+        out, hi = [], n
+        while hi > 0:
+            out.append((max(0, hi - k), hi))
+            hi = max(0, hi - k)
+        return out
+
+    def grad_buckets(self):
+        """[(tag, params)] in the order BERT's backward finalises them, like DDP's readiness-ordered
+        buckets (ct_clip/CTCLIPTrainer.py:213-217): every ``bucket_layers`` encoder layers from the
+        top down, the lowest group together with the embeddings (and the unused pooler).  Each
+        layer's query / key / value weights then biases stay adjacent, so the fused QKV GEMM reads
+        them as one slice of the trainer's arenas (functional.bf_cat).  The forward marks each
+        group's lowest layer (dist_sync.mark_ready) so its all-reduce goes out as soon as that
+        layer's backward has run -- beside the rest of BERT's backward and the 3D-ViT's."""
+        groups = self._bucket_groups()
+        out = []
+        for lo, hi in groups:
+            ps = []
+            for li in range(hi - 1, lo - 1, -1):
+                ps += self._layer_params(li)
+            out.append((f'text_{lo}', ps))
+        seen = {id(p) for _, ps in out for p in ps}
+        out[-1][1].extend(p for p in self.parameters() if id(p) not in seen)
+        return out
+
     def param_order(self):
         """All parameters, each layer's query / key / value weights then biases first and adjacent,
         so the fused QKV GEMM reads them as one slice of the trainer's arenas (functional.bf_cat)."""
@@ -158,7 +195,10 @@ class BertModel(nn.Module):
         xf, xb = Fn.BertEmbedFn.apply(ids, e.word_embeddings.weight, e.position_embeddings.weight,
                                       e.token_type_embeddings.weight, e.LayerNorm.weight, e.LayerNorm.bias,
                                       c.layer_norm_eps, (ph, seed(0, 3)))
-        dist_sync.mark_ready(xf, 'text')   # every BERT .grad is final once the embeddings' backward ran
+        # gradient buckets (grad_buckets): the lowest group's .grad are final once the embeddings'
+        # backward ran, every other group's once its lowest layer's backward ran
+        lows = {lo for lo, _ in self._bucket_groups()}
+        dist_sync.mark_ready(xf, 'text_0')
         for li, lyr in enumerate(self.encoder.layer):
             a = lyr.attention
             xf, xb = Fn.BertLayerFn.apply(
@@ -169,4 +209,6 @@ class BertModel(nn.Module):
                 lyr.intermediate.dense.bias, lyr.output.dense.weight, lyr.output.dense.bias,
                 lyr.output.LayerNorm.weight, lyr.output.LayerNorm.bias,
                 (ph, pa, seed(li + 1, 0), seed(li + 1, 1), seed(li + 1, 2)))
+            if li in lows and li > 0:
+                dist_sync.mark_ready(xf, f'text_{li}')
         return (xf.view(B, L, c.hidden_size), None)

@@ -67,6 +67,7 @@ class CTCLIP(nn.Module):
         self._wvis = (None, None)
         self.defer_text_backward = False     # set by CTClipTrainer (see encode)
         self._deferred_text = None
+        self._deferred_image = None
         self._t_gather = None
 
     # ------------------------------------------------------------------ checkpoint
@@ -95,6 +96,9 @@ class CTCLIP(nn.Module):
         return self._wvis[1]
 
     def _project(self, W, Wb, pooled, pooled_b):
+        from . import precise
+        if precise.vit_precision() == 'f32' and not (torch.is_grad_enabled() and W.requires_grad):
+            return precise.project_f32(W, pooled)       # the opt-in f32 image tower, exact f32
         return Fn.ImageProjFn.apply(pooled, pooled_b, W, Wb)
 
     def encode(self, text, image, gather=False):
@@ -133,6 +137,12 @@ class CTCLIP(nn.Module):
             t_raw = leaf
         W = self.to_visual_latent.weight
         i_raw = self._project(W, self._visual_weight_bf16(W), pooled, pooled_b)
+        if self.defer_text_backward and torch.is_grad_enabled() and i_raw.requires_grad:
+            # the image tower's backward is deferred too (CTClipTrainer.forward_backward): BERT's
+            # backward -- and its gradient buckets' all-reduces -- are queued before the 3D-ViT's
+            ileaf = i_raw.detach().requires_grad_(True)
+            self._deferred_image = [i_raw, ileaf]
+            i_raw = ileaf
         return enc_text, pooled, t_raw, i_raw
 
     def forward(self, text, image, device=None, return_loss=False, return_encodings=False, return_latents=False,
@@ -180,17 +190,26 @@ class CTCLIP(nn.Module):
         with torch.cuda.stream(ts):
             torch.autograd.backward(t_raw, g)
 
+    def backward_deferred_image(self):
+        """Back-propagate the image tower whose graph ``encode`` detached (after BERT's, see
+        CTClipTrainer.forward_backward), on the current stream."""
+        d, self._deferred_image = self._deferred_image, None
+        if d is None or d[1].grad is None:
+            return
+        torch.autograd.backward(d[0], d[1].grad)
+
     def grad_buckets(self):
-        """Gradient all-reduce buckets in the order the backward finalises them (dist_sync): the
-        3D-ViT's temporal stack, spatial stack, the rest of the image tower (patch embed, CPB),
-        then BERT (back-propagated last, see encode)."""
+        """Gradient all-reduce buckets in the order the backward finalises them (dist_sync): BERT's
+        layer groups from the top down (its backward is queued first, CTClipTrainer.forward_backward),
+        the 3D-ViT's temporal stack, spatial stack, the rest of the image tower (patch embed, CPB),
+        then the CTCLIP-level heads (projections, temperature), launched last."""
         vt = self.visual_transformer
-        order = getattr(self.text_transformer, 'param_order', None)
-        text_first = order() if order is not None else []
-        return [('vit_temporal', list(vt.enc_temporal_transformer.parameters())),
-                ('vit_spatial', list(vt.enc_spatial_transformer.parameters())),
-                ('vit_rest', list(vt.parameters())),
-                ('text', text_first + list(self.parameters()))]
+        tb = getattr(self.text_transformer, 'grad_buckets', None)
+        text = tb() if tb is not None else [('text_0', list(self.text_transformer.parameters()))]
+        return text + [('vit_temporal', list(vt.enc_temporal_transformer.parameters())),
+                       ('vit_spatial', list(vt.enc_spatial_transformer.parameters())),
+                       ('vit_rest', list(vt.parameters())),
+                       ('head', list(self.parameters()))]
 
     def _pool_tokens(self, tokens):
         """mean over t + flatten of already-quantised tokens (ct_clip.py:724,740)."""

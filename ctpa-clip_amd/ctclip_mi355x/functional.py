@@ -143,6 +143,33 @@ def bf(W):
     return sh if sh is not None else K.cast_bf16(W.contiguous())
 
 
+# The text tower's forward GEMMs read each weight as W = hi + lo (two bf16 images, ~16 mantissa
+# bits; gemm.hip walks K twice into one f32 accumulator): the bf16 rounding of BERT-base's weights
+# is what put its latents 1.4e-3 off the f32 reference (tools/bert_precision.py: 6e-4 without
+# it).  CTCLIP_TEXT_SPLIT=0 restores single bf16 weights (A/B switch).
+_TEXT_SPLIT = os.environ.get('CTCLIP_TEXT_SPLIT', '1') != '0'
+
+
+def bf_split(W):
+    """(hi, lo) bf16 images of f32 weight W: the Adam-maintained shadows when current, else a split cast."""
+    sh = shadow_bf16(W)
+    lo = getattr(W, '_ctclip_bf16_lo', None)
+    if sh is not None and lo is not None:
+        return sh, lo
+    return K.cast_bf16_split(W.detach().contiguous())
+
+
+def bf_cat_split(ws):
+    """bf_split of torch.cat(ws, 0): views of the shadow arenas when the weights are adjacent there."""
+    if all(shadow_bf16(w) is not None and getattr(w, '_ctclip_bf16_lo', None) is not None for w in ws):
+        a = _adjacent(ws, lambda f: f.bf16)
+        if a is not None:
+            arena, lo, hi = a
+            shp = (-1, *ws[0].shape[1:])
+            return arena[lo:hi].view(shp), ws[0]._ctclip_flat.bf16_lo[lo:hi].view(shp)
+    return K.cast_bf16_split(torch.cat([w.detach() for w in ws], 0).contiguous())
+
+
 def _adjacent(ts, arena_of):
     """(arena, first offset) when tensors ts are consecutive, in order, in one arena."""
     flat = getattr(ts[0], '_ctclip_flat', None)
@@ -703,25 +730,28 @@ class BertLayerFn(torch.autograd.Function):
         ph, pa, s_attn, s_out1, s_out2 = drop
         Hd = xf.shape[1]
         dh = Hd // heads
-        Wqkv = bf_cat([Wq, Wk, Wv])
+        split = _TEXT_SPLIT
+        if split:
+            (Wqkv, Wqkv_lo), (Wo_b, Wo_lo), (Wi_b, Wi_lo), (Wout_b, Wout_lo) = (
+                bf_cat_split([Wq, Wk, Wv]), bf_split(Wo), bf_split(Wi), bf_split(Wout))
+        else:
+            Wqkv, Wo_b, Wi_b, Wout_b = bf_cat([Wq, Wk, Wv]), bf(Wo), bf(Wi), bf(Wout)
+            Wqkv_lo = Wo_lo = Wi_lo = Wout_lo = None
         bqkv = cat_f32([bq, bk, bv])
-        qkv = K.linear(xb, Wqkv, bias=bqkv)
+        qkv = K.linear(xb, Wqkv, bias=bqkv, w_lo=Wqkv_lo)
         ctxv, lse = K.attn_fwd(qkv[:, :Hd], qkv[:, Hd:2 * Hd], qkv[:, 2 * Hd:], L=L, H=heads, D=dh, nseq=B,
                                scale=1.0 / math.sqrt(dh), seq=(1, L, 0, 1), kmask=kmask, dropout=(pa, s_attn))
-        Wo_b = bf(Wo)
         if ph > 0:       # LN(dropout(dense(ctx)) + x): the residual leaves the GEMM epilogue
-            a = K.dropout(K.linear(ctxv, Wo_b, bias=bo, out_dtype=F32), ph, s_out1, res=xf)[0]
+            a = K.dropout(K.linear(ctxv, Wo_b, bias=bo, out_dtype=F32, w_lo=Wo_lo), ph, s_out1, res=xf)[0]
         else:
-            a = K.linear(ctxv, Wo_b, bias=bo, residual=xf, out_dtype=F32)
+            a = K.linear(ctxv, Wo_b, bias=bo, residual=xf, out_dtype=F32, w_lo=Wo_lo)
         x1b, x1f, m1, r1 = K.layernorm_fwd(a, ln1_w, ln1_b, eps, out_bf16=True, out_f32=True)
-        Wi_b = bf(Wi)
         hpre = torch.empty(xf.shape[0], Wi.shape[0], device=xf.device, dtype=BF16)
-        hact = K.linear(x1b, Wi_b, bias=bi, act=K.ACT_GELU, out2=hpre)
-        Wout_b = bf(Wout)
+        hact = K.linear(x1b, Wi_b, bias=bi, act=K.ACT_GELU, out2=hpre, w_lo=Wi_lo)
         if ph > 0:
-            b2 = K.dropout(K.linear(hact, Wout_b, bias=bout, out_dtype=F32), ph, s_out2, res=x1f)[0]
+            b2 = K.dropout(K.linear(hact, Wout_b, bias=bout, out_dtype=F32, w_lo=Wout_lo), ph, s_out2, res=x1f)[0]
         else:
-            b2 = K.linear(hact, Wout_b, bias=bout, residual=x1f, out_dtype=F32)
+            b2 = K.linear(hact, Wout_b, bias=bout, residual=x1f, out_dtype=F32, w_lo=Wout_lo)
         x2b, x2f, m2, r2 = K.layernorm_fwd(b2, ln2_w, ln2_b, eps, out_bf16=True, out_f32=True)
         ctx.save_for_backward(xb, kmask, qkv, ctxv, lse, a, m1, r1, x1b, hpre, hact, b2, m2, r2, Wqkv, Wo_b, Wi_b,
                               Wout_b, ln1_w, ln2_w)

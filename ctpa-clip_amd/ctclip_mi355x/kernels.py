@@ -60,24 +60,26 @@ TIMER = KernelTimer()
 
 def gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, *, C2=None, ldc2=0, bias=None,
              R=None, ldr=0, alpha=1.0, act=ACT_NONE, accumulate=False, split_k=1, batch=1,
-             sA=0, sB=0, sC=0, sC2=0, sR=0, tag=None, flops=None, n2=0):
+             sA=0, sB=0, sC=0, sC2=0, sR=0, tag=None, flops=None, n2=0, B2=None):
     end = TIMER(tag, flops if flops is not None else 2.0 * M * N * K * batch) if tag else None
     _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, C2=C2, ldc2=ldc2, bias=bias, R=R, ldr=ldr,
               alpha=alpha, act=act, accumulate=accumulate, split_k=split_k, batch=batch, sA=sA, sB=sB, sC=sC,
-              sC2=sC2, sR=sR, n2=n2)
+              sC2=sC2, sR=sR, n2=n2, B2=B2)
     if end is not None:
         end.record()
 
 
 def _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, *, C2=None, ldc2=0, bias=None,
               R=None, ldr=0, alpha=1.0, act=ACT_NONE, accumulate=False, split_k=1, batch=1,
-              sA=0, sB=0, sC=0, sC2=0, sR=0, n2=0):
+              sA=0, sB=0, sC=0, sC2=0, sR=0, n2=0, B2=None):
+    if B2 is not None:
+        assert B2.dtype == B.dtype and B2.shape == B.shape and B2.stride() == B.stride()
     s = _auto_split(M, N, K, act, split_k, batch, accumulate, C)
     if s > 1:
         # skinny GEMM (text tower, M = B * L tokens): split K into f32 slabs over ~4x more
         # workgroups than output tiles, then combine with the epilogue in one pass
         slabs = torch.empty(s, M, N, device=C.device, dtype=F32)
-        _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, slabs, N, alpha=alpha, split_k=s)
+        _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, slabs, N, alpha=alpha, split_k=s, B2=B2)
         a = GemmArgs()
         a.C, a.ldc, a.c_f32 = ptr(C), ldc, int(C.dtype == F32)
         a.C2, a.ldc2 = ptr(C2), ldc2
@@ -97,6 +99,7 @@ def _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, *, C2=None,
     a.alpha, a.act, a.accumulate, a.split_k, a.batch = alpha, act, int(accumulate), split_k, batch
     a.sA, a.sB, a.sC, a.sC2, a.sR = sA, sB, sC, sC2, sR
     a.n2 = n2
+    a.B2 = ptr(B2)
     call('ctclip_gemm', _lib.ctypes.byref(a), stream_ptr())
 
 
@@ -111,9 +114,10 @@ def _auto_split(M, N, K, act, split_k, batch, accumulate, C):
 
 
 def linear(x, w, *, bias=None, residual=None, out=None, out_dtype=BF16, act=ACT_NONE, out2=None, alpha=1.0,
-           accumulate=False, tag=None, flops=None, l2n_scale=None, l2n_cols=0):
+           accumulate=False, tag=None, flops=None, l2n_scale=None, l2n_cols=0, w_lo=None):
     """y[M,N] = x[M,K] @ w[N,K]^T (+bias) (+residual); x, w bf16 row-major.  l2n_scale (the [32]
-    head-dim scale): out2[:, :l2n_cols] = per 32-column head l2norm(y) * scale, fused (act 5)."""
+    head-dim scale): out2[:, :l2n_cols] = per 32-column head l2norm(y) * scale, fused (act 5).
+    w_lo: the bf16 lo image of a split f32 weight (cast_bf16_split): y = x @ (w + w_lo)^T."""
     M, K = x.shape
     N = w.shape[0]
     assert w.shape[1] == K and x.stride(1) == 1 and w.stride(1) == 1
@@ -126,7 +130,7 @@ def linear(x, w, *, bias=None, residual=None, out=None, out_dtype=BF16, act=ACT_
     gemm_raw(M, N, K, x, x.stride(0), True, w, w.stride(0), True, out, out.stride(0),
              C2=out2, ldc2=out2.stride(0) if out2 is not None else 0, bias=bias, R=residual,
              ldr=residual.stride(0) if residual is not None else 0, alpha=alpha, act=act, accumulate=accumulate,
-             tag=tag, flops=flops, n2=l2n_cols)
+             tag=tag, flops=flops, n2=l2n_cols, B2=w_lo)
     return out
 
 
@@ -424,6 +428,16 @@ def cast_bf16(x, out=None):
     return out
 
 
+def cast_bf16_split(x, hi=None, lo=None):
+    """(hi, lo) = (bf16(x), bf16(x - hi)) of an f32 tensor: x to ~16 mantissa bits as two bf16 images."""
+    if hi is None:
+        hi = torch.empty(x.shape, device=x.device, dtype=BF16)
+    if lo is None:
+        lo = torch.empty(x.shape, device=x.device, dtype=BF16)
+    call('ctclip_cast_f32_bf16_split', ptr(x), ptr(hi), ptr(lo), x.numel(), stream_ptr())
+    return hi, lo
+
+
 def add_f32(a, b, out=None, out_bf16=None):
     call('ctclip_add_f32', ptr(a), ptr(b), ptr(out), ptr(out_bf16), a.numel(), stream_ptr())
 
@@ -697,9 +711,9 @@ def weights_epoch():
     return _WEIGHTS_EPOCH[0]
 
 
-def adam(p, g, m, v, *, lr, b1, b2, eps, wd, step, coef=None, p_bf16=None, zero_grad=False):
+def adam(p, g, m, v, *, lr, b1, b2, eps, wd, step, coef=None, p_bf16=None, p_bf16_lo=None, zero_grad=False):
     call('ctclip_adam', ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, b1, b2, eps, wd, step, ptr(coef), ptr(p_bf16),
-         int(zero_grad), stream_ptr())
+         ptr(p_bf16_lo), int(zero_grad), stream_ptr())
     _WEIGHTS_EPOCH[0] += 1
 
 
@@ -769,3 +783,44 @@ def dropout(x, p, seed, *, res=None, out_f32=True, out_bf16=False):
     call('ctclip_dropout', ptr(x), ptr(res), ptr(yf), ptr(yb), x.numel(), float(p), int(seed) & (2 ** 64 - 1),
          stream_ptr())
     return yf, yb
+
+
+# ---------------------------------------------------------------- f32 image tower (precise.py)
+def patch_ln_f32(video, is_hu, PT, P, offs, gamma, beta, eps=1e-5):
+    """to_patch_emb's Rearrange + LayerNorm(pd) with affine, f32 rows [tokens, pd]."""
+    B, C, Fr, H, W = video.shape
+    T, Hg, Wg = Fr // PT, H // P, W // P
+    pd = C * PT * P * P
+    out = torch.empty(B * T * Hg * Wg, pd, device=video.device, dtype=F32)
+    call('ctclip_patch_ln_f32', ptr(video), int(video.dtype == F32), int(is_hu), B, C, Fr, H, W, PT, P, ptr(offs),
+         eps, ptr(gamma), ptr(beta), ptr(out), pd, stream_ptr())
+    return out
+
+
+def peg_fwd_f32(x, B, T, H, W, weight, bias, mode):
+    out = torch.empty_like(x)
+    call('ctclip_peg_fwd_f32', ptr(x), B, T, H, W, x.shape[1], ptr(weight), ptr(bias), mode, ptr(out), stream_ptr())
+    return out
+
+
+def l2norm_scale_fwd_f32(x, H, D, scale):
+    out = torch.empty(x.shape[0], H * D, device=x.device, dtype=F32)
+    call('ctclip_l2norm_scale_fwd_f32', ptr(x), x.stride(0), x.shape[0], H, D, ptr(scale), ptr(out), out.stride(0),
+         stream_ptr())
+    return out
+
+
+def geglu_f32(h):
+    rows, two = h.shape
+    inner = two // 2
+    g = torch.empty(rows, inner, device=h.device, dtype=F32)
+    call('ctclip_geglu_f32', ptr(h), h.stride(0), rows, inner, ptr(g), g.stride(0), stream_ptr())
+    return g
+
+
+def attn_fwd_f32(q, k, v, *, L, H, D, nseq, scale, seq, bias_u=None, grid=(0, 0)):
+    M = q.shape[0]
+    o = torch.empty(M, H * D, device=q.device, dtype=F32)
+    a = _attn_args(q, k, v, o, L=L, H=H, D=D, nseq=nseq, M=M, scale=scale, seq=seq, bias_u=bias_u, grid=grid)
+    call('ctclip_attn_fwd_f32', _lib.ctypes.byref(a), stream_ptr())
+    return o

@@ -34,6 +34,9 @@ class FlatParams:
         # (shadows only on the GPU: the CPU arenas serve the gloo rehearsal tests of the sync logic)
         gpu = torch.device(device).type == 'cuda' and os.environ.get('CTCLIP_BF16_SHADOW', '1') != '0'
         self.bf16 = torch.empty(n, device=device, dtype=torch.bfloat16) if gpu else None
+        # ... and its lo residual, bf16(p - bf16(p)): the text tower's GEMMs read W = hi + lo
+        # (functional.bf_split, gemm.hip B2); 2 more bytes per parameter written by the same Adam pass
+        self.bf16_lo = torch.empty(n, device=device, dtype=torch.bfloat16) if gpu else None
         self.views = []
         off = 0
         for p in self.params:
@@ -44,12 +47,13 @@ class FlatParams:
             p.grad = g
             if gpu:
                 p._ctclip_bf16 = self.bf16[off:off + k].view_as(p)
+                p._ctclip_bf16_lo = self.bf16_lo[off:off + k].view_as(p)
                 p._ctclip_off = off
                 p._ctclip_flat = self
             self.views.append((off, k, g))
             off += k
         if gpu and n:
-            K.cast_bf16(self.data, out=self.bf16)
+            K.cast_bf16_split(self.data, hi=self.bf16, lo=self.bf16_lo)
             self.sync_shadows(0, n)
 
     def sync_shadows(self, lo, hi):
@@ -76,7 +80,8 @@ class FlatParams:
 
 def grad_buckets(model):
     """[(tag, params)] with every parameter in exactly one bucket, in the model's readiness order
-    (``model.grad_buckets()``, e.g. CTCLIP: text, vit_temporal, vit_spatial, rest)."""
+    (``model.grad_buckets()``, e.g. CTCLIP: BERT layer groups, vit_temporal, vit_spatial, vit_rest,
+    head)."""
     spec = model.grad_buckets() if hasattr(model, 'grad_buckets') else [('all', list(model.parameters()))]
     seen, out = set(), []
     for tag, ps in spec:
@@ -130,9 +135,14 @@ class CTClipTrainer:
             self.model.defer_text_backward = True
         try:
             loss = self.model(text, video, device=self.device, return_loss=True)
-            loss.backward()                      # loss + 3D-ViT
+            loss.backward()                      # the loss node (both towers' latents are leaves)
             if defer:
-                self.model.backward_deferred_text()   # then BERT (text stream), beside the ViT tail
+                # BERT first (text stream): its layer-group buckets go out to RCCL as its backward
+                # finalises them, ahead of the 3D-ViT's (main stream), whose backward runs beside it
+                self.model.backward_deferred_text()
+                back_img = getattr(self.model, 'backward_deferred_image', None)
+                if back_img is not None:
+                    back_img()
         except BaseException:
             dist_sync.disarm()
             K.discard_deferred()
@@ -158,15 +168,20 @@ class CTClipTrainer:
         # (~110 M), holding the next step's image tower back by ~0.8 ms; queued after it, the
         # BERT update overlaps the next step's compute-bound image-tower GEMMs instead.
         ts = streams.text_stream(self.device)
-        text = [b for b in self.grad_sync.buckets if b[0] == 'text'] if ts is not None else []
-        skip = [(text[0][1], text[0][2])] if text else []
+        text = [b for b in self.grad_sync.buckets if b[0].startswith('text')] if ts is not None else []
+        skip = []
+        if text:          # the text buckets are adjacent in the arena (one slice)
+            off = min(b[1] for b in text)
+            n = sum(b[2] for b in text)
+            assert max(b[1] + b[2] for b in text) == off + n
+            skip = [(off, n)]
         lo = 0
         for off, n in skip + [(self.flat.numel, 0)]:
             if off > lo:
                 self._adam(lo, off - lo)
             lo = off + n
-        if text:
-            _, off, n = text[0]
+        if skip:
+            off, n = skip[0]
             ts.wait_stream(torch.cuda.current_stream(self.device))   # clip coefficient ready
             with torch.cuda.stream(ts):
                 self._adam(off, n)
@@ -175,7 +190,8 @@ class CTClipTrainer:
         sl = slice(off, off + n)
         K.adam(self.flat.data[sl], self.flat.grad[sl], self.m[sl], self.v[sl], lr=self.lr, b1=self.betas[0],
                b2=self.betas[1], eps=self.eps, wd=self.wd, step=self.steps, coef=self.norm,
-               p_bf16=self.flat.bf16[sl] if self.flat.bf16 is not None else None, zero_grad=True)
+               p_bf16=self.flat.bf16[sl] if self.flat.bf16 is not None else None,
+               p_bf16_lo=self.flat.bf16_lo[sl] if self.flat.bf16_lo is not None else None, zero_grad=True)
         self.flat.sync_shadows(off, off + n)
 
     def train_step(self, text, video):

@@ -59,6 +59,11 @@ typedef struct {
   int32_t batch;
   int64_t sA, sB, sC, sC2, sR;      /* batch strides in elements */
   int32_t n2;                       /* act 5: normalised columns (multiple of 64, <= N) */
+  const void* B2;                   /* optional: a second B with B's layout / ldb / sB, summed in:
+                                     * C = epilogue(alpha * (A.B + A.B2)).  With B = bf16(W) and
+                                     * B2 = bf16(W - bf16(W)) the GEMM sees W to ~16 mantissa bits
+                                     * (the text tower's hi / lo split weights); 128-tile kernel only,
+                                     * not with act 3 */
 } ctclip_gemm_args;
 int ctclip_gemm(const ctclip_gemm_args* a, void* stream);
 /* diagnostic: large-tile kernel variant (8 = 8-phase 256x256x64 default, 1 = 128x256x32,
@@ -162,6 +167,8 @@ int ctclip_gelu_f32(const float* x, float* y, int64_t n, void* stream);
 int ctclip_dropout(const float* x, const float* res, float* yf, void* yb, int64_t n, float p, uint64_t seed,
                    void* stream);
 int ctclip_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
+/* hi = bf16(x), lo = bf16(x - hi) (round to nearest even both): x = hi + lo to ~16 bits */
+int ctclip_cast_f32_bf16_split(const float* x, void* hi, void* lo, int64_t n, void* stream);
 int ctclip_add_f32(const float* a, const float* b, float* y, void* y_bf16, int64_t n, void* stream);
 
 /* ---------------------------------------------------------------- patch embedding
@@ -238,6 +245,25 @@ typedef struct {
 int ctclip_attn_fwd(const ctclip_attn_args* a, void* stream);
 int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream);
 int ctclip_attn_bwd_ws_floats(const ctclip_attn_args* a);
+int ctclip_attn_fwd_f32(const ctclip_attn_args* a, void* stream);   /* f32 image tower, see below */
+
+/* ---------------------------------------------------------------- f32 image tower (opt-in)
+ * Exact-f32 forward stages of functional.set_vit_precision('f32') (csrc/f32path.hip); the linears
+ * of that mode run on ctclip_sgemm.  All tensors f32.
+ *   patch_ln_f32: to_patch_emb's Rearrange + nn.LayerNorm(pd) with affine (ct_clip/ctvit.py:169-174)
+ *   peg_fwd_f32:  out = x + PEG(x), canonical rows, mode as ctclip_peg_fwd (attention.py:56-84,324)
+ *   l2norm_scale_fwd_f32: per head x / max(||x||, 1e-12) * scale (attention.py:152-154)
+ *   geglu_f32:    g[:, c] = gelu_erf(h[:, inner + c]) * h[:, c] (attention.py:39-42, un-interleaved W1)
+ *   attn_fwd_f32: ctclip_attn_args with f32 q / k / v / o (lse unused); no kmask, no dropout */
+int ctclip_patch_ln_f32(const void* video, int32_t is_f32, int32_t is_hu, int64_t B, int32_t C, int32_t F,
+                        int32_t H, int32_t W, int32_t PT, int32_t P, const int32_t* offs, float eps,
+                        const float* gamma, const float* beta, float* out, int64_t ldo, void* stream);
+int ctclip_peg_fwd_f32(const float* x, int64_t B, int32_t T, int32_t H, int32_t W, int32_t D,
+                       const float* weight, const float* bias, int32_t mode, float* out, void* stream);
+int ctclip_l2norm_scale_fwd_f32(const float* x, int64_t ldx, int64_t rows, int32_t H, int32_t D,
+                                const float* scale, float* y, int64_t ldy, void* stream);
+int ctclip_geglu_f32(const float* h, int64_t ldh, int64_t rows, int32_t inner, float* g, int64_t ldg,
+                     void* stream);
 
 /* ---------------------------------------------------------------- vector quantiser
  * vector_quantize_pytorch==1.1.2 cosine codebook (ct_clip/ctvit.py:187,421-427).
@@ -300,7 +326,8 @@ int ctclip_embed_bwd(const int64_t* ids, int64_t B, int32_t L, int32_t Hd, const
  * p, g, m, v must share one alignment modulo 16 B (slices of arenas with one layout): CT_EALIGN. */
 int ctclip_grad_norm(const float* g, int64_t n, float max_norm, float* part, int32_t nblk, float* out, void* stream);
 int ctclip_adam(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
-                float wd, int32_t step, const float* coef, void* p_bf16, int32_t zero_grad, void* stream);
+                float wd, int32_t step, const float* coef, void* p_bf16, void* p_bf16_lo, int32_t zero_grad,
+                void* stream);   /* p_bf16_lo (needs p_bf16): bf16(p - bf16(p)), the split-weight lo image */
 
 /* ---------------------------------------------------------------- volume preprocessing
  * Replaces the host-side per-sample loader arithmetic:

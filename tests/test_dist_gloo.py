@@ -162,27 +162,50 @@ class _SinkMM(torch.autograd.Function):
 
 
 class _Toy(torch.nn.Module):
-    """Two 2-layer 'towers' + a temperature, image tower first as in CTCLIP.encode."""
+    """A 3-layer text 'tower' in two readiness-ordered buckets (the top two layers, then the bottom
+    one, as BertModel.grad_buckets groups layers), a 2-layer image tower and a temperature; both
+    towers' backward deferred like CTCLIP's under the trainer (text first, then image)."""
 
     def __init__(self):
         super().__init__()
         g = torch.Generator().manual_seed(3)
         mk = lambda *s: torch.nn.Parameter(torch.randn(*s, generator=g, dtype=torch.float64).float())  # noqa: E731
-        self.wt1, self.wt2, self.wi1, self.wi2 = mk(DIN, DIN), mk(DIN, DL), mk(DIN, DIN), mk(DIN, DL)
+        self.wt1, self.wt2, self.wt3 = mk(DIN, DIN), mk(DIN, DIN), mk(DIN, DL)
+        self.wi1, self.wi2 = mk(DIN, DIN), mk(DIN, DL)
         self.lt = torch.nn.Parameter(torch.tensor(1.0))
+        self.defer_text_backward = False
+        self._deferred = {}
 
     def grad_buckets(self):
-        return [('text', [self.wt1, self.wt2]), ('image', [self.wi1, self.wi2]), ('rest', [self.lt])]
+        return [('text_1', [self.wt3, self.wt2]), ('text_0', [self.wt1]), ('image', [self.wi1, self.wi2]),
+                ('rest', [self.lt])]
+
+    def _leaf(self, x, key):
+        if not self.defer_text_backward:
+            return x
+        leaf = x.detach().requires_grad_(True)
+        self._deferred[key] = (x, leaf)
+        return leaf
+
+    def backward_deferred_text(self):
+        x, leaf = self._deferred.pop('text')
+        torch.autograd.backward(x, leaf.grad)
+
+    def backward_deferred_image(self):
+        x, leaf = self._deferred.pop('image')
+        torch.autograd.backward(x, leaf.grad)
 
     def forward(self, text, video, device=None, return_loss=True):
         from ctclip_mi355x import dist_sync
         from ctclip_mi355x.functional import ClipLossFn
         h = _SinkMM.apply(video, self.wi1)
         dist_sync.mark_ready(h, 'image')
-        i = _SinkMM.apply(h, self.wi2)
+        i = self._leaf(_SinkMM.apply(h, self.wi2), 'image')
         u = _SinkMM.apply(text, self.wt1)
-        dist_sync.mark_ready(u, 'text')
-        t = _SinkMM.apply(u, self.wt2)
+        dist_sync.mark_ready(u, 'text_0')
+        u2 = _SinkMM.apply(u, self.wt2)
+        dist_sync.mark_ready(u2, 'text_1')
+        t = self._leaf(_SinkMM.apply(u2, self.wt3), 'text')
         return ClipLossFn.apply(t, i, self.lt, oracle_clip_loss)
 
 
@@ -196,23 +219,41 @@ def _bucket_worker(rank, port, out_dir):
         ref = _Toy()
         tr = CTClipTrainer(model)
         # arena order follows the buckets, each bucket one contiguous slice
-        assert [t for t, _, _ in tr.grad_sync.buckets] == ['text', 'image', 'rest']
-        assert model.wt1.grad.data_ptr() == tr.flat.grad.data_ptr()
+        order = ['text_1', 'text_0', 'image', 'rest']
+        assert [t for t, _, _ in tr.grad_sync.buckets] == order
+        assert model.wt3.grad.data_ptr() == tr.flat.grad.data_ptr()
+        gs = tr.grad_sync
+        fold = gs.before_launch
         rows = slice(rank * B, (rank + 1) * B)
         for step in range(2):     # hooks re-arm every step
+            snaps = {}
+
+            def snap(tag):        # the bucket's slice at the moment its all-reduce is launched
+                fold(tag)
+                _, off, n = next(b for b in gs.buckets if b[0] == tag)
+                snaps[tag] = tr.flat.grad[off:off + n].clone()
+            gs.before_launch = snap
             tr.flat.grad.zero_()
             tr.forward_backward(xt[rows], xi[rows])
-            # the text and image buckets went out from autograd hooks during the backward, the
-            # image one after the text one (the toy's text tower is the newer); 'rest' has no
-            # hook and goes out in finish
-            assert tr.grad_sync.launched == ['text', 'image'], tr.grad_sync.launched
-            tr.grad_sync.finish()
-            assert tr.grad_sync.launched == ['text', 'image', 'rest']
-        t = _SinkMM.apply(_SinkMM.apply(xt, ref.wt1), ref.wt2)
+            # the text buckets went out from autograd hooks during the (first-queued) text backward,
+            # top layers first, then the image one; 'rest' has no hook and goes out in finish
+            assert gs.launched == ['text_1', 'text_0', 'image'], gs.launched
+            gs.finish()
+            assert gs.launched == order
+            # launched final: each bucket's local gradient at launch time is bit-identical to the
+            # local gradient once the whole backward has run (sum them before the collective)
+            local = {}
+            for tag, off, n in gs.buckets:
+                if tag in snaps:
+                    local[tag] = snaps[tag]
+            for tag, off, n in gs.buckets[:3]:
+                assert local[tag].abs().sum().item() > 0, tag
+            gs.before_launch = fold
+        t = _SinkMM.apply(_SinkMM.apply(_SinkMM.apply(xt, ref.wt1), ref.wt2), ref.wt3)
         i = _SinkMM.apply(_SinkMM.apply(xi, ref.wi1), ref.wi2)
         loss = O.infonce(torch.nn.functional.normalize(t, dim=-1), torch.nn.functional.normalize(i, dim=-1), ref.lt)
         loss.backward()
-        for name in ('wt1', 'wt2', 'wi1', 'wi2', 'lt'):
+        for name in ('wt1', 'wt2', 'wt3', 'wi1', 'wi2', 'lt'):
             torch.testing.assert_close(getattr(model, name).grad, getattr(ref, name).grad, rtol=1e-5, atol=1e-6)
         open(os.path.join(out_dir, f'ok{rank}'), 'w').close()
     finally:

@@ -1,0 +1,125 @@
+"""The opt-in f32 image tower (ctclip_mi355x/precise.py, csrc/f32path.hip) against f64 / oracle
+references: every stage at f32 accuracy (relative 1e-6 level, far below the bf16 path's 1e-3..1e-2),
+then the whole tower at base widths on the reduced volume against the fp32 oracle."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import ctclip_oracle as O
+from test_gpu_ops import _attn_ref, _cpb_table, _gather_rows, _peg_ref, rel
+
+pytestmark = pytest.mark.gpu
+dev = 'cuda'
+
+
+@pytest.fixture(scope='module')
+def K():
+    from ctclip_mi355x import kernels
+    return kernels
+
+
+@pytest.mark.parametrize('mode', [0, 1])
+@pytest.mark.parametrize('shape,D', [((2, 6, 5, 7), 128), ((1, 24, 24, 24), 512), ((2, 2, 3, 4), 24)])
+def test_peg_f32(K, mode, shape, D):
+    torch.manual_seed(2)
+    M = shape[0] * shape[1] * shape[2] * shape[3]
+    x = torch.randn(M, D, device=dev)
+    w = torch.randn(D, 1, 3, 3, 3, device=dev) * 0.2
+    b = torch.randn(D, device=dev) * 0.1
+    out = K.peg_fwd_f32(x, *shape, w, b, mode)
+    ref = _peg_ref(x.double(), w.double(), b.double(), shape, mode)
+    assert rel(out, ref) < 2e-7, rel(out, ref)
+
+
+@pytest.mark.parametrize('case', ['spatial', 'spatial_6x6', 'temporal'])
+def test_attention_f32(K, case):
+    torch.manual_seed(3)
+    if case.startswith('spatial'):
+        gh = gw = 24 if case == 'spatial' else 6
+        L, H, D, nseq = gh * gw, 8, 32, 3
+        M, seq, grid = nseq * L, (1, L, 0, 1), (gh, gw)
+        u, bins = _cpb_table(H, gh, gw)
+        bias = u[:, bins].double()
+    else:
+        B, T, HW, H = 2, 24, 20, 8
+        L, D, nseq = T, 32, B * HW
+        M, seq, grid = B * T * HW, (HW, T * HW, 1, HW), (0, 0)
+        u, bias = None, None
+    rows = _gather_rows(*seq, nseq, L)
+    q = F.normalize(torch.randn(M, H, D, device=dev), dim=-1).reshape(M, H * D)
+    kv = torch.randn(M, 2 * H * D, device=dev)
+    kv[:, :H * D] = F.normalize(kv[:, :H * D].reshape(M, H, D), dim=-1).reshape(M, H * D)
+    k, v = kv[:, :H * D], kv[:, H * D:]
+    o = K.attn_fwd_f32(q, k, v, L=L, H=H, D=D, nseq=nseq, scale=8.0, seq=seq, bias_u=u, grid=grid)
+    ref = _attn_ref(q.double(), k.double(), v.double(), rows, H, D, 8.0, bias)
+    assert rel(o, ref) < 1e-6, rel(o, ref)
+
+
+def test_l2norm_geglu_patch_f32(K):
+    torch.manual_seed(4)
+    x = torch.randn(999, 512, device=dev)
+    sc = torch.randn(32, device=dev) * 0.1 + 1
+    y = K.l2norm_scale_fwd_f32(x[:, :256], 8, 32, sc)
+    ref = F.normalize(x[:, :256].double().reshape(-1, 8, 32), dim=-1) * sc.double()
+    assert rel(y.reshape(-1, 8, 32), ref) < 2e-7
+    h = torch.randn(999, 2 * 1365, device=dev)
+    g = K.geglu_f32(h)
+    hd = h.double()
+    assert rel(g, F.gelu(hd[:, 1365:]) * hd[:, :1365]) < 2e-7
+    # patchify + LayerNorm(4000) with affine against the oracle's Rearrange + LayerNorm
+    from oracle import weights as W
+    from ctclip_mi355x.layers import patch_offsets
+    vit = O.ViTConfig(dim=512, codebook_size=64, image_size=80, patch_size=20, temporal_patch_size=10,
+                      spatial_depth=1, temporal_depth=1, dim_head=32, heads=8, frames=20)
+    hu = W.make_hu(2, vit)
+    gam = torch.randn(4000) * 0.1 + 1
+    bet = torch.randn(4000) * 0.1
+    offs = patch_offsets(1, 10, 20, 20, 80, 80).to(dev)
+    out = K.patch_ln_f32(hu.to(dev), True, 10, 20, offs, gam.to(dev), bet.to(dev))
+    v = O.normalize_hu(hu).double()
+    p = v.reshape(2, 1, 2, 10, 4, 20, 4, 20).permute(0, 2, 4, 6, 1, 3, 5, 7).reshape(-1, 4000)
+    ref = F.layer_norm(p, (4000,), gam.double(), bet.double(), 1e-5)
+    assert rel(out, ref) < 2e-7, rel(out, ref)
+
+
+def test_f32_tower_matches_oracle_small(K):
+    """precise.encode_tokens_f32 (base widths, 160 x 160 x 40 volume, 2 + 2 layers) against the fp32
+    oracle: pre-VQ tokens at the f32 level, VQ indices identical except oracle near-ties, and the
+    forward refuses to run where autograd would need the bf16 backward."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location('tgm', os.path.join(os.path.dirname(__file__), 'test_gpu_model.py'))
+    tgm = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(tgm)
+    from oracle import weights as W
+    from ctclip_mi355x import precise
+    cfg = tgm.cfg_small()
+    model = tgm.build(cfg)
+    sd = W.make_state_dict(cfg)
+    hu = W.make_hu(2, cfg.vit)
+    ids, mask = W.make_text(2, 32, cfg.bert.vocab_size, ragged=True)
+    trace = {}
+    with torch.no_grad():
+        ref = O.ctclip_forward(sd, ids, mask, O.normalize_hu(hu), cfg, training=False, trace=trace)
+    vt = model.visual_transformer
+    model.eval()
+    old = precise.set_vit_precision('f32')
+    try:
+        with pytest.raises(NotImplementedError):
+            vt.encode_tokens(hu.cuda())              # grad enabled + trainable weights: refused
+        with torch.no_grad():
+            zf, _, _ = vt.encode_tokens(hu.cuda())
+            ids_h = vt(hu.cuda(), return_only_codebook_ids=True).reshape(-1).cpu()
+    finally:
+        precise.set_vit_precision(old)
+    zo = trace['temporal_out'].reshape(-1, cfg.vit.dim)
+    r = rel(zf, zo)
+    E = sd['visual_transformer.vq._codebook.embed'][0]
+    so = F.normalize(zo, dim=-1) @ E.t()
+    top2 = so.topk(2, dim=1)
+    margin = top2.values[:, 0] - top2.values[:, 1]
+    diff = ids_h != ref['indices'].reshape(-1).cpu()
+    print(f'f32 tower (small): tokens rel {r:.2e}, VQ diffs {diff.sum().item()} '
+          f'({(diff & (margin >= 1e-6)).sum().item()} above the 1e-6 margin)')
+    assert r < 1e-5
+    assert (diff & (margin >= 1e-6)).sum().item() == 0

@@ -134,3 +134,44 @@ def test_argmax_epilogue(K, M):
     got = idx.gather(1, best[:, None])[:, 0].long()
     ref = s.argmax(1)
     assert (got == ref).float().mean().item() > 0.999
+
+
+@pytest.mark.parametrize('M,N,K_,act', [(1024, 2304, 768, 0), (1024, 3072, 768, 1), (1024, 768, 3072, 0),
+                                        (300, 136, 200, 0)])
+def test_linear_split_weight(K, M, N, K_, act):
+    """Text-tower GEMMs on hi / lo split weights (gemm.hip B2, kernels.cast_bf16_split): the f32
+    weight seen to ~16 mantissa bits, so against an f32 matmul with the SAME bf16 activations the
+    error is the f32-accumulation level, far below one bf16 rounding of the weight.  Covers the
+    split-K combine path (K = 3072, M = 1024) and ragged edges."""
+    torch.manual_seed(5)
+    x = torch.randn(M, K_, device='cuda').bfloat16()
+    W = torch.randn(N, K_, device='cuda') * 0.05
+    b = torch.randn(N, device='cuda')
+    hi, lo = K.cast_bf16_split(W)
+    assert torch.equal(hi, W.bfloat16()) and torch.equal(lo, (W - hi.float()).bfloat16())
+    pre = torch.empty(M, N, device='cuda', dtype=torch.bfloat16) if act else None
+    y = K.linear(x, hi, bias=b, out_dtype=torch.float32, w_lo=lo, act=act, out2=pre)
+    ref = x.float() @ W.t() + b
+    if act:
+        assert _rel(pre, ref) < 4e-3          # bf16 pre-activation copy
+        ref = torch.nn.functional.gelu(ref)
+    e_split = _rel(y, ref)
+    e_hi = _rel(K.linear(x, hi, bias=b, out_dtype=torch.float32, act=act,
+                         out2=torch.empty_like(pre) if act else None), ref)
+    print(f'split {e_split:.2e}  hi-only {e_hi:.2e}')
+    assert e_split < 2e-5 and e_hi > 20 * e_split
+
+
+def test_adam_writes_split_shadow(K):
+    """The Adam pass writes hi = bf16(p) and lo = bf16(p - hi) of the UPDATED parameter."""
+    torch.manual_seed(6)
+    n = 100003
+    p, g = torch.randn(n, device='cuda'), torch.randn(n, device='cuda')
+    m, v = torch.zeros(n, device='cuda'), torch.zeros(n, device='cuda')
+    hi = torch.empty(n, device='cuda', dtype=torch.bfloat16)
+    lo = torch.empty_like(hi)
+    K.adam(p[1:], g[1:], m[1:], v[1:], lr=1e-3, b1=0.9, b2=0.99, eps=1e-8, wd=0.0, step=1, p_bf16=hi[1:],
+           p_bf16_lo=lo[1:])
+    torch.cuda.synchronize()
+    assert torch.equal(hi[1:], p[1:].bfloat16())
+    assert torch.equal(lo[1:], (p[1:] - hi[1:].float()).bfloat16())

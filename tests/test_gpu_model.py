@@ -4,7 +4,8 @@ Config: the base CT-CLIP widths (ViT d=512, 8x32 heads, FF 1365, codebook 8192; 
 on a reduced volume (160x160x40 -> 4x8x8 tokens), 2+2 ViT layers and 2 BERT layers, so the
 fp32 oracle finishes in seconds.  The vector quantiser's argmax is compared separately (index
 agreement rate, near-ties allowed); everything downstream is compared with the oracle forced
-onto the HIP path's indices.  Tolerances are bf16-path tolerances: latents and
+onto the HIP path's indices (every index difference must be a near-tie explained by the token's
+measured pre-VQ error).  Tolerances are bf16-path tolerances: latents and
 loss within 1e-3, intermediate activations / gradients as stated per check."""
 import types
 
@@ -87,12 +88,29 @@ def test_forward_latents_and_loss(setup):
         enc_text, pooled, t_raw, i_raw = model.encode(text, hu.cuda())
         idx = model.visual_transformer.vq.state.last_indices.cpu()
         scores = model(text, hu.cuda(), return_loss=False)
+        zf, _, _ = model.visual_transformer.encode_tokens(hu.cuda())
+    trace = {}
     with torch.no_grad():
-        free = O.ctclip_forward(sd, ids, mask, video, cfg, training=False)
+        free = O.ctclip_forward(sd, ids, mask, video, cfg, training=False, trace=trace)
         forced = O.ctclip_forward(sd, ids, mask, video, cfg, training=False, force_ind=idx)
-    agree = (free['indices'].reshape(-1) == idx.long()).float().mean().item()
-    print('VQ index agreement', agree)
-    assert agree > 0.9
+    # VQ contract, margin-based: every index the bf16 path picks differently from the
+    # oracle must be a near-tie its own pre-VQ error explains -- the oracle's score gap between its
+    # winner and the HIP choice at most 2 * |l2norm(z_hip) - l2norm(z_oracle)| (both unit-code
+    # scores move by at most that much); the count above the literal 1e-6 margin is reported (the
+    # f32 image tower meets it literally: test_gpu_f32path.py, test_gpu_base.py)
+    zo = trace['temporal_out'].reshape(-1, cfg.vit.dim)
+    oi, hi = free['indices'].reshape(-1).long(), idx.long()
+    diff = (oi != hi).nonzero().flatten()
+    E = sd['visual_transformer.vq._codebook.embed'][0]
+    xo = torch.nn.functional.normalize(zo, dim=-1)
+    xh = torch.nn.functional.normalize(zf.cpu(), dim=-1)
+    so = xo[diff] @ E.t()
+    gap = so.gather(1, oi[diff][:, None]).squeeze(1) - so.gather(1, hi[diff][:, None]).squeeze(1)
+    bound = 2 * (xh[diff] - xo[diff]).norm(dim=1)
+    print(f'VQ: {diff.numel()} of {oi.numel()} indices differ, {(gap >= 1e-6).sum().item()} with oracle gap '
+          f'>= 1e-6, max gap {gap.max().item() if diff.numel() else 0:.2e}; all within their token-error bound: '
+          f'{bool((gap <= bound + 1e-6).all())}')
+    assert (gap > bound + 1e-6).sum().item() == 0
     tl = torch.nn.functional.normalize(t_raw, dim=-1)
     il = torch.nn.functional.normalize(i_raw, dim=-1)
     assert (tl.cpu() - forced['text_latents']).abs().max().item() < 1e-3
@@ -192,12 +210,15 @@ def test_grad_buckets_final_when_launched(setup):
     """Backward-overlapped gradient sync (dist_sync.BucketedGradSync): with the
     hooks forced on at world 1, each bucket's gradient slice at the moment its hook launches the
     all-reduce must already equal its final value (bit-exact), the hooks must fire in bucket
-    order during the backward (3D-ViT stacks, rest of the image tower, then BERT)."""
+    order during the backward: BERT's layer groups from the top down (here one layer per bucket),
+    queued first, then the 3D-ViT stacks and the rest of the image tower."""
     cfg, model, hu, ids, mask, text = setup
     from ctclip_mi355x.trainer import CTClipTrainer
+    model.text_transformer.bucket_layers = 1
     tr = CTClipTrainer(model, lr=1e-4)
     gs = tr.grad_sync
-    assert [t for t, _, _ in gs.buckets] == ['vit_temporal', 'vit_spatial', 'vit_rest', 'text']
+    order = ['text_1', 'text_0', 'vit_temporal', 'vit_spatial', 'vit_rest']
+    assert [t for t, _, _ in gs.buckets] == order
     snaps = {}
     fold = gs.before_launch
 
@@ -209,12 +230,13 @@ def test_grad_buckets_final_when_launched(setup):
     gs.force = True
     tr.flat.grad.zero_()
     tr.forward_backward(text, hu.cuda())
-    assert gs.launched == ['vit_temporal', 'vit_spatial', 'vit_rest', 'text'], gs.launched
+    assert gs.launched == order, gs.launched
     gs.finish()
     torch.cuda.synchronize()
     for tag, off, n in gs.buckets:
         assert torch.equal(snaps[tag], tr.flat.grad[off:off + n]), tag
         assert snaps[tag].abs().sum().item() > 0, tag
+    model.text_transformer.bucket_layers = 3
 
 
 def test_zero_shot_matches_oracle(setup):

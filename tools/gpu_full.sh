@@ -8,10 +8,10 @@ tag=${1:-run}
 sel=${2:-}
 mkdir -p gpurun_out
 if [ -n "$sel" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$sel" \
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread -k "$sel" \
     > gpurun_out/${tag}_gpu_tests.log 2>&1
 else
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 300 --timeout-method thread \
     > gpurun_out/${tag}_gpu_tests.log 2>&1
 fi
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${tag}_smoke.log 2>&1
