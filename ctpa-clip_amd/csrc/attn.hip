@@ -202,7 +202,12 @@ __device__ __forceinline__ void load_tables(const AP& p, char* tab, int Lp, int 
 // RUN (bias shapes with Wg % 4 == 0 and L % 32 == 0): the 4 keys a lane scores per MFMA block
 // are consecutive in one grid row, so their bins are cq - kb[k0] - 0..3 -- one table read and one
 // address for all four bias reads (fixed offsets) -- and there are no padded keys to mask.
-template <int D, bool BIAS, int W = (BIAS ? 12 : NW), bool RUN = false>
+// QB query blocks per wave are processed TOGETHER (same key chunk loop): their score / softmax /
+// PV chains are independent, so they interleave and hide each other's MFMA -> VALU -> LDS
+// latencies (the kernel ran at ~3 waves per SIMD with one dependent chain each), and the K / V
+// fragments of a key chunk are read from LDS once for all QB blocks.  Per-query arithmetic is
+// unchanged (bit-identical to QB = 1).
+template <int D, bool BIAS, int W = (BIAS ? 12 : NW), bool RUN = false, int QB = 1>
 __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KK = D / 32, DB = D / 16, RS = Img<D>::RS, NTH = W * 64;
@@ -232,96 +237,125 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
   const int g = lane >> 4, li = lane & 15;
   const int nqb = (L + 15) >> 4;
   const float sc2 = p.scale * LOG2E;
-  for (int qb = wi; qb < nqb; qb += wpp) {
-    const int q = qb * 16 + li;
-    const bool qv = q < L;
-    const int64_t qrow = qv ? seq_row(p, s, q) : 0;
-    bf16x8 qf[KK];
+  for (int qb0 = wi; qb0 < nqb; qb0 += QB * wpp) {
+    int q[QB], cq[QB];
+    bool qv[QB];
+    int64_t qrow[QB];
+    bf16x8 qf[QB][KK];
+    float m[QB], lsum[QB];
+    f32x4 o[QB][DB];
 #pragma unroll
-    for (int kk = 0; kk < KK; ++kk) qf[kk] = qv ? gload8(p.q + qrow * p.ldq + h * D + kk * 32 + 8 * g) : zero8();
-    const int cq = BIAS ? kb[min(q, L - 1)] + boff(p) : 0;   // padded queries: any in-range bin
-    float m = -INFINITY, lsum = 0.f;
-    f32x4 o[DB];
+    for (int u = 0; u < QB; ++u) {
+      q[u] = (qb0 + u * wpp) * 16 + li;           // blocks qb0, qb0 + wpp, ... (an idle block has q >= L)
+      qv[u] = q[u] < L;
+      qrow[u] = qv[u] ? seq_row(p, s, q[u]) : 0;
 #pragma unroll
-    for (int d = 0; d < DB; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int kk = 0; kk < KK; ++kk)
+        qf[u][kk] = qv[u] ? gload8(p.q + qrow[u] * p.ldq + h * D + kk * 32 + 8 * g) : zero8();
+      cq[u] = BIAS ? kb[min(q[u], L - 1)] + boff(p) : 0;   // padded queries: any in-range bin
+      m[u] = -INFINITY;
+      lsum[u] = 0.f;
+#pragma unroll
+      for (int d = 0; d < DB; ++d) o[u][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     for (int kc = 0; kc < Lp; kc += 32) {
-      f32x4 sa[2];
-#pragma unroll
-      for (int bi = 0; bi < 2; ++bi) {
-        sa[bi] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < KK; ++kk)
-          sa[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag<D>(Kimg, kc + 16 * bi, kk, lane), qf[kk], sa[bi], 0, 0, 0);
-      }
-      float cmax = -INFINITY;
-#pragma unroll
-      for (int bi = 0; bi < 2; ++bi) {
-        const int k0 = kc + 16 * bi + 4 * g;
-        if constexpr (RUN) {
-          const float* up = ub + (cq - kb[k0] - 3);   // up[3 - r] = ub[bin(q, k0 + r)]
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float x = sa[bi][r] * sc2 + up[3 - r];
-            sa[bi][r] = x;
-            cmax = fmaxf(cmax, x);
-          }
-          continue;
-        }
-        const f32x4 ma = *(const f32x4*)(mrow + k0);
-        int4 kbv;
-        if (BIAS) kbv = *(const int4*)(kb + k0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float x = sa[bi][r] * sc2 + ma[r];
-          if (BIAS) x += ub[cq - kbv[r]];
-          sa[bi][r] = x;
-          cmax = fmaxf(cmax, x);
-        }
-      }
-      cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
-      cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
-      const float mnew = fmaxf(m, cmax);
-      const float msafe = mnew == -INFINITY ? 0.f : mnew;
-      const float alpha = fexp2(m - msafe);
-      float psum = 0.f;
+      bf16x8 kf[2][KK];
 #pragma unroll
       for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float e = fexp2(sa[bi][r] - msafe);
-          sa[bi][r] = e;
-          psum += e;
-        }
-      lsum = lsum * alpha + psum;
-      m = mnew;
-      if constexpr (!BIAS) {
-        if (p.drop_p > 0.f) {
+        for (int kk = 0; kk < KK; ++kk) kf[bi][kk] = rowfrag<D>(Kimg, kc + 16 * bi, kk, lane);
+      f32x4 sa[QB][2];
 #pragma unroll
-          for (int bi = 0; bi < 2; ++bi)
+      for (int u = 0; u < QB; ++u)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) sa[bi][r] *= drop_keep(p, s, h, q, kc + 16 * bi + 4 * g + r);
+        for (int bi = 0; bi < 2; ++bi) {
+          sa[u][bi] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < KK; ++kk)
+            sa[u][bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[bi][kk], qf[u][kk], sa[u][bi], 0, 0, 0);
         }
+      bf16x8 pb[QB];
+      float alpha[QB];
+#pragma unroll
+      for (int u = 0; u < QB; ++u) {
+        float cmax = -INFINITY;
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi) {
+          const int k0 = kc + 16 * bi + 4 * g;
+          if constexpr (RUN) {
+            const float* up = ub + (cq[u] - kb[k0] - 3);   // up[3 - r] = ub[bin(q, k0 + r)]
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float x = sa[u][bi][r] * sc2 + up[3 - r];
+              sa[u][bi][r] = x;
+              cmax = fmaxf(cmax, x);
+            }
+            continue;
+          }
+          const f32x4 ma = *(const f32x4*)(mrow + k0);
+          int4 kbv;
+          if (BIAS) kbv = *(const int4*)(kb + k0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float x = sa[u][bi][r] * sc2 + ma[r];
+            if (BIAS) x += ub[cq[u] - kbv[r]];
+            sa[u][bi][r] = x;
+            cmax = fmaxf(cmax, x);
+          }
+        }
+        cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+        cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+        const float mnew = fmaxf(m[u], cmax);
+        const float msafe = mnew == -INFINITY ? 0.f : mnew;
+        alpha[u] = fexp2(m[u] - msafe);
+        float psum = 0.f;
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float e = fexp2(sa[u][bi][r] - msafe);
+            sa[u][bi][r] = e;
+            psum += e;
+          }
+        lsum[u] = lsum[u] * alpha[u] + psum;
+        m[u] = mnew;
+        if constexpr (!BIAS) {
+          if (p.drop_p > 0.f) {
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) sa[u][bi][r] *= drop_keep(p, s, h, q[u], kc + 16 * bi + 4 * g + r);
+          }
+        }
+        pb[u] = pack_perm(sa[u][0], sa[u][1]);
       }
-      const bf16x8 pb = pack_perm(sa[0], sa[1]);
 #pragma unroll
       for (int d = 0; d < DB; ++d) {
-        o[d] *= alpha;
-        o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag<D>(Vimg, kc, d * 16, lane), pb, o[d], 0, 0, 0);
+        const bf16x8 vf = trfrag<D>(Vimg, kc, d * 16, lane);
+#pragma unroll
+        for (int u = 0; u < QB; ++u) {
+          o[u][d] *= alpha[u];
+          o[u][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[u], o[u][d], 0, 0, 0);
+        }
       }
     }
-    lsum += __shfl_xor(lsum, 16, 64);
-    lsum += __shfl_xor(lsum, 32, 64);
-    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
-    if (qv) {
 #pragma unroll
-      for (int d = 0; d < DB; ++d) {
-        uint2 pk;
-        pk.x = pack2(o[d][0] * inv, o[d][1] * inv);
-        pk.y = pack2(o[d][2] * inv, o[d][3] * inv);
-        *(uint2*)(p.out + qrow * p.ldout + h * D + d * 16 + 4 * g) = pk;
+    for (int u = 0; u < QB; ++u) {
+      float ls = lsum[u];
+      ls += __shfl_xor(ls, 16, 64);
+      ls += __shfl_xor(ls, 32, 64);
+      const float inv = ls > 0.f ? 1.f / ls : 0.f;
+      if (qv[u]) {
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+          uint2 pk;
+          pk.x = pack2(o[u][d][0] * inv, o[u][d][1] * inv);
+          pk.y = pack2(o[u][d][2] * inv, o[u][d][3] * inv);
+          *(uint2*)(p.out + qrow[u] * p.ldout + h * D + d * 16 + 4 * g) = pk;
+        }
+        // natural-log LSE: ln(sum exp(x)) = (m2 + log2(lsum)) * ln 2
+        if (g == 0 && p.lse) p.lse[(int64_t)h * p.M + qrow[u]] = ls > 0.f ? (m[u] + __log2f(ls)) * LN2 : INFINITY;
       }
-      // natural-log LSE: ln(sum exp(x)) = (m2 + log2(lsum)) * ln 2
-      if (g == 0 && p.lse) p.lse[(int64_t)h * p.M + qrow] = lsum > 0.f ? (m + __log2f(lsum)) * LN2 : INFINITY;
     }
   }
 }
@@ -1113,6 +1147,10 @@ void set_attrs() {
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<32, true, 12, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<32, true, 12, true, 2>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<32, true, 12, true, 3>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<32, true, 12, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
@@ -1166,11 +1204,19 @@ size_t table_bytes(const AP& p, int Lp, bool bins) {
   return b;
 }
 
+int g_fwd_qb = -1;
+
 template <int D>
 void launch_fwd(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
   if constexpr (D == 32) {
     if (run_ok(p)) {
-      hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true>), grid, dim3(12 * 64), lds, st, p);
+      // query blocks processed together per wave (1 = the r02 kernel): CTCLIP_ATTN_FWD_QB or
+      // ctclip_attn_set_fwd_qb (A/B, bit-identical results)
+      if (g_fwd_qb < 0) { const char* e = getenv("CTCLIP_ATTN_FWD_QB"); g_fwd_qb = e ? atoi(e) : 3; }
+      const int qb = g_fwd_qb;
+      if (qb == 3) hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true, 3>), grid, dim3(12 * 64), lds, st, p);
+      else if (qb == 2) hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true, 2>), grid, dim3(12 * 64), lds, st, p);
+      else hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true>), grid, dim3(12 * 64), lds, st, p);
       return;
     }
   }
@@ -1538,4 +1584,13 @@ extern "C" int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream) {
   }
   CT_CHECK_LAUNCH();
   return 0;
+}
+
+// diagnostic: query blocks per wave of the spatial forward kernel (1, 2 or 3; results are
+// bit-identical); returns the previous setting
+extern "C" int ctclip_attn_set_fwd_qb(int qb) {
+  if (g_fwd_qb < 0) { const char* e = getenv("CTCLIP_ATTN_FWD_QB"); g_fwd_qb = e ? atoi(e) : 3; }
+  const int old = g_fwd_qb;
+  if (qb >= 1 && qb <= 3) g_fwd_qb = qb;
+  return old;
 }

@@ -8,6 +8,7 @@ downsample_image_embeds=False, no multiview augmentation.  Anything else raises.
 from __future__ import annotations
 
 import copy
+import os
 from pathlib import Path
 
 import torch
@@ -16,6 +17,10 @@ from torch import nn
 from . import dist_sync
 from . import functional as Fn
 from . import streams
+
+
+# queue BERT's forward before the image tower's (A/B switch, default: image tower first)
+TEXT_FWD_FIRST = os.environ.get('CTCLIP_TEXT_FWD_FIRST', '0') != '0'
 
 
 class _nullctx:
@@ -111,9 +116,14 @@ class CTCLIP(nn.Module):
         # only after an event taken before the image tower, so the two run side by side.
         dev = image.device
         ready = torch.cuda.current_stream(dev).record_event() if streams.text_stream(dev) else None
-        pooled, pooled_b = self.visual_transformer.encode_pooled(image)
-        enc_text = self.text_transformer(text.input_ids, attention_mask=text.attention_mask, join=False,
-                                         ready=ready)[0]
+        if TEXT_FWD_FIRST:      # A/B: BERT's launches queued before the image tower's
+            enc_text = self.text_transformer(text.input_ids, attention_mask=text.attention_mask, join=False,
+                                             ready=ready)[0]
+            pooled, pooled_b = self.visual_transformer.encode_pooled(image)
+        else:
+            pooled, pooled_b = self.visual_transformer.encode_pooled(image)
+            enc_text = self.text_transformer(text.input_ids, attention_mask=text.attention_mask, join=False,
+                                             ready=ready)[0]
         ts = streams.text_stream(dev)
         with torch.cuda.stream(ts) if ts is not None else _nullctx():
             t_raw = Fn.TextProjFn.apply(enc_text[:, 0, :].contiguous(), self.to_text_latent.weight)
@@ -198,7 +208,7 @@ class CTCLIP(nn.Module):
             return
         torch.autograd.backward(d[0], d[1].grad)
 
-    def grad_buckets(self):
+    def grad_buckets(self, text_first=True):
         """Gradient all-reduce buckets in the order the backward finalises them (dist_sync): BERT's
         layer groups from the top down (its backward is queued first, CTClipTrainer.forward_backward),
         the 3D-ViT's temporal stack, spatial stack, the rest of the image tower (patch embed, CPB),
@@ -206,10 +216,11 @@ class CTCLIP(nn.Module):
         vt = self.visual_transformer
         tb = getattr(self.text_transformer, 'grad_buckets', None)
         text = tb() if tb is not None else [('text_0', list(self.text_transformer.parameters()))]
-        return text + [('vit_temporal', list(vt.enc_temporal_transformer.parameters())),
-                       ('vit_spatial', list(vt.enc_spatial_transformer.parameters())),
-                       ('vit_rest', list(vt.parameters())),
-                       ('head', list(self.parameters()))]
+        vit = [('vit_temporal', list(vt.enc_temporal_transformer.parameters())),
+               ('vit_spatial', list(vt.enc_spatial_transformer.parameters())),
+               ('vit_rest', list(vt.parameters()))]
+        head = [('head', list(self.parameters()))]
+        return text + vit + head if text_first else vit + text + head
 
     def _pool_tokens(self, tokens):
         """mean over t + flatten of already-quantised tokens (ct_clip.py:724,740)."""

@@ -78,11 +78,21 @@ class FlatParams:
                 p.grad = g
 
 
+# queue BERT's backward before the 3D-ViT's (CTCLIP_TEXT_FIRST=0: after it, the r02 order; A/B)
+TEXT_FIRST = os.environ.get('CTCLIP_TEXT_FIRST', '1') != '0'
+
+
 def grad_buckets(model):
     """[(tag, params)] with every parameter in exactly one bucket, in the model's readiness order
     (``model.grad_buckets()``, e.g. CTCLIP: BERT layer groups, vit_temporal, vit_spatial, vit_rest,
     head)."""
-    spec = model.grad_buckets() if hasattr(model, 'grad_buckets') else [('all', list(model.parameters()))]
+    if not hasattr(model, 'grad_buckets'):
+        spec = [('all', list(model.parameters()))]
+    else:
+        try:
+            spec = model.grad_buckets(text_first=TEXT_FIRST)
+        except TypeError:
+            spec = model.grad_buckets()
     seen, out = set(), []
     for tag, ps in spec:
         mine = []
@@ -139,9 +149,12 @@ class CTClipTrainer:
             if defer:
                 # BERT first (text stream): its layer-group buckets go out to RCCL as its backward
                 # finalises them, ahead of the 3D-ViT's (main stream), whose backward runs beside it
-                self.model.backward_deferred_text()
+                # (TEXT_FIRST = False: the r02 order, 3D-ViT queued first)
                 back_img = getattr(self.model, 'backward_deferred_image', None)
-                if back_img is not None:
+                if not TEXT_FIRST and back_img is not None:
+                    back_img()
+                self.model.backward_deferred_text()
+                if TEXT_FIRST and back_img is not None:
                     back_img()
         except BaseException:
             dist_sync.disarm()

@@ -246,6 +246,9 @@ int ctclip_attn_fwd(const ctclip_attn_args* a, void* stream);
 int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream);
 int ctclip_attn_bwd_ws_floats(const ctclip_attn_args* a);
 int ctclip_attn_fwd_f32(const ctclip_attn_args* a, void* stream);   /* f32 image tower, see below */
+/* diagnostic: query blocks per wave processed together by the spatial (CPB-bias) forward kernel,
+ * 1..3 (default 3); results are bit-identical.  Returns the previous setting. */
+int ctclip_attn_set_fwd_qb(int qb);
 
 /* ---------------------------------------------------------------- f32 image tower (opt-in)
  * Exact-f32 forward stages of functional.set_vit_precision('f32') (csrc/f32path.hip); the linears

@@ -260,11 +260,24 @@ def test_f32_image_mode_vq_contract(base):
     dlog = (tl @ il.t() * e - g['out.text_latents'] @ g['out.image_latents'].t() * e).abs().max().item()
     di = (il - g['out.image_latents']).abs().max().item()
     dl = abs(loss.item() - g['out.loss'].item())
+    # the remaining index differences are f32 ties (margin < 1e-6: the oracle and the reference,
+    # both fp32 CPU, split on them too -- test_oracle_full_size_matches_fixture); a tie swaps one
+    # codebook row into the pooled latent, so latents / logits are compared with the oracle on the
+    # same indices (ties resolved alike)
+    with torch.no_grad():
+        forced = O.ctclip_forward(sd, base['ids'], base['mask'], O.normalize_hu(base['hu']), CFG,
+                                  training=False, force_ind=idx.to(torch.int32))
+    fi = (il - forced['image_latents']).abs().max().item()
+    flog = (tl @ il.t() * e - forced['text_latents'] @ forced['image_latents'].t() * e).abs().max().item()
+    fl = abs(loss.item() - forced['loss'].item())
     print(f'f32 image tower: pre-VQ tokens rel {tok:.2e} vs oracle; VQ {diff.sum().item()} of {gi.numel()} differ '
-          f'from the reference ({above} with oracle margin >= 1e-6); image latents {di:.2e}, logits {dlog:.2e}, '
-          f'loss |d| {dl:.2e}; image-tower forward at B=2: f32 {ms_f32:.1f} ms vs bf16 {ms_bf16:.1f} ms')
+          f'from the reference ({above} with oracle margin >= 1e-6); free-running vs the reference: image latents '
+          f'{di:.2e}, logits {dlog:.2e}, loss |d| {dl:.2e}; vs the oracle on the same indices: image latents '
+          f'{fi:.2e}, logits {flog:.2e}, loss |d| {fl:.2e}; image-tower forward at B=2: f32 {ms_f32:.1f} ms vs '
+          f'bf16 {ms_bf16:.1f} ms')
     assert above == 0
-    assert di < 1e-3 and dlog < 1e-3 and dl < 1e-3
+    assert dl < 1e-3
+    assert fi < 1e-4 and flog < 1e-3 and fl < 1e-3
     model.train()
 
 

@@ -79,7 +79,7 @@ def test_l2norm_geglu_patch_f32(K):
     v = O.normalize_hu(hu).double()
     p = v.reshape(2, 1, 2, 10, 4, 20, 4, 20).permute(0, 2, 4, 6, 1, 3, 5, 7).reshape(-1, 4000)
     ref = F.layer_norm(p, (4000,), gam.double(), bet.double(), 1e-5)
-    assert rel(out, ref) < 2e-7, rel(out, ref)
+    assert rel(out.cpu(), ref) < 2e-7, rel(out.cpu(), ref)
 
 
 def test_f32_tower_matches_oracle_small(K):
@@ -113,7 +113,7 @@ def test_f32_tower_matches_oracle_small(K):
     finally:
         precise.set_vit_precision(old)
     zo = trace['temporal_out'].reshape(-1, cfg.vit.dim)
-    r = rel(zf, zo)
+    r = rel(zf.cpu(), zo)
     E = sd['visual_transformer.vq._codebook.embed'][0]
     so = F.normalize(zo, dim=-1) @ E.t()
     top2 = so.topk(2, dim=1)

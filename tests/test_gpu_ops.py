@@ -123,7 +123,7 @@ def _attn_ref(q, k, v, rows, H, D, scale, bias=None, kmask=None):
         s = s.masked_fill(~kmask[:, None, None, :].bool(), float('-inf'))
     a = s.softmax(-1)
     o = torch.einsum('shij,shjd->shid', a, g(v))
-    out = torch.zeros(q.shape[0], H * D, device=dev)
+    out = torch.zeros(q.shape[0], H * D, device=dev, dtype=q.dtype)
     out = out.index_copy(0, rows.reshape(-1), o.permute(0, 2, 1, 3).reshape(nseq * L, H * D))
     return out
 
@@ -436,3 +436,27 @@ def test_deferred_reductions_shared_output(K):
         arr[i].slabs, arr[i].nslab, arr[i].cols = p.data_ptr(), p.shape[0], 512
         arr[i].out, arr[i].accumulate = out.data_ptr(), 1
     assert _lib.lib().ctclip_reduce_slabs_multi(arr, 2, st.cuda_stream) == 1001
+
+
+def test_attention_fwd_query_blocks_bit_identical(K):
+    """The spatial forward kernel processing 1, 2 or 3 query blocks per wave together
+    (ctclip_attn_set_fwd_qb) gives bit-identical outputs and LSE at the base 24 x 24 grid."""
+    from ctclip_mi355x import _lib
+    torch.manual_seed(5)
+    gh = gw = 24
+    L, H, D, nseq = gh * gw, 8, 32, 5
+    M = nseq * L
+    u, _ = _cpb_table(H, gh, gw)
+    q = F.normalize(torch.randn(M, H, D, device=dev), dim=-1).reshape(M, H * D).bfloat16()
+    kv = (torch.randn(M, 2 * H * D, device=dev) * 0.18).bfloat16()
+    outs = []
+    old = _lib.lib().ctclip_attn_set_fwd_qb(1)
+    try:
+        for qb in (1, 2, 3):
+            _lib.lib().ctclip_attn_set_fwd_qb(qb)
+            outs.append(K.attn_fwd(q, kv[:, :H * D], kv[:, H * D:], L=L, H=H, D=D, nseq=nseq, scale=8.0,
+                                   seq=(1, L, 0, 1), bias_u=u, grid=(gh, gw)))
+    finally:
+        _lib.lib().ctclip_attn_set_fwd_qb(old)
+    for o, lse in outs[1:]:
+        assert torch.equal(o, outs[0][0]) and torch.equal(lse, outs[0][1])
