@@ -207,7 +207,14 @@ __device__ __forceinline__ void load_tables(const AP& p, char* tab, int Lp, int 
 // latencies (the kernel ran at ~3 waves per SIMD with one dependent chain each), and the K / V
 // fragments of a key chunk are read from LDS once for all QB blocks.  Per-query arithmetic is
 // unchanged (bit-identical to QB = 1).
-template <int D, bool BIAS, int W = (BIAS ? 12 : NW), bool RUN = false, int QB = 1>
+// SMAX (RUN shapes): the softmax max is a per-query STATIC bound instead of the online running
+// max -- |q.k| <= ||q|| max_k ||k|| (Cauchy-Schwarz), so x <= Mq = scale ||q|| max||k|| + max bias
+// (log2 units) -- which removes the per-chunk cross-lane max, the rescale of the running sum and
+// of the output, and keeps every probability <= 1.  Used for a query group only while the bound's
+// span (2 scale ||q|| max||k|| + bias range) stays <= 64, so no probability can underflow more
+// than exp2(-64) below the row's largest; otherwise that group runs the online-max code.  Same
+// softmax in exact arithmetic, f32-level differences in rounding.
+template <int D, bool BIAS, int W = (BIAS ? 12 : NW), bool RUN = false, int QB = 1, bool SMAX = false>
 __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KK = D / 32, DB = D / 16, RS = Img<D>::RS, NTH = W * 64;
@@ -237,6 +244,35 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
   const int g = lane >> 4, li = lane & 15;
   const int nqb = (L + 15) >> 4;
   const float sc2 = p.scale * LOG2E;
+  float kmax2 = 0.f, bhi = 0.f, blo = 0.f;
+  if constexpr (SMAX) {
+    // max_k ||k||^2 of this pair's keys and the bias table's range (log2 units): one block reduction
+    float k2 = 0.f, bh = -INFINITY, bl = INFINITY;
+    for (int r = tid; r < L; r += NTH) {
+      float s2 = 0.f;
+#pragma unroll
+      for (int c = 0; c < D / 8; ++c) {
+        float x[8];
+        unpack8(*(const u32x4*)(Kimg + r * RS + c * 16), x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s2 = fmaf(x[j], x[j], s2);
+      }
+      k2 = fmaxf(k2, s2);
+    }
+    for (int i = tid; i < p.nbins; i += NTH) { bh = fmaxf(bh, ub[i]); bl = fminf(bl, ub[i]); }
+#pragma unroll
+    for (int o_ = 1; o_ < 64; o_ <<= 1) {
+      k2 = fmaxf(k2, __shfl_xor(k2, o_, 64));
+      bh = fmaxf(bh, __shfl_xor(bh, o_, 64));
+      bl = fminf(bl, __shfl_xor(bl, o_, 64));
+    }
+    float* red = madd + p.pp * Lp;      // 3 * W floats past the tables (host: + 256 B)
+    if (lane == 0) { red[w] = k2; red[W + w] = bh; red[2 * W + w] = bl; }
+    __syncthreads();
+    kmax2 = red[0]; bhi = red[W]; blo = red[2 * W];
+#pragma unroll
+    for (int i = 1; i < W; ++i) { kmax2 = fmaxf(kmax2, red[i]); bhi = fmaxf(bhi, red[W + i]); blo = fminf(blo, red[2 * W + i]); }
+  }
   for (int qb0 = wi; qb0 < nqb; qb0 += QB * wpp) {
     int q[QB], cq[QB];
     bool qv[QB];
@@ -258,6 +294,66 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
 #pragma unroll
       for (int d = 0; d < DB; ++d) o[u][d] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    bool use_static = false;
+    if constexpr (SMAX) {
+      bool ok = true;
+#pragma unroll
+      for (int u = 0; u < QB; ++u) {
+        float q2 = 0.f;
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) q2 = fmaf((float)qf[u][kk][j], (float)qf[u][kk][j], q2);
+        q2 += __shfl_xor(q2, 16, 64);
+        q2 += __shfl_xor(q2, 32, 64);
+        const float xb = sc2 * sqrtf(q2 * kmax2);
+        m[u] = xb + bhi;                           // the static bound Mq (log2 units)
+        ok = ok && 2.f * xb + (bhi - blo) <= 64.f;
+      }
+      use_static = __all(ok);
+    }
+    if (use_static) {
+      if constexpr (SMAX) {
+        for (int kc = 0; kc < Lp; kc += 32) {
+          bf16x8 kf[2][KK];
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk) kf[bi][kk] = rowfrag<D>(Kimg, kc + 16 * bi, kk, lane);
+          bf16x8 pb[QB];
+#pragma unroll
+          for (int u = 0; u < QB; ++u) {
+            f32x4 sa[2];
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi) {
+              sa[bi] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int kk = 0; kk < KK; ++kk)
+                sa[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[bi][kk], qf[u][kk], sa[bi], 0, 0, 0);
+            }
+#pragma unroll
+            for (int bi = 0; bi < 2; ++bi) {
+              const float* up = ub + (cq[u] - kb[kc + 16 * bi + 4 * g] - 3);   // up[3 - r] = ub[bin(q, k0 + r)]
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float e = fexp2(fmaf(sa[bi][r], sc2, up[3 - r]) - m[u]);
+                sa[bi][r] = e;
+                lsum[u] += e;
+              }
+            }
+            pb[u] = pack_perm(sa[0], sa[1]);
+          }
+#pragma unroll
+          for (int d = 0; d < DB; ++d) {
+            const bf16x8 vf = trfrag<D>(Vimg, kc, d * 16, lane);
+#pragma unroll
+            for (int u = 0; u < QB; ++u) o[u][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[u], o[u][d], 0, 0, 0);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+    for (int u = 0; u < QB; ++u) m[u] = -INFINITY;
     for (int kc = 0; kc < Lp; kc += 32) {
       bf16x8 kf[2][KK];
 #pragma unroll
@@ -338,6 +434,7 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
           o[u][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[u], o[u][d], 0, 0, 0);
         }
       }
+    }
     }
 #pragma unroll
     for (int u = 0; u < QB; ++u) {
@@ -1151,6 +1248,8 @@ void set_attrs() {
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<32, true, 12, true, 3>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<32, true, 12, true, 3, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<32, true, 12, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
@@ -1205,6 +1304,7 @@ size_t table_bytes(const AP& p, int Lp, bool bins) {
 }
 
 int g_fwd_qb = -1;
+int g_fwd_smax = -1;   // static-bound softmax in the QB = 3 forward (CTCLIP_ATTN_FWD_SMAX, default on)
 
 template <int D>
 void launch_fwd(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
@@ -1214,7 +1314,10 @@ void launch_fwd(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
       // ctclip_attn_set_fwd_qb (A/B, bit-identical results)
       if (g_fwd_qb < 0) { const char* e = getenv("CTCLIP_ATTN_FWD_QB"); g_fwd_qb = e ? atoi(e) : 3; }
       const int qb = g_fwd_qb;
-      if (qb == 3) hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true, 3>), grid, dim3(12 * 64), lds, st, p);
+      if (g_fwd_smax < 0) { const char* e = getenv("CTCLIP_ATTN_FWD_SMAX"); g_fwd_smax = e ? atoi(e) != 0 : 1; }
+      if (qb == 3 && g_fwd_smax)
+        hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true, 3, true>), grid, dim3(12 * 64), lds, st, p);
+      else if (qb == 3) hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true, 3>), grid, dim3(12 * 64), lds, st, p);
       else if (qb == 2) hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true, 2>), grid, dim3(12 * 64), lds, st, p);
       else hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true>), grid, dim3(12 * 64), lds, st, p);
       return;
@@ -1482,7 +1585,7 @@ extern "C" int ctclip_attn_fwd(const ctclip_attn_args* a, void* stream) {
     return 0;
   }
   const size_t RSb = a->D * 2 + 16;
-  const size_t lds = (size_t)p.pp * 2 * Lp * RSb + table_bytes(p, Lp, false);
+  const size_t lds = (size_t)p.pp * 2 * Lp * RSb + table_bytes(p, Lp, false) + 256;   // + block-reduce scratch
   if (lds > 160 * 1024) return CT_ESHAPE;
   dim3 grid(cdiv(pairs, p.pp));
   if (a->D == 32) launch_fwd<32>(p, grid, lds, (hipStream_t)stream);
@@ -1588,6 +1691,13 @@ extern "C" int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream) {
 
 // diagnostic: query blocks per wave of the spatial forward kernel (1, 2 or 3; results are
 // bit-identical); returns the previous setting
+extern "C" int ctclip_attn_set_fwd_smax(int on) {
+  if (g_fwd_smax < 0) { const char* e = getenv("CTCLIP_ATTN_FWD_SMAX"); g_fwd_smax = e ? atoi(e) != 0 : 1; }
+  const int old = g_fwd_smax;
+  g_fwd_smax = on != 0;
+  return old;
+}
+
 extern "C" int ctclip_attn_set_fwd_qb(int qb) {
   if (g_fwd_qb < 0) { const char* e = getenv("CTCLIP_ATTN_FWD_QB"); g_fwd_qb = e ? atoi(e) : 3; }
   const int old = g_fwd_qb;

@@ -440,7 +440,9 @@ def test_deferred_reductions_shared_output(K):
 
 def test_attention_fwd_query_blocks_bit_identical(K):
     """The spatial forward kernel processing 1, 2 or 3 query blocks per wave together
-    (ctclip_attn_set_fwd_qb) gives bit-identical outputs and LSE at the base 24 x 24 grid."""
+    (ctclip_attn_set_fwd_qb) gives bit-identical outputs and LSE at the base 24 x 24 grid; the
+    static-bound softmax (ctclip_attn_set_fwd_smax) matches the online max to rounding, and falls
+    back to it (bit-identical) where the bound's span is too wide."""
     from ctclip_mi355x import _lib
     torch.manual_seed(5)
     gh = gw = 24
@@ -449,14 +451,31 @@ def test_attention_fwd_query_blocks_bit_identical(K):
     u, _ = _cpb_table(H, gh, gw)
     q = F.normalize(torch.randn(M, H, D, device=dev), dim=-1).reshape(M, H * D).bfloat16()
     kv = (torch.randn(M, 2 * H * D, device=dev) * 0.18).bfloat16()
+    lib = _lib.lib()
+
+    def run(qv):
+        return K.attn_fwd(qv, kv[:, :H * D], kv[:, H * D:], L=L, H=H, D=D, nseq=nseq, scale=8.0,
+                          seq=(1, L, 0, 1), bias_u=u, grid=(gh, gw))
     outs = []
-    old = _lib.lib().ctclip_attn_set_fwd_qb(1)
+    old, old_s = lib.ctclip_attn_set_fwd_qb(1), lib.ctclip_attn_set_fwd_smax(0)
     try:
         for qb in (1, 2, 3):
-            _lib.lib().ctclip_attn_set_fwd_qb(qb)
-            outs.append(K.attn_fwd(q, kv[:, :H * D], kv[:, H * D:], L=L, H=H, D=D, nseq=nseq, scale=8.0,
-                                   seq=(1, L, 0, 1), bias_u=u, grid=(gh, gw)))
+            lib.ctclip_attn_set_fwd_qb(qb)
+            outs.append(run(q))
+        for o, lse in outs[1:]:
+            assert torch.equal(o, outs[0][0]) and torch.equal(lse, outs[0][1])
+        # static-bound softmax (3 blocks): the same softmax, f32-level rounding differences only
+        lib.ctclip_attn_set_fwd_smax(1)
+        o_s, lse_s = run(q)
+        assert rel(o_s, outs[0][0]) < 2e-3 and (lse_s - outs[0][1]).abs().max().item() < 1e-4
+        # query norms large enough that the bound's span exceeds 64: the kernel keeps the online max
+        # for those groups (bit-identical to the online kernel)
+        q3 = (q.float() * 3).bfloat16()
+        lib.ctclip_attn_set_fwd_smax(0)
+        o_ref3 = run(q3)
+        lib.ctclip_attn_set_fwd_smax(1)
+        o_s3 = run(q3)
+        assert torch.equal(o_s3[0], o_ref3[0]) and torch.equal(o_s3[1], o_ref3[1])
     finally:
-        _lib.lib().ctclip_attn_set_fwd_qb(old)
-    for o, lse in outs[1:]:
-        assert torch.equal(o, outs[0][0]) and torch.equal(lse, outs[0][1])
+        lib.ctclip_attn_set_fwd_qb(old)
+        lib.ctclip_attn_set_fwd_smax(old_s)
