@@ -1304,7 +1304,11 @@ size_t table_bytes(const AP& p, int Lp, bool bins) {
 }
 
 int g_fwd_qb = -1;
-int g_fwd_smax = -1;   // static-bound softmax in the QB = 3 forward (CTCLIP_ATTN_FWD_SMAX, default on)
+// static-bound softmax in the QB = 3 forward (CTCLIP_ATTN_FWD_SMAX=1): measured SLOWER at the base
+// shape, 254 vs 235 us per layer (profiles/r03d_attnsmax_ab.log) -- its per-workgroup prologue (the
+// key norms and bias-table range over 576 rows + 2,209 bins, a block reduction and a barrier for
+// each of 1,536 workgroups) costs more than the per-chunk max / rescale it removes -- so off
+int g_fwd_smax = -1;
 
 template <int D>
 void launch_fwd(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
@@ -1314,7 +1318,7 @@ void launch_fwd(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
       // ctclip_attn_set_fwd_qb (A/B, bit-identical results)
       if (g_fwd_qb < 0) { const char* e = getenv("CTCLIP_ATTN_FWD_QB"); g_fwd_qb = e ? atoi(e) : 3; }
       const int qb = g_fwd_qb;
-      if (g_fwd_smax < 0) { const char* e = getenv("CTCLIP_ATTN_FWD_SMAX"); g_fwd_smax = e ? atoi(e) != 0 : 1; }
+      if (g_fwd_smax < 0) { const char* e = getenv("CTCLIP_ATTN_FWD_SMAX"); g_fwd_smax = e ? atoi(e) != 0 : 0; }
       if (qb == 3 && g_fwd_smax)
         hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true, 3, true>), grid, dim3(12 * 64), lds, st, p);
       else if (qb == 3) hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true, 3>), grid, dim3(12 * 64), lds, st, p);
@@ -1692,7 +1696,7 @@ extern "C" int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream) {
 // diagnostic: query blocks per wave of the spatial forward kernel (1, 2 or 3; results are
 // bit-identical); returns the previous setting
 extern "C" int ctclip_attn_set_fwd_smax(int on) {
-  if (g_fwd_smax < 0) { const char* e = getenv("CTCLIP_ATTN_FWD_SMAX"); g_fwd_smax = e ? atoi(e) != 0 : 1; }
+  if (g_fwd_smax < 0) { const char* e = getenv("CTCLIP_ATTN_FWD_SMAX"); g_fwd_smax = e ? atoi(e) != 0 : 0; }
   const int old = g_fwd_smax;
   g_fwd_smax = on != 0;
   return old;

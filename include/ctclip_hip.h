@@ -249,8 +249,8 @@ int ctclip_attn_fwd_f32(const ctclip_attn_args* a, void* stream);   /* f32 image
 /* diagnostic: query blocks per wave processed together by the spatial (CPB-bias) forward kernel,
  * 1..3 (default 3); results are bit-identical.  Returns the previous setting. */
 int ctclip_attn_set_fwd_qb(int qb);
-/* diagnostic: static-bound softmax in the 3-block spatial forward (1, default) or the online max
- * (0); see attn.hip.  Returns the previous setting. */
+/* diagnostic: static-bound softmax in the 3-block spatial forward (1) or the online max (0, default:
+ * measured faster); see attn.hip.  Returns the previous setting. */
 int ctclip_attn_set_fwd_smax(int on);
 
 /* ---------------------------------------------------------------- f32 image tower (opt-in)

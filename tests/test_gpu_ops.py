@@ -467,7 +467,7 @@ def test_attention_fwd_query_blocks_bit_identical(K):
         # static-bound softmax (3 blocks): the same softmax, f32-level rounding differences only
         lib.ctclip_attn_set_fwd_smax(1)
         o_s, lse_s = run(q)
-        assert rel(o_s, outs[0][0]) < 2e-3 and (lse_s - outs[0][1]).abs().max().item() < 1e-4
+        assert rel(o_s, outs[0][0]) < 6e-3 and (lse_s - outs[0][1]).abs().max().item() < 1e-4   # bf16 o: 1-ulp flips
         # query norms large enough that the bound's span exceeds 64: the kernel keeps the online max
         # for those groups (bit-identical to the online kernel)
         q3 = (q.float() * 3).bfloat16()
