@@ -46,18 +46,8 @@ struct P {
   int group_gx;  // grouped (8-row) tile walk when the N tile count >= this (CTCLIP_GEMM_GROUP_GX, default 8)
   int stagger;   // start delay (s_sleep units of 64 cycles) for the second co-resident workgroup
   int gz;        // batch * split_k (8-phase tile count = ceil(N/256) * ceil(M/256) * gz)
-  // 8-phase: persistent workgroups (one per CU) walking the tile sequence (bit 0); bit 1: dynamic
-  // tile queues, bits 2+: their slot in g_tile_q (packed into this field: the kernel is at its
-  // SGPR limit, and one more live kernel argument spilled SGPRs into 20-30 VGPRs)
-  int persist;
+  int persist;   // 8-phase: persistent workgroups (one per CU) walking the tile sequence
 };
-
-// Dynamic tile queues of the persistent 8-phase kernel: a ring of slots, one per launch (the host
-// takes the next slot for every launch, so a slot is reused only NSLOT_Q launches later); per slot
-// [0, 8) the per-XCD-label tile counters, [8] the exit counter, [64, 128) dummy words for the lanes
-// of the dequeue instruction that do not dequeue.  The last workgroup to exit zeroes its slot.
-constexpr int NSLOT_Q = 256, QWORDS = 128;
-__device__ unsigned g_tile_q[NSLOT_Q][QWORDS];
 
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
 
@@ -967,7 +957,7 @@ __device__ unsigned long long g_stamps[256][32][6];
 #define STAMP(k, v) do { } while (0)
 #endif
 
-template <bool AK, bool BKC, int EP, bool DYN>
+template <bool AK, bool BKC, int EP>
 __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
   using namespace p8;
   constexpr bool TR = EP >= 0;
@@ -1043,38 +1033,6 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
         }
     __builtin_amdgcn_s_setprio(0);
   };
-  // ---- dynamic tile walk (p.tq): the tiles of XCD label l (tile_at's remap: lin = l + 8 j walks
-  // label l's contiguous tile range) are handed out by one device-scope counter per label, the first
-  // round statically (j = blockIdx.x / 8).  A workgroup that starts late -- its CU still held by
-  // another stream's workgroups -- or runs slow takes fewer tiles instead of delaying the whole
-  // launch; once its own label is exhausted it takes tiles of the other labels.  A tile's successor
-  // is dequeued one tile ahead, during the previous tile's epilogue (all 64 lanes of wave 0 issue
-  // one atomic: lane 0 on the counter, the others add 0 to dummy words, so no exec-masked load needs
-  // its value merged early), and reaches the other waves through a 2-slot LDS ring read after the
-  // main loop's closing barrier.
-  // (a template parameter: any run-time use of the dynamic lin in the static kernels' tile loop made
-  // hipcc spill 20-30 more VGPRs there, so the static instantiations keep the plain lin += lstride)
-  const bool dyn = DYN && ntiles > (int)gridDim.x;
-  const int label = (int)blockIdx.x & 7;
-  auto lab_cnt = [&](int l) { return (ntiles >> 3) + (l < (ntiles & 7) ? 1 : 0); };
-  auto lab_first = [&](int l) { return ((int)gridDim.x >> 3) + (l < ((int)gridDim.x & 7) ? 1 : 0); };
-  unsigned* const tq = &g_tile_q[p.persist >> 2][0];   // a relocatable constant, rematerialised
-  int* const nxt_lds = (int*)(smem + SMEM_P);   // two ints past the kernel's staging (host: + 16 B)
-  unsigned deq = 0;
-  auto dequeue_issue = [&]() {   // wave 0 only
-    const unsigned* a = lane == 0 ? tq + label : tq + 64 + lane;
-    deq = __hip_atomic_fetch_add((unsigned*)a, lane == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  auto next_lin = [&]() -> int {   // wave 0, lane 0 only: the next tile's lin, or -1
-    int j = lab_first(label) + (int)deq;
-    if (j < lab_cnt(label)) return label + 8 * j;
-    for (int t = 1; t < 8; ++t) {
-      const int l = (label + t) & 7;
-      const int jj = lab_first(l) + (int)__hip_atomic_fetch_add(tq + l, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (jj < lab_cnt(l)) return l + 8 * jj;
-    }
-    return -1;
-  };
   auto wait_ahead = [&](bool younger_issued) {
     if (younger_issued) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1085,10 +1043,6 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  if (dyn && w == 0) {   // the second tile's lin into slot 1 (slot k & 1 holds the k-th tile's lin)
-    dequeue_issue();
-    if (lane == 0) nxt_lds[1] = next_lin();
-  }
   // cold prologue: tile 0 complete in E, tile 1's A0/B0 halves in flight
   stage(A0, 0); stage(A1, 0); stage(B0, 0); stage(B1, 0);
   stage(A0, 1); stage(B0, 1);
@@ -1133,24 +1087,13 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
     if (wr == 0) bar();   // balance the stagger barrier
     __syncthreads();      // every wave's last fragment reads done before LDS is refilled / reused
     STAMP(3, __builtin_amdgcn_s_memtime());
-    if (dyn) {
-      // written during the previous tile's epilogue; readfirstlane keeps the tile geometry in
-      // SGPRs (a VGPR lin made every tile field a per-lane value live across the main loop)
-      lin = __builtin_amdgcn_readfirstlane(nxt_lds[(tcount + 1) & 1]);
-      if (lin < 0 || lin >= ntiles) lin = ntiles;   // done (never an out-of-range tile)
-    } else {
-      lin += lstride;
-    }
+    lin += lstride;
     const bool more = lin < ntiles;
     if (more) {
       const Tile nx = tile_at(p, lin, gx, gy, ntiles);
       stage_of(nx, A0, 0); stage_of(nx, A1, 0); stage_of(nx, B0, 0); stage_of(nx, B1, 0);
       if constexpr (TR) { stage_of(nx, A0, 1); stage_of(nx, B0, 1); }
     }
-    // dequeue the tile AFTER next during this epilogue (its latency hides under the stores; the
-    // result lives in a register only until the epilogue ends, then in LDS slot tcount & 1)
-    const bool deq_now = dyn && more && w == 0;
-    if (deq_now) dequeue_issue();
     if (p.debug & 1) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -1170,18 +1113,9 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
       // staging in buffer O and beyond (the next tile's tile 0 is landing in E)
       epilogue<EP == -2 || EP == -3 || EP == -5 ? EP : -1>(p, acc, smem + TILEB, w, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
     }
-    if (deq_now && lane == 0) nxt_lds[tcount & 1] = next_lin();   // lane 0 alone: steals dequeue for real
     STAMP(4, __builtin_amdgcn_s_memtime());
     ++tcount;
-    if (!more) {
-      if (dyn && threadIdx.x == 0) {
-        // the last workgroup out zeroes the slot for its next use (NSLOT_Q launches later)
-        const unsigned done = __hip_atomic_fetch_add(tq + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (done == gridDim.x - 1)
-          for (int i = 0; i <= 8; ++i) __hip_atomic_exchange(tq + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      break;
-    }
+    if (!more) break;
     T = tile_at(p, lin, gx, gy, ntiles);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -1198,24 +1132,16 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
 // persistent grid cap (workgroups; default 256 = one per CU): lets two GEMMs on two streams share
 // the chip (ctclip_gemm_set_grid_cap)
 static int g_grid_cap = 0;
-static int g_dyn = -1;          // dynamic tile queues (CTCLIP_GEMM_DYN, default off)
-static unsigned g_slot = 0;
-
-template <bool AK, bool BKC, int EP, bool DYN>
-void launch8_k(const P& p, dim3 grid, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<AK, BKC, EP, DYN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              p8::SMEM_P + 16);
-    attr = true;
-  }
-  hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP, DYN>), grid, dim3(p8::NTH), p8::SMEM_P + 16, st, p);
-}
 
 template <bool AK, bool BKC, int EP>
 int launch8(const P& p, int batch, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<AK, BKC, EP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              p8::SMEM_P);
+    attr = true;
+  }
   const int64_t ntiles = cdiv(p.N, p8::BNN) * cdiv(p.M, p8::BM) * (int64_t)p.gz;
-  if (g_dyn < 0) { const char* e = getenv("CTCLIP_GEMM_DYN"); g_dyn = e ? atoi(e) != 0 : 0; }
   static bool cap_env = false;   // CTCLIP_GEMM_GRID_CAP (A/B): persistent grid below one per CU
   if (!cap_env) {
     const char* e = getenv("CTCLIP_GEMM_GRID_CAP");
@@ -1225,16 +1151,10 @@ int launch8(const P& p, int batch, hipStream_t st) {
   if (p.persist) {
     const int64_t cap = g_grid_cap > 0 && g_grid_cap < 256 ? g_grid_cap : 256;
     dim3 grid((unsigned)(ntiles < cap ? ntiles : cap));
-    if (g_dyn && ntiles > cap) {
-      P pp = p;
-      pp.persist = 1 | 2 | (int)((g_slot++ % NSLOT_Q) << 2);
-      launch8_k<AK, BKC, EP, true>(pp, grid, st);
-    } else {
-      launch8_k<AK, BKC, EP, false>(p, grid, st);
-    }
+    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP>), grid, dim3(p8::NTH), p8::SMEM_P, st, p);
   } else {
     dim3 grid(cdiv(p.N, p8::BNN), cdiv(p.M, p8::BM), batch * p.split_k);
-    launch8_k<AK, BKC, EP, false>(p, grid, st);
+    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP>), grid, dim3(p8::NTH), p8::SMEM_P, st, p);
   }
   CT_CHECK_LAUNCH();
   return 0;
@@ -1367,14 +1287,6 @@ extern "C" int ctclip_gemm_set_stagger(int v) {
 extern "C" int ctclip_gemm_set_grid_cap(int v) {
   const int old = g256::g_grid_cap;
   g256::g_grid_cap = v > 0 ? v : 0;
-  return old;
-}
-
-// diagnostic: dynamic tile queues of the persistent 8-phase kernel on / off; returns the previous value
-extern "C" int ctclip_gemm_set_dynamic(int v) {
-  if (g256::g_dyn < 0) { const char* e = getenv("CTCLIP_GEMM_DYN"); g256::g_dyn = e ? atoi(e) != 0 : 0; }
-  const int old = g256::g_dyn;
-  g256::g_dyn = v != 0;
   return old;
 }
 

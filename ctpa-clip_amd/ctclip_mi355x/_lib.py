@@ -98,7 +98,6 @@ _SIGS = {
     'ctclip_gemm_set_stagger': [c_i32],
     'ctclip_gemm_set_persist': [c_i32],
     'ctclip_gemm_set_grid_cap': [c_i32],
-    'ctclip_gemm_set_dynamic': [c_i32],
     'ctclip_reduce_slabs_ep': [c_vp, c_i64, c_i64, c_i64, c_i64, ctypes.POINTER(GemmArgs), c_vp],
     'ctclip_reduce_slabs': [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp],
     'ctclip_reduce_slabs_multi': [ctypes.POINTER(SlabJob), c_i32, c_vp],

@@ -77,9 +77,6 @@ int ctclip_gemm_set_persist(int on);
 /* 8-phase persistent grid cap (workgroups) for the launches that follow; 0 = one per CU (default).
  * Two GEMMs on two streams, each capped, share the chip.  Returns the previous cap. */
 int ctclip_gemm_set_grid_cap(int workgroups);
-/* 8-phase persistent kernel: dynamic tile queues (1, default) or the static tile walk (0); both
- * compute identical results.  Returns the previous setting. */
-int ctclip_gemm_set_dynamic(int on);
 
 /* sum f32 slabs [s][rows][ld] -> out (f32 or bf16), optional accumulate into f32 out */
 int ctclip_reduce_slabs(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,

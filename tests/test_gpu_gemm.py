@@ -177,35 +177,3 @@ def test_adam_writes_split_shadow(K):
     assert torch.equal(lo[1:], (p[1:] - hi[1:].float()).bfloat16())
 
 
-def test_dynamic_tile_queue_bit_identical(K):
-    """ctclip_gemm_set_dynamic: the persistent 8-phase kernel hands tiles out from per-XCD-label
-    device counters instead of the static stride.  A tile's result does not depend on which
-    workgroup computes it, so outputs are bit-identical; 300 launches wrap the 256-slot counter ring
-    (each slot is zeroed by its launch's last workgroup), and two streams run launches concurrently."""
-    from ctclip_mi355x._lib import lib
-    torch.manual_seed(11)
-    x = torch.randn(40960, 512, device="cuda").bfloat16()       # 160 x 11 and 160 x 2 tiles > 256 workgroups
-    w1 = torch.randn(2816, 512, device='cuda').bfloat16()
-    w2 = torch.randn(512, 2816, device='cuda').bfloat16()
-    r = torch.randn(40960, 512, device="cuda")
-    old = lib().ctclip_gemm_set_dynamic(0)
-    try:
-        ref1 = K.linear(x, w1)
-        ref2 = K.linear(ref1, w2, residual=r, out_dtype=torch.float32)
-        ref3 = K.matmul_tn(ref1, x)
-        torch.cuda.synchronize()
-        lib().ctclip_gemm_set_dynamic(1)
-        s2 = torch.cuda.Stream()
-        for i in range(150):
-            y1 = K.linear(x, w1)
-            with torch.cuda.stream(s2):
-                y3 = K.matmul_tn(ref1, x)
-            y2 = K.linear(y1, w2, residual=r, out_dtype=torch.float32)
-            torch.cuda.current_stream().wait_stream(s2)
-            if i % 50 == 0 or i == 149:
-                assert torch.equal(y1, ref1)
-                assert torch.equal(y2, ref2)
-                assert torch.equal(y3, ref3)
-        torch.cuda.synchronize()
-    finally:
-        lib().ctclip_gemm_set_dynamic(old)
