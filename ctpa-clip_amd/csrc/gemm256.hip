@@ -12,6 +12,7 @@
 // 16-B row chunks with the same fused ops as gemm.hip (bias, residual, GELU, GEGLU in
 // 32-column pairs, argmax, split-K slabs).  Requires K % 64 == 0 (checked by the caller).
 #include "common.h"
+#include <string.h>
 #include "../../include/ctclip_hip.h"
 
 namespace g256 {
@@ -47,6 +48,15 @@ struct P {
   int stagger;   // start delay (s_sleep units of 64 cycles) for the second co-resident workgroup
   int gz;        // batch * split_k (8-phase tile count = ceil(N/256) * ceil(M/256) * gz)
   int persist;   // 8-phase: persistent workgroups (one per CU) walking the tile sequence
+  // LayerNorm epilogues (EP -6 forward, -7 backward; ctclip_gemm_ln)
+  const float* ln_gamma; const float* ln_beta; float ln_eps;
+  u16* ln_y; int64_t ln_ldy;         // -6: LN output (bf16)
+  float* ln_mean; float* ln_rstd;    // -6: written; -7: read
+  const u16* ln_x; int64_t ln_ldx;   // -7: the LN input (bf16)
+  float* ln_pg; float* ln_pb;        // -7: [M / 128][N] column partials (dgamma, dbeta)
+  unsigned long long* xchg;          // [2 tiles][M][2] {epoch, value} granules
+  unsigned epoch;
+  int* status;
 };
 
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
@@ -896,6 +906,307 @@ __device__ __forceinline__ void epilogue_geglu_bwd(const P& p, f32x4 (&acc)[8][4
   }
 }
 
+// ============================================================================================
+// LayerNorm fused into the epilogue of an N = 512 GEMM (ctclip_gemm_ln; the 3D-ViT's d = 512
+// rows).  A row's 512 columns are two 256-column tiles.  In the persistent walk tile_at hands the
+// row block's tiles 2k, 2k + 1 to workgroups w, w ^ 8 of the SAME round whenever ntiles % 16 == 0
+// and the grid is min(ntiles, 256) (the host checks both), so the pair is co-scheduled and each
+// waits only on the other.  Each tile reduces its 256 columns per row (a wave: 8 lanes x 8 values
+// through xor shuffles, then the 4 column waves through LDS), publishes the two per-row values as
+// 8-byte {epoch, value} granules (relaxed agent-scope atomic stores, sc1: the data is the flag,
+// MI355X_MICROARCH.md § visibility, R2) and polls the partner's with relaxed agent-scope loads
+// (sc1, bypassing L1; bounded: a timeout sets *status and continues).  Both tiles combine the two
+// halves with symmetric formulas, so the two halves of a row see bit-identical statistics.
+//   MODE 6 (forward): v = alpha acc + bias + R -> C (f32) and C2 (bf16); per-row (mean, M2) merged
+//     pairwise at equal counts (Chan et al.), y = (v - mean) rstd gamma + beta -> ln_y (bf16);
+//     tile 0 writes mean / rstd.  Replaces residual GEMM + ln_fwd_kernel.
+//   MODE 7 (backward): dy = bf16(alpha acc) (what the unfused GEMM stored), xh = (x - mean) rstd,
+//     g = dy gamma; the row sums of g and g xh are exchanged; C = rstd (g - mean(g) - xh mean(g xh))
+//     + R, C2 = bf16(C); per 128-row block the column sums of dy xh / dy -> ln_pg / ln_pb.  Replaces
+//     the GEMM + ln_bwd_kernel pair (same arithmetic, the sums in another order).
+// LDS: the staging area of the general epilogue (buffer O and beyond) plus 10 KB of statistics.
+// ============================================================================================
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) int gi32;
+constexpr int LN_ST = p8::SMEM_P;                // [2 wr][128 rows][4 wc] float2 per-wave row values
+constexpr int LN_FIN = LN_ST + 2 * 128 * 4 * 8;  // [256 rows] float2 (mean, rstd) / (mean g, mean g xh)
+constexpr int SMEM_LN = LN_FIN + 256 * 8;
+constexpr unsigned LN_SPIN_LIMIT = 1u << 21;     // ~0.1 s of polling before giving up
+
+// merge two equal-count (mean, M2) partials; symmetric in its arguments, so the lanes / tiles of
+// a pair that merge (a, b) and (b, a) agree bit for bit
+__device__ __forceinline__ void chan(float& m, float& M2, float mb, float M2b, float half_n) {
+  const float d = m - mb;
+  M2 = (M2 + M2b) + d * d * half_n;
+  m = 0.5f * (m + mb);
+}
+
+template <int MODE>
+__device__ __forceinline__ void epilogue_ln(const P& p, f32x4 (&acc)[8][4], char* smem, int w, int wr, int wc,
+                                            int lane, int64_t m0, int64_t n0) {
+  float* cs = (float*)(smem + p8::TILEB + w * (32 * EP_LD * 4));
+  float2* st = (float2*)(smem + LN_ST);
+  float2* fin = (float2*)(smem + LN_FIN);
+  const int tx = (int)(n0 >> 8);
+  const int64_t wrow0 = m0 + wr * 128, wcol0 = n0 + wc * 64;
+  const int cc = (lane & 7) * 8, rl = lane >> 3;
+  const int64_t gn = wcol0 + cc;
+  float gam[8], bet[8];
+  {
+    const f32x4 a = *(const f32x4*)(p.ln_gamma + gn), b = *(const f32x4*)(p.ln_gamma + gn + 4);
+    f32x4 c = f32x4{0.f, 0.f, 0.f, 0.f}, d = c;
+    if (MODE == 6 && p.ln_beta) { c = *(const f32x4*)(p.ln_beta + gn); d = *(const f32x4*)(p.ln_beta + gn + 4); }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { gam[j] = a[j]; gam[4 + j] = b[j]; bet[j] = c[j]; bet[4 + j] = d[j]; }
+  }
+  f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
+  if (MODE == 6 && p.bias) { b0 = *(const f32x4*)(p.bias + gn); b1 = *(const f32x4*)(p.bias + gn + 4); }
+  float keep[4][4][8];        // MODE 6: v per quarter / row chunk
+  float pg[8], pb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { pg[j] = 0.f; pb[j] = 0.f; }
+
+#pragma unroll
+  for (int quarter = 0; quarter < 4; ++quarter) {
+    __builtin_amdgcn_sched_barrier(0);   // no hoisting of a later quarter's loads over this one
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          cs[(i * 16 + (lane >> 4) * 4 + r) * EP_LD + j * 16 + (lane & 15)] = acc[quarter * 2 + i][j][r];
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    const int64_t rbase = wrow0 + quarter * 32;
+    if constexpr (MODE == 6) {
+      f32x4 ra[4], rb[4];
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const float* Rp = (const float*)p.R + (rbase + it * 8 + rl) * p.ldr + gn;
+        ra[it] = *(const f32x4*)Rp;
+        rb[it] = *(const f32x4*)(Rp + 4);
+      }
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const f32x4 lo = *(const f32x4*)(cs + (it * 8 + rl) * EP_LD + cc);
+        const f32x4 hi = *(const f32x4*)(cs + (it * 8 + rl) * EP_LD + cc + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          keep[quarter][it][j] = lo[j] * p.alpha + b0[j] + ra[it][j];
+          keep[quarter][it][4 + j] = hi[j] * p.alpha + b1[j] + rb[it][j];
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const float* v = keep[quarter][it];
+        float* Cf = (float*)p.C + (rbase + it * 8 + rl) * p.ldc + gn;
+        *(f32x4*)Cf = f32x4{v[0], v[1], v[2], v[3]};
+        *(f32x4*)(Cf + 4) = f32x4{v[4], v[5], v[6], v[7]};
+      }
+      if (p.C2) {
+#pragma unroll
+        for (int it = 0; it < 4; ++it) *(u32x4*)(p.C2 + (rbase + it * 8 + rl) * p.ldc2 + gn) = pack8(keep[quarter][it]);
+      }
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const float* v = keep[quarter][it];
+        float m = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m += v[j];
+        m *= 0.125f;
+        float M2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { const float d = v[j] - m; M2 += d * d; }
+#pragma unroll
+        for (int o = 1; o <= 4; o <<= 1) chan(m, M2, __shfl_xor(m, o, 64), __shfl_xor(M2, o, 64), 4.f * o);
+        if ((lane & 7) == 0) st[(wr * 128 + quarter * 32 + it * 8 + rl) * 4 + wc] = make_float2(m, M2);
+      }
+    } else {
+      float mu[4], rs[4];
+      u32x4 kx[4];
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int64_t row = rbase + it * 8 + rl;
+        kx[it] = *(const u32x4*)(p.ln_x + row * p.ln_ldx + gn);
+        mu[it] = p.ln_mean[row];
+        rs[it] = p.ln_rstd[row];
+      }
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const f32x4 lo = *(const f32x4*)(cs + (it * 8 + rl) * EP_LD + cc);
+        const f32x4 hi = *(const f32x4*)(cs + (it * 8 + rl) * EP_LD + cc + 4);
+        float d[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { d[j] = lo[j] * p.alpha; d[4 + j] = hi[j] * p.alpha; }
+        const u32x4 kd = pack8(d);
+        // dy parks in C2 (the bf16 dx output, same shape): re-read by this lane in the final pass
+        // and overwritten there (registers cannot hold it across the exchange without spilling)
+        *(u32x4*)(p.C2 + (rbase + it * 8 + rl) * p.ldc2 + gn) = kd;
+        float dy[8], xv[8];
+        unpack8(kd, dy);
+        unpack8(kx[it], xv);
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = (xv[j] - mu[it]) * rs[it];
+          const float g = dy[j] * gam[j];
+          s1 += g;
+          s2 += g * xh;
+        }
+#pragma unroll
+        for (int o = 1; o <= 4; o <<= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+        if ((lane & 7) == 0) st[(wr * 128 + quarter * 32 + it * 8 + rl) * 4 + wc] = make_float2(s1, s2);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // staging reads done before the next quarter overwrites
+  }
+  __syncthreads();
+  if (wc == 0) {
+    // this tile's per-row values (rows lane, lane + 64 of the wave row) -> granules; the partner's
+    gu64* X = (gu64*)p.xchg;
+    const unsigned long long tag = (unsigned long long)p.epoch << 32;
+    float a0[2], a1[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = lane + 64 * h;
+      const float2 s0 = st[(wr * 128 + r) * 4 + 0], s1 = st[(wr * 128 + r) * 4 + 1];
+      const float2 s2 = st[(wr * 128 + r) * 4 + 2], s3 = st[(wr * 128 + r) * 4 + 3];
+      if constexpr (MODE == 6) {
+        float m = s0.x, M2 = s0.y, mm = s2.x, MM = s2.y;
+        chan(m, M2, s1.x, s1.y, 32.f);
+        chan(mm, MM, s3.x, s3.y, 32.f);
+        chan(m, M2, mm, MM, 64.f);
+        a0[h] = m;
+        a1[h] = M2;
+      } else {
+        a0[h] = (s0.x + s1.x) + (s2.x + s3.x);
+        a1[h] = (s0.y + s1.y) + (s2.y + s3.y);
+      }
+      gu64* g = X + ((int64_t)tx * p.M + wrow0 + r) * 2;
+      __hip_atomic_store(g, tag | __float_as_uint(a0[h]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(g + 1, tag | __float_as_uint(a1[h]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const gu64* Y = X + (int64_t)(1 - tx) * p.M * 2;
+    unsigned long long q[2][2];
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          q[h][k] = __hip_atomic_load(Y + (wrow0 + lane + 64 * h) * 2 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = ok && (unsigned)(q[h][k] >> 32) == p.epoch;
+        }
+      if (__all(ok)) break;
+      if (spins >= LN_SPIN_LIMIT) {
+        if (lane == 0 && p.status) __hip_atomic_store((gi32*)p.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = lane + 64 * h;
+      const float o0 = __uint_as_float((unsigned)q[h][0]), o1 = __uint_as_float((unsigned)q[h][1]);
+      float2 f;
+      if constexpr (MODE == 6) {
+        float m = a0[h], M2 = a1[h];
+        chan(m, M2, o0, o1, 128.f);
+        const float rstd = rsqrtf(M2 * (1.f / 512.f) + p.ln_eps);
+        f = make_float2(m, rstd);
+        if (tx == 0) {
+          p.ln_mean[wrow0 + r] = m;
+          p.ln_rstd[wrow0 + r] = rstd;
+        }
+      } else {
+        f = make_float2((a0[h] + o0) * (1.f / 512.f), (a1[h] + o1) * (1.f / 512.f));
+      }
+      fin[wr * 128 + r] = f;
+    }
+  }
+  __syncthreads();
+  const u16* lx = p.ln_x;
+  u16* lc2 = p.C2;
+  const float* lmean = p.ln_mean;
+  const float* lrstd = p.ln_rstd;
+  // opaque copy of this lane's row / column origin: no first-pass row address is reused (kept live)
+  int64_t frow0 = wrow0 + rl, fcol = gn;
+  asm volatile("" : "+v"(frow0), "+v"(fcol));
+#pragma unroll
+  for (int quarter = 0; quarter < 4; ++quarter) {
+    __builtin_amdgcn_sched_barrier(0);
+    const int64_t rbase = frow0 - rl + quarter * 32;
+    if constexpr (MODE == 6) {
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const float2 f = fin[wr * 128 + quarter * 32 + it * 8 + rl];
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (keep[quarter][it][j] - f.x) * f.y * gam[j] + bet[j];
+        *(u32x4*)(p.ln_y + (rbase + it * 8 + rl) * p.ln_ldy + gn) = pack8(o);
+      }
+    } else {
+      // 32-bit element offsets (the host checks M * ld < 2^31); two row chunks per step (the
+      // loads of four in flight at once pushed the kernel past 256 VGPRs into spills)
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 ra[2], rb[2];
+        float mu[2], rs[2];
+        u32x4 kx[2], kd[2];
+        const int r0 = (int)frow0 + quarter * 32 + half * 16, c0 = (int)fcol;
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          const int row = r0 + it * 8;
+          kx[it] = *(const u32x4*)(lx + (row * (int)p.ln_ldx + c0));
+          kd[it] = *(const u32x4*)(lc2 + (row * (int)p.ldc2 + c0));
+          const float* Rp = (const float*)p.R + (row * (int)p.ldr + c0);   // mode 2 requires R
+          ra[it] = *(const f32x4*)Rp;
+          rb[it] = *(const f32x4*)(Rp + 4);
+          mu[it] = lmean[row];
+          rs[it] = lrstd[row];
+        }
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          const int row = r0 + it * 8;
+          const float2 f = fin[wr * 128 + quarter * 32 + half * 16 + it * 8 + rl];
+          float dy[8], xv[8], o[8];
+          unpack8(kd[it], dy);
+          unpack8(kx[it], xv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float xh = (xv[j] - mu[it]) * rs[it];
+            pg[j] += dy[j] * xh;
+            pb[j] += dy[j];
+            o[j] = rs[it] * (dy[j] * gam[j] - f.x - xh * f.y) + (j < 4 ? ra[it][j] : rb[it][j - 4]);
+          }
+          float* Cf = (float*)p.C + (row * (int)p.ldc + c0);
+          *(f32x4*)Cf = f32x4{o[0], o[1], o[2], o[3]};
+          *(f32x4*)(Cf + 4) = f32x4{o[4], o[5], o[6], o[7]};
+          *(u32x4*)(lc2 + (row * (int)p.ldc2 + c0)) = pack8(o);
+        }
+      }
+    }
+  }
+  if constexpr (MODE == 7) {
+    // column partials of this wave's 128 rows (lanes of equal lane & 7 hold the same columns),
+    // one slab row per 128-row block
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int o = 8; o <= 32; o <<= 1) { pg[j] += __shfl_xor(pg[j], o, 64); pb[j] += __shfl_xor(pb[j], o, 64); }
+    if (rl == 0) {
+      const int64_t slab = ((m0 >> 7) + wr) * p.N + gn;
+      *(f32x4*)(p.ln_pg + slab) = f32x4{pg[0], pg[1], pg[2], pg[3]};
+      *(f32x4*)(p.ln_pg + slab + 4) = f32x4{pg[4], pg[5], pg[6], pg[7]};
+      if (p.ln_pb) {
+        *(f32x4*)(p.ln_pb + slab) = f32x4{pb[0], pb[1], pb[2], pb[3]};
+        *(f32x4*)(p.ln_pb + slab + 4) = f32x4{pb[4], pb[5], pb[6], pb[7]};
+      }
+    }
+  }
+}
+
 // TR = true: MFMA operands swapped (transposed accumulator) + the LDS-free epilogue_t, used for
 // bf16 outputs; TR = false: the LDS-staged row-chunk epilogue, used for f32 / residual / argmax
 // outputs (measured faster there: full-row f32 chunks, one argmax pass per staged quarter).
@@ -1109,6 +1420,8 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
       epilogue_t<3>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
     } else if constexpr (EP == 6) {
       epilogue_t<6>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
+    } else if constexpr (EP == -6 || EP == -7) {
+      epilogue_ln<EP == -6 ? 6 : 7>(p, acc, smem, w, wr, wc, lane, T.m0, T.n0);
     } else {
       // staging in buffer O and beyond (the next tile's tile 0 is landing in E)
       epilogue<EP == -2 || EP == -3 || EP == -5 ? EP : -1>(p, acc, smem + TILEB, w, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
@@ -1135,10 +1448,11 @@ static int g_grid_cap = 0;
 
 template <bool AK, bool BKC, int EP>
 int launch8(const P& p, int batch, hipStream_t st) {
+  constexpr int smem = EP == -6 || EP == -7 ? SMEM_LN : p8::SMEM_P;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm8p_kernel<AK, BKC, EP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              p8::SMEM_P);
+                              smem);
     attr = true;
   }
   const int64_t ntiles = cdiv(p.N, p8::BNN) * cdiv(p.M, p8::BM) * (int64_t)p.gz;
@@ -1151,10 +1465,10 @@ int launch8(const P& p, int batch, hipStream_t st) {
   if (p.persist) {
     const int64_t cap = g_grid_cap > 0 && g_grid_cap < 256 ? g_grid_cap : 256;
     dim3 grid((unsigned)(ntiles < cap ? ntiles : cap));
-    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP>), grid, dim3(p8::NTH), p8::SMEM_P, st, p);
+    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP>), grid, dim3(p8::NTH), smem, st, p);
   } else {
     dim3 grid(cdiv(p.N, p8::BNN), cdiv(p.M, p8::BM), batch * p.split_k);
-    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP>), grid, dim3(p8::NTH), p8::SMEM_P, st, p);
+    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP>), grid, dim3(p8::NTH), smem, st, p);
   }
   CT_CHECK_LAUNCH();
   return 0;
@@ -1273,6 +1587,65 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
     return a->a_kcontig ? launch8_any<true>(p, a->b_kcontig, batch, st) : launch8_any<false>(p, a->b_kcontig, batch, st);
   if (tile_rows() == 2) return launch_any<2>(p, a->a_kcontig, a->b_kcontig, batch, st);
   return launch_any<1>(p, a->a_kcontig, a->b_kcontig, batch, st);
+}
+
+// LayerNorm-fused N = 512 GEMM (include/ctclip_hip.h).  The pair exchange needs the persistent
+// 8-phase walk on its full grid with ntiles % 16 == 0 (tile_at pairs tiles 2k, 2k + 1 on
+// workgroups w, w ^ 8 of one round); anything else is refused (CT_EINVAL) and the caller runs the
+// GEMM and the LayerNorm kernel separately.
+extern "C" int ctclip_gemm_ln(const ctclip_gemm_args* a, const ctclip_ln_epilogue* ln, void* stream) {
+  using namespace g256;
+  if (!a || !ln || (ln->mode != 1 && ln->mode != 2)) return CT_EINVAL;
+  if (a->M == 0) return 0;
+  CT_REQUIRE(a->N == 512 && a->M > 0 && a->M % 2048 == 0 && a->K > 0 && a->K % 64 == 0, CT_ESHAPE);
+  CT_REQUIRE(a->split_k <= 1 && a->batch <= 1 && a->act == 0 && !a->accumulate && a->c_f32 && !a->B2, CT_EINVAL);
+  CT_REQUIRE(variant() == 8 && g_persist != 0 && g_grid_cap == 0, CT_EINVAL);
+  CT_REQUIRE(aligned16(a->A) && aligned16(a->B) && aligned16(a->C) && a->lda % 8 == 0 && a->ldb % 8 == 0 &&
+                 a->ldc % 8 == 0, CT_EALIGN);
+  if (a->C2) CT_REQUIRE(aligned16(a->C2) && a->ldc2 % 8 == 0, CT_EALIGN);
+  if (a->R) CT_REQUIRE(a->r_f32 && aligned16(a->R) && a->ldr % 8 == 0, CT_EINVAL);
+  if (a->bias) CT_REQUIRE(ln->mode == 1 && aligned16(a->bias), CT_EINVAL);
+  CT_REQUIRE(ln->gamma && aligned16(ln->gamma) && ln->mean && ln->rstd && ln->xchg && ln->epoch != 0 &&
+                 (((uintptr_t)ln->xchg) & 7) == 0, CT_EINVAL);
+  {
+    const int64_t ldmax = std::max(std::max(a->ldc, a->ldc2), std::max(a->ldr, ln->ldx));
+    CT_REQUIRE(a->M * ldmax < ((int64_t)1 << 31), CT_ESHAPE);   // 32-bit element offsets (mode 2)
+  }
+  if (ln->mode == 1) {
+    CT_REQUIRE(a->R && ln->Y && aligned16(ln->Y) && ln->ldy % 8 == 0, CT_EINVAL);
+    if (ln->beta) CT_REQUIRE(aligned16(ln->beta), CT_EALIGN);
+  } else {
+    CT_REQUIRE(ln->X && aligned16(ln->X) && ln->ldx % 8 == 0 && ln->part_gamma && !ln->beta && a->C2 && a->R,
+               CT_EINVAL);
+  }
+  P p;
+  memset(&p, 0, sizeof(p));
+  p.M = a->M; p.N = a->N; p.K = a->K;
+  p.A = (const u16*)a->A; p.lda = a->lda;
+  p.B = (const u16*)a->B; p.ldb = a->ldb;
+  p.C = a->C; p.ldc = a->ldc; p.c_f32 = 1;
+  p.C2 = (u16*)a->C2; p.ldc2 = a->ldc2;
+  p.bias = a->bias;
+  p.R = a->R; p.ldr = a->ldr; p.r_f32 = 1;
+  p.alpha = a->alpha; p.act = 0; p.accumulate = 0; p.split_k = 1;
+  p.kper = a->K;
+  p.debug = 0;
+  p.group_gx = 1 << 30;   // plain row-major tile order: the pairing above relies on it
+  p.stagger = 0;
+  p.gz = 1;
+  p.persist = 1;
+  p.ln_gamma = ln->gamma; p.ln_beta = ln->beta; p.ln_eps = ln->eps;
+  p.ln_y = (u16*)ln->Y; p.ln_ldy = ln->ldy;
+  p.ln_mean = ln->mean; p.ln_rstd = ln->rstd;
+  p.ln_x = (const u16*)ln->X; p.ln_ldx = ln->ldx;
+  p.ln_pg = ln->part_gamma; p.ln_pb = ln->part_beta;
+  p.xchg = (unsigned long long*)ln->xchg;
+  p.epoch = ln->epoch;
+  p.status = ln->status;
+  hipStream_t st = (hipStream_t)stream;
+  if (!a->a_kcontig) return CT_EINVAL;
+  if (ln->mode == 1) return a->b_kcontig ? launch8<true, true, -6>(p, 1, st) : launch8<true, false, -6>(p, 1, st);
+  return a->b_kcontig ? launch8<true, true, -7>(p, 1, st) : launch8<true, false, -7>(p, 1, st);
 }
 
 // diagnostic: 8-phase kernel start stagger (see gemm8p_kernel); returns the previous value

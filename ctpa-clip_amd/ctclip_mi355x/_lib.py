@@ -47,6 +47,20 @@ class GemmArgs(ctypes.Structure):
     ]
 
 
+class LnEpilogueArgs(ctypes.Structure):
+    """ctclip_ln_epilogue (include/ctclip_hip.h): LayerNorm fused into an N = 512 GEMM."""
+    _fields_ = [
+        ('mode', c_i32),
+        ('gamma', c_vp), ('beta', c_vp), ('eps', c_f32),
+        ('Y', c_vp), ('ldy', c_i64),
+        ('mean', c_vp), ('rstd', c_vp),
+        ('X', c_vp), ('ldx', c_i64),
+        ('part_gamma', c_vp), ('part_beta', c_vp),
+        ('xchg', c_vp), ('epoch', ctypes.c_uint32),
+        ('status', c_vp),
+    ]
+
+
 class MxGemmArgs(ctypes.Structure):
     _fields_ = [
         ('M', c_i64), ('N', c_i64), ('Kp', c_i64),
@@ -90,6 +104,7 @@ _SIGS = {
     'ctclip_version': [],
     'ctclip_device_arch': [ctypes.c_char_p, c_i32],
     'ctclip_gemm': [ctypes.POINTER(GemmArgs), c_vp],
+    'ctclip_gemm_ln': [ctypes.POINTER(GemmArgs), ctypes.POINTER(LnEpilogueArgs), c_vp],
     'ctclip_quant_mxfp8': [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp],
     'ctclip_gemm_mxfp8': [ctypes.POINTER(MxGemmArgs), c_vp],
     'ctclip_gemm_mxfp8_set_tile': [c_i32],

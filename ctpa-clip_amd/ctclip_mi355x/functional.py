@@ -412,12 +412,17 @@ class ViTLayerFn(torch.autograd.Function):
         use_bias = bias_u is not None
         o, lse = K.attn_fwd(qn, kn, kv[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
                             bias_u=bias_u if use_bias else None, grid=(geo.Hg, geo.Wg) if use_bias else (0, 0))
-        x2b = torch.empty_like(xb)
-        if fp8:
-            x2f = fp8_linear(o, Wo, 'o', Wo_b, residual=x1f, out_f32=True, out2=x2b)
+        fused = None if fp8 else K.linear_residual_ln(o, Wo_b, x1f, ff_w, ff_b, 1e-5)
+        if fused is not None:
+            # to_out + residual + the FeedForward's LayerNorm in one launch (gemm256.hip, EP -6)
+            x2f, x2b, xn2, m2, r2 = fused
         else:
-            x2f = K.linear(o, Wo_b, residual=x1f, out_dtype=F32, out2=x2b)
-        xn2, _, m2, r2 = K.layernorm_fwd(x2f, ff_w, ff_b, 1e-5)
+            x2b = torch.empty_like(xb)
+            if fp8:
+                x2f = fp8_linear(o, Wo, 'o', Wo_b, residual=x1f, out_f32=True, out2=x2b)
+            else:
+                x2f = K.linear(o, Wo_b, residual=x1f, out_dtype=F32, out2=x2b)
+            xn2, _, m2, r2 = K.layernorm_fwd(x2f, ff_w, ff_b, 1e-5)
         W1p, W2p = pack_ff1(W1), pack_ff2(W2)
         g = torch.empty(xf.shape[0], W2p.shape[1], device=xf.device, dtype=BF16)
         x3b = torch.empty_like(xb)
@@ -454,10 +459,16 @@ class ViTLayerFn(torch.autograd.Function):
         dh_ = K.matmul_nn_geglu_bwd(dx3b, W2p, h)      # dg = dx3 . W2 and the GEGLU backward, fused
         M_ = dx3b.shape[0]
         dW2p = K.matmul_tn(dx3b, g, tag='dw', flops=2.0 * M_ * W2.shape[0] * W2.shape[1])
-        dxn2 = K.matmul_nn(dh_, W1p)
+        # dx2 = LN'(dh . W1) + dx3 in one launch where the shape allows (gemm256.hip, EP -7)
+        fused = K.matmul_nn_ln_bwd(dh_, W1p, x2b, m2, r2, ff_w, dx3f, dgamma_out=gsink(ff_w), dbeta_out=gsink(ff_b))
+        if fused is None:
+            dxn2 = K.matmul_nn(dh_, W1p)
         dW1p = K.matmul_tn(dh_, xn2, tag='dw', flops=2.0 * M_ * W1.shape[0] * W1.shape[1])
-        dx2f, dx2b, _, _ = K.layernorm_bwd(dxn2, x2b, m2, r2, ff_w, dres=dx3f, dgamma_out=gsink(ff_w),
-                                           dbeta_out=gsink(ff_b))
+        if fused is not None:
+            dx2f, dx2b = fused
+        else:
+            dx2f, dx2b, _, _ = K.layernorm_bwd(dxn2, x2b, m2, r2, ff_w, dres=dx3f, dgamma_out=gsink(ff_w),
+                                               dbeta_out=gsink(ff_b))
         K.unpack_rows(dW1p, gsink(W1), rowmap=ff1_rowmap(W1.shape[0] // 2, dev), accumulate=True)
         K.unpack_rows(dW2p, gsink(W2), cols=W2.shape[1], accumulate=True)
         # attention
@@ -474,12 +485,22 @@ class ViTLayerFn(torch.autograd.Function):
         dq = torch.empty_like(q)
         K.l2norm_scale_bwd(q, dqn, H, dh, q_scale, dq, ds_out=gsink(q_scale))
         K.l2norm_scale_bwd(kv[:, :inner], dkn, H, dh, k_scale, dkv[:, :inner], ds_out=gsink(k_scale))
-        dxn = K.matmul_nn(dq, Wq_b)
+        fusable = K.ln_fusable(dq.shape[0], Wq_b.shape[1], bwd=True)
+        if not fusable:
+            dxn = K.matmul_nn(dq, Wq_b)
         K.matmul_tn(dq, xn, out=gsink(Wq), accumulate=True, tag='dw')
         K.matmul_tn(dkv, x1b, out=gsink(Wkv), accumulate=True, tag='dw')
         dx1kv = K.matmul_nn(dkv, Wkv_b, residual=dx2f, out_dtype=F32)
-        dx1f, dx1b, _, _ = K.layernorm_bwd(dxn, x1b, m1, r1, norm_g, dres=dx1kv, want_beta=False,
-                                           dgamma_out=gsink(norm_g))
+        # dx1 = LN'(dq . Wq) + (dkv . Wkv + dx2) in one launch where the shape allows (EP -7)
+        fused = K.matmul_nn_ln_bwd(dq, Wq_b, x1b, m1, r1, norm_g, dx1kv, dgamma_out=gsink(norm_g)) \
+            if fusable else None
+        if fused is not None:
+            dx1f, dx1b = fused
+        else:
+            if fusable:
+                dxn = K.matmul_nn(dq, Wq_b)
+            dx1f, dx1b, _, _ = K.layernorm_bwd(dxn, x1b, m1, r1, norm_g, dres=dx1kv, want_beta=False,
+                                               dgamma_out=gsink(norm_g))
         # PEG
         dxf, dxb, dpw, dpb = K.peg_bwd(dx1b, dx1f, xb, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, geo.mode)
         put_shadow(dxf, dxb)

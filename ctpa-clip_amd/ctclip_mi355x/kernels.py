@@ -7,7 +7,7 @@ import os
 import torch
 
 from . import _lib
-from ._lib import GemmArgs, call, ptr, stream_ptr
+from ._lib import GemmArgs, LnEpilogueArgs, call, ptr, stream_ptr
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -144,6 +144,124 @@ def matmul_nn(dy, w, *, out=None, out_dtype=BF16, residual=None, accumulate=Fals
     gemm_raw(M, K, N, dy, dy.stride(0), True, w, w.stride(0), False, out, out.stride(0), R=residual,
              ldr=residual.stride(0) if residual is not None else 0, accumulate=accumulate, alpha=alpha)
     return out
+
+
+# ------------------------------------------- LayerNorm fused into N = 512 GEMM epilogues
+# ctclip_gemm_ln: the two 256-column tiles of a row block exchange per-row statistics inside the
+# launch through a per-stream buffer of {epoch, value} granules (zeroed once; every launch uses a
+# fresh epoch, so nothing needs clearing between launches).  CTCLIP_LN_FUSED=0: the GEMM and the
+# LayerNorm kernel run separately (A/B switch).
+LN_FUSED = os.environ.get('CTCLIP_LN_FUSED', '1') != '0'
+# the backward form (GEMM + LayerNorm backward + residual) measured SLOWER than the pair it
+# replaces (profiles/r03o_ln_bench.log: 510 vs 476 us at K = 2,816, 265 vs 226 us at K = 256; the
+# stand-alone LayerNorm backward streams at ~6 TB/s, the fused epilogue at 8 waves per CU does not),
+# so it is opt-in; the forward form is the default (171 vs 192 us)
+LN_FUSED_BWD = os.environ.get('CTCLIP_LN_FUSED_BWD', '0') != '0'
+_XCHG = {}       # (device, stream) -> [int64 buffer, last epoch]
+_LN_STATUS = {}  # device -> int32[1], set by a launch whose partner statistics never arrived
+_CT_EINVAL, _CT_ESHAPE = 1001, 1003
+
+
+def _xchg(M, device):
+    st = torch.cuda.current_stream(device)
+    key = (device.index, st.cuda_stream)
+    e = _XCHG.get(key)
+    if e is None or e[0].numel() < 4 * M:
+        e = _XCHG[key] = [torch.zeros(4 * M, dtype=torch.int64, device=device), 0]
+    if e[1] >= 0xFFFFFFFF:        # epochs exhausted: clear the granules (stream-ordered) and restart
+        e[0].zero_()
+        e[1] = 0
+    e[1] += 1
+    return e[0], e[1]
+
+
+def _ln_status(device):
+    s = _LN_STATUS.get(device.index)
+    if s is None:
+        s = _LN_STATUS[device.index] = torch.zeros(1, dtype=torch.int32, device=device)
+    return s
+
+
+def ln_fused_status(device=None):
+    """1 if any LayerNorm-fused GEMM on `device` gave up waiting for its partner tile (then its
+    outputs are wrong); 0 otherwise.  Synchronises."""
+    s = _LN_STATUS.get((device or torch.device('cuda', torch.cuda.current_device())).index)
+    return 0 if s is None else int(s.item())
+
+
+def ln_fusable(M, N, bwd=False):
+    return LN_FUSED and (LN_FUSED_BWD or not bwd) and N == 512 and M > 0 and M % 2048 == 0
+
+
+def _gemm_ln(M, K, A, B, b_kcontig, C, C2, R, ln, tag=None, flops=None):
+    """Returns False (nothing launched) when the library refuses the configuration."""
+    a = GemmArgs()
+    a.M, a.N, a.K = M, 512, K
+    a.A, a.lda, a.a_kcontig = ptr(A), A.stride(0), 1
+    a.B, a.ldb, a.b_kcontig = ptr(B), B.stride(0), int(b_kcontig)
+    a.C, a.ldc, a.c_f32 = ptr(C), C.stride(0), 1
+    a.C2, a.ldc2 = ptr(C2), C2.stride(0) if C2 is not None else 0
+    a.R, a.ldr, a.r_f32 = ptr(R), R.stride(0) if R is not None else 0, 1
+    a.alpha, a.act, a.accumulate, a.split_k, a.batch = 1.0, 0, 0, 1, 1
+    xb, ep = _xchg(M, A.device)
+    ln.xchg, ln.epoch = ptr(xb), ep
+    ln.status = ptr(_ln_status(A.device))
+    end = TIMER(tag, flops if flops is not None else 2.0 * M * 512 * K) if tag else None
+    rc = _lib.lib().ctclip_gemm_ln(_lib.ctypes.byref(a), _lib.ctypes.byref(ln), stream_ptr())
+    if rc in (_CT_EINVAL, _CT_ESHAPE):
+        return False
+    if rc != 0:
+        raise _lib.KernelError(f'ctclip_gemm_ln failed: {rc}')
+    if end is not None:
+        end.record()
+    return True
+
+
+def linear_residual_ln(x, w, residual, gamma, beta, eps, *, tag=None):
+    """x1 = residual + x @ w^T (w [512, K] nn.Linear weight) and y = LayerNorm(x1) (gamma, beta;
+    bf16) in ONE launch (ctclip_gemm_ln mode 1).  Returns (x1 f32, x1 bf16, y bf16, mean, rstd),
+    or None when the shape / configuration does not allow the fused form."""
+    M, K = x.shape
+    if not ln_fusable(M, w.shape[0]) or K % 64 or residual.dtype != F32:
+        return None
+    dev = x.device
+    x1f = torch.empty(M, 512, device=dev, dtype=F32)
+    x1b = torch.empty(M, 512, device=dev, dtype=BF16)
+    y = torch.empty(M, 512, device=dev, dtype=BF16)
+    mean = torch.empty(M, device=dev, dtype=F32)
+    rstd = torch.empty(M, device=dev, dtype=F32)
+    ln = LnEpilogueArgs()
+    ln.mode, ln.gamma, ln.beta, ln.eps = 1, ptr(gamma), ptr(beta), eps
+    ln.Y, ln.ldy, ln.mean, ln.rstd = ptr(y), 512, ptr(mean), ptr(rstd)
+    if not _gemm_ln(M, K, x, w, True, x1f, x1b, residual, ln, tag=tag):
+        return None
+    return x1f, x1b, y, mean, rstd
+
+
+def matmul_nn_ln_bwd(dy, w, x, mean, rstd, gamma, dres, *, dgamma_out, dbeta_out=None):
+    """dx = LayerNorm'(dy @ w) + dres in ONE launch (ctclip_gemm_ln mode 2): dy [M, N] bf16,
+    w [N, 512] (the nn.Linear weight whose input was LayerNorm(x)), x [M, 512] bf16 with the
+    forward's mean / rstd; the gamma / beta gradients accumulate into dgamma_out / dbeta_out
+    (deferred partial reductions).  Returns (dx f32, dx bf16), or None when not fusable."""
+    M, N = dy.shape
+    if not (LN_FUSED_BWD and ln_fusable(M, w.shape[1])) or N % 64 or dres is None or dres.dtype != F32:
+        return None
+    dev = dy.device
+    dxf = torch.empty(M, 512, device=dev, dtype=F32)
+    dxb = torch.empty(M, 512, device=dev, dtype=BF16)
+    nb = M // 128
+    pg = torch.empty(nb, 512, device=dev, dtype=F32)
+    pb = torch.empty(nb, 512, device=dev, dtype=F32) if dbeta_out is not None else None
+    ln = LnEpilogueArgs()
+    ln.mode, ln.gamma, ln.beta, ln.eps = 2, ptr(gamma), None, 0.0
+    ln.mean, ln.rstd, ln.X, ln.ldx = ptr(mean), ptr(rstd), ptr(x), x.stride(0)
+    ln.part_gamma, ln.part_beta = ptr(pg), ptr(pb)
+    if not _gemm_ln(M, N, dy, w, False, dxf, dxb, dres, ln):
+        return None
+    reduce_param_partials(pg, dgamma_out, True)
+    if dbeta_out is not None:
+        reduce_param_partials(pb, dbeta_out, True)
+    return dxf, dxb
 
 
 def split_for(m_rows, tiles):

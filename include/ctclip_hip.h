@@ -78,6 +78,36 @@ int ctclip_gemm_set_persist(int on);
  * Two GEMMs on two streams, each capped, share the chip.  Returns the previous cap. */
 int ctclip_gemm_set_grid_cap(int workgroups);
 
+/* LayerNorm fused into the epilogue of an N = 512 GEMM (the 3D-ViT's d = 512 token rows).  The
+ * two 256-column tiles of a row block exchange per-row partial statistics inside the launch.
+ * a: the GEMM (A K-contiguous, alpha, C f32 [M][512], optional bf16 copy C2, optional f32
+ * residual R, optional bias in mode 1); act 0, no split-K / batch / accumulate / B2.
+ *   mode 1, forward (replaces Linear + residual + LayerNorm: the to_out / FeedForward residual of
+ *     ct_clip/attention.py:324-326 feeding the next LayerNorm, attention.py:28-35,47):
+ *       C = alpha A.B (+ bias) + R;  Y = (C - mean) * rstd * gamma (+ beta) in bf16;
+ *       mean / rstd [M] written (f32, eps as given).
+ *   mode 2, backward (replaces the dX GEMM + ctclip_layernorm_bwd): dy = bf16(alpha A.B) is the
+ *       gradient of LN(X) (X bf16, mean / rstd from the forward); C = LN'(dy) + R, C2 = bf16(C)
+ *       (R and C2 required); part_gamma (required) / part_beta (optional) [M / 128][512]: per
+ *       128-row block column sums of
+ *       dy * xhat and dy (reduce with ctclip_reduce_slabs).  beta must be NULL.
+ * Requires M % 2048 == 0, N == 512, K % 64 == 0, the default 8-phase persistent GEMM (no grid cap);
+ * otherwise CT_EINVAL / CT_ESHAPE and nothing runs (call the two kernels instead).
+ * xchg: >= 4 * M u64 words, zeroed once when allocated; epoch: nonzero and different from every
+ * earlier launch on that buffer; launches sharing one xchg buffer must be stream-ordered.
+ * status (optional): set to 1 if a partner tile's statistics never arrived (bounded wait). */
+typedef struct {
+  int32_t mode;
+  const float* gamma; const float* beta; float eps;
+  void* Y; int64_t ldy;
+  float* mean; float* rstd;
+  const void* X; int64_t ldx;
+  float* part_gamma; float* part_beta;
+  void* xchg; uint32_t epoch;
+  int32_t* status;
+} ctclip_ln_epilogue;
+int ctclip_gemm_ln(const ctclip_gemm_args* a, const ctclip_ln_epilogue* ln, void* stream);
+
 /* sum f32 slabs [s][rows][ld] -> out (f32 or bf16), optional accumulate into f32 out */
 int ctclip_reduce_slabs(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,
                         void* out, int64_t ldo, int32_t out_f32, int32_t accumulate, void* stream);
