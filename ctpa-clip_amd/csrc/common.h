@@ -141,3 +141,16 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 static inline bool aligned16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
+
+// Hidden-state dropout keep factor of the BERT text tower (ctclip_dropout and the kernels it is
+// fused into): element i (flat index of a contiguous [rows][D] tensor) is kept iff the splitmix64
+// finaliser of seed ^ i*phi is >= thresh = p * 2^32; returns scale = 1 / (1 - p) or 0.
+__device__ __forceinline__ float hid_keep(uint64_t seed, int64_t i, unsigned thresh, float scale) {
+  uint64_t x = seed ^ ((uint64_t)i * 0x9E3779B97F4A7C15ull);
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (unsigned)x >= thresh ? scale : 0.f;
+}

@@ -185,16 +185,6 @@ extern "C" int ctclip_gelu_f32(const float* x, float* y, int64_t n, void* stream
 // (+ res), element i kept iff its splitmix64 hash >= p * 2^32.  The backward is the same call on
 // the gradient with the same seed (res = null).
 namespace {
-__device__ __forceinline__ float hid_keep(uint64_t seed, int64_t i, unsigned thresh, float scale) {
-  uint64_t x = seed ^ ((uint64_t)i * 0x9E3779B97F4A7C15ull);
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdull;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ull;
-  x ^= x >> 33;
-  return (unsigned)x >= thresh ? scale : 0.f;
-}
-
 __global__ __launch_bounds__(256) void dropout_kernel(const float* __restrict__ x, const float* __restrict__ res,
                                                       float* __restrict__ yf, u16* __restrict__ yb, int64_t n4,
                                                       unsigned thresh, float scale, uint64_t seed) {

@@ -257,7 +257,14 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] += p.bias[gn + j];
     }
-    if (p.R) {
+    if (p.act == 6) {
+      // GELU backward: C = acc * gelu'(R) with R the bf16 pre-activation (the act-1 C2), replacing
+      // a bf16 dX GEMM + ctclip_gelu_bwd (one rounding fewer: acc is not rounded to bf16 first)
+      float rr[8];
+      unpack8(*(const u32x4*)((const u16*)p.R + bidx * p.sR + gm * p.ldr + gn), rr);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= gelu_erf_grad(rr[j]);
+    } else if (p.R) {
       if (p.r_f32) {
         const float* Rp = (const float*)p.R + bidx * p.sR + gm * p.ldr + gn;
         const f32x4 a = *(const f32x4*)Rp, b = *(const f32x4*)(Rp + 4);
@@ -388,7 +395,9 @@ __global__ __launch_bounds__(1024) void reduce_slabs_skinny_kernel(const float* 
 // consecutive columns of one row.  Lets skinny GEMMs (M = 1024 text-tower tokens) split K over
 // 4-6x more workgroups than they have output tiles.
 __global__ __launch_bounds__(256) void reduce_slabs_ep_kernel(const float* __restrict__ s, int64_t nslab,
-                                                              int64_t rows, int64_t cols, int64_t ld, P p) {
+                                                              int64_t rows, int64_t cols, int64_t ld, P p,
+                                                              unsigned thresh = 0u, float dscale = 1.f,
+                                                              uint64_t seed = 0, int drop = 0) {
   const int64_t n8 = cols / 8;
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= rows * n8) return;
@@ -404,6 +413,10 @@ __global__ __launch_bounds__(256) void reduce_slabs_ep_kernel(const float* __res
     const f32x4 a = *(const f32x4*)(p.bias + c), b = *(const f32x4*)(p.bias + c + 4);
 #pragma unroll
     for (int j = 0; j < 4; ++j) { v[j] += a[j]; v[4 + j] += b[j]; }
+  }
+  if (drop) {   // BERT hidden dropout of the dense output, before the residual (ctclip_dropout's mask)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= hid_keep(seed, r * cols + c + j, thresh, dscale);
   }
   if (p.R) {
     if (p.r_f32) {
@@ -467,12 +480,14 @@ extern "C" int ctclip_gemm(const ctclip_gemm_args* a, void* stream) {
   }
   if (a->act == 2) CT_REQUIRE(a->N % 64 == 0 && a->ldc2 % 8 == 0, CT_ESHAPE);
   if (a->act == 4) CT_REQUIRE(a->N % 32 == 0 && a->R && !a->r_f32 && !a->c_f32 && a->split_k <= 1, CT_EINVAL);
+  if (a->act == 6)
+    CT_REQUIRE(a->R && !a->r_f32 && !a->bias && !a->accumulate && !a->C2 && split == 1 && (a->batch <= 1), CT_EINVAL);
   if (a->act == 5)
     CT_REQUIRE(a->C2 && a->bias && aligned16(a->bias) && !a->R && !a->c_f32 && !a->accumulate && split == 1 &&
                    (a->batch <= 1) && a->N % 64 == 0 && a->n2 > 0 && a->n2 % 64 == 0 && a->n2 <= a->N,
                CT_EINVAL);
   if (a->B2) CT_REQUIRE(aligned16(a->B2) && a->act != 3, CT_EINVAL);
-  if (!a->B2) {
+  if (!a->B2 && a->act != 6) {   // act 6 (GELU backward): the 128-tile kernel only (text tower)
     const int b = a->batch > 0 ? a->batch : 1;
     const int64_t tiles256 = ((a->M + 255) / 256) * ((a->N + 255) / 256) * split * b;
     if (a->K % 64 == 0 && a->M >= 256 && a->N >= 256 && tiles256 >= 160 && (split == 1 || (a->K / split) >= 512) &&
@@ -535,6 +550,30 @@ extern "C" int ctclip_reduce_slabs_ep(const float* slabs, int64_t nslab, int64_t
   const int64_t total = rows * (cols / 8);
   hipLaunchKernelGGL(reduce_slabs_ep_kernel, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream, slabs, nslab,
                      rows, cols, ld, p);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+// the same with BERT's hidden dropout on (sum + bias) before the residual: C = drop(sum + bias) + R
+// (the mask of ctclip_dropout on a contiguous [rows][cols] tensor; requires ldc == cols)
+extern "C" int ctclip_reduce_slabs_ep_drop(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,
+                                           const ctclip_gemm_args* a, float dp, uint64_t seed, void* stream) {
+  if (rows == 0 || cols == 0) return 0;
+  CT_REQUIRE(a && a->act == 0 && !a->accumulate && a->ldc == cols && dp >= 0.f && dp < 1.f, CT_EINVAL);
+  CT_REQUIRE(cols % 8 == 0 && ld % 4 == 0 && aligned16(slabs) && aligned16(a->C), CT_EALIGN);
+  if (a->bias) CT_REQUIRE(aligned16(a->bias), CT_EALIGN);
+  if (a->R) CT_REQUIRE(aligned16(a->R) && a->ldr % 8 == 0, CT_EALIGN);
+  if (a->C2) CT_REQUIRE(aligned16(a->C2) && a->ldc2 % 8 == 0, CT_EALIGN);
+  P p{};
+  p.C = a->C; p.ldc = a->ldc; p.c_f32 = a->c_f32;
+  p.C2 = (u16*)a->C2; p.ldc2 = a->ldc2;
+  p.bias = a->bias;
+  p.R = a->R; p.ldr = a->ldr; p.r_f32 = a->r_f32;
+  p.act = 0; p.accumulate = 0;
+  const unsigned thresh = (unsigned)std::min(4294967295.0, (double)dp * 4294967296.0);
+  const int64_t total = rows * (cols / 8);
+  hipLaunchKernelGGL(reduce_slabs_ep_kernel, dim3(cdiv(total, 256)), dim3(256), 0, (hipStream_t)stream, slabs, nslab,
+                     rows, cols, ld, p, thresh, 1.f / (1.f - dp), seed, 1);
   CT_CHECK_LAUNCH();
   return 0;
 }

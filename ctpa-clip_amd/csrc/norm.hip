@@ -131,7 +131,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
 }
 
 // dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)) [+ dres];  dgamma/dbeta partials.
-template <int CPL, bool DYF, bool XF>
+// DROP (BERT's hidden dropout fused): the bf16 output is bf16(dx * keep(seed, row * D + col)) --
+// the gradient of the dense branch of LN(dropout(dense) + residual), the f32 output the residual
+// branch's -- and part_d gets per-block column sums of that bf16 output (the dense bias gradient).
+template <int CPL, bool DYF, bool XF, bool DROP = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy, int64_t lddy,
                                                      const void* __restrict__ x, int64_t ldx,
                                                      const float* __restrict__ mean_in,
@@ -139,16 +142,18 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
                                                      int64_t rows, int D, const float* __restrict__ dres,
                                                      int64_t lddres, float* __restrict__ dxf, int64_t lddxf,
                                                      u16* __restrict__ dxb, int64_t lddxb,
-                                                     float* __restrict__ part_g, float* __restrict__ part_b) {
-  __shared__ float red[4][2][CPL * 512];
+                                                     float* __restrict__ part_g, float* __restrict__ part_b,
+                                                     unsigned thresh = 0u, float dscale = 1.f, uint64_t seed = 0,
+                                                     float* __restrict__ part_d = nullptr) {
+  __shared__ float red[4][DROP ? 3 : 2][CPL * 512];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float gv[CPL][8];
   load_param<CPL>(gamma, D, lane, 1.f, gv);
-  float ag[CPL][8], ab[CPL][8];
+  float ag[CPL][8], ab[CPL][8], ad[CPL][8];
 #pragma unroll
   for (int c = 0; c < CPL; ++c)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { ag[c][j] = 0.f; ab[c][j] = 0.f; }
+    for (int j = 0; j < 8; ++j) { ag[c][j] = 0.f; ab[c][j] = 0.f; ad[c][j] = 0.f; }
   const float invD = 1.f / D;
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < rows; row += nw) {
@@ -191,7 +196,18 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
         *(f32x4*)p = f32x4{o[0], o[1], o[2], o[3]};
         *(f32x4*)(p + 4) = f32x4{o[4], o[5], o[6], o[7]};
       }
-      if (dxb) *(u32x4*)(dxb + row * lddxb + col) = pack8(o);
+      if constexpr (DROP) {
+        float m[8], mb[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) m[j] = o[j] * hid_keep(seed, row * D + col + j, thresh, dscale);
+        const u32x4 pk = pack8(m);
+        *(u32x4*)(dxb + row * lddxb + col) = pk;
+        unpack8(pk, mb);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ad[c][j] += mb[j];
+      } else {
+        if (dxb) *(u32x4*)(dxb + row * lddxb + col) = pack8(o);
+      }
     }
   }
   if (!part_g) return;
@@ -201,11 +217,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const void* __restrict__ dy
     for (int j = 0; j < 8; ++j) {
       red[w][0][(c * 64 + lane) * 8 + j] = ag[c][j];
       red[w][1][(c * 64 + lane) * 8 + j] = ab[c][j];
+      if constexpr (DROP) red[w][2][(c * 64 + lane) * 8 + j] = ad[c][j];
     }
   __syncthreads();
   for (int i = threadIdx.x; i < D; i += 256) {
     part_g[(int64_t)blockIdx.x * D + i] = red[0][0][i] + red[1][0][i] + red[2][0][i] + red[3][0][i];
     if (part_b) part_b[(int64_t)blockIdx.x * D + i] = red[0][1][i] + red[1][1][i] + red[2][1][i] + red[3][1][i];
+    if constexpr (DROP) {
+      if (part_d) part_d[(int64_t)blockIdx.x * D + i] = red[0][2][i] + red[1][2][i] + red[2][2][i] + red[3][2][i];
+    }
   }
 }
 
@@ -403,6 +423,23 @@ extern "C" int ctclip_layernorm_bwd(const void* dy, int32_t dy_f32, int64_t lddy
                      lddxf, (u16*)dx_bf16, lddxb, part_gamma, part_beta);
   else
     return CT_ESHAPE;  // D > 1024 not needed on the backward path (patch LN uses the folded-weight trick)
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+// LayerNorm backward with BERT's hidden dropout fused (include/ctclip_hip.h)
+extern "C" int ctclip_layernorm_bwd_drop(const void* dy, int32_t dy_f32, int64_t lddy, const void* x, int32_t x_f32,
+                                         int64_t ldx, const float* mean, const float* rstd, const float* gamma,
+                                         int64_t rows, int32_t D, float* dx_f32, int64_t lddxf, void* dx_bf16,
+                                         int64_t lddxb, float* part_gamma, float* part_beta, float* part_drop,
+                                         int32_t nblocks, float p, uint64_t seed, void* stream) {
+  if (rows == 0) return 0;
+  CT_REQUIRE(D % 8 == 0 && ln_cpl(D) == 2 && dy_f32 && x_f32 && dx_bf16 && part_gamma, CT_EINVAL);
+  CT_REQUIRE(p >= 0.f && p < 1.f, CT_EINVAL);
+  const unsigned thresh = (unsigned)std::min(4294967295.0, (double)p * 4294967296.0);
+  hipLaunchKernelGGL((ln_bwd_kernel<2, true, true, true>), dim3(nblocks), dim3(256), 0, (hipStream_t)stream, dy,
+                     lddy, x, ldx, mean, rstd, gamma, rows, D, (const float*)nullptr, (int64_t)0, dx_f32, lddxf,
+                     (u16*)dx_bf16, lddxb, part_gamma, part_beta, thresh, 1.f / (1.f - p), seed, part_drop);
   CT_CHECK_LAUNCH();
   return 0;
 }

@@ -114,6 +114,10 @@ _SIGS = {
     'ctclip_gemm_set_persist': [c_i32],
     'ctclip_gemm_set_grid_cap': [c_i32],
     'ctclip_reduce_slabs_ep': [c_vp, c_i64, c_i64, c_i64, c_i64, ctypes.POINTER(GemmArgs), c_vp],
+    'ctclip_reduce_slabs_ep_drop': [c_vp, c_i64, c_i64, c_i64, c_i64, ctypes.POINTER(GemmArgs), c_f32, ctypes.c_uint64,
+                                    c_vp],
+    'ctclip_layernorm_bwd_drop': [c_vp, c_i32, c_i64, c_vp, c_i32, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_i64,
+                                  c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_f32, ctypes.c_uint64, c_vp],
     'ctclip_reduce_slabs': [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp],
     'ctclip_reduce_slabs_multi': [ctypes.POINTER(SlabJob), c_i32, c_vp],
     'ctclip_layernorm_fwd': [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_f32, c_vp, c_i64, c_vp, c_i64,

@@ -10,6 +10,7 @@ compatibility; the pooler output is unused by CT-CLIP and is not computed.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
@@ -18,6 +19,11 @@ from torch import nn
 from . import dist_sync
 from . import functional as Fn
 from . import streams
+
+
+# diagnostic only (A/B of what the dropout sites cost): CTCLIP_BERT_NODROP=1 runs train mode without
+# dropout, which is NOT the reference's work
+_NO_DROP = os.environ.get('CTCLIP_BERT_NODROP', '0') != '0'
 
 
 @dataclass
@@ -184,8 +190,8 @@ class BertModel(nn.Module):
         # train-mode dropout (HF BertEmbeddings / BertSelfAttention / BertSelfOutput / BertOutput):
         # one 64-bit seed per (forward call, layer, site); the masks are hashes of it (no host RNG state
         # on the step path, the backward regenerates them)
-        ph = float(c.hidden_dropout_prob) if self.training else 0.0
-        pa = float(c.attention_probs_dropout_prob) if self.training else 0.0
+        ph = float(c.hidden_dropout_prob) if self.training and not _NO_DROP else 0.0
+        pa = float(c.attention_probs_dropout_prob) if self.training and not _NO_DROP else 0.0
         self._drop_calls = getattr(self, '_drop_calls', 0) + 1
         base = (torch.initial_seed() * 0x2545F4914F6CDD1D + self._drop_calls * 0x9E3779B97F4A7C15) & (2 ** 64 - 1)
 

@@ -148,6 +148,10 @@ def bf(W):
 # is what put its latents 1.4e-3 off the f32 reference (tools/bert_precision.py: 6e-4 without
 # it).  CTCLIP_TEXT_SPLIT=0 restores single bf16 weights (A/B switch).
 _TEXT_SPLIT = os.environ.get('CTCLIP_TEXT_SPLIT', '1') != '0'
+# BERT hidden dropout folded into the split-K combine (forward) and the LayerNorm backward, the
+# GELU backward into the dX GEMM (act 6), the dense bias gradients into the LayerNorm backward's
+# partials; CTCLIP_BERT_FUSE=0 restores the stand-alone dropout / gelu_bwd / colsum kernels (A/B)
+_BERT_FUSE = os.environ.get('CTCLIP_BERT_FUSE', '1') != '0'
 
 
 def bf_split(W):
@@ -762,14 +766,18 @@ class BertLayerFn(torch.autograd.Function):
         qkv = K.linear(xb, Wqkv, bias=bqkv, w_lo=Wqkv_lo)
         ctxv, lse = K.attn_fwd(qkv[:, :Hd], qkv[:, Hd:2 * Hd], qkv[:, 2 * Hd:], L=L, H=heads, D=dh, nseq=B,
                                scale=1.0 / math.sqrt(dh), seq=(1, L, 0, 1), kmask=kmask, dropout=(pa, s_attn))
-        if ph > 0:       # LN(dropout(dense(ctx)) + x): the residual leaves the GEMM epilogue
+        if ph > 0 and _BERT_FUSE:   # LN(dropout(dense(ctx)) + x): the dropout in the split-K combine
+            a = K.linear(ctxv, Wo_b, bias=bo, residual=xf, out_dtype=F32, w_lo=Wo_lo, dropout=(ph, s_out1))
+        elif ph > 0:     # (A/B: the stand-alone dropout kernel; the residual leaves the GEMM epilogue)
             a = K.dropout(K.linear(ctxv, Wo_b, bias=bo, out_dtype=F32, w_lo=Wo_lo), ph, s_out1, res=xf)[0]
         else:
             a = K.linear(ctxv, Wo_b, bias=bo, residual=xf, out_dtype=F32, w_lo=Wo_lo)
         x1b, x1f, m1, r1 = K.layernorm_fwd(a, ln1_w, ln1_b, eps, out_bf16=True, out_f32=True)
         hpre = torch.empty(xf.shape[0], Wi.shape[0], device=xf.device, dtype=BF16)
         hact = K.linear(x1b, Wi_b, bias=bi, act=K.ACT_GELU, out2=hpre, w_lo=Wi_lo)
-        if ph > 0:
+        if ph > 0 and _BERT_FUSE:
+            b2 = K.linear(hact, Wout_b, bias=bout, residual=x1f, out_dtype=F32, w_lo=Wout_lo, dropout=(ph, s_out2))
+        elif ph > 0:
             b2 = K.dropout(K.linear(hact, Wout_b, bias=bout, out_dtype=F32, w_lo=Wout_lo), ph, s_out2, res=x1f)[0]
         else:
             b2 = K.linear(hact, Wout_b, bias=bout, residual=x1f, out_dtype=F32, w_lo=Wout_lo)
@@ -791,28 +799,42 @@ class BertLayerFn(torch.autograd.Function):
         ph, pa, s_attn, s_out1, s_out2 = ctx.drop
         Hd = heads * dh
 
-        def wgrad(dy, x, W, b):          # dW += dy^T x, db += colsum(dy), into the parameters' .grad
+        def wgrad(dy, x, W, b, bias_done=False):   # dW += dy^T x, db += colsum(dy), into .grad
             if W.requires_grad:
                 K.matmul_tn(dy, x, out=gsink(W), accumulate=True)
-            if b.requires_grad:
+            if b.requires_grad and not bias_done:
                 K.colsum(dy, out=gsink(b), accumulate=True)
 
-        # LN2 + FF out
-        db2f, db2b, _, _ = K.layernorm_bwd(dx2f.contiguous(), b2, m2, r2, ln2_w, dgamma_out=gsink(ln2_w),
-                                           dbeta_out=gsink(ln2_b))
-        if ph > 0:       # gradient through the output dropout (the residual path bypasses it)
-            db2b = K.dropout(db2f, ph, s_out2, out_f32=False, out_bf16=True)[1]
-        dhact = K.matmul_nn(db2b, Wout_b)
-        wgrad(db2b, hact, Wout, bout)
-        dhpre = K.gelu_bwd(dhact, hpre)
+        fuse = ph > 0 and _BERT_FUSE
+        # LN2 + FF out; with dropout the LN backward also emits the dense branch's masked bf16
+        # gradient and its column sums (the dense bias gradient)
+        if fuse:
+            db2f, db2b = K.layernorm_bwd_drop(dx2f.contiguous(), b2, m2, r2, ln2_w, ph, s_out2,
+                                              dgamma_out=gsink(ln2_w), dbeta_out=gsink(ln2_b),
+                                              dbias_out=gsink(bout) if bout.requires_grad else None)
+        else:
+            db2f, db2b, _, _ = K.layernorm_bwd(dx2f.contiguous(), b2, m2, r2, ln2_w, dgamma_out=gsink(ln2_w),
+                                               dbeta_out=gsink(ln2_b))
+            if ph > 0:       # gradient through the output dropout (the residual path bypasses it)
+                db2b = K.dropout(db2f, ph, s_out2, out_f32=False, out_bf16=True)[1]
+        if _BERT_FUSE:       # dhpre = (db2 . Wout) * gelu'(hpre) in one GEMM (act 6)
+            dhpre = K.matmul_nn_gelu_bwd(db2b, Wout_b, hpre)
+        else:
+            dhpre = K.gelu_bwd(K.matmul_nn(db2b, Wout_b), hpre)
+        wgrad(db2b, hact, Wout, bout, bias_done=fuse)
         dx1 = K.matmul_nn(dhpre, Wi_b, residual=db2f, out_dtype=F32)
         wgrad(dhpre, x1b, Wi, bi)
         # LN1 + attention out
-        daf, dab, _, _ = K.layernorm_bwd(dx1, a, m1, r1, ln1_w, dgamma_out=gsink(ln1_w), dbeta_out=gsink(ln1_b))
-        if ph > 0:
-            dab = K.dropout(daf, ph, s_out1, out_f32=False, out_bf16=True)[1]
+        if fuse:
+            daf, dab = K.layernorm_bwd_drop(dx1, a, m1, r1, ln1_w, ph, s_out1, dgamma_out=gsink(ln1_w),
+                                            dbeta_out=gsink(ln1_b), dbias_out=gsink(bo) if bo.requires_grad else None)
+        else:
+            daf, dab, _, _ = K.layernorm_bwd(dx1, a, m1, r1, ln1_w, dgamma_out=gsink(ln1_w),
+                                             dbeta_out=gsink(ln1_b))
+            if ph > 0:
+                dab = K.dropout(daf, ph, s_out1, out_f32=False, out_bf16=True)[1]
         dctx = K.matmul_nn(dab, Wo_b)
-        wgrad(dab, ctxv, Wo, bo)
+        wgrad(dab, ctxv, Wo, bo, bias_done=fuse)
         dqkv = torch.empty_like(qkv)
         K.attn_bwd(qkv[:, :Hd], qkv[:, Hd:2 * Hd], qkv[:, 2 * Hd:], ctxv, lse, dctx, dqkv[:, :Hd],
                    dqkv[:, Hd:2 * Hd], dqkv[:, 2 * Hd:], L=L, H=heads, D=dh, nseq=B, scale=1.0 / math.sqrt(dh),

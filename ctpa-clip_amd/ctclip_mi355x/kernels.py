@@ -12,7 +12,7 @@ from ._lib import GemmArgs, LnEpilogueArgs, call, ptr, stream_ptr
 BF16 = torch.bfloat16
 F32 = torch.float32
 
-ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_ARGMAX, ACT_GEGLU_BWD, ACT_L2N = 0, 1, 2, 3, 4, 5
+ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_ARGMAX, ACT_GEGLU_BWD, ACT_L2N, ACT_GELU_BWD = 0, 1, 2, 3, 4, 5, 6
 
 
 def _chk(t, name, dtype=None):
@@ -60,21 +60,39 @@ TIMER = KernelTimer()
 
 def gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, *, C2=None, ldc2=0, bias=None,
              R=None, ldr=0, alpha=1.0, act=ACT_NONE, accumulate=False, split_k=1, batch=1,
-             sA=0, sB=0, sC=0, sC2=0, sR=0, tag=None, flops=None, n2=0, B2=None):
+             sA=0, sB=0, sC=0, sC2=0, sR=0, tag=None, flops=None, n2=0, B2=None, drop=None):
     end = TIMER(tag, flops if flops is not None else 2.0 * M * N * K * batch) if tag else None
     _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, C2=C2, ldc2=ldc2, bias=bias, R=R, ldr=ldr,
               alpha=alpha, act=act, accumulate=accumulate, split_k=split_k, batch=batch, sA=sA, sB=sB, sC=sC,
-              sC2=sC2, sR=sR, n2=n2, B2=B2)
+              sC2=sC2, sR=sR, n2=n2, B2=B2, drop=drop)
     if end is not None:
         end.record()
 
 
 def _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, *, C2=None, ldc2=0, bias=None,
               R=None, ldr=0, alpha=1.0, act=ACT_NONE, accumulate=False, split_k=1, batch=1,
-              sA=0, sB=0, sC=0, sC2=0, sR=0, n2=0, B2=None):
+              sA=0, sB=0, sC=0, sC2=0, sR=0, n2=0, B2=None, drop=None):
+    """drop = (p, seed): BERT hidden dropout on (A.B + bias) before the residual R (f32 C, act 0)."""
     if B2 is not None:
         assert B2.dtype == B.dtype and B2.shape == B.shape and B2.stride() == B.stride()
     s = _auto_split(M, N, K, act, split_k, batch, accumulate, C)
+    if drop is not None:
+        assert act == ACT_NONE and not accumulate and C.dtype == F32 and batch == 1 and ldc == N
+        if s <= 1:     # no split-K combine to fold it into: GEMM (+ bias), then the dropout kernel
+            _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, bias=bias, alpha=alpha, B2=B2)
+            call('ctclip_dropout', ptr(C), ptr(R), ptr(C), ptr(C2), M * N, float(drop[0]),
+                 int(drop[1]) & (2 ** 64 - 1), stream_ptr())
+            return
+        slabs = torch.empty(s, M, N, device=C.device, dtype=F32)
+        _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, slabs, N, alpha=alpha, split_k=s, B2=B2)
+        a = GemmArgs()
+        a.C, a.ldc, a.c_f32 = ptr(C), ldc, 1
+        a.C2, a.ldc2 = ptr(C2), ldc2
+        a.bias = ptr(bias)
+        a.R, a.ldr, a.r_f32 = ptr(R), ldr, int(R is not None and R.dtype == F32)
+        call('ctclip_reduce_slabs_ep_drop', ptr(slabs), s, M, N, N, _lib.ctypes.byref(a), float(drop[0]),
+             int(drop[1]) & (2 ** 64 - 1), stream_ptr())
+        return
     if s > 1:
         # skinny GEMM (text tower, M = B * L tokens): split K into f32 slabs over ~4x more
         # workgroups than output tiles, then combine with the epilogue in one pass
@@ -114,7 +132,7 @@ def _auto_split(M, N, K, act, split_k, batch, accumulate, C):
 
 
 def linear(x, w, *, bias=None, residual=None, out=None, out_dtype=BF16, act=ACT_NONE, out2=None, alpha=1.0,
-           accumulate=False, tag=None, flops=None, l2n_scale=None, l2n_cols=0, w_lo=None):
+           accumulate=False, tag=None, flops=None, l2n_scale=None, l2n_cols=0, w_lo=None, dropout=None):
     """y[M,N] = x[M,K] @ w[N,K]^T (+bias) (+residual); x, w bf16 row-major.  l2n_scale (the [32]
     head-dim scale): out2[:, :l2n_cols] = per 32-column head l2norm(y) * scale, fused (act 5).
     w_lo: the bf16 lo image of a split f32 weight (cast_bf16_split): y = x @ (w + w_lo)^T."""
@@ -130,7 +148,7 @@ def linear(x, w, *, bias=None, residual=None, out=None, out_dtype=BF16, act=ACT_
     gemm_raw(M, N, K, x, x.stride(0), True, w, w.stride(0), True, out, out.stride(0),
              C2=out2, ldc2=out2.stride(0) if out2 is not None else 0, bias=bias, R=residual,
              ldr=residual.stride(0) if residual is not None else 0, alpha=alpha, act=act, accumulate=accumulate,
-             tag=tag, flops=flops, n2=l2n_cols, B2=w_lo)
+             tag=tag, flops=flops, n2=l2n_cols, B2=w_lo, drop=dropout)
     return out
 
 
@@ -262,6 +280,19 @@ def matmul_nn_ln_bwd(dy, w, x, mean, rstd, gamma, dres, *, dgamma_out, dbeta_out
     if dbeta_out is not None:
         reduce_param_partials(pb, dbeta_out, True)
     return dxf, dxb
+
+
+def matmul_nn_gelu_bwd(dy, w, pre, out=None):
+    """dx = (dy @ w) * gelu'(pre) in one GEMM (act 6): dy [M, N] bf16, w [N, K] (the nn.Linear
+    weight), pre [M, K] bf16 (the act-1 pre-activation); returns dx [M, K] bf16."""
+    M, N = dy.shape
+    K = w.shape[1]
+    assert w.shape[0] == N and pre.shape == (M, K) and pre.dtype == BF16
+    if out is None:
+        out = torch.empty(M, K, device=dy.device, dtype=BF16)
+    gemm_raw(M, K, N, dy, dy.stride(0), True, w, w.stride(0), False, out, out.stride(0), R=pre, ldr=pre.stride(0),
+             act=ACT_GELU_BWD)
+    return out
 
 
 def split_for(m_rows, tiles):
@@ -465,6 +496,29 @@ def layernorm_bwd(dy, x, mean, rstd, gamma, *, dres=None, want_beta=True, dx_f32
             db = torch.empty(D, device=x.device, dtype=F32)
             reduce_slabs(pb.view(nb, 1, D), db.view(1, D))
     return dxf, dxb, dg, db
+
+
+def layernorm_bwd_drop(dy, x, mean, rstd, gamma, p, seed, *, dgamma_out, dbeta_out, dbias_out=None):
+    """Backward of LN(dropout(dense) + res) (BERT, p > 0): returns (dx f32 = the residual
+    branch's gradient, bf16(dropout(dx)) = the dense output's gradient); the LN gamma / beta
+    gradients and, if given, the dense bias gradient (column sums of the bf16 output) accumulate
+    into dgamma_out / dbeta_out / dbias_out (deferred partial reductions)."""
+    rows, D = x.shape
+    assert dy.dtype == F32 and x.dtype == F32
+    nb = nblocks_for(rows, _LNB_CAP)
+    dxf = torch.empty(rows, D, device=x.device, dtype=F32)
+    dxb = torch.empty(rows, D, device=x.device, dtype=BF16)
+    pg = torch.empty(nb, D, device=x.device, dtype=F32)
+    pb = torch.empty(nb, D, device=x.device, dtype=F32)
+    pd = torch.empty(nb, D, device=x.device, dtype=F32) if dbias_out is not None else None
+    call('ctclip_layernorm_bwd_drop', ptr(dy), 1, dy.stride(0), ptr(x), 1, x.stride(0), ptr(mean), ptr(rstd),
+         ptr(gamma), rows, D, ptr(dxf), D, ptr(dxb), D, ptr(pg), ptr(pb), ptr(pd), nb, float(p),
+         int(seed) & (2 ** 64 - 1), stream_ptr())
+    reduce_param_partials(pg, dgamma_out, True)
+    reduce_param_partials(pb, dbeta_out, True)
+    if dbias_out is not None:
+        reduce_param_partials(pd, dbias_out, True)
+    return dxf, dxb
 
 
 def l2norm_scale_fwd(x, H, D, scale, out=None):

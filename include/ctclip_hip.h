@@ -42,6 +42,9 @@ int ctclip_device_arch(char* buf, int n); /* writes gcnArchName of the current d
  *        5 l2norm: C = bf16 result (N % 64 == 0), C2[:, :n2] = per 32-column head
  *          l2norm(C) * bias[c % 32] (Attention's l2norm(q) * q_scale, attention.py:152-154;
  *          bias = the [32] scale) — replaces a GEMM + ctclip_l2norm_scale_fwd
+ *        6 GELU backward: C = acc * gelu'(R) with R the bf16 pre-activation (act 1's C2; no
+ *          bias / C2 / split-K / accumulate) — replaces a dX GEMM + ctclip_gelu_bwd (BERT's
+ *          intermediate dense, ct_clip/ct_clip.py:685)
  *   split_k > 1: C is an f32 slab array [split_k][M][ldc] of partial sums (no epilogue).
  */
 typedef struct {
@@ -77,6 +80,22 @@ int ctclip_gemm_set_persist(int on);
 /* 8-phase persistent grid cap (workgroups) for the launches that follow; 0 = one per CU (default).
  * Two GEMMs on two streams, each capped, share the chip.  Returns the previous cap. */
 int ctclip_gemm_set_grid_cap(int workgroups);
+
+/* BERT hidden dropout (hidden_dropout_prob, train mode) fused into its neighbours, same mask as
+ * ctclip_dropout (element i of a contiguous [rows][cols] tensor kept iff splitmix64(seed ^ i phi)
+ * >= p 2^32, kept values scaled by 1 / (1 - p)):
+ *  - split-K combine of the dense output: C = dropout(sum_z slabs[z] + bias) + R (act 0, ldc = cols)
+ *    -- BertSelfOutput / BertOutput's dense -> dropout -> + input, ahead of their LayerNorm;
+ *  - LayerNorm backward: dx_f32 = LN'(dy) (to the residual branch), dx_bf16 = bf16(dropout(dx))
+ *    (to the dense branch), part_drop [nblocks][D] (optional) the column partials of dx_bf16
+ *    (the dense bias gradient); dy, x f32, D in (512, 1024]. */
+int ctclip_reduce_slabs_ep_drop(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,
+                                const ctclip_gemm_args* ep, float p, uint64_t seed, void* stream);
+int ctclip_layernorm_bwd_drop(const void* dy, int32_t dy_f32, int64_t lddy, const void* x, int32_t x_f32, int64_t ldx,
+                              const float* mean, const float* rstd, const float* gamma, int64_t rows, int32_t D,
+                              float* dx_f32, int64_t lddxf, void* dx_bf16, int64_t lddxb, float* part_gamma,
+                              float* part_beta, float* part_drop, int32_t nblocks, float p, uint64_t seed,
+                              void* stream);
 
 /* LayerNorm fused into the epilogue of an N = 512 GEMM (the 3D-ViT's d = 512 token rows).  The
  * two 256-column tiles of a row block exchange per-row partial statistics inside the launch.

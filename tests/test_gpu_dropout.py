@@ -194,3 +194,59 @@ def test_bert_layer_dropout_grads_match_torch(K):
         assert e < 5e-2, (n, e)
     # the key bias gradient: both sides are rounding noise around 0, far below the query bias's
     assert got[names.index("bk")].norm() < 3e-2 * got[names.index("bq")].norm()
+
+
+def test_dropout_fused_into_split_k_combine(K):
+    """linear(..., dropout=(p, seed)) (BertSelfOutput / BertOutput dense -> dropout -> + input): the
+    mask applied in the split-K combine equals the stand-alone kernel bit for bit."""
+    torch.manual_seed(3)
+    M, N, Kd = 1024, 768, 3072
+    x = (torch.randn(M, Kd, device=dev) * 0.5).bfloat16()
+    W = (torch.randn(N, Kd, device=dev) / Kd ** 0.5).bfloat16()
+    b = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev)
+    seed = 0x1234_5678_9ABC_DEF1
+    fused = K.linear(x, W, bias=b, residual=res, out_dtype=torch.float32, dropout=(0.1, seed))
+    plain = K.dropout(K.linear(x, W, bias=b, out_dtype=torch.float32), 0.1, seed, res=res)[0]
+    assert torch.equal(fused, plain)
+    # and the torch restatement of the mask
+    idx = torch.arange(M * N, device=dev, dtype=torch.int64).view(M, N)
+    ref = (x.float() @ W.float().t() + b) * keep_mask(idx, seed, 0.1).float() / 0.9 + res
+    assert rel(fused, ref) < 1e-4
+
+
+def test_layernorm_bwd_drop(K):
+    """LN backward with BERT's hidden dropout fused: the f32 output equals the plain LN backward, the
+    bf16 output equals the stand-alone dropout of it, the dense-bias partials equal colsum."""
+    torch.manual_seed(4)
+    rows, D = 1024, 768
+    x = torch.randn(rows, D, device=dev) * 2 + 0.3
+    g, bt = torch.randn(D, device=dev), torch.randn(D, device=dev)
+    _, _, mean, rstd = K.layernorm_fwd(x, g, bt, 1e-12)
+    dy = torch.randn(rows, D, device=dev)
+    seed = 0xDEAD_BEEF_0BAD_F00D
+    dg1, db1, dbias1 = (torch.zeros(D, device=dev) for _ in range(3))
+    dxf, dxb = K.layernorm_bwd_drop(dy, x, mean, rstd, g, 0.1, seed, dgamma_out=dg1, dbeta_out=db1, dbias_out=dbias1)
+    dg0, db0 = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+    ref_f, _, _, _ = K.layernorm_bwd(dy, x, mean, rstd, g, dgamma_out=dg0, dbeta_out=db0)
+    ref_b = K.dropout(ref_f, 0.1, seed, out_f32=False, out_bf16=True)[1]
+    torch.cuda.synchronize()
+    assert torch.equal(dxf, ref_f) and torch.equal(dxb, ref_b)
+    assert torch.equal(dg1, dg0) and torch.equal(db1, db0)
+    assert rel(dbias1, ref_b.float().sum(0)) < 1e-5
+
+
+def test_matmul_nn_gelu_bwd(K):
+    """dhpre = (dy . W) * gelu'(pre) in one GEMM (act 6) vs torch fp32."""
+    torch.manual_seed(5)
+    M, N, Kd = 1024, 768, 3072
+    dy = (torch.randn(M, N, device=dev) * 0.1).bfloat16()
+    W = (torch.randn(N, Kd, device=dev) / N ** 0.5).bfloat16()
+    pre = torch.randn(M, Kd, device=dev).bfloat16()
+    out = K.matmul_nn_gelu_bwd(dy, W, pre)
+    xp = pre.float()
+    gg = 0.5 * (1 + torch.erf(xp / math.sqrt(2))) + xp * torch.exp(-0.5 * xp * xp) / math.sqrt(2 * math.pi)
+    ref = (dy.float() @ W.float()) * gg
+    assert rel(out.float(), ref) < 5e-3
+    two = K.gelu_bwd(K.matmul_nn(dy, W), pre)
+    assert rel(out.float(), two.float()) < 5e-3

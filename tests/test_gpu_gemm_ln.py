@@ -128,3 +128,42 @@ def test_refused_shapes_fall_back(K):
     """Shapes the pair exchange cannot take (M % 2048 != 0) are refused without launching."""
     o, W, res, gamma, beta = _fwd_case(2304, 256, 5)
     assert K.linear_residual_ln(o, W, res, gamma, beta, 1e-5) is None
+
+
+def test_transformer_layer_fused_vs_unfused(K):
+    """A 3D-ViT layer (temporal geometry, B = 8 full size: 110,592 tokens) with the fused
+    to_out + residual + LayerNorm forward (and the opt-in fused backward) against the unfused
+    kernels: outputs and parameter gradients agree to f32 / bf16 rounding."""
+    from ctclip_mi355x import attention as A, functional as Fn
+    torch.manual_seed(0)
+    tr = A.Transformer(512, depth=1, dim_head=32, heads=8).cuda()
+    with torch.no_grad():
+        for p in tr.parameters():
+            p.add_(0.02 * torch.randn_like(p))
+    geo = Fn.Geo(B=8, T=24, Hg=24, Wg=24, heads=8, dim_head=32, mode=1)
+    xf0 = torch.randn(geo.M, 512, device='cuda')
+    xb0 = xf0.bfloat16()
+    dy = torch.randn(geo.M, 512, device='cuda') * 1e-2
+
+    def run(fused, fused_bwd):
+        K.LN_FUSED, K.LN_FUSED_BWD = fused, fused_bwd
+        for p in tr.parameters():
+            p.grad = None
+        xf = xf0.clone().requires_grad_(True)
+        yf, yb = tr.run(xf, xb0, geo)
+        yf.backward(dy)
+        torch.cuda.synchronize()
+        return yf.detach(), xf.grad, [p.grad.clone() for p in tr.parameters() if p.grad is not None]
+
+    prev = K.LN_FUSED, K.LN_FUSED_BWD
+    try:
+        y0, dx0, g0 = run(False, False)
+        y1, dx1, g1 = run(True, False)
+        y2, dx2, g2 = run(True, True)
+    finally:
+        K.LN_FUSED, K.LN_FUSED_BWD = prev
+    assert _rel(y1, y0) < 2e-3 and _rel(y2, y0) < 2e-3
+    assert _rel(dx1, dx0) < 1e-2 and _rel(dx2, dx0) < 1e-2
+    for a, b, c in zip(g0, g1, g2):
+        assert _rel(b, a) < 2e-2 and _rel(c, a) < 2e-2
+    assert K.ln_fused_status() == 0
