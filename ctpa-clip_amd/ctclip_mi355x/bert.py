@@ -214,7 +214,8 @@ class BertModel(nn.Module):
                 a.output.LayerNorm.weight, a.output.LayerNorm.bias, lyr.intermediate.dense.weight,
                 lyr.intermediate.dense.bias, lyr.output.dense.weight, lyr.output.dense.bias,
                 lyr.output.LayerNorm.weight, lyr.output.LayerNorm.bias,
-                (ph, pa, seed(li + 1, 0), seed(li + 1, 1), seed(li + 1, 2)))
+                (ph, pa, seed(li + 1, 0), seed(li + 1, 1), seed(li + 1, 2)),
+                li >= len(self.encoder.layer) - Fn._TEXT_SPLIT_LAYERS)
             if li in lows and li > 0:
                 dist_sync.mark_ready(xf, f'text_{li}')
         return (xf.view(B, L, c.hidden_size), None)

@@ -148,6 +148,8 @@ def bf(W):
 # is what put its latents 1.4e-3 off the f32 reference (tools/bert_precision.py: 6e-4 without
 # it).  CTCLIP_TEXT_SPLIT=0 restores single bf16 weights (A/B switch).
 _TEXT_SPLIT = os.environ.get('CTCLIP_TEXT_SPLIT', '1') != '0'
+# hi / lo split weights on the top CTCLIP_TEXT_SPLIT_LAYERS BERT layers only (default: all 12)
+_TEXT_SPLIT_LAYERS = int(os.environ.get('CTCLIP_TEXT_SPLIT_LAYERS', '1000'))
 # BERT hidden dropout folded into the split-K combine (forward) and the LayerNorm backward, the
 # GELU backward into the dX GEMM (act 6), the dense bias gradients into the LayerNorm backward's
 # partials; CTCLIP_BERT_FUSE=0 restores the stand-alone dropout / gelu_bwd / colsum kernels (A/B)
@@ -751,11 +753,11 @@ class BertLayerFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xf, xb, kmask, B, L, heads, eps, Wq, bq, Wk, bk, Wv, bv, Wo, bo, ln1_w, ln1_b, Wi, bi, Wout,
-                bout, ln2_w, ln2_b, drop=(0.0, 0.0, 0, 0, 0)):
+                bout, ln2_w, ln2_b, drop=(0.0, 0.0, 0, 0, 0), split=None):
         ph, pa, s_attn, s_out1, s_out2 = drop
         Hd = xf.shape[1]
         dh = Hd // heads
-        split = _TEXT_SPLIT
+        split = _TEXT_SPLIT if split is None else (split and _TEXT_SPLIT)
         if split:
             (Wqkv, Wqkv_lo), (Wo_b, Wo_lo), (Wi_b, Wi_lo), (Wout_b, Wout_lo) = (
                 bf_cat_split([Wq, Wk, Wv]), bf_split(Wo), bf_split(Wi), bf_split(Wout))
@@ -849,4 +851,4 @@ class BertLayerFn(torch.autograd.Function):
         else:
             for i, (W, b) in enumerate(((Wq, bq), (Wk, bk), (Wv, bv))):
                 wgrad(dqkv[:, i * Hd:(i + 1) * Hd], xb, W, b)
-        return (dx, None, None, None, None, None, None) + (None,) * 17
+        return (dx, None, None, None, None, None, None) + (None,) * 18
