@@ -990,7 +990,7 @@ __global__ __launch_bounds__(DQD_NT) void attn_bwd_dq_bias_dma_kernel(AP p, int 
           const float x = sa[bi][r] * sc2 + up[3 - r];
           const float ds = fexp2(x - l2) * (da[bi][r] - dl);
           acc[ci][bi][r] += ds;
-          sa[bi][r] = ds * p.scale;
+          sa[bi][r] = ds;   // the score scale is applied once per dQ output below (exact for 8)
         }
       }
       const bf16x8 dsb = pack_perm(sa[0], sa[1]);
@@ -998,6 +998,8 @@ __global__ __launch_bounds__(DQD_NT) void attn_bwd_dq_bias_dma_kernel(AP p, int 
       for (int d = 0; d < DB; ++d)
         dq[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag_sw(Kimg, kc, d * 16, lane), dsb, dq[d], 0, 0, 0);
     }
+#pragma unroll
+    for (int d = 0; d < DB; ++d) dq[d] *= p.scale;
     // combine the key parts of this frame's dQ through the finished buffer (after every wave's
     // last K / V read of it); part 0 sums and stores
     float* xch = (float*)(smem + b * BUF);   // [KP - 1][4 sub-blocks][64 lanes][8]
@@ -1191,7 +1193,7 @@ __global__ __launch_bounds__(DKP_NT) void attn_bwd_dkv_persist_kernel(AP p) {
             const float pr = fexp2(x - lv[r]);
             const float ds = pr * (da[bi][r] - dlq[r]);
             sa[bi][r] = pr;
-            da[bi][r] = ds * p.scale;
+            da[bi][r] = ds;   // the score scale is applied once per dK output below (exact for 8)
           }
         }
         const bf16x8 pa = pack_perm(sa[0], sa[1]);
@@ -1202,6 +1204,8 @@ __global__ __launch_bounds__(DKP_NT) void attn_bwd_dkv_persist_kernel(AP p) {
           dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsa, trfrag_sw(Qimg, qc, d * 16, lane), dk[d], 0, 0, 0);
         }
       }
+#pragma unroll
+      for (int d = 0; d < DB; ++d) dk[d] *= p.scale;
       // C[key][d]: rows = keys kbk*16 + 4g + r, col = d*16 + li
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
