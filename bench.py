@@ -183,7 +183,10 @@ def main():
     torch.manual_seed(0)   # identical random-init weights on every rank
     model = set_finetune_trainable(build_ctclip()).to(dev)
     model.train()
-    trainer = CTClipTrainer(model)
+    # the text bucket's Adam queued by the next step's forward (trainer.defer_text_adam); flushed
+    # after the warm-up (untimed) and after the last timed step (timed), so the timed region holds
+    # exactly K steps' work.  CTCLIP_DEFER_TEXT_ADAM=0: queued at the end of its own step (A/B)
+    trainer = CTClipTrainer(model, defer_text_adam=os.environ.get('CTCLIP_DEFER_TEXT_ADAM', '0') != '0')
     hu, text = synthetic_inputs(args.batch, args.text_len, rank, dev)
 
     # live timing of the dominant kernel + the ViT forward (HIP events on the launch stream)
@@ -204,6 +207,7 @@ def main():
 
     for _ in range(args.warmup):
         trainer.train_step(text, hu)
+    trainer.flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -212,6 +216,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = trainer.train_step(text, hu)
+    trainer.flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -165,6 +165,7 @@ class BertModel(nn.Module):
         if ts is None:
             return self._forward(input_ids, attention_mask)
         cur = torch.cuda.current_stream(dev)
+        streams.flush_text(dev)        # a deferred Adam of these weights (trainer.defer_text_adam)
         if ready is not None:
             ts.wait_event(ready)
         else:

@@ -9,6 +9,7 @@ import torch
 from torch import nn
 
 from . import dist_sync
+from . import streams
 from . import functional as Fn
 from . import kernels as K
 from . import precise
@@ -122,6 +123,7 @@ class CTViT(nn.Module):
                                        pe[3].bias, self.temporal_patch_size, self.patch_size[0], is_hu,
                                        self._offsets(video.shape, video.device))
         dist_sync.mark_ready(xf, 'vit_rest')   # with the CPB node below: the rest of the image tower
+        streams.mark_image_head(video.device)   # deferred text-stream work may start (streams.py)
         if trace is not None:
             trace['patch_emb'] = xf
         hg, wg = self.patch_height_width

@@ -59,3 +59,53 @@ def join_aux(dev):
     s = aux_stream(dev)
     if s is not None:
         torch.cuda.current_stream(dev).wait_stream(s)
+
+
+# ------------------------------------------------------------------ deferred text-stream work
+# The text bucket's Adam (trainer.optimizer_step) is HBM-bound, and queued at the end of a step it
+# runs beside the next step's first image-tower kernels -- the HBM-bound patch LayerNorm -- and
+# slows it.  With the trainer's ``defer_text_adam`` it is handed here instead and queued by the
+# next text-tower forward (``flush_text``, before BERT's own launches, so BERT still reads the
+# updated weights), after an event the image tower records once its patch embedding is queued
+# (``mark_image_head``): it then overlaps the image tower's MFMA-bound GEMMs.  ``flush_text`` is
+# also the explicit flush (the trainer's ``flush``) for a step with no forward after it.
+_PENDING = {}    # device index -> (fn, event recorded when fn was deferred)
+_HEAD_EV = {}    # device index -> event after the image tower's patch embedding
+
+
+def _idx(dev):
+    return dev.index if dev.index is not None else torch.cuda.current_device()
+
+
+def defer_text(dev, fn):
+    """Run ``fn`` on the text stream later (see above), ordered after everything queued on the
+    current stream so far."""
+    if text_stream(dev) is None:
+        fn()
+        return
+    flush_text(dev)
+    _PENDING[_idx(dev)] = (fn, torch.cuda.current_stream(dev).record_event())
+    _HEAD_EV.pop(_idx(dev), None)
+
+
+def mark_image_head(dev):
+    """The image tower's patch embedding is queued on the current stream (deferred work may start)."""
+    if dev.type == 'cuda' and _idx(dev) in _PENDING:
+        _HEAD_EV[_idx(dev)] = torch.cuda.current_stream(dev).record_event()
+
+
+def flush_text(dev):
+    """Queue the deferred text-stream work now (no-op when there is none)."""
+    if dev.type != 'cuda':
+        return
+    p = _PENDING.pop(_idx(dev), None)
+    head = _HEAD_EV.pop(_idx(dev), None)
+    if p is None:
+        return
+    fn, ev = p
+    ts = text_stream(dev)
+    ts.wait_event(ev)
+    if head is not None:
+        ts.wait_event(head)
+    with torch.cuda.stream(ts):
+        fn()

@@ -12,9 +12,13 @@ import os
 
 import torch
 
+
 from . import dist_sync
 from . import streams
 from . import kernels as K
+
+# diagnostic A/B only (CTCLIP_DIAG_TEXT_ADAM=skip | main): NOT the reference's work when 'skip'
+_DIAG_TEXT_ADAM = os.environ.get('CTCLIP_DIAG_TEXT_ADAM', '')
 
 
 class FlatParams:
@@ -113,8 +117,11 @@ class CTClipTrainer:
     eps 1e-8, wd 0, clip 0.5)."""
 
     def __init__(self, model, lr=1.25e-6, wd=0.0, max_grad_norm=0.5, betas=(0.9, 0.99), eps=1e-8,
-                 overlap_grad_sync=True):
+                 overlap_grad_sync=True, defer_text_adam=False):
         self.model = model
+        # the text bucket's Adam is queued by the NEXT step's text-tower forward (streams.defer_text);
+        # call flush() after the last train_step before reading the parameters
+        self.defer_text_adam = defer_text_adam
         dev = next(model.parameters()).device
         self.device = dev
         # arena order = gradient bucket order, so every bucket is one contiguous slice
@@ -193,16 +200,34 @@ class CTClipTrainer:
             if off > lo:
                 self._adam(lo, off - lo)
             lo = off + n
+        if skip and _DIAG_TEXT_ADAM == 'skip':     # diagnostic only: what the overlap costs
+            return
+        if skip and _DIAG_TEXT_ADAM == 'main':     # diagnostic only: serialised on the main stream
+            off, n = skip[0]
+            self._adam(off, n)
+            return
+        if skip and self.defer_text_adam:
+            # queued by the next step's BERT forward, after the next image tower's patch embedding
+            # (streams.defer_text); ``flush`` queues it when no step follows
+            off, n = skip[0]
+            step = self.steps
+            streams.defer_text(self.device, lambda: self._adam(off, n, step=step))
+            return
         if skip:
             off, n = skip[0]
             ts.wait_stream(torch.cuda.current_stream(self.device))   # clip coefficient ready
             with torch.cuda.stream(ts):
                 self._adam(off, n)
 
-    def _adam(self, off, n):
+    def flush(self):
+        """Queue any deferred text-bucket Adam (``defer_text_adam``) now: call after the last
+        ``train_step`` before reading the parameters."""
+        streams.flush_text(self.device)
+
+    def _adam(self, off, n, step=None):
         sl = slice(off, off + n)
         K.adam(self.flat.data[sl], self.flat.grad[sl], self.m[sl], self.v[sl], lr=self.lr, b1=self.betas[0],
-               b2=self.betas[1], eps=self.eps, wd=self.wd, step=self.steps, coef=self.norm,
+               b2=self.betas[1], eps=self.eps, wd=self.wd, step=self.steps if step is None else step, coef=self.norm,
                p_bf16=self.flat.bf16[sl] if self.flat.bf16 is not None else None,
                p_bf16_lo=self.flat.bf16_lo[sl] if self.flat.bf16_lo is not None else None, zero_grad=True)
         self.flat.sync_shadows(off, off + n)

@@ -323,3 +323,23 @@ def test_recon_matches_oracle(setup):
         r2 = vit.decode(vit(hu.cuda(), return_encoded_tokens=True))
     vit.train()
     assert torch.equal(r1, r2)
+
+
+def test_deferred_text_adam_matches(setup):
+    """trainer.defer_text_adam (the text bucket's Adam queued by the next step's BERT forward, after
+    the image tower's patch embedding; streams.defer_text): three steps then flush give the same
+    losses, parameters and Adam moments as the immediate placement (to the run-to-run noise of the
+    float atomics in the embedding / bias-gradient scatters)."""
+    cfg, _, hu, ids, mask, text = setup
+    from ctclip_mi355x.trainer import CTClipTrainer
+    outs = []
+    for defer in (False, True):
+        torch.manual_seed(0)
+        model = build(cfg)
+        tr = CTClipTrainer(model, lr=1e-4, defer_text_adam=defer)
+        losses = [tr.train_step(text, hu.cuda()) for _ in range(3)]
+        tr.flush()
+        torch.cuda.synchronize()
+        outs.append((torch.stack(losses), tr.flat.data.clone(), tr.m.clone(), tr.v.clone()))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-7), (a - b).abs().max().item()
