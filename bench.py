@@ -265,6 +265,9 @@ def main():
                                     '(e4m3, e8m0 per 32 k), backward bf16'} if args.fp8 else {})},
         'loss': round(loss_v, 5),
     }
+    # the LayerNorm-fused GEMMs' in-launch tile-pair exchange never timed out (a timeout would have
+    # left wrong LayerNorm outputs behind; ctclip_gemm_ln's status word)
+    result['ln_exchange_ok'] = K.ln_fused_status() == 0
     if in_sync is not None:
         result['ranks_in_sync'] = in_sync
         result['dist'] = {'backend': dist.get_backend(), 'world_size': dist.get_world_size(),

@@ -154,6 +154,8 @@ _TEXT_SPLIT_LAYERS = int(os.environ.get('CTCLIP_TEXT_SPLIT_LAYERS', '1000'))
 # GELU backward into the dX GEMM (act 6), the dense bias gradients into the LayerNorm backward's
 # partials; CTCLIP_BERT_FUSE=0 restores the stand-alone dropout / gelu_bwd / colsum kernels (A/B)
 _BERT_FUSE = os.environ.get('CTCLIP_BERT_FUSE', '1') != '0'
+# A/B only: the FeedForward's K = 2,816 dX GEMM (a plain bf16 output) on hipBLASLt via torch.matmul
+_DXN2_BLAS = os.environ.get('CTCLIP_DXN2_BLAS', '0') != '0'
 
 
 def bf_split(W):
@@ -468,7 +470,10 @@ class ViTLayerFn(torch.autograd.Function):
         # dx2 = LN'(dh . W1) + dx3 in one launch where the shape allows (gemm256.hip, EP -7)
         fused = K.matmul_nn_ln_bwd(dh_, W1p, x2b, m2, r2, ff_w, dx3f, dgamma_out=gsink(ff_w), dbeta_out=gsink(ff_b))
         if fused is None:
-            dxn2 = K.matmul_nn(dh_, W1p)
+            if _DXN2_BLAS:    # A/B: hipBLASLt (torch.matmul) for this plain bf16 GEMM, W1 packed K-contiguous
+                dxn2 = torch.matmul(dh_, W1p.t().contiguous().t())
+            else:
+                dxn2 = K.matmul_nn(dh_, W1p)
         dW1p = K.matmul_tn(dh_, xn2, tag='dw', flops=2.0 * M_ * W1.shape[0] * W1.shape[1])
         if fused is not None:
             dx2f, dx2b = fused

@@ -328,12 +328,14 @@ def test_recon_matches_oracle(setup):
 def test_deferred_text_adam_matches(setup):
     """trainer.defer_text_adam (the text bucket's Adam queued by the next step's BERT forward, after
     the image tower's patch embedding; streams.defer_text): three steps then flush give the same
-    losses, parameters and Adam moments as the immediate placement (to the run-to-run noise of the
-    float atomics in the embedding / bias-gradient scatters)."""
+    losses, parameters and Adam moments as the immediate placement, up to the run-to-run noise of
+    two immediate runs (float atomics in the embedding / bias-gradient scatters perturb the
+    gradients at 1e-7, and Adam's first step, m / sqrt(v) = sign(g), turns that into lr-sized
+    differences where g ~ 0)."""
     cfg, _, hu, ids, mask, text = setup
     from ctclip_mi355x.trainer import CTClipTrainer
     outs = []
-    for defer in (False, True):
+    for defer in (False, False, True):
         torch.manual_seed(0)
         model = build(cfg)
         tr = CTClipTrainer(model, lr=1e-4, defer_text_adam=defer)
@@ -341,5 +343,8 @@ def test_deferred_text_adam_matches(setup):
         tr.flush()
         torch.cuda.synchronize()
         outs.append((torch.stack(losses), tr.flat.data.clone(), tr.m.clone(), tr.v.clone()))
-    for a, b in zip(outs[0], outs[1]):
-        assert torch.allclose(a, b, rtol=1e-5, atol=1e-7), (a - b).abs().max().item()
+    for a, a2, b in zip(*outs):
+        noise = (a - a2).abs().max().item()
+        d = (a - b).abs().max().item()
+        print(f'immediate vs immediate {noise:.3e}, immediate vs deferred {d:.3e}')
+        assert d <= 4 * noise + 1e-6 * a.abs().max().item()
