@@ -418,6 +418,7 @@ class ViTLayerFn(torch.autograd.Function):
             kn = K.l2norm_scale_fwd(kv[:, :inner], H, dh, k_scale)
         L, nseq, seq = geo.seq()
         use_bias = bias_u is not None
+        streams.mark_image_head(xf.device, 'attn')   # deferred text-stream work may start (streams.py)
         o, lse = K.attn_fwd(qn, kn, kv[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
                             bias_u=bias_u if use_bias else None, grid=(geo.Hg, geo.Wg) if use_bias else (0, 0))
         fused = None if fp8 else K.linear_residual_ln(o, Wo_b, x1f, ff_w, ff_b, 1e-5)

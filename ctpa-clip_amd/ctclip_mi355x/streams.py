@@ -67,7 +67,7 @@ def join_aux(dev):
 # slows it.  With the trainer's ``defer_text_adam`` it is handed here instead and queued by the
 # next text-tower forward (``flush_text``, before BERT's own launches, so BERT still reads the
 # updated weights), after an event the image tower records once its patch embedding is queued
-# (``mark_image_head``): it then overlaps the image tower's MFMA-bound GEMMs.  ``flush_text`` is
+# (``mark_image_head``): it then overlaps the image tower's later kernels instead.  ``flush_text`` is
 # also the explicit flush (the trainer's ``flush``) for a step with no forward after it.
 _PENDING = {}    # device index -> (fn, event recorded when fn was deferred)
 _HEAD_EV = {}    # device index -> event after the image tower's patch embedding
@@ -88,10 +88,18 @@ def defer_text(dev, fn):
     _HEAD_EV.pop(_idx(dev), None)
 
 
-def mark_image_head(dev):
-    """The image tower's patch embedding is queued on the current stream (deferred work may start)."""
-    if dev.type == 'cuda' and _idx(dev) in _PENDING:
-        _HEAD_EV[_idx(dev)] = torch.cuda.current_stream(dev).record_event()
+def mark_image_head(dev, site='patch'):
+    """Deferred text-stream work may start once the current stream reaches this point: the first
+    call of a forward at ``MARK_SITE`` ('patch': after the patch embedding; 'attn': before the first
+    spatial attention kernel, whose latency-bound launch leaves HBM idle) records the event."""
+    if site != MARK_SITE or dev.type != 'cuda':
+        return
+    i = _idx(dev)
+    if i in _PENDING and i not in _HEAD_EV:
+        _HEAD_EV[i] = torch.cuda.current_stream(dev).record_event()
+
+
+MARK_SITE = os.environ.get('CTCLIP_DEFER_SITE', 'attn')
 
 
 def flush_text(dev):
