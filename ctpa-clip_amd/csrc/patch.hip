@@ -273,28 +273,39 @@ bool s_strip20_attr = false;
 
 // Given G = dy^T . xhat  [N][K] (f32) and colsum(dy) cs[N], produce the grads of the folded
 // LayerNorm+Linear pair: dW = G*g + cs (x) b, dgamma[k] = sum_n W[n,k] G[n,k], dbeta[k] = sum_n W[n,k] cs[n].
-__global__ __launch_bounds__(256) void patch_wgrad_kernel(const float* __restrict__ G, const float* __restrict__ cs,
+__global__ __launch_bounds__(512) void patch_wgrad_kernel(const float* __restrict__ G, const float* __restrict__ cs,
                                                           const float* __restrict__ Wt, const float* __restrict__ g,
                                                           const float* __restrict__ bt, int N, int K,
                                                           float* __restrict__ dW, float* __restrict__ dg,
                                                           float* __restrict__ db, int accumulate) {
-  // grid (K / 256, row chunks): dW is elementwise; dg / db partial sums of the chunk go out with
-  // one atomic add per column (the launcher zeroes them first when not accumulating)
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= K) return;
-  const int n0 = (int)((int64_t)N * blockIdx.y / gridDim.y), n1 = (int)((int64_t)N * (blockIdx.y + 1) / gridDim.y);
+  // 64 columns x 8 row groups (one wave each: rows n = wave, wave + 8, ...); dW is elementwise,
+  // the row groups' dgamma / dbeta partials fold in group order through LDS (no float atomics:
+  // bit-reproducible)
+  __shared__ float red[2][8][64];
+  const int lane = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int k = blockIdx.x * 64 + lane;
   float sg = 0.f, sb = 0.f;
-  const float gk = g[k], bk = bt[k];
-  for (int n = n0; n < n1; ++n) {
-    const float Gv = G[(int64_t)n * K + k], w = Wt[(int64_t)n * K + k];
-    sg += w * Gv;
-    sb += w * cs[n];
-    const float d = Gv * gk + cs[n] * bk;
-    float* p = dW + (int64_t)n * K + k;
-    *p = accumulate ? *p + d : d;
+  if (k < K) {
+    const float gk = g[k], bk = bt[k];
+    for (int n = rg; n < N; n += 8) {
+      const float Gv = G[(int64_t)n * K + k], w = Wt[(int64_t)n * K + k], c = cs[n];
+      sg += w * Gv;
+      sb += w * c;
+      const float d = Gv * gk + c * bk;
+      float* p = dW + (int64_t)n * K + k;
+      *p = accumulate ? *p + d : d;
+    }
   }
-  atomicAdd(dg + k, sg);
-  atomicAdd(db + k, sb);
+  red[0][rg][lane] = sg;
+  red[1][rg][lane] = sb;
+  __syncthreads();
+  if (rg < 2 && k < K) {
+    float v = red[rg][0][lane];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) v += red[rg][i][lane];
+    float* o = (rg == 0 ? dg : db) + k;
+    *o = accumulate ? *o + v : v;
+  }
 }
 
 }  // namespace
@@ -430,13 +441,9 @@ extern "C" int ctclip_patch_ln(const void* video, int32_t is_f32, int32_t is_hu,
 extern "C" int ctclip_patch_wgrad(const float* G, const float* cs, const float* Wt, const float* g, const float* b,
                                   int32_t N, int32_t K, float* dW, float* dg, float* db, int32_t accumulate,
                                   void* stream) {
-  if (!accumulate) {
-    (void)hipMemsetAsync(dg, 0, (size_t)K * 4, (hipStream_t)stream);
-    (void)hipMemsetAsync(db, 0, (size_t)K * 4, (hipStream_t)stream);
-  }
-  const int nch = std::max(1, std::min(N, 32));   // 16 column blocks x 32 row chunks at 512 x 4000
-  hipLaunchKernelGGL(patch_wgrad_kernel, dim3(cdiv(K, 256), nch), dim3(256), 0, (hipStream_t)stream, G, cs, Wt, g, b,
-                     N, K, dW, dg, db, accumulate);
+  if (K <= 0) return 0;
+  hipLaunchKernelGGL(patch_wgrad_kernel, dim3(cdiv(K, 64)), dim3(512), 0, (hipStream_t)stream, G, cs, Wt, g, b, N, K,
+                     dW, dg, db, accumulate);
   CT_CHECK_LAUNCH();
   return 0;
 }

@@ -136,23 +136,29 @@ __global__ __launch_bounds__(256) void vq_gather_kernel(const int32_t* __restric
   }
 }
 
-// EMA statistics: bins[c] += count, esum[c][:] += xn rows (f32 atomics)
+// EMA statistics: bins[c] += count (f32 adds of 1: exact below 2^24), esum[c][:] += xn rows in
+// signed 2^-40 fixed point (int64 adds): integer addition is associative, so the sums are
+// bit-identical whatever order the atomics land in, on one GPU and through the SUM all-reduce
+// across ranks (dist_sync.sum_codebook_stats).  xn rows are unit vectors: |sum| < 2^23 rows.
+constexpr float VQ_FX = 0x1p40f;
 __global__ __launch_bounds__(256) void vq_ema_accum_kernel(const int32_t* __restrict__ idx,
                                                            const float* __restrict__ xn, int64_t rows, int D,
-                                                           float* __restrict__ bins, float* __restrict__ esum) {
+                                                           float* __restrict__ bins,
+                                                           unsigned long long* __restrict__ esum) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += nw) {
     const int ci = idx[row];
     if (lane == 0) atomicAdd(&bins[ci], 1.f);
-    for (int c = lane; c < D; c += 64) atomicAdd(&esum[(int64_t)ci * D + c], xn[row * D + c]);
+    for (int c = lane; c < D; c += 64)
+      atomicAdd(&esum[(int64_t)ci * D + c], (unsigned long long)(long long)rintf(xn[row * D + c] * VQ_FX));
   }
 }
 
 // cluster_size = cs*decay + bins*(1-decay);  en = l2norm(esum / max(bins,1)); zero bins keep the
 // old code;  embed = embed*decay + en*(1-decay);  also refresh the bf16 working codebook.
 __global__ __launch_bounds__(64) void vq_ema_finalize_kernel(const float* __restrict__ bins,
-                                                             const float* __restrict__ esum, int C, int D,
+                                                             const long long* __restrict__ esum, int C, int D,
                                                              float decay, float* __restrict__ embed,
                                                              float* __restrict__ cluster, u16* __restrict__ embed_bf16) {
   const int c = blockIdx.x;
@@ -165,13 +171,14 @@ __global__ __launch_bounds__(64) void vq_ema_finalize_kernel(const float* __rest
       for (int k = lane; k < D; k += 64) embed_bf16[(int64_t)c * D + k] = f2bf(e[k]);
     return;
   }
-  const float* s = esum + (int64_t)c * D;
+  const long long* s = esum + (int64_t)c * D;
+  constexpr double FX_INV = 0x1p-40;
   float ss = 0.f;
-  for (int k = lane; k < D; k += 64) { const float v = s[k] / nb; ss += v * v; }
+  for (int k = lane; k < D; k += 64) { const float v = (float)((double)s[k] * FX_INV) / nb; ss += v * v; }
   ss = warp_sum(ss);
   const float inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
   for (int k = lane; k < D; k += 64) {
-    const float en = s[k] / nb * inv;
+    const float en = (float)((double)s[k] * FX_INV) / nb * inv;
     const float v = e[k] * decay + en * (1.f - decay);
     e[k] = v;
     if (embed_bf16) embed_bf16[(int64_t)c * D + k] = f2bf(v);
@@ -234,17 +241,18 @@ extern "C" int ctclip_vq_gather(const int32_t* idx, const float* codebook, int64
 }
 
 extern "C" int ctclip_vq_ema_accum(const int32_t* idx, const float* xn, int64_t rows, int32_t D, float* bins,
-                                   float* esum, void* stream) {
+                                   int64_t* esum, void* stream) {
   const int blocks = (int)std::min<int64_t>(4096, std::max<int64_t>(1, rows / 16));
   hipLaunchKernelGGL(vq_ema_accum_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, idx, xn, rows, D, bins,
-                     esum);
+                     (unsigned long long*)esum);
   CT_CHECK_LAUNCH();
   return 0;
 }
 
-extern "C" int ctclip_vq_ema_finalize(const float* bins, const float* esum, int32_t C, int32_t D, float decay,
+extern "C" int ctclip_vq_ema_finalize(const float* bins, const int64_t* esum, int32_t C, int32_t D, float decay,
                                       float* embed, float* cluster_size, void* embed_bf16, void* stream) {
-  hipLaunchKernelGGL(vq_ema_finalize_kernel, dim3(C), dim3(64), 0, (hipStream_t)stream, bins, esum, C, D, decay,
+  hipLaunchKernelGGL(vq_ema_finalize_kernel, dim3(C), dim3(64), 0, (hipStream_t)stream, bins, (const long long*)esum,
+                     C, D, decay,
                      embed, cluster_size, (u16*)embed_bf16);
   CT_CHECK_LAUNCH();
   return 0;

@@ -168,7 +168,7 @@ _SIGS = {
     'ctclip_sgemm': [c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_f32,
                      c_i32, c_f32, c_vp, c_i64, c_i64, c_i32, c_vp, c_i32, c_vp],
     'ctclip_embed_fwd': [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
-    'ctclip_embed_bwd': [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
+    'ctclip_embed_bwd': [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
     'ctclip_grad_norm': [c_vp, c_i64, c_f32, c_vp, c_i32, c_vp, c_vp],
     'ctclip_adam': [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_i32, c_vp, c_vp, c_vp, c_i32,
                     c_vp],

@@ -38,12 +38,14 @@ class BertConfig:
     layer_norm_eps: float = 1e-12
     hidden_dropout_prob: float = 0.1
     attention_probs_dropout_prob: float = 0.1
+    pad_token_id: int = 0
 
 
 class _Embeddings(nn.Module):
     def __init__(self, c):
         super().__init__()
-        self.word_embeddings = nn.Embedding(c.vocab_size, c.hidden_size)
+        # padding_idx as transformers' BertEmbeddings: the pad row gets no gradient
+        self.word_embeddings = nn.Embedding(c.vocab_size, c.hidden_size, padding_idx=c.pad_token_id)
         self.position_embeddings = nn.Embedding(c.max_position_embeddings, c.hidden_size)
         self.token_type_embeddings = nn.Embedding(c.type_vocab_size, c.hidden_size)
         self.LayerNorm = nn.LayerNorm(c.hidden_size, eps=c.layer_norm_eps)
@@ -201,7 +203,7 @@ class BertModel(nn.Module):
 
         xf, xb = Fn.BertEmbedFn.apply(ids, e.word_embeddings.weight, e.position_embeddings.weight,
                                       e.token_type_embeddings.weight, e.LayerNorm.weight, e.LayerNorm.bias,
-                                      c.layer_norm_eps, (ph, seed(0, 3)))
+                                      c.layer_norm_eps, (ph, seed(0, 3)), c.pad_token_id)
         # gradient buckets (grad_buckets): the lowest group's .grad are final once the embeddings'
         # backward ran, every other group's once its lowest layer's backward ran
         lows = {lo for lo, _ in self._bucket_groups()}

@@ -573,7 +573,7 @@ class VQPoolFn(torch.autograd.Function):
 
             def ema():
                 bins = torch.zeros(C, device=zf.device, dtype=F32)
-                esum = torch.zeros(C, D, device=zf.device, dtype=F32)
+                esum = torch.zeros(C, D, device=zf.device, dtype=torch.int64)   # 2^-40 fixed point
                 K.vq_ema_accum(idx, xn, bins, esum)
                 dist_sync.sum_codebook_stats(bins, esum)
                 K.vq_ema_finalize(bins, esum, decay, cb, cluster.view(-1), cb_b)
@@ -725,8 +725,9 @@ class BertEmbedFn(torch.autograd.Function):
     """BertEmbeddings: word + position + token_type(0), LayerNorm(eps 1e-12)."""
 
     @staticmethod
-    def forward(ctx, ids, word, pos, typ, ln_w, ln_b, eps, drop=(0.0, 0)):
+    def forward(ctx, ids, word, pos, typ, ln_w, ln_b, eps, drop=(0.0, 0), pad_id=-1):
         x = K.embed_fwd(ids, word, pos, typ[0])
+        ctx.pad_id = pad_id
         if drop[0] > 0:
             _, yf, mean, rstd = K.layernorm_fwd(x, ln_w, ln_b, eps, out_bf16=False, out_f32=True)
             yf, yb = K.dropout(yf, drop[0], drop[1], out_f32=True, out_bf16=True)
@@ -748,9 +749,10 @@ class BertEmbedFn(torch.autograd.Function):
         dx, _, _, _ = K.layernorm_bwd(dyf, x, mean, rstd, ln_w, dx_bf16=False,
                                       dgamma_out=gsink(ln_w), dbeta_out=gsink(ln_b))
         dtyp = gsink(typ)
-        # scatter-add straight into the parameters' .grad
-        K.embed_bwd(ids, dx, gsink(word), gsink(pos), dtyp[0] if dtyp is not None else None)
-        return None, None, None, None, None, None, None, None
+        # accumulated straight into the parameters' .grad; the pad id's row gets nothing
+        # (padding_idx of transformers' BertEmbeddings word table)
+        K.embed_bwd(ids, dx, gsink(word), gsink(pos), dtyp[0] if dtyp is not None else None, ctx.pad_id)
+        return None, None, None, None, None, None, None, None, None
 
 
 class BertLayerFn(torch.autograd.Function):

@@ -723,9 +723,10 @@ def attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, *, L, H, D, nseq, scale, seq, bi
     call('ctclip_attn_bwd', _lib.ctypes.byref(a), stream_ptr())
 
 
-# the bias-gradient workspace (deterministic slab reduction) measured no faster than the atomics
-# (spatial backward 822 vs 810 us, profiles/r02bc_attn_ws_ab.log): opt-in via CTCLIP_ATTN_BIAS_WS=1
-_ATTN_BIAS_WS = os.environ.get('CTCLIP_ATTN_BIAS_WS', '0') != '0'
+# the bias-gradient workspace (deterministic slab reduction) costs within noise of the global
+# float atomics (spatial backward 822 vs 810 us, profiles/r02bc_attn_ws_ab.log) and makes the bias
+# gradient bit-reproducible: default since round 3 (CTCLIP_ATTN_BIAS_WS=0 = the atomics)
+_ATTN_BIAS_WS = os.environ.get('CTCLIP_ATTN_BIAS_WS', '1') != '0'
 
 
 # ----------------------------------------------------------------------------- VQ
@@ -763,10 +764,14 @@ def vq_gather(idx, codebook_f32):
 
 
 def vq_ema_accum(idx, xn, bins, esum):
+    """bins (f32 counts) and esum (int64 [C][D], token sums in 2^-40 fixed point: bit-identical
+    whatever order the adds land in) accumulate the EMA statistics of rows xn (unit vectors)."""
+    assert esum.dtype == torch.int64 and bins.dtype == F32
     call('ctclip_vq_ema_accum', ptr(idx), ptr(xn), xn.shape[0], xn.shape[1], ptr(bins), ptr(esum), stream_ptr())
 
 
 def vq_ema_finalize(bins, esum, decay, embed, cluster, embed_bf16=None):
+    assert esum.dtype == torch.int64
     C, D = esum.shape
     call('ctclip_vq_ema_finalize', ptr(bins), ptr(esum), C, D, decay, ptr(embed), ptr(cluster), ptr(embed_bf16),
          stream_ptr())
@@ -860,9 +865,12 @@ def embed_fwd(ids, word, pos, type0):
     return out
 
 
-def embed_bwd(ids, dx, dword, dpos, dtype0):
+def embed_bwd(ids, dx, dword, dpos, dtype0, pad_id=-1):
+    """Accumulate the embedding-table gradients (no float atomics: bit-reproducible); the rows of
+    tokens with id == pad_id add nothing to dword (nn.Embedding padding_idx)."""
     B, L = ids.shape
-    call('ctclip_embed_bwd', ptr(ids), B, L, dx.shape[1], ptr(dx), ptr(dword), ptr(dpos), ptr(dtype0), stream_ptr())
+    call('ctclip_embed_bwd', ptr(ids), B, L, dx.shape[1], ptr(dx), ptr(dword), ptr(dpos), ptr(dtype0), pad_id,
+         stream_ptr())
 
 
 # ----------------------------------------------------------------------------- optimizer

@@ -337,10 +337,13 @@ int ctclip_vq_pool(const int32_t* idx, const float* codebook, int64_t B, int32_t
 int ctclip_vq_pool_bwd(const float* dpooled, int64_t B, int32_t T, int32_t HW, int32_t D, float* dx, void* dx_bf16,
                        void* stream);
 int ctclip_vq_gather(const int32_t* idx, const float* codebook, int64_t rows, int32_t D, float* out, void* stream);
-/* training-mode EMA codebook update (bins / embed_sum accumulate, then finalize) */
-int ctclip_vq_ema_accum(const int32_t* idx, const float* xn, int64_t rows, int32_t D, float* bins, float* esum,
+/* training-mode EMA codebook update (bins / embed_sum accumulate, then finalize).  esum [C][D]
+ * holds the per-code token sums in signed 2^-40 fixed point (int64, zeroed by the caller; xn rows
+ * are unit vectors): integer sums are bit-identical whatever the order of the adds, on one GPU and
+ * through a SUM all-reduce across ranks (bins: f32 counts, exact below 2^24). */
+int ctclip_vq_ema_accum(const int32_t* idx, const float* xn, int64_t rows, int32_t D, float* bins, int64_t* esum,
                         void* stream);
-int ctclip_vq_ema_finalize(const float* bins, const float* esum, int32_t C, int32_t D, float decay, float* embed,
+int ctclip_vq_ema_finalize(const float* bins, const int64_t* esum, int32_t C, int32_t D, float decay, float* embed,
                            float* cluster_size, void* embed_bf16, void* stream);
 
 /* ---------------------------------------------------------------- contrastive loss
@@ -371,8 +374,11 @@ int ctclip_sgemm(int64_t M, int64_t N, int64_t K, const float* A, int64_t sam, i
 /* ---------------------------------------------------------------- BERT embeddings */
 int ctclip_embed_fwd(const int64_t* ids, int64_t B, int32_t L, int32_t Hd, const float* word, const float* pos,
                      const float* type0, float* out, void* stream);
+/* accumulates into dword / dpos / dtype0 (each may be NULL) without float atomics: bit-reproducible.
+ * Tokens whose id == pad_id add nothing to dword (nn.Embedding padding_idx: transformers'
+ * BertEmbeddings word table, pad_token_id 0); pad_id < 0 = none.  Hd % 4 == 0, 16-byte aligned rows. */
 int ctclip_embed_bwd(const int64_t* ids, int64_t B, int32_t L, int32_t Hd, const float* dx, float* dword,
-                     float* dpos, float* dtype0, void* stream);
+                     float* dpos, float* dtype0, int64_t pad_id, void* stream);
 
 /* ---------------------------------------------------------------- optimizer (CTCLIPTrainer.py:347-353)
  * grad norm -> out[0] = norm, out[1] = clip coef (torch clip_grad_norm_ semantics);

@@ -76,6 +76,7 @@ class BertConfig:
     max_position: int = 512
     type_vocab: int = 2
     eps: float = 1e-12
+    pad_id: int = 0     # word table padding_idx (transformers BertEmbeddings, pad_token_id)
 
 
 @dataclass(frozen=True)
@@ -313,7 +314,8 @@ def bert_forward(sd, p, ids, mask, cfg: BertConfig):
     dropout 0).  Returns last_hidden_state (b, L, hidden)."""
     b, L = ids.shape
     pos = torch.arange(L)
-    x = sd[p + 'embeddings.word_embeddings.weight'][ids] \
+    # padding_idx: the pad id's row takes part in the forward but gets no gradient
+    x = F.embedding(ids, sd[p + 'embeddings.word_embeddings.weight'], padding_idx=cfg.pad_id) \
         + sd[p + 'embeddings.token_type_embeddings.weight'][0] \
         + sd[p + 'embeddings.position_embeddings.weight'][pos]
     x = _ln(x, sd[p + 'embeddings.LayerNorm.weight'], sd[p + 'embeddings.LayerNorm.bias'], cfg.eps)

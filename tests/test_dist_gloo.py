@@ -99,6 +99,13 @@ def _worker(rank, port, out_dir):
         ref_esum = torch.zeros(C, D).index_add_(0, idx.reshape(-1), tok.reshape(-1, D))
         assert torch.equal(bins, ref_bins)
         torch.testing.assert_close(esum, ref_esum)
+        # the GPU path's 2^-40 fixed-point (int64) token sums: the cross-rank SUM is exact, so
+        # every rank holds the single-process sums bit for bit
+        fx = (tok * 2 ** 40).round().long()
+        esum_fx = torch.zeros(C, D, dtype=torch.int64).index_add_(0, idx[rank], fx[rank])
+        dist_sync.sum_codebook_stats(esum_fx)
+        assert torch.equal(esum_fx, torch.zeros(C, D, dtype=torch.int64).index_add_(0, idx.reshape(-1),
+                                                                                   fx.reshape(-1, D)))
 
         # the text latents' gather started early (CTCLIP.encode, text stream) gives the same step
         wt.grad = None

@@ -25,7 +25,7 @@ def cfg_small():
     return O.ClipConfig(vit=vit, bert=bert, dim_latent=512)
 
 
-def build(cfg):
+def build(cfg, dropout=0.0):
     from ctclip_mi355x.models import build_ctclip, set_finetune_trainable
     from ctclip_mi355x.bert import BertConfig
     v, b = cfg.vit, cfg.bert
@@ -35,7 +35,7 @@ def build(cfg):
     bert = BertConfig(vocab_size=b.vocab_size, hidden_size=b.hidden, num_hidden_layers=b.layers,
                       num_attention_heads=b.heads, intermediate_size=b.intermediate,
                       max_position_embeddings=b.max_position,
-                      hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)   # parity runs: SURVEY §8(c)
+                      hidden_dropout_prob=dropout, attention_probs_dropout_prob=dropout)   # parity runs: 0
     m = build_ctclip(vit, bert, cfg.dim_latent)
     m.load_state_dict(W.make_state_dict(cfg), strict=True)
     return set_finetune_trainable(m).cuda()
@@ -348,6 +348,43 @@ def test_deferred_text_adam_matches(setup):
     (l0, p0), (l1, p1) = outs
     assert ((l0 - l1).abs() / l0.abs()).max().item() < 1e-3
     assert (p0 - p1).abs().max().item() <= 6 * lr
+
+
+def test_train_step_bit_reproducible():
+    """Two runs of three training steps from the same seed give bit-identical losses, parameters,
+    Adam moments, VQ codebook and cluster sizes, BERT dropout on, ragged reports (pad ids): no
+    float atomics on the step's path (CPB bias gradient through the per-workgroup workspace,
+    embedding and patch-LN gradients in fixed order, VQ statistics in fixed point).  A third run
+    with the text Adam deferred (trainer.defer_text_adam) is bit-identical too.  The spatial
+    stage runs the base shape (24 x 24 grid, L = 576), whose bias-gradient kernel has the
+    workspace; other grids bin with atomics (kernels.attn_bwd)."""
+    from ctclip_mi355x.trainer import CTClipTrainer
+    vit = O.ViTConfig(dim=512, codebook_size=8192, image_size=480, patch_size=20, temporal_patch_size=10,
+                      spatial_depth=1, temporal_depth=1, dim_head=32, heads=8, frames=20)
+    bert = O.BertConfig(vocab_size=1000, hidden=768, layers=2, heads=12, intermediate=3072, max_position=64)
+    cfg = O.ClipConfig(vit=vit, bert=bert, dim_latent=512)
+    torch.manual_seed(1)
+    hu = W.make_hu(2, cfg.vit).cuda()
+    ids, mask = W.make_text(2, 32, bert.vocab_size, ragged=True)
+    assert (ids == 0).any()
+    text = types.SimpleNamespace(input_ids=ids.cuda(), attention_mask=mask.cuda())
+    runs = []
+    for defer in (False, False, True):
+        torch.manual_seed(0)
+        model = build(cfg, dropout=0.1)
+        tr = CTClipTrainer(model, lr=1e-4, defer_text_adam=defer)
+        losses = torch.stack([tr.train_step(text, hu) for _ in range(3)])
+        tr.flush()
+        torch.cuda.synchronize()
+        cbk = model.visual_transformer.vq._codebook
+        runs.append([losses, tr.flat.data.clone(), tr.m.clone(), tr.v.clone(), cbk.embed.clone(),
+                     cbk.cluster_size.clone()])
+        del model, tr
+    names = ['losses', 'parameters', 'adam m', 'adam v', 'codebook', 'cluster size']
+    for r in runs[1:]:
+        for n, a, b in zip(names, runs[0], r):
+            assert torch.equal(a, b), f'{n} differ: max {(a.double() - b.double()).abs().max().item():.3e}'
+    assert torch.isfinite(runs[0][0]).all()
 
 
 def test_defer_text_ordering():

@@ -227,8 +227,13 @@ def test_vq_select_and_pool(K):
     assert rel(pooled, refp) < 1e-6
     # EMA restatement vs oracle
     bins = torch.zeros(C, device=dev)
-    esum = torch.zeros(C, D, device=dev)
+    esum = torch.zeros(C, D, device=dev, dtype=torch.int64)
     K.vq_ema_accum(idx, xno, bins, esum)
+    # fixed-point sums: order-independent, so equal to the 2^-40-rounded rows summed on the host
+    fx = torch.zeros(C, D, dtype=torch.int64).index_add_(0, idx.long().cpu(),
+                                                         torch.round(xno.cpu().double() * 2 ** 40).long())
+    assert torch.equal(esum.cpu(), fx)
+    assert torch.equal(bins.cpu(), torch.bincount(idx.long().cpu(), minlength=C).float())
     emb = cb.clone()
     cs = torch.zeros(C, device=dev)
     K.vq_ema_finalize(bins, esum, 0.8, emb, cs)
@@ -336,6 +341,42 @@ def test_embed(K):
     assert rel(dw, refw) < 1e-6
     assert rel(dp[:16], dx.reshape(3, 16, 64).sum(0)) < 1e-6
     assert rel(dt, dx.sum(0)) < 1e-6
+
+
+@pytest.mark.parametrize('B,L,V,Hd', [(8, 128, 50, 768), (2, 600, 3000, 1200), (1, 1, 10, 4)])
+def test_embed_bwd_padding_and_reproducible(K, B, L, V, Hd):
+    """Ragged reports: pad id 0 gets no word-table gradient (transformers BertEmbeddings builds
+    the table with padding_idx = pad_token_id; torch F.embedding(padding_idx=0) is the
+    reference); many repeated ids (V small); no float atomics, so repeated calls are bit-equal;
+    accumulates into existing .grad."""
+    g = torch.Generator(device=dev).manual_seed(B * 1000 + L)
+    ids = torch.randint(1, V, (B, L), device=dev, generator=g)
+    for b in range(B):
+        ids[b, L - L // (b + 2):] = 0                  # ragged tails of pad id 0
+    word = torch.randn(V, Hd, device=dev, generator=g, requires_grad=True)
+    pos = torch.randn(L + 3, Hd, device=dev, generator=g, requires_grad=True)
+    typ = torch.randn(2, Hd, device=dev, generator=g, requires_grad=True)
+    dx = torch.randn(B * L, Hd, device=dev, generator=g)
+    x = torch.nn.functional.embedding(ids, word, padding_idx=0) + pos[:L][None] + typ[0]
+    x.backward(dx.reshape(B, L, Hd))
+    base = [torch.randn(V, Hd, device=dev, generator=g), torch.randn(L + 3, Hd, device=dev, generator=g),
+            torch.randn(Hd, device=dev, generator=g)]
+    outs = []
+    for _ in range(3):
+        dw, dp, dt = (t.clone() for t in base)
+        K.embed_bwd(ids, dx, dw, dp, dt, pad_id=0)
+        outs.append((dw, dp, dt))
+    for o in outs[1:]:
+        assert all(torch.equal(a, b) for a, b in zip(o, outs[0]))
+    dw, dp, dt = outs[0]
+    assert torch.equal(dw[0], base[0][0])               # pad row untouched
+    assert rel(dw - base[0], word.grad) < 1e-6
+    assert rel(dp - base[1], pos.grad) < 1e-6
+    assert rel(dt - base[2], typ.grad[0]) < 1e-6
+    # only the tables asked for
+    dw2 = base[0].clone()
+    K.embed_bwd(ids, dx, dw2, None, None, pad_id=0)
+    assert torch.equal(dw2, dw)
 
 
 def test_adam_and_norm(K):
