@@ -273,21 +273,21 @@ bool s_strip20_attr = false;
 
 // Given G = dy^T . xhat  [N][K] (f32) and colsum(dy) cs[N], produce the grads of the folded
 // LayerNorm+Linear pair: dW = G*g + cs (x) b, dgamma[k] = sum_n W[n,k] G[n,k], dbeta[k] = sum_n W[n,k] cs[n].
-__global__ __launch_bounds__(512) void patch_wgrad_kernel(const float* __restrict__ G, const float* __restrict__ cs,
+__global__ __launch_bounds__(1024) void patch_wgrad_kernel(const float* __restrict__ G, const float* __restrict__ cs,
                                                           const float* __restrict__ Wt, const float* __restrict__ g,
                                                           const float* __restrict__ bt, int N, int K,
                                                           float* __restrict__ dW, float* __restrict__ dg,
                                                           float* __restrict__ db, int accumulate) {
-  // 64 columns x 8 row groups (one wave each: rows n = wave, wave + 8, ...); dW is elementwise,
+  // 64 columns x 16 row groups (one wave each: rows n = wave, wave + 16, ...); dW is elementwise,
   // the row groups' dgamma / dbeta partials fold in group order through LDS (no float atomics:
   // bit-reproducible)
-  __shared__ float red[2][8][64];
+  __shared__ float red[2][16][64];
   const int lane = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int k = blockIdx.x * 64 + lane;
   float sg = 0.f, sb = 0.f;
   if (k < K) {
     const float gk = g[k], bk = bt[k];
-    for (int n = rg; n < N; n += 8) {
+    for (int n = rg; n < N; n += 16) {
       const float Gv = G[(int64_t)n * K + k], w = Wt[(int64_t)n * K + k], c = cs[n];
       sg += w * Gv;
       sb += w * c;
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(512) void patch_wgrad_kernel(const float* __restric
   if (rg < 2 && k < K) {
     float v = red[rg][0][lane];
 #pragma unroll
-    for (int i = 1; i < 8; ++i) v += red[rg][i][lane];
+    for (int i = 1; i < 16; ++i) v += red[rg][i][lane];
     float* o = (rg == 0 ? dg : db) + k;
     *o = accumulate ? *o + v : v;
   }
@@ -442,7 +442,7 @@ extern "C" int ctclip_patch_wgrad(const float* G, const float* cs, const float* 
                                   int32_t N, int32_t K, float* dW, float* dg, float* db, int32_t accumulate,
                                   void* stream) {
   if (K <= 0) return 0;
-  hipLaunchKernelGGL(patch_wgrad_kernel, dim3(cdiv(K, 64)), dim3(512), 0, (hipStream_t)stream, G, cs, Wt, g, b, N, K,
+  hipLaunchKernelGGL(patch_wgrad_kernel, dim3(cdiv(K, 64)), dim3(1024), 0, (hipStream_t)stream, G, cs, Wt, g, b, N, K,
                      dW, dg, db, accumulate);
   CT_CHECK_LAUNCH();
   return 0;

@@ -141,18 +141,40 @@ __global__ __launch_bounds__(256) void vq_gather_kernel(const int32_t* __restric
 // bit-identical whatever order the atomics land in, on one GPU and through the SUM all-reduce
 // across ranks (dist_sync.sum_codebook_stats).  xn rows are unit vectors: |sum| < 2^23 rows.
 constexpr float VQ_FX = 0x1p40f;
+constexpr int VQ_EMA_RUN = 16;   // consecutive rows per wave
+// a wave walks VQ_EMA_RUN consecutive rows, summing runs of equal codes in registers (neighbouring
+// tokens often share a code; an untrained codebook sends most tokens to a few) and adding each
+// run once; lane owns columns lane + 64 j, D <= 1024
 __global__ __launch_bounds__(256) void vq_ema_accum_kernel(const int32_t* __restrict__ idx,
                                                            const float* __restrict__ xn, int64_t rows, int D,
                                                            float* __restrict__ bins,
                                                            unsigned long long* __restrict__ esum) {
   const int lane = threadIdx.x & 63;
-  const int64_t nw = (int64_t)gridDim.x * 4;
-  for (int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); row < rows; row += nw) {
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * VQ_EMA_RUN;
+  const int64_t r1 = r0 + VQ_EMA_RUN < rows ? r0 + VQ_EMA_RUN : rows;
+  long long acc[16];
+  int cur = -1, cnt = 0;
+  auto flush = [&]() {
+    if (lane == 0) atomicAdd(&bins[cur], (float)cnt);
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (lane + 64 * j < D) atomicAdd(&esum[(int64_t)cur * D + lane + 64 * j], (unsigned long long)acc[j]);
+  };
+  for (int64_t row = r0; row < r1; ++row) {
     const int ci = idx[row];
-    if (lane == 0) atomicAdd(&bins[ci], 1.f);
-    for (int c = lane; c < D; c += 64)
-      atomicAdd(&esum[(int64_t)ci * D + c], (unsigned long long)(long long)rintf(xn[row * D + c] * VQ_FX));
+    if (ci != cur) {
+      if (cur >= 0) flush();
+      cur = ci;
+      cnt = 0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc[j] = 0;
+    }
+    ++cnt;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (lane + 64 * j < D) acc[j] += (long long)rintf(xn[row * D + lane + 64 * j] * VQ_FX);
   }
+  if (cur >= 0) flush();
 }
 
 // cluster_size = cs*decay + bins*(1-decay);  en = l2norm(esum / max(bins,1)); zero bins keep the
@@ -242,7 +264,9 @@ extern "C" int ctclip_vq_gather(const int32_t* idx, const float* codebook, int64
 
 extern "C" int ctclip_vq_ema_accum(const int32_t* idx, const float* xn, int64_t rows, int32_t D, float* bins,
                                    int64_t* esum, void* stream) {
-  const int blocks = (int)std::min<int64_t>(4096, std::max<int64_t>(1, rows / 16));
+  if (rows == 0) return 0;
+  CT_REQUIRE(D <= 1024, CT_EINVAL);
+  const int blocks = cdiv(rows, 4 * VQ_EMA_RUN);
   hipLaunchKernelGGL(vq_ema_accum_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, idx, xn, rows, D, bins,
                      (unsigned long long*)esum);
   CT_CHECK_LAUNCH();
