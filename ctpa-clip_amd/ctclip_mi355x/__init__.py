@@ -4,3 +4,5 @@ Drop-in for the reference's ``ct_clip.CTCLIP`` / ``ct_clip.ctvit.CTViT`` /
 ``ctpa_report.vqa_meditron.VisionFeatureExtractor`` forward signatures and state_dict layout.
 """
 __version__ = '0.1.0'
+
+from . import ops  # noqa: E402,F401  (registers the torch.ops.ctclip.* custom ops)

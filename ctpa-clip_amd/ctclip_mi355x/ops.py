@@ -1,0 +1,242 @@
+"""``torch.library`` custom ops over the C-ABI ("wrapped by torch.library custom ops
+with autograd Functions inside ctclip_mi355x").  Namespace ``ctclip``; each op launches the HIP
+kernels of ``kernels.py`` on torch's current stream, has a fake (meta) implementation for shape
+propagation, and the differentiable ones register their backward with ``register_autograd``.
+
+The model itself runs the fused autograd Functions of ``functional.py`` (one Function per
+transformer layer, parameter gradients written straight into the flat gradient arena); these ops
+are the same kernels exposed one operation at a time, for callers that compose their own graph:
+
+    torch.ops.ctclip.gemm_bf16(x, w, bias, residual)            # y = x @ w^T (+ bias) (+ residual)
+    torch.ops.ctclip.layernorm(x, gamma, beta, eps)
+    torch.ops.ctclip.cos_attn(q, k, v, q_scale, k_scale, heads, seq_len, layout, scale, bias, grid)
+    torch.ops.ctclip.clip_infonce(text_latents, image_latents, log_temp)
+    torch.ops.ctclip.vq_cos_argmax(x, codebook)                 # (idx int32, l2norm(x))
+
+Device tensors only (the ops are registered for the "cuda" device type, which is HIP on ROCm):
+a CPU tensor raises, and with the library missing every op raises (``_lib.lib``).  Reference
+call sites: ct_clip/attention.py:44-52,88-181 (linears, LayerNorm, cosine attention),
+ct_clip/ct_clip.py:796-812 (InfoNCE), ct_clip/ctvit.py:421-427 (VQ cosine argmax)."""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+from torch import Tensor
+
+from . import kernels as K
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def _need(cond, msg):
+    if not cond:
+        raise ValueError(msg)
+
+
+# ------------------------------------------------------------------------------ gemm_bf16
+@torch.library.custom_op('ctclip::gemm_bf16', mutates_args=(), device_types='cuda')
+def gemm_bf16(x: Tensor, w: Tensor, bias: Optional[Tensor] = None, residual: Optional[Tensor] = None) -> Tensor:
+    """nn.Linear on the MFMA GEMM: x [M, K] bf16, w [N, K] bf16, bias [N] f32, residual [M, N] f32.
+    Output bf16, or f32 when a residual is added (the residual stream is f32)."""
+    _need(x.dtype == BF16 and w.dtype == BF16, 'gemm_bf16: x and w must be bf16')
+    _need(x.dim() == 2 and w.dim() == 2 and x.shape[1] == w.shape[1], 'gemm_bf16: x [M, K], w [N, K]')
+    _need(bias is None or (bias.dtype == F32 and bias.shape == (w.shape[0],)), 'gemm_bf16: bias [N] f32')
+    _need(residual is None or (residual.dtype == F32 and residual.shape == (x.shape[0], w.shape[0])),
+          'gemm_bf16: residual [M, N] f32')
+    return K.linear(x.contiguous(), w.contiguous(), bias=bias,
+                    residual=residual.contiguous() if residual is not None else None,
+                    out_dtype=F32 if residual is not None else BF16)
+
+
+@gemm_bf16.register_fake
+def _(x, w, bias=None, residual=None):
+    return x.new_empty(x.shape[0], w.shape[0], dtype=F32 if residual is not None else BF16)
+
+
+def _gemm_setup(ctx, inputs, output):
+    x, w, bias, residual = inputs
+    ctx.save_for_backward(x, w)
+    ctx.has_bias, ctx.has_res = bias is not None, residual is not None
+
+
+def _gemm_bwd(ctx, dy):
+    x, w = ctx.saved_tensors
+    dyb = dy.to(BF16).contiguous()
+    dx = K.matmul_nn(dyb, w.contiguous()) if ctx.needs_input_grad[0] else None
+    dw = K.matmul_tn(dyb, x.contiguous()).to(w.dtype) if ctx.needs_input_grad[1] else None
+    db = K.colsum(dy.contiguous()) if ctx.has_bias and ctx.needs_input_grad[2] else None
+    dres = dy.to(F32) if ctx.has_res and ctx.needs_input_grad[3] else None
+    return dx, dw, db, dres
+
+
+gemm_bf16.register_autograd(_gemm_bwd, setup_context=_gemm_setup)
+
+
+# ------------------------------------------------------------------------------ layernorm
+@torch.library.custom_op('ctclip::layernorm', mutates_args=(), device_types='cuda')
+def _layernorm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float) -> Tuple[Tensor, Tensor, Tensor]:
+    _need(x.dim() == 2 and x.dtype == F32, 'layernorm: x [rows, D] f32')
+    _need(gamma.dtype == F32 and beta.dtype == F32 and gamma.shape == (x.shape[1],) == beta.shape,
+          'layernorm: gamma / beta [D] f32')
+    _, y, mean, rstd = K.layernorm_fwd(x.contiguous(), gamma, beta, eps, out_bf16=False, out_f32=True)
+    return y, mean, rstd
+
+
+@_layernorm.register_fake
+def _(x, gamma, beta, eps):
+    return x.new_empty(x.shape), x.new_empty(x.shape[0]), x.new_empty(x.shape[0])
+
+
+def _ln_setup(ctx, inputs, output):
+    x, gamma, _, _ = inputs
+    _, mean, rstd = output
+    ctx.save_for_backward(x, gamma, mean, rstd)
+
+
+def _ln_bwd(ctx, dy, _dmean, _drstd):
+    x, gamma, mean, rstd = ctx.saved_tensors
+    dx, _, dg, db = K.layernorm_bwd(dy.contiguous(), x.contiguous(), mean, rstd, gamma, want_beta=True,
+                                    dx_f32=True, dx_bf16=False)
+    return dx, dg, db, None
+
+
+_layernorm.register_autograd(_ln_bwd, setup_context=_ln_setup)
+
+
+def layernorm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float = 1e-5) -> Tensor:
+    """LayerNorm over the last dim of x [rows, D] (f32 in / out); ct_clip/attention.py:28-35."""
+    return _layernorm(x, gamma, beta, eps)[0]
+
+
+# ------------------------------------------------------------------------------- cos_attn
+@torch.library.custom_op('ctclip::cos_attn', mutates_args=(), device_types='cuda')
+def _cos_attn(q: Tensor, k: Tensor, v: Tensor, q_scale: Tensor, k_scale: Tensor, heads: int, seq_len: int,
+              layout: List[int], scale: float, bias: Optional[Tensor], grid: List[int]) -> Tuple[Tensor, Tensor]:
+    M, HD = q.shape
+    D = HD // heads
+    _need(q.dtype == k.dtype == v.dtype == BF16 and k.shape == q.shape == v.shape, 'cos_attn: q / k / v [M, H*D] bf16')
+    _need(D in (32, 64) and HD == heads * D, 'cos_attn: dim_head 32 or 64')
+    _need(len(layout) == 4 and len(grid) == 2, 'cos_attn: layout (n_inner, s_outer, s_inner, s_pos), grid (h, w)')
+    _need(M % seq_len == 0, 'cos_attn: rows must be a whole number of sequences')
+    _need(bias is None or (bias.dtype == F32 and bias.dim() == 2 and bias.shape[0] == heads
+                           and grid[0] * grid[1] == seq_len
+                           and bias.shape[1] == (2 * grid[0] - 1) * (2 * grid[1] - 1)),
+          'cos_attn: bias [heads, (2h-1)(2w-1)] f32 over an h x w grid of seq_len keys')
+    qn = K.l2norm_scale_fwd(q.contiguous(), heads, D, q_scale)
+    kn = K.l2norm_scale_fwd(k.contiguous(), heads, D, k_scale)
+    o, lse = K.attn_fwd(qn, kn, v.contiguous(), L=seq_len, H=heads, D=D, nseq=M // seq_len, scale=scale,
+                        seq=tuple(layout), bias_u=bias, grid=tuple(grid) if bias is not None else (0, 0))
+    return o, lse
+
+
+@_cos_attn.register_fake
+def _(q, k, v, q_scale, k_scale, heads, seq_len, layout, scale, bias, grid):
+    return q.new_empty(q.shape), q.new_empty(heads, q.shape[0], dtype=F32)
+
+
+def _attn_setup(ctx, inputs, output):
+    q, k, v, q_scale, k_scale, heads, seq_len, layout, scale, bias, grid = inputs
+    o, lse = output
+    ctx.save_for_backward(q, k, v, q_scale, k_scale, o, lse, bias)
+    ctx.cfg = (heads, seq_len, tuple(layout), scale, tuple(grid), bias is not None)
+
+
+def _attn_bwd(ctx, do, _dlse):
+    q, k, v, q_scale, k_scale, o, lse, bias = ctx.saved_tensors
+    heads, L, layout, scale, grid, has_bias = ctx.cfg
+    M, HD = q.shape
+    D = HD // heads
+    q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+    qn = K.l2norm_scale_fwd(q, heads, D, q_scale)
+    kn = K.l2norm_scale_fwd(k, heads, D, k_scale)
+    dqn, dkn, dv = torch.empty_like(qn), torch.empty_like(kn), torch.empty_like(v)
+    du = torch.zeros_like(bias) if has_bias else None
+    K.attn_bwd(qn, kn, v, o, lse, do.to(BF16).contiguous(), dqn, dkn, dv, L=L, H=heads, D=D, nseq=M // L,
+               scale=scale, seq=layout, bias_u=bias if has_bias else None, dbias_u=du,
+               grid=grid if has_bias else (0, 0))
+    dq, dk = torch.empty_like(q), torch.empty_like(k)
+    dqs = K.l2norm_scale_bwd(q, dqn, heads, D, q_scale, dq)
+    dks = K.l2norm_scale_bwd(k, dkn, heads, D, k_scale, dk)
+    return dq, dk, dv, dqs, dks, None, None, None, None, du, None
+
+
+_cos_attn.register_autograd(_attn_bwd, setup_context=_attn_setup)
+
+
+def cos_attn(q: Tensor, k: Tensor, v: Tensor, q_scale: Tensor, k_scale: Tensor, heads: int, seq_len: int,
+             layout=None, scale: float = 8.0, bias: Optional[Tensor] = None, grid=(0, 0)) -> Tensor:
+    """Cosine-similarity attention of ct_clip/attention.py:88-181: per head, q and k are
+    l2-normalised and multiplied by the learned q_scale / k_scale [dim_head], sim = scale * q.k
+    (+ the continuous position bias bias[h][bin(query, key)] over an h x w grid), softmax, . v.
+    Rows [M, heads*dim_head] bf16; `layout` maps (sequence, position) to a row (default:
+    contiguous sequences of seq_len rows; functional.Geo.seq gives the spatial / temporal ones)."""
+    if layout is None:
+        layout = (1, seq_len, 0, 1)
+    return _cos_attn(q, k, v, q_scale, k_scale, heads, seq_len, list(layout), float(scale), bias, list(grid))[0]
+
+
+# --------------------------------------------------------------------------- clip_infonce
+@torch.library.custom_op('ctclip::clip_infonce', mutates_args=(), device_types='cuda')
+def _clip_infonce(text_latents: Tensor, image_latents: Tensor, log_temp: Tensor) -> Tuple[Tensor, Tensor, Tensor,
+                                                                                            Tensor]:
+    _need(text_latents.dtype == image_latents.dtype == log_temp.dtype == F32, 'clip_infonce: f32 inputs')
+    _need(text_latents.shape == image_latents.shape and text_latents.dim() == 2, 'clip_infonce: [B, dim_latent]')
+    _need(log_temp.numel() == 1, 'clip_infonce: log_temp is a scalar')
+    loss, dt, di, dlt, _, _, _ = K.clip_loss(text_latents.contiguous(), image_latents.contiguous(),
+                                             log_temp.reshape(1).contiguous())
+    return loss.reshape(()), dt, di, dlt.reshape(log_temp.shape)
+
+
+@_clip_infonce.register_fake
+def _(text_latents, image_latents, log_temp):
+    return (text_latents.new_empty(()), torch.empty_like(text_latents), torch.empty_like(image_latents),
+            torch.empty_like(log_temp))
+
+
+def _clip_setup(ctx, inputs, output):
+    _, dt, di, dlt = output
+    ctx.save_for_backward(dt, di, dlt)
+
+
+def _clip_bwd(ctx, dloss, *_):
+    dt, di, dlt = ctx.saved_tensors
+    return dt * dloss, di * dloss, dlt * dloss
+
+
+_clip_infonce.register_autograd(_clip_bwd, setup_context=_clip_setup)
+
+
+def clip_infonce(text_latents: Tensor, image_latents: Tensor, log_temp: Tensor) -> Tensor:
+    """Symmetric InfoNCE of ct_clip/ct_clip.py:796-812 on raw latents: l2-normalise both, sim =
+    exp(log_temp) * t . i^T, loss = (CE(sim, arange) + CE(sim^T, arange)) / 2 (scalar)."""
+    return _clip_infonce(text_latents, image_latents, log_temp)[0]
+
+
+# -------------------------------------------------------------------------- vq_cos_argmax
+@torch.library.custom_op('ctclip::vq_cos_argmax', mutates_args=(), device_types='cuda')
+def vq_cos_argmax(x: Tensor, codebook: Tensor) -> Tuple[Tensor, Tensor]:
+    """Exact f32 cosine argmax of each row of x [M, D] against codebook [C, D] (f32 rows), as
+    vector_quantize_pytorch's cosine codebook (ct_clip/ctvit.py:421-427): bf16 MFMA scores with a
+    per-64-code-group (best, second-best) epilogue, then the f32 re-score of every code within the
+    bf16 error margin.  Returns (indices int32 [M], l2norm(x) f32 [M, D])."""
+    _need(x.dtype == F32 and codebook.dtype == F32 and x.dim() == 2 and codebook.dim() == 2
+          and x.shape[1] == codebook.shape[1], 'vq_cos_argmax: x [M, D], codebook [C, D], f32')
+    _need(x.shape[1] % 8 == 0, 'vq_cos_argmax: D % 8 == 0')
+    x = x.contiguous()
+    cb = codebook.contiguous()
+    M, D = x.shape
+    C = cb.shape[0]
+    xn_b = K.l2norm_scale_fwd(K.cast_bf16(x), 1, D, torch.ones(D, device=x.device, dtype=F32))
+    nt = (C + 63) // 64
+    cand = torch.empty(M, nt, 2, device=x.device, dtype=F32)
+    cand2 = torch.empty(M, nt, device=x.device, dtype=F32)
+    K.gemm_raw(M, C, D, xn_b, D, True, K.cast_bf16(cb), D, True, cand, nt, C2=cand2, ldc2=nt, act=K.ACT_ARGMAX)
+    idx, xn = K.vq_select(cand, x, cb, want_xn=True, cand2=cand2)
+    return idx, xn
+
+
+@vq_cos_argmax.register_fake
+def _(x, codebook):
+    return x.new_empty(x.shape[0], dtype=torch.int32), x.new_empty(x.shape)

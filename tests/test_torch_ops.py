@@ -1,0 +1,206 @@
+"""torch.library custom ops (ctclip_mi355x/ops.py): registration, fake (meta)
+shapes and CPU refusal here; numerics and gradients against torch fp32 references of the same op
+on the GPU (the kernels behind them are the model's own, called through the C-ABI)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+from torch._subclasses.fake_tensor import FakeTensorMode
+
+from ctclip_mi355x import ops  # noqa: F401  (registers torch.ops.ctclip)
+
+BF, F32 = torch.bfloat16, torch.float32
+OPS = ('gemm_bf16', 'layernorm', 'cos_attn', 'clip_infonce', 'vq_cos_argmax')
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+# ------------------------------------------------------------------------------ host side
+def test_ops_registered_with_fake_shapes():
+    for n in OPS:
+        assert hasattr(torch.ops.ctclip, n), n
+    with FakeTensorMode():
+        x = torch.empty(256, 512, dtype=BF, device='cuda')
+        w = torch.empty(1024, 512, dtype=BF, device='cuda')
+        assert torch.ops.ctclip.gemm_bf16(x, w).dtype == BF
+        r = torch.empty(256, 1024, dtype=F32, device='cuda')
+        y = torch.ops.ctclip.gemm_bf16(x, w, None, r)
+        assert y.shape == (256, 1024) and y.dtype == F32
+        xf = torch.empty(300, 512, device='cuda')
+        g = torch.empty(512, device='cuda')
+        yl, m, s = torch.ops.ctclip.layernorm(xf, g, g, 1e-5)
+        assert yl.shape == xf.shape and m.shape == s.shape == (300,)
+        q = torch.empty(4 * 64, 8 * 32, dtype=BF, device='cuda')
+        sc = torch.empty(32, device='cuda')
+        o, lse = torch.ops.ctclip.cos_attn(q, q, q, sc, sc, 8, 64, [1, 64, 0, 1], 8.0, None, [0, 0])
+        assert o.shape == q.shape and lse.shape == (8, 256)
+        t = torch.empty(8, 512, device='cuda')
+        lt = torch.empty(1, device='cuda')
+        loss, dt, di, dlt = torch.ops.ctclip.clip_infonce(t, t, lt)
+        assert loss.shape == () and dt.shape == t.shape and dlt.shape == lt.shape
+        idx, xn = torch.ops.ctclip.vq_cos_argmax(xf, torch.empty(8192, 512, device='cuda'))
+        assert idx.shape == (300,) and idx.dtype == torch.int32 and xn.shape == xf.shape
+
+
+def test_ops_refuse_host_tensors():
+    """Registered for the HIP ("cuda") device type only: no silent CPU path."""
+    with pytest.raises(NotImplementedError):
+        torch.ops.ctclip.gemm_bf16(torch.zeros(4, 4, dtype=BF), torch.zeros(4, 4, dtype=BF))
+    with pytest.raises(NotImplementedError):
+        ops.layernorm(torch.zeros(2, 8), torch.ones(8), torch.zeros(8))
+
+
+# ------------------------------------------------------------------------------ GPU numerics
+dev = 'cuda'
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('bias,res', [(False, False), (True, True)])
+def test_gemm_bf16_fwd_bwd(bias, res):
+    g = torch.Generator(device=dev).manual_seed(1)
+    M, Kd, N = 1024, 512, 768
+    x = torch.randn(M, Kd, device=dev, generator=g).to(BF).requires_grad_(True)
+    w = (torch.randn(N, Kd, device=dev, generator=g) / Kd ** 0.5).to(BF).requires_grad_(True)
+    b = torch.randn(N, device=dev, generator=g).requires_grad_(True) if bias else None
+    r = torch.randn(M, N, device=dev, generator=g).requires_grad_(True) if res else None
+    y = ops.gemm_bf16(x, w, b, r)
+    assert y.dtype == (F32 if res else BF)
+    xr, wr = x.detach().float().requires_grad_(True), w.detach().float().requires_grad_(True)
+    br = b.detach().clone().requires_grad_(True) if bias else None
+    rr = r.detach().clone().requires_grad_(True) if res else None
+    yr = F.linear(xr, wr, br) + (rr if res else 0)
+    assert rel(y.float(), yr) < 1e-2
+    dy = torch.randn(M, N, device=dev, generator=g).to(y.dtype)
+    y.backward(dy)
+    yr.backward(dy.float())
+    assert rel(x.grad.float(), xr.grad) < 1e-2 and x.grad.dtype == BF
+    assert rel(w.grad.float(), wr.grad) < 1e-2 and w.grad.dtype == BF
+    if bias:
+        assert rel(b.grad, br.grad) < 1e-5
+    if res:
+        assert torch.equal(r.grad, dy)
+
+
+@pytest.mark.gpu
+def test_layernorm_fwd_bwd():
+    g = torch.Generator(device=dev).manual_seed(2)
+    x = (torch.randn(3000, 512, device=dev, generator=g) * 3 + 1).requires_grad_(True)
+    gam = (1 + 0.1 * torch.randn(512, device=dev, generator=g)).requires_grad_(True)
+    bet = (0.1 * torch.randn(512, device=dev, generator=g)).requires_grad_(True)
+    y = ops.layernorm(x, gam, bet, 1e-5)
+    xr, gr, br = (t.detach().clone().requires_grad_(True) for t in (x, gam, bet))
+    yr = F.layer_norm(xr, (512,), gr, br, 1e-5)
+    assert rel(y, yr) < 1e-5
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy)
+    for a, b in ((x, xr), (gam, gr), (bet, br)):
+        assert rel(a.grad, b.grad) < 1e-4
+
+
+def _attn_ref(q, k, v, qs, ks, H, L, scale, bias, grid, layout):
+    M, HD = q.shape
+    D = HD // H
+    n_in, s_out, s_in, s_pos = layout
+    s = torch.arange(M // L, device=q.device)
+    rows = ((s // n_in) * s_out + (s % n_in) * s_in)[:, None] + torch.arange(L, device=q.device)[None] * s_pos
+
+    def heads(t):
+        return t.float()[rows].view(M // L, L, H, D).transpose(1, 2)
+    qn = F.normalize(heads(q), dim=-1) * qs
+    kn = F.normalize(heads(k), dim=-1) * ks
+    sim = qn @ kn.transpose(-1, -2) * scale
+    if bias is not None:
+        gh, gw = grid
+        p = torch.arange(L, device=q.device)
+        dh = (p // gw)[:, None] - (p // gw)[None]
+        dw = (p % gw)[:, None] - (p % gw)[None]
+        sim = sim + bias[:, (dh + gh - 1) * (2 * gw - 1) + dw + gw - 1][None]
+    o = sim.softmax(-1) @ heads(v)
+    out = torch.empty(M, HD, device=q.device, dtype=o.dtype)
+    out[rows.reshape(-1)] = o.transpose(1, 2).reshape(-1, HD)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('case', ['bert_like', 'spatial_bias', 'temporal'])
+def test_cos_attn_fwd_bwd(case):
+    g = torch.Generator(device=dev).manual_seed(3)
+    H, D = 8, 32
+    if case == 'bert_like':
+        L, nseq, layout, bias, grid, D = 128, 4, None, None, (0, 0), 64
+    elif case == 'spatial_bias':
+        L, nseq, layout, grid = 64, 6, None, (8, 8)
+        bias = torch.randn(H, 15 * 15, device=dev, generator=g).requires_grad_(True)
+    else:   # temporal rows (b, t, h*w): sequences over t, '(b h w) t d' (functional.Geo.seq)
+        B, T, HW = 2, 8, 16
+        L, nseq, layout, bias, grid = T, B * HW, (HW, T * HW, 1, HW), None, (0, 0)
+    M = L * nseq
+    q, k, v = ((torch.randn(M, H * D, device=dev, generator=g)).to(BF).requires_grad_(True) for _ in range(3))
+    qs = (1 + 0.1 * torch.randn(D, device=dev, generator=g)).requires_grad_(True)
+    ks = (1 + 0.1 * torch.randn(D, device=dev, generator=g)).requires_grad_(True)
+    scale = 8.0 if case != 'bert_like' else 1 / math.sqrt(D)
+    o = ops.cos_attn(q, k, v, qs, ks, H, L, layout, scale, bias, grid)
+    lay = layout or (1, L, 0, 1)
+    ins = [t.detach().clone().requires_grad_(True) for t in (q, k, v, qs, ks)]
+    br = bias.detach().clone().requires_grad_(True) if bias is not None else None
+    ref = _attn_ref(*ins, H, L, scale, br, grid, lay)
+    assert rel(o.float(), ref) < 1e-2
+    do = torch.randn(M, H * D, device=dev, generator=g).to(BF)
+    o.backward(do)
+    ref.backward(do.float())
+    for name, a, b in zip(('q', 'k', 'v', 'q_scale', 'k_scale'), (q, k, v, qs, ks), ins):
+        assert rel(a.grad.float(), b.grad) < 3e-2, name
+    if bias is not None:
+        assert rel(bias.grad, br.grad) < 3e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('Bg', [2, 8, 64])
+def test_clip_infonce(Bg):
+    g = torch.Generator(device=dev).manual_seed(4)
+    t = torch.randn(Bg, 512, device=dev, generator=g).requires_grad_(True)
+    i = torch.randn(Bg, 512, device=dev, generator=g).requires_grad_(True)
+    lt = torch.tensor([math.log(1 / 0.07)], device=dev).requires_grad_(True)
+    loss = ops.clip_infonce(t, i, lt)
+    tr, ir, lr = (x.detach().clone().requires_grad_(True) for x in (t, i, lt))
+    sim = F.normalize(tr, dim=-1) @ F.normalize(ir, dim=-1).t() * lr.exp()
+    lab = torch.arange(Bg, device=dev)
+    ref = (F.cross_entropy(sim, lab) + F.cross_entropy(sim.t(), lab)) / 2
+    assert abs(loss.item() - ref.item()) < 1e-5 * max(1.0, abs(ref.item()))
+    (2.0 * loss).backward()
+    (2.0 * ref).backward()
+    assert rel(t.grad, tr.grad) < 1e-4 and rel(i.grad, ir.grad) < 1e-4 and rel(lt.grad, lr.grad) < 1e-4
+
+
+@pytest.mark.gpu
+def test_vq_cos_argmax():
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(4000, 512, device=dev, generator=g)
+    cb = F.normalize(torch.randn(8192, 512, device=dev, generator=g), dim=-1)
+    idx, xn = ops.vq_cos_argmax(x, cb)
+    s64 = F.normalize(x.double(), dim=-1) @ cb.double().t()
+    top2 = s64.topk(2, dim=1).values
+    tie = (top2[:, 0] - top2[:, 1]) < 1e-6          # only f32-level ties may differ
+    assert (idx.long() != s64.argmax(1))[~tie].sum().item() == 0
+    assert rel(xn, F.normalize(x, dim=-1)) < 1e-6
+
+
+@pytest.mark.gpu
+def test_opcheck_registrations():
+    """torch.library.opcheck: schema, fake tensor and autograd-registration checks on device inputs."""
+    g = torch.Generator(device=dev).manual_seed(6)
+    x = torch.randn(256, 512, device=dev, generator=g).to(BF)
+    w = torch.randn(512, 512, device=dev, generator=g).to(BF)
+    utils = ('test_schema', 'test_faketensor', 'test_autograd_registration')
+    torch.library.opcheck(torch.ops.ctclip.gemm_bf16, (x, w, None, None), test_utils=utils)
+    xf = torch.randn(256, 512, device=dev, generator=g)
+    gam = torch.ones(512, device=dev)
+    torch.library.opcheck(torch.ops.ctclip.layernorm, (xf, gam, gam * 0, 1e-5), test_utils=utils)
+    t = torch.randn(8, 512, device=dev, generator=g)
+    torch.library.opcheck(torch.ops.ctclip.clip_infonce, (t, t.flip(0), torch.ones(1, device=dev)),
+                          test_utils=utils)
