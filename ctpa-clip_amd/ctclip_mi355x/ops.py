@@ -12,10 +12,13 @@ are the same kernels exposed one operation at a time, for callers that compose t
     torch.ops.ctclip.cos_attn(q, k, v, q_scale, k_scale, heads, seq_len, layout, scale, bias, grid)
     torch.ops.ctclip.clip_infonce(text_latents, image_latents, log_temp)
     torch.ops.ctclip.vq_cos_argmax(x, codebook)                 # (idx int32, l2norm(x))
+    torch.ops.ctclip.peg_dwconv3d(x, weight, bias, shape, mode)  # x + PEG(x), canonical rows
+    torch.ops.ctclip.cpb_mlp(rel, w0, b0, w1, b1, w2, b2)        # CPB table [heads, bins]
 
 Device tensors only (the ops are registered for the "cuda" device type, which is HIP on ROCm):
 a CPU tensor raises, and with the library missing every op raises (``_lib.lib``).  Reference
-call sites: ct_clip/attention.py:44-52,88-181 (linears, LayerNorm, cosine attention),
+call sites: ct_clip/attention.py:44-52,88-181 (linears, LayerNorm, cosine attention), :56-84
+(PEG), :229-276 (continuous position bias),
 ct_clip/ct_clip.py:796-812 (InfoNCE), ct_clip/ctvit.py:421-427 (VQ cosine argmax)."""
 from __future__ import annotations
 
@@ -240,3 +243,107 @@ def vq_cos_argmax(x: Tensor, codebook: Tensor) -> Tuple[Tensor, Tensor]:
 @vq_cos_argmax.register_fake
 def _(x, codebook):
     return x.new_empty(x.shape[0], dtype=torch.int32), x.new_empty(x.shape)
+
+
+# --------------------------------------------------------------------------- peg_dwconv3d
+@torch.library.custom_op('ctclip::peg_dwconv3d', mutates_args=(), device_types='cuda')
+def peg_dwconv3d(x: Tensor, weight: Tensor, bias: Tensor, shape: List[int], mode: int) -> Tensor:
+    """x + PEG(x) (ct_clip/attention.py:56-84,324): depthwise 3x3x3 Conv3d, causal in time (pad
+    (1, 1, 1, 1, 2, 0)), on token rows x [B*T*H*W, D] f32 in canonical (b, t, h, w) order.  mode 0:
+    the spatial transformer's view; mode 1: the temporal transformer's raw-reshape view of its
+    '(b h w) t d' tensor (attention.py:69-70).  weight [D, 1, 3, 3, 3] f32, bias [D] f32.  The
+    conv reads the bf16 rounding of x (as in the model); the residual is the f32 x."""
+    B, T, H, W = shape
+    D = x.shape[1]
+    _need(x.dtype == F32 and x.dim() == 2 and x.shape[0] == B * T * H * W, 'peg_dwconv3d: x [B*T*H*W, D] f32')
+    _need(weight.dtype == F32 and weight.numel() == D * 27 and bias.dtype == F32 and bias.shape == (D,),
+          'peg_dwconv3d: weight [D, 1, 3, 3, 3], bias [D] f32')
+    _need(mode in (0, 1), 'peg_dwconv3d: mode 0 (spatial) or 1 (temporal)')
+    x = x.contiguous()
+    outf, _ = K.peg_fwd(K.cast_bf16(x), x, B, T, H, W, weight.contiguous(), bias.contiguous(), mode)
+    return outf
+
+
+@peg_dwconv3d.register_fake
+def _(x, weight, bias, shape, mode):
+    return torch.empty_like(x)
+
+
+def _peg_setup(ctx, inputs, output):
+    x, weight, _, shape, mode = inputs
+    ctx.save_for_backward(x, weight)
+    ctx.cfg = (tuple(shape), mode)
+
+
+def _peg_bwd(ctx, dy):
+    x, weight = ctx.saved_tensors
+    (B, T, H, W), mode = ctx.cfg
+    dy = dy.contiguous()
+    dxf, _, dw, db = K.peg_bwd(K.cast_bf16(dy), dy, K.cast_bf16(x.contiguous()), B, T, H, W,
+                               weight.contiguous(), mode)
+    return dxf, dw.reshape(weight.shape), db, None, None
+
+
+peg_dwconv3d.register_autograd(_peg_bwd, setup_context=_peg_setup)
+
+
+# -------------------------------------------------------------------------------- cpb_mlp
+@torch.library.custom_op('ctclip::cpb_mlp', mutates_args=(), device_types='cuda')
+def _cpb_mlp(rel: Tensor, w0: Tensor, b0: Tensor, w1: Tensor, b1: Tensor, w2: Tensor,
+             b2: Tensor) -> Tuple[Tensor, Tensor, Tensor]:
+    _need(all(t.dtype == F32 for t in (rel, w0, b0, w1, b1, w2, b2)), 'cpb_mlp: f32 tensors')
+    _need(rel.dim() == 2 and rel.shape[1] == w0.shape[1] and w1.shape == (w0.shape[0], w0.shape[0])
+          and w2.shape[1] == w0.shape[0], 'cpb_mlp: rel [bins, 2], w0 [d, 2], w1 [d, d], w2 [heads, d]')
+    rel = rel.contiguous()
+    nb, H = rel.shape[0], w2.shape[0]
+    h1 = K.slinear(rel, w0.contiguous(), b0.contiguous(), act=1)
+    h2 = K.slinear(h1, w1.contiguous(), b1.contiguous(), act=1)
+    u = torch.empty(H, nb, device=rel.device, dtype=F32)
+    w2 = w2.contiguous()
+    K.sgemm(nb, H, h2.shape[1], h2, h2.stride(0), 1, w2, 1, w2.stride(0), u, 1, nb, bias=b2.contiguous())
+    return u, h1, h2
+
+
+@_cpb_mlp.register_fake
+def _(rel, w0, b0, w1, b1, w2, b2):
+    nb, d = rel.shape[0], w0.shape[0]
+    return rel.new_empty(w2.shape[0], nb), rel.new_empty(nb, d), rel.new_empty(nb, d)
+
+
+def _cpb_setup(ctx, inputs, output):
+    rel, w0, _, w1, _, w2, _ = inputs
+    _, h1, h2 = output
+    ctx.save_for_backward(rel, w0, w1, w2, h1, h2)
+
+
+def _cpb_bwd(ctx, du, _dh1, _dh2):
+    rel, w0, w1, w2, h1, h2 = ctx.saved_tensors
+    du = du.contiguous()
+    H, nb = du.shape
+    dev = du.device
+    w0, w1, w2 = w0.contiguous(), w1.contiguous(), w2.contiguous()
+    dz2 = torch.empty(nb, w2.shape[1], device=dev, dtype=F32)   # d(pre-activation of layer 2)
+    K.sgemm(nb, w2.shape[1], H, du, 1, nb, w2, w2.stride(0), 1, dz2, dz2.stride(0), 1, act=2, aux=h2,
+            sxm=h2.stride(0), sxn=1)
+    dw2 = K.smm(du, h2)
+    db2 = torch.empty(H, device=dev, dtype=F32)
+    ones = torch.ones(nb, device=dev, dtype=F32)
+    K.sgemm(H, 1, nb, du, nb, 1, ones, 1, 0, db2, 1, 1)
+    dw1 = K.smm(dz2.t(), h1)
+    db1 = K.colsum(dz2)
+    dz1 = K.smm(dz2, w1, act=2, aux=h1)
+    dw0 = K.smm(dz1.t(), rel.contiguous())
+    db0 = K.colsum(dz1)
+    drel = K.smm(dz1, w0) if ctx.needs_input_grad[0] else None
+    return drel, dw0, db0, dw1, db1, dw2, db2
+
+
+_cpb_mlp.register_autograd(_cpb_bwd, setup_context=_cpb_setup)
+
+
+def cpb_mlp(rel: Tensor, w0: Tensor, b0: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor) -> Tensor:
+    """ContinuousPositionBias's MLP (ct_clip/attention.py:229-276: Linear(2, d), LeakyReLU(0.1),
+    Linear(d, d), LeakyReLU(0.1), Linear(d, heads)) on the distinct relative offsets rel [bins, 2]
+    (functional.cpb_table: sign(x) log(|x| + 1) of the (dh, dw) offsets of an h x w grid).
+    Returns the bias table [heads, bins] that cos_attn(bias=..., grid=(h, w)) consumes."""
+    return _cpb_mlp(rel, w0, b0, w1, b1, w2, b2)[0]

@@ -11,7 +11,7 @@ from torch._subclasses.fake_tensor import FakeTensorMode
 from ctclip_mi355x import ops  # noqa: F401  (registers torch.ops.ctclip)
 
 BF, F32 = torch.bfloat16, torch.float32
-OPS = ('gemm_bf16', 'layernorm', 'cos_attn', 'clip_infonce', 'vq_cos_argmax')
+OPS = ('gemm_bf16', 'layernorm', 'cos_attn', 'clip_infonce', 'vq_cos_argmax', 'peg_dwconv3d', 'cpb_mlp')
 
 
 def rel(a, b):
@@ -44,6 +44,13 @@ def test_ops_registered_with_fake_shapes():
         assert loss.shape == () and dt.shape == t.shape and dlt.shape == lt.shape
         idx, xn = torch.ops.ctclip.vq_cos_argmax(xf, torch.empty(8192, 512, device='cuda'))
         assert idx.shape == (300,) and idx.dtype == torch.int32 and xn.shape == xf.shape
+        xp = torch.empty(2 * 3 * 4 * 5, 64, device='cuda')
+        assert torch.ops.ctclip.peg_dwconv3d(xp, torch.empty(64, 1, 3, 3, 3, device='cuda'),
+                                             torch.empty(64, device='cuda'), [2, 3, 4, 5], 1).shape == xp.shape
+        rel_ = torch.empty(2209, 2, device='cuda')
+        u, _, _ = torch.ops.ctclip.cpb_mlp(rel_, torch.empty(512, 2, device='cuda'), g, torch.empty(512, 512, device='cuda'),
+                                           g, torch.empty(8, 512, device='cuda'), torch.empty(8, device='cuda'))
+        assert u.shape == (8, 2209)
 
 
 def test_ops_refuse_host_tensors():
@@ -188,6 +195,75 @@ def test_vq_cos_argmax():
     tie = (top2[:, 0] - top2[:, 1]) < 1e-6          # only f32-level ties may differ
     assert (idx.long() != s64.argmax(1))[~tie].sum().item() == 0
     assert rel(xn, F.normalize(x, dim=-1)) < 1e-6
+
+
+def _peg_torch(x, w, b, shape, mode):
+    """x + causal depthwise conv3d in the reference's view (attention.py:56-84; mode 1 views the
+    '(b h w) t d' tensor through a raw reshape to (b, t, h, w))."""
+    B, T, H, W = shape
+    D = x.shape[1]
+    if mode == 1:
+        xv = x.reshape(B, T, H, W, D).permute(0, 2, 3, 1, 4).reshape(B, T, H, W, D)   # raw reshape
+    else:
+        xv = x.reshape(B, T, H, W, D)
+    v = F.pad(xv.permute(0, 4, 1, 2, 3), (1, 1, 1, 1, 2, 0))
+    y = F.conv3d(v, w, b, groups=D).permute(0, 2, 3, 4, 1)
+    if mode == 1:
+        y = y.reshape(B, H, W, T, D).permute(0, 3, 1, 2, 4)
+    return x + y.reshape(-1, D)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('mode', [0, 1])
+@pytest.mark.parametrize('shape,D', [((2, 6, 5, 7), 128), ((1, 4, 24, 24), 512)])
+def test_peg_dwconv3d(mode, shape, D):
+    g = torch.Generator(device=dev).manual_seed(7)
+    M = shape[0] * shape[1] * shape[2] * shape[3]
+    x = torch.randn(M, D, device=dev, generator=g).bfloat16().float().requires_grad_(True)
+    w = (torch.randn(D, 1, 3, 3, 3, device=dev, generator=g) * 0.2).requires_grad_(True)
+    b = (torch.randn(D, device=dev, generator=g) * 0.1).requires_grad_(True)
+    y = ops.peg_dwconv3d(x, w, b, list(shape), mode)
+    xr, wr, br = (t.detach().clone().requires_grad_(True) for t in (x, w, b))
+    yr = _peg_torch(xr, wr, br, shape, mode)
+    assert rel(y, yr) < 1e-5
+    dy = torch.randn(M, D, device=dev, generator=g).bfloat16().float()
+    y.backward(dy)
+    yr.backward(dy)
+    assert rel(x.grad, xr.grad) < 1e-5 and rel(w.grad, wr.grad) < 1e-5 and rel(b.grad, br.grad) < 1e-5
+
+
+@pytest.mark.gpu
+def test_cpb_mlp_and_biased_attention():
+    """CPB table from the op feeds cos_attn's bias; gradients flow through both ops back to the
+    MLP weights (ContinuousPositionBias -> Attention, attention.py:229-276,160-165)."""
+    from ctclip_mi355x import functional as Fn
+    g = torch.Generator(device=dev).manual_seed(8)
+    gh, gw, H, D, d = 6, 6, 8, 32, 64
+    rel_ = Fn.cpb_table(gh, gw, dev)
+    ws = [torch.randn(d, 2, device=dev, generator=g) * 0.5, torch.randn(d, device=dev, generator=g) * 0.1,
+          torch.randn(d, d, device=dev, generator=g) / 8, torch.randn(d, device=dev, generator=g) * 0.1,
+          torch.randn(H, d, device=dev, generator=g) / 8, torch.randn(H, device=dev, generator=g) * 0.1]
+    ws = [t.requires_grad_(True) for t in ws]
+    u = ops.cpb_mlp(rel_, *ws)
+    wr = [t.detach().clone().requires_grad_(True) for t in ws]
+    h = F.leaky_relu(F.linear(rel_, wr[0], wr[1]), 0.1)
+    h = F.leaky_relu(F.linear(h, wr[2], wr[3]), 0.1)
+    ur = F.linear(h, wr[4], wr[5]).t()
+    assert rel(u, ur) < 1e-5
+    L, nseq = gh * gw, 4
+    q, k, v = (torch.randn(L * nseq, H * D, device=dev, generator=g).to(BF) for _ in range(3))
+    one = torch.ones(D, device=dev)
+    o = ops.cos_attn(q, k, v, one, one, H, L, None, 8.0, u, (gh, gw))
+    orf = _attn_ref(q, k, v, one, one, H, L, 8.0, ur, (gh, gw), (1, L, 0, 1))
+    assert rel(o.float(), orf) < 1e-2
+    do = torch.randn_like(orf)
+    o.backward(do.to(BF))
+    orf.backward(do.to(BF).float())
+    errs = [rel(a.grad, b_.grad) for a, b_ in zip(ws[:5], wr[:5])]
+    # the last bias adds a per-head constant to every score, which the softmax cancels: its exact
+    # gradient is 0 (the torch reference gives 9e-6), so it is held to the scale of the other grads
+    errs.append(((ws[5].grad - wr[5].grad).norm() / wr[4].grad.norm()).item())
+    assert max(errs) < 3e-2, errs
 
 
 @pytest.mark.gpu
