@@ -819,26 +819,52 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_bias_kernel(AP p, int nfc) {
       }
     }
   }
-  // bin the frame-summed dS once
-  if (qv) {
+  // bin the frame-summed dS once, without LDS float atomics (bit-reproducible): the 8 waves'
+  // (16 queries x key half) tiles go to LDS one at a time, over the K / V images (free now:
+  // 16 x 32 nc0 floats <= 2 Lp RS bytes), and each thread sums whole bins along their diagonals,
+  // bin (dh, dw) += sum over the tile's queries q of dS[q][q - (dh, dw)], in a fixed order
+  // (key half, query sub-block, query)
+  {
+    float* S = (float*)smem;
+    const int LH = nc0 * 32;
+    const int Wg = p.Wg, Hg = p.Hg, W2 = 2 * Wg - 1;
+    for (int part = 0; part < 8; ++part) {
+      const int ph = part >> 2, pq = part & 3;
+      __syncthreads();   // every wave past its last K / V read (part 0) / the previous tile's sums
+      if (khalf == ph && qsub == pq) {
 #pragma unroll
-    for (int ci = 0; ci < MAXCH; ++ci) {
-      const int c = c_begin + ci;
-      if (c < c_end) {
+        for (int ci = 0; ci < MAXCH; ++ci) {
+          const int c = c_begin + ci;
+          if (c < c_end) {
 #pragma unroll
-        for (int bi = 0; bi < 2; ++bi)
+            for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int key = c * 32 + 16 * bi + 4 * g + r;
-            if (key < L) atomicAdd(&bins[cq - kb[key]], acc[ci][bi][r]);
+              for (int r = 0; r < 4; ++r) S[li * LH + (c - c_begin) * 32 + 16 * bi + 4 * g + r] = acc[ci][bi][r];
           }
+        }
+      }
+      __syncthreads();
+      const int k0 = ph * LH, k1 = min(L, k0 + LH);
+      const int q0 = qg * 64 + pq * 16;
+      for (int b = tid; b < p.nbins; b += NT) {
+        const int dh = b / W2 - (Hg - 1), dw = b % W2 - (Wg - 1);
+        float sum = 0.f;
+        for (int j = 0; j < 16 && q0 + j < L; ++j) {
+          const int qi = q0 + j, kh = qi / Wg - dh, kw = qi % Wg - dw;
+          if (kh >= 0 && kh < Hg && kw >= 0 && kw < Wg) {
+            const int key = kh * Wg + kw;
+            if (key >= k0 && key < k1) sum += S[j * LH + key - k0];
+          }
+        }
+        bins[b] += sum;
       }
     }
   }
   __syncthreads();
   for (int i = tid; i < p.nbins; i += NT) {
     const float v = bins[i];
-    if (v != 0.f) atomicAdd(&p.dbias_u[(int64_t)h * p.nbins + i], v);
+    if (p.dbias_ws) p.dbias_ws[((int64_t)(qg * nfc + fc) * p.H + h) * p.nbins + i] = v;
+    else if (v != 0.f) atomicAdd(&p.dbias_u[(int64_t)h * p.nbins + i], v);
   }
 }
 
@@ -1640,7 +1666,7 @@ extern "C" int ctclip_attn_bwd_ws_floats(const ctclip_attn_args* a) {
   AP p;
   if (fill(p, a)) return 0;
   DqPlan pl;
-  if (!CTCLIP_ATTN_DIAG_BIN || !dq_plan(p, a->D, pl) || !pl.dma || (p.H * p.nbins) % 4) return 0;
+  if (!dq_plan(p, a->D, pl) || (pl.dma && !CTCLIP_ATTN_DIAG_BIN) || (p.H * p.nbins) % 4) return 0;
   return pl.nqg * pl.nfc * p.H * p.nbins;
 }
 
@@ -1668,7 +1694,7 @@ extern "C" int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream) {
     // frame-inner dQ + bias-gradient kernel (see attn_bwd_dq_bias_kernel)
     const int nqg = pl.nqg, nfc = pl.nfc;
     if (pl.lds > 160 * 1024) return CT_ESHAPE;
-    const bool slab = CTCLIP_ATTN_DIAG_BIN && pl.dma && p.dbias_ws && (p.H * p.nbins) % 4 == 0 &&
+    const bool slab = (CTCLIP_ATTN_DIAG_BIN || !pl.dma) && p.dbias_ws && (p.H * p.nbins) % 4 == 0 &&
                       a->dbias_ws_floats >= (int64_t)nqg * nfc * p.H * p.nbins;
     if (!slab) p.dbias_ws = nullptr;
     if (pl.dma)
