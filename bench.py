@@ -70,8 +70,21 @@ def cpu_baseline(batch, runs=3):
     import statistics
     from oracle import ctclip_oracle as O
     from oracle import weights as W
+    # BASELINE.md / SURVEY 8(d) ask for torch.set_num_threads(os.cpu_count()).  On the GPU box
+    # os.cpu_count() reports the whole host (all logical CPUs) while this process's cgroup gets a
+    # share of them (16 for one GPU, also exported as OMP_NUM_THREADS): more threads than that share
+    # only time-slice.  So: os.cpu_count(), capped by the cgroup CPU quota and OMP_NUM_THREADS,
+    # each cap stated in the line.
     threads = os.cpu_count() or 1
-    threads = min(threads, int(os.environ.get('OMP_NUM_THREADS', threads)))
+    caps = []
+    quota = _cgroup_cpus()
+    if quota is not None and quota < threads:
+        threads = quota
+        caps.append(f'cgroup CPU quota {quota}')
+    omp = os.environ.get('OMP_NUM_THREADS')
+    if omp and omp.isdigit() and int(omp) < threads:
+        threads = int(omp)
+        caps.append(f'OMP_NUM_THREADS={omp}')
     torch.set_num_threads(threads)
     cfg = O.BASE
     sd = W.make_state_dict(cfg)
@@ -111,10 +124,32 @@ def cpu_baseline(batch, runs=3):
         pass
     return {'value': round(batch / dt, 4), 'unit': 'pairs/s', 'cores': threads, 'kind': 'port',
             'sample': f'contrastive step (fwd+bwd+clip+Adam), base config, batch {batch}, 128-token text, fp32 '
-                      f'eager oracle on CPU ({cpu_name}, {threads} threads of {os.cpu_count()} logical CPUs): '
+                      f'eager oracle on CPU ({cpu_name}, {threads} threads of {os.cpu_count()} logical CPUs'
+                      f'{" -- capped by " + " and ".join(caps) if caps else ""}): '
                       f'1 warm-up ({warm:.1f} s) then median of {runs} steps '
                       f'({", ".join(f"{t:.1f}" for t in times)} s)',
             'step_s_median': round(dt, 3), 'step_s_runs': [round(t, 3) for t in times]}
+
+
+def _cgroup_cpus():
+    """CPUs of this process's cgroup quota (cgroup v2 cpu.max / v1 cfs), or None if unlimited."""
+    try:
+        q, per = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if q != 'max':
+            return max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us').read())
+        per = int(open('/sys/fs/cgroup/cpu/cpu.cfs_period_us').read())
+        if q > 0:
+            return max(1, q // per)
+    except (OSError, ValueError):
+        pass
+    try:
+        return len(os.sched_getaffinity(0)) if len(os.sched_getaffinity(0)) < (os.cpu_count() or 0) else None
+    except (AttributeError, OSError):
+        return None
 
 
 def rocprof_avg_ms(key):
@@ -265,9 +300,11 @@ def main():
                                     '(e4m3, e8m0 per 32 k), backward bf16'} if args.fp8 else {})},
         'loss': round(loss_v, 5),
     }
-    # the LayerNorm-fused GEMMs' in-launch tile-pair exchange never timed out (a timeout would have
-    # left wrong LayerNorm outputs behind; ctclip_gemm_ln's status word)
-    result['ln_exchange_ok'] = K.ln_fused_status() == 0
+    # the LayerNorm-fused GEMMs' in-launch tile-pair exchange never timed out: the trainer's own
+    # per-step check of ctclip_gemm_ln's status word (a timeout raises LayerNormExchangeError in
+    # train_step / flush and its step's Adam update is skipped on the device)
+    result['ln_exchange_ok'] = trainer.ln_steps_checked == args.warmup + args.steps
+    result['ln_exchange_steps_checked'] = trainer.ln_steps_checked
     if in_sync is not None:
         result['ranks_in_sync'] = in_sync
         result['dist'] = {'backend': dist.get_backend(), 'world_size': dist.get_world_size(),

@@ -57,6 +57,8 @@ struct P {
   unsigned long long* xchg;          // [2 tiles][M][2] {epoch, value} granules
   unsigned epoch;
   int* status;
+  unsigned spin_limit;               // polls before giving up on the partner (status = 1)
+  int ln_debug;                      // test knob: tile 1 of row block 0 never publishes
 };
 
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
@@ -931,7 +933,7 @@ typedef __attribute__((address_space(1))) int gi32;
 constexpr int LN_ST = p8::SMEM_P;                // [2 wr][128 rows][4 wc] float2 per-wave row values
 constexpr int LN_FIN = LN_ST + 2 * 128 * 4 * 8;  // [256 rows] float2 (mean, rstd) / (mean g, mean g xh)
 constexpr int SMEM_LN = LN_FIN + 256 * 8;
-constexpr unsigned LN_SPIN_LIMIT = 1u << 21;     // ~0.1 s of polling before giving up
+constexpr unsigned LN_SPIN_LIMIT = 1u << 21;     // default: ~0.1 s of polling before giving up
 
 // merge two equal-count (mean, M2) partials; symmetric in its arguments, so the lanes / tiles of
 // a pair that merge (a, b) and (b, a) agree bit for bit
@@ -1083,8 +1085,10 @@ __device__ __forceinline__ void epilogue_ln(const P& p, f32x4 (&acc)[8][4], char
         a1[h] = (s0.y + s1.y) + (s2.y + s3.y);
       }
       gu64* g = X + ((int64_t)tx * p.M + wrow0 + r) * 2;
-      __hip_atomic_store(g, tag | __float_as_uint(a0[h]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(g + 1, tag | __float_as_uint(a1[h]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!(p.ln_debug && tx == 1 && m0 == 0)) {   // (test knob: a partner that never publishes)
+        __hip_atomic_store(g, tag | __float_as_uint(a0[h]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(g + 1, tag | __float_as_uint(a1[h]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     const gu64* Y = X + (int64_t)(1 - tx) * p.M * 2;
     unsigned long long q[2][2];
@@ -1098,7 +1102,7 @@ __device__ __forceinline__ void epilogue_ln(const P& p, f32x4 (&acc)[8][4], char
           ok = ok && (unsigned)(q[h][k] >> 32) == p.epoch;
         }
       if (__all(ok)) break;
-      if (spins >= LN_SPIN_LIMIT) {
+      if (spins >= p.spin_limit) {
         if (lane == 0 && p.status) __hip_atomic_store((gi32*)p.status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -1642,6 +1646,8 @@ extern "C" int ctclip_gemm_ln(const ctclip_gemm_args* a, const ctclip_ln_epilogu
   p.xchg = (unsigned long long*)ln->xchg;
   p.epoch = ln->epoch;
   p.status = ln->status;
+  p.spin_limit = ln->spin_limit ? ln->spin_limit : LN_SPIN_LIMIT;
+  p.ln_debug = ln->debug;
   hipStream_t st = (hipStream_t)stream;
   if (!a->a_kcontig) return CT_EINVAL;
   if (ln->mode == 1) return a->b_kcontig ? launch8<true, true, -6>(p, 1, st) : launch8<true, false, -6>(p, 1, st);

@@ -51,7 +51,8 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
                                                    float* __restrict__ m, float* __restrict__ v, int64_t n, int head,
                                                    float lr, float b1, float b2, float eps, float wd, float bc1,
                                                    float bc2_sqrt, const float* __restrict__ coef,
-                                                   u16* __restrict__ pb, u16* __restrict__ pbl, int zero_grad) {
+                                                   u16* __restrict__ pb, u16* __restrict__ pbl, int zero_grad,
+                                                   const int* __restrict__ skip) {
   const float c = coef ? coef[1] : 1.f;
   const float step = lr / bc1;
   const int64_t n4 = (n - head) >> 2;
@@ -59,6 +60,20 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
   f32x4* g4 = (f32x4*)(g + head);
   f32x4* m4 = (f32x4*)(m + head);
   f32x4* v4 = (f32x4*)(v + head);
+  // the step's guard word (the LayerNorm-fused GEMM status): a step whose forward produced wrong
+  // LayerNorm outputs is dropped -- parameters and moments stay as they are, its gradients are
+  // cleared (zero_grad) so they do not leak into a later step
+  if (skip && *skip) {
+    if (!zero_grad) return;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x)
+      g4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (blockIdx.x == 0 && threadIdx.x < 8) {
+      const int t = threadIdx.x;
+      const int64_t i = t < 4 ? (t < head ? t : -1) : head + 4 * n4 + (t - 4);
+      if (i >= 0 && i < n) g[i] = 0.f;
+    }
+    return;
+  }
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
     f32x4 pi = p4[i], gi = g4[i], mi = m4[i], vi = v4[i];
     float o[4];
@@ -111,7 +126,7 @@ extern "C" int ctclip_grad_norm(const float* g, int64_t n, float max_norm, float
 
 extern "C" int ctclip_adam(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2,
                            float eps, float wd, int32_t step, const float* coef, void* p_bf16, void* p_bf16_lo,
-                           int32_t zero_grad, void* stream) {
+                           int32_t zero_grad, const int32_t* skip, void* stream) {
   const float bc1 = 1.f - powf(b1, (float)step);
   const float bc2 = sqrtf(1.f - powf(b2, (float)step));
   if (n <= 0) return 0;
@@ -123,7 +138,7 @@ extern "C" int ctclip_adam(float* p, float* g, float* m, float* v, int64_t n, fl
   const int64_t n4 = (n - head) / 4;
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(4096, (n4 + 255) / 256));
   hipLaunchKernelGGL(adam_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, head, lr, b1, b2,
-                     eps, wd, bc1, bc2, coef, (u16*)p_bf16, (u16*)p_bf16_lo, zero_grad);
+                     eps, wd, bc1, bc2, coef, (u16*)p_bf16, (u16*)p_bf16_lo, zero_grad, skip);
   CT_CHECK_LAUNCH();
   return 0;
 }

@@ -58,6 +58,7 @@ class LnEpilogueArgs(ctypes.Structure):
         ('part_gamma', c_vp), ('part_beta', c_vp),
         ('xchg', c_vp), ('epoch', ctypes.c_uint32),
         ('status', c_vp),
+        ('spin_limit', ctypes.c_uint32), ('debug', c_i32),
     ]
 
 
@@ -171,7 +172,7 @@ _SIGS = {
     'ctclip_embed_bwd': [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
     'ctclip_grad_norm': [c_vp, c_i64, c_f32, c_vp, c_i32, c_vp, c_vp],
     'ctclip_adam': [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_i32, c_vp, c_vp, c_vp, c_i32,
-                    c_vp],
+                    c_vp, c_vp],
 }
 
 

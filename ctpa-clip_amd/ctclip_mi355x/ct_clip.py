@@ -83,6 +83,15 @@ class CTCLIP(nn.Module):
         pt = torch.load(str(path), map_location='cpu', weights_only=True)
         return self.load_state_dict(pt, strict=False)
 
+    def state_dict(self, *args, **kwargs):
+        """The reference key layout; a text-tower Adam the trainer deferred to the next step
+        (CTClipTrainer(defer_text_adam=True)) is queued first, so the weights read are current."""
+        for p in self.text_transformer.parameters():
+            if p.is_cuda:
+                streams.flush_text(p.device)
+            break
+        return super().state_dict(*args, **kwargs)
+
     # ------------------------------------------------------------------ helpers
     def _visual_weight_bf16(self, W):
         """bf16 to_visual_latent weight (151 M parameters): the Adam-kept shadow when W trains,

@@ -421,9 +421,10 @@ class ViTLayerFn(torch.autograd.Function):
         streams.mark_image_head(xf.device, 'attn')   # deferred text-stream work may start (streams.py)
         o, lse = K.attn_fwd(qn, kn, kv[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
                             bias_u=bias_u if use_bias else None, grid=(geo.Hg, geo.Wg) if use_bias else (0, 0))
-        fused = None if fp8 else K.linear_residual_ln(o, Wo_b, x1f, ff_w, ff_b, 1e-5)
+        # to_out + residual + the FeedForward's LayerNorm in one launch (gemm256.hip, EP -6) -- only
+        # where a caller checks the launch's status word every step (kernels.ln_guard: the trainer)
+        fused = None if fp8 or not K.ln_guarded() else K.linear_residual_ln(o, Wo_b, x1f, ff_w, ff_b, 1e-5)
         if fused is not None:
-            # to_out + residual + the FeedForward's LayerNorm in one launch (gemm256.hip, EP -6)
             x2f, x2b, xn2, m2, r2 = fused
         else:
             x2b = torch.empty_like(xb)
@@ -469,7 +470,8 @@ class ViTLayerFn(torch.autograd.Function):
         M_ = dx3b.shape[0]
         dW2p = K.matmul_tn(dx3b, g, tag='dw', flops=2.0 * M_ * W2.shape[0] * W2.shape[1])
         # dx2 = LN'(dh . W1) + dx3 in one launch where the shape allows (gemm256.hip, EP -7)
-        fused = K.matmul_nn_ln_bwd(dh_, W1p, x2b, m2, r2, ff_w, dx3f, dgamma_out=gsink(ff_w), dbeta_out=gsink(ff_b))
+        fused = K.matmul_nn_ln_bwd(dh_, W1p, x2b, m2, r2, ff_w, dx3f, dgamma_out=gsink(ff_w),
+                                   dbeta_out=gsink(ff_b)) if K.ln_guarded() else None
         if fused is None:
             if _DXN2_BLAS:    # A/B: hipBLASLt (torch.matmul) for this plain bf16 GEMM, W1 packed K-contiguous
                 dxn2 = torch.matmul(dh_, W1p.t().contiguous().t())
@@ -497,7 +499,7 @@ class ViTLayerFn(torch.autograd.Function):
         dq = torch.empty_like(q)
         K.l2norm_scale_bwd(q, dqn, H, dh, q_scale, dq, ds_out=gsink(q_scale))
         K.l2norm_scale_bwd(kv[:, :inner], dkn, H, dh, k_scale, dkv[:, :inner], ds_out=gsink(k_scale))
-        fusable = K.ln_fusable(dq.shape[0], Wq_b.shape[1], bwd=True)
+        fusable = K.ln_guarded() and K.ln_fusable(dq.shape[0], Wq_b.shape[1], bwd=True)
         if not fusable:
             dxn = K.matmul_nn(dq, Wq_b)
         K.matmul_tn(dq, xn, out=gsink(Wq), accumulate=True, tag='dw')

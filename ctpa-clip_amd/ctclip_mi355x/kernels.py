@@ -178,6 +178,43 @@ LN_FUSED_BWD = os.environ.get('CTCLIP_LN_FUSED_BWD', '0') != '0'
 _XCHG = {}       # (device, stream) -> [int64 buffer, last epoch]
 _LN_STATUS = {}  # device -> int32[1], set by a launch whose partner statistics never arrived
 _CT_EINVAL, _CT_ESHAPE = 1001, 1003
+# Fail loud: the exchange's partner wait is bounded, and a launch that gives up leaves
+# wrong LayerNorm outputs and sets the device status word.  The fused form is therefore only used
+# where something reads that word every step: inside ``ln_guard()`` (trainer.CTClipTrainer wraps
+# its forward / backward in it, passes the word to the Adam kernel as its skip guard -- a step with
+# a timed-out exchange is never applied -- and raises ``LayerNormExchangeError`` on the host, at
+# the latest two steps later, or in ``check()`` / ``flush()``).  Elsewhere the GEMM and the
+# LayerNorm kernel run separately.
+_LN_GUARD = [0]
+_LN_DEBUG = {'skip_publish': 0, 'spin_limit': 0}
+
+
+class _LnGuard:
+    def __enter__(self):
+        _LN_GUARD[0] += 1
+        return self
+
+    def __exit__(self, *exc):
+        _LN_GUARD[0] -= 1
+        return False
+
+
+def ln_guard():
+    """Context in which the model may use the LayerNorm-fused GEMMs: the caller promises to read
+    ``ln_status_tensor`` (trainer.CTClipTrainer does, every step)."""
+    return _LnGuard()
+
+
+def ln_guarded():
+    return _LN_GUARD[0] > 0
+
+
+def set_ln_debug(skip_publish=False, spin_limit=0):
+    """Test knob: tile 1 of row block 0 never publishes its statistics (its partner times out after
+    ``spin_limit`` polls, 0 = the library default ~0.1 s).  Returns the previous setting."""
+    old = dict(_LN_DEBUG)
+    _LN_DEBUG['skip_publish'], _LN_DEBUG['spin_limit'] = int(bool(skip_publish)), int(spin_limit)
+    return old
 
 
 def _xchg(M, device):
@@ -193,11 +230,22 @@ def _xchg(M, device):
     return e[0], e[1]
 
 
-def _ln_status(device):
-    s = _LN_STATUS.get(device.index)
+def ln_status_tensor(device):
+    """The device's sticky int32[1] status word of the LayerNorm-fused GEMMs (created zeroed)."""
+    device = torch.device(device)
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _LN_STATUS.get(idx)
     if s is None:
-        s = _LN_STATUS[device.index] = torch.zeros(1, dtype=torch.int32, device=device)
+        s = _LN_STATUS[idx] = torch.zeros(1, dtype=torch.int32, device=torch.device('cuda', idx))
     return s
+
+
+_ln_status = ln_status_tensor
+
+
+def reset_ln_status(device=None):
+    """Clear the status word (after handling a LayerNormExchangeError)."""
+    ln_status_tensor(device or torch.device('cuda', torch.cuda.current_device())).zero_()
 
 
 def ln_fused_status(device=None):
@@ -224,6 +272,7 @@ def _gemm_ln(M, K, A, B, b_kcontig, C, C2, R, ln, tag=None, flops=None):
     xb, ep = _xchg(M, A.device)
     ln.xchg, ln.epoch = ptr(xb), ep
     ln.status = ptr(_ln_status(A.device))
+    ln.spin_limit, ln.debug = _LN_DEBUG['spin_limit'], _LN_DEBUG['skip_publish']
     end = TIMER(tag, flops if flops is not None else 2.0 * M * 512 * K) if tag else None
     rc = _lib.lib().ctclip_gemm_ln(_lib.ctypes.byref(a), _lib.ctypes.byref(ln), stream_ptr())
     if rc in (_CT_EINVAL, _CT_ESHAPE):
@@ -767,6 +816,12 @@ def vq_ema_accum(idx, xn, bins, esum):
     """bins (f32 counts) and esum (int64 [C][D], token sums in 2^-40 fixed point: bit-identical
     whatever order the adds land in) accumulate the EMA statistics of rows xn (unit vectors)."""
     assert esum.dtype == torch.int64 and bins.dtype == F32
+    # the 2^-40 fixed-point sums stay exact while every code's GLOBAL row count (summed over ranks
+    # by dist_sync.sum_codebook_stats) is below 2^23; the f32 bins are exact below 2^24
+    from . import dist_sync
+    if xn.shape[0] * dist_sync.world_rank()[0] >= (1 << 23):
+        raise ValueError(f'vq_ema_accum: {xn.shape[0]} rows x {dist_sync.world_rank()[0]} ranks may exceed the 2^23 '
+                         'rows per code that the int64 2^-40 fixed-point sums hold exactly')
     call('ctclip_vq_ema_accum', ptr(idx), ptr(xn), xn.shape[0], xn.shape[1], ptr(bins), ptr(esum), stream_ptr())
 
 
@@ -891,9 +946,12 @@ def weights_epoch():
     return _WEIGHTS_EPOCH[0]
 
 
-def adam(p, g, m, v, *, lr, b1, b2, eps, wd, step, coef=None, p_bf16=None, p_bf16_lo=None, zero_grad=False):
+def adam(p, g, m, v, *, lr, b1, b2, eps, wd, step, coef=None, p_bf16=None, p_bf16_lo=None, zero_grad=False,
+         skip=None):
+    """skip: optional device int32[1] guard word; when nonzero the launch changes nothing."""
+    assert skip is None or (skip.dtype == torch.int32 and skip.is_cuda)
     call('ctclip_adam', ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), lr, b1, b2, eps, wd, step, ptr(coef), ptr(p_bf16),
-         ptr(p_bf16_lo), int(zero_grad), stream_ptr())
+         ptr(p_bf16_lo), int(zero_grad), ptr(skip), stream_ptr())
     _WEIGHTS_EPOCH[0] += 1
 
 

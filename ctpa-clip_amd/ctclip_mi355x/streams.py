@@ -117,3 +117,15 @@ def flush_text(dev):
         ts.wait_event(head)
     with torch.cuda.stream(ts):
         fn()
+
+
+def pending_text(dev):
+    """True while deferred text-stream work of ``dev`` waits to be queued."""
+    return dev.type == 'cuda' and _idx(dev) in _PENDING
+
+
+def drop_text(dev):
+    """Forget the deferred work of ``dev`` (error paths)."""
+    if dev.type == 'cuda':
+        _PENDING.pop(_idx(dev), None)
+        _HEAD_EV.pop(_idx(dev), None)

@@ -8,6 +8,7 @@ never syncs the host: the clip coefficient stays on the device).
 """
 from __future__ import annotations
 
+import collections
 import os
 
 import torch
@@ -82,6 +83,13 @@ class FlatParams:
                 p.grad = g
 
 
+class LayerNormExchangeError(RuntimeError):
+    """A LayerNorm-fused GEMM (kernels.linear_residual_ln, gemm256.hip EP -6 / -7) gave up waiting for
+    its partner tile's row statistics: that step's LayerNorm outputs were wrong.  The step's Adam
+    update was not applied (the status word is the Adam kernel's skip guard); later steps are not
+    applied either until ``kernels.reset_ln_status()``."""
+
+
 # queue BERT's backward before the 3D-ViT's (CTCLIP_TEXT_FIRST=0: after it, the r02 order; A/B)
 TEXT_FIRST = os.environ.get('CTCLIP_TEXT_FIRST', '1') != '0'
 
@@ -141,6 +149,13 @@ class CTClipTrainer:
         self.steps = 0
         self.norm = torch.zeros(2, device=dev, dtype=torch.float32)
         self.world = dist_sync.world_rank()[0]
+        # per-step host check of the LayerNorm-fused GEMMs' status word (kernels.ln_guard): an async
+        # copy into pinned memory after each step, read once its event completed -- never more than
+        # two steps after the step it covers, so the host stays up to two steps ahead of the GPU
+        self._guard = dev.type == 'cuda'
+        self._ln_pending = collections.deque()       # (step, event, pinned int32[1])
+        self._ln_host = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(4)] if self._guard else []
+        self.ln_steps_checked = 0
 
     def _fold_bucket(self, tag):
         self.flat.rebind_grads(self.bucket_params.get(tag, ()))
@@ -173,6 +188,14 @@ class CTClipTrainer:
         return loss
 
     def optimizer_step(self):
+        if streams.pending_text(self.device):
+            # the previous step's deferred text Adam was never queued (no text-tower forward ran
+            # since): this step's text gradients were summed onto that step's and the shared clip
+            # coefficient is about to be overwritten -- refuse rather than train on mixed gradients
+            streams.drop_text(self.device)
+            raise RuntimeError('CTClipTrainer: a deferred text-tower Adam is still pending at optimizer_step '
+                               '(defer_text_adam needs a text-tower forward between optimizer steps; call '
+                               'flush() after the last train_step)')
         # SUM (ClipLossFn gives each rank its own rows): buckets already in flight since their
         # tower's backward finished; the last one goes out here and all are waited on.  BERT's
         # backward ran on the text stream (streams.py): order the norm / Adam after it.
@@ -220,21 +243,62 @@ class CTClipTrainer:
                 self._adam(off, n)
 
     def flush(self):
-        """Queue any deferred text-bucket Adam (``defer_text_adam``) now: call after the last
-        ``train_step`` before reading the parameters."""
+        """Queue any deferred text-bucket Adam (``defer_text_adam``) now and verify every step's
+        LayerNorm-exchange status (synchronises): call after the last ``train_step`` before reading
+        the parameters."""
         streams.flush_text(self.device)
+        self.check()
+
+    def check(self):
+        """Wait for every queued step-status copy and raise LayerNormExchangeError if a step's
+        LayerNorm-fused GEMM timed out."""
+        self._check_ln(block_upto=self.steps)
+
+    def _queue_ln_check(self):
+        if not self._guard:
+            return
+        host = self._ln_host[self.steps % len(self._ln_host)]
+        host.copy_(K.ln_status_tensor(self.device), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._ln_pending.append((self.steps, ev, host))
+
+    def _check_ln(self, block_upto):
+        """Consume the status copies: those of steps <= block_upto are waited for, newer ones are
+        read only if already complete."""
+        while self._ln_pending:
+            step, ev, host = self._ln_pending[0]
+            if step <= block_upto:
+                ev.synchronize()
+            elif not ev.query():
+                break
+            self._ln_pending.popleft()
+            if int(host[0]) != 0:
+                self._ln_pending.clear()
+                raise LayerNormExchangeError(
+                    f'LayerNorm-fused GEMM exchange timed out (status word set by step {step} or earlier): '
+                    'its LayerNorm outputs were wrong and the Adam update of that step was skipped on the '
+                    'device; kernels.reset_ln_status() clears the word (CTCLIP_LN_FUSED=0 runs the unfused '
+                    'GEMM + LayerNorm pair instead)')
+            self.ln_steps_checked = step
 
     def _adam(self, off, n, step=None):
         sl = slice(off, off + n)
         K.adam(self.flat.data[sl], self.flat.grad[sl], self.m[sl], self.v[sl], lr=self.lr, b1=self.betas[0],
                b2=self.betas[1], eps=self.eps, wd=self.wd, step=self.steps if step is None else step, coef=self.norm,
                p_bf16=self.flat.bf16[sl] if self.flat.bf16 is not None else None,
-               p_bf16_lo=self.flat.bf16_lo[sl] if self.flat.bf16_lo is not None else None, zero_grad=True)
+               p_bf16_lo=self.flat.bf16_lo[sl] if self.flat.bf16_lo is not None else None, zero_grad=True,
+               skip=K.ln_status_tensor(self.device) if self._guard else None)
         self.flat.sync_shadows(off, off + n)
 
     def train_step(self, text, video):
-        """One contrastive step; returns the loss tensor (no host sync)."""
+        """One contrastive step; returns the loss tensor (no host sync).  Raises
+        LayerNormExchangeError once the status copy of an earlier step shows a timed-out LayerNorm
+        exchange (at the latest two steps later; ``check()`` / ``flush()`` wait for all)."""
+        self._check_ln(block_upto=self.steps - 2)
         self.model.train()
-        loss = self.forward_backward(text, video)
+        with K.ln_guard():
+            loss = self.forward_backward(text, video)
         self.optimizer_step()
+        self._queue_ln_check()
         return loss.detach()

@@ -114,7 +114,12 @@ int ctclip_layernorm_bwd_drop(const void* dy, int32_t dy_f32, int64_t lddy, cons
  * otherwise CT_EINVAL / CT_ESHAPE and nothing runs (call the two kernels instead).
  * xchg: >= 4 * M u64 words, zeroed once when allocated; epoch: nonzero and different from every
  * earlier launch on that buffer; launches sharing one xchg buffer must be stream-ordered.
- * status (optional): set to 1 if a partner tile's statistics never arrived (bounded wait). */
+ * status (optional): set to 1 if a partner tile's statistics never arrived (bounded wait: spin_limit
+ * polls, 0 = the default ~0.1 s); the outputs of that launch are then wrong.  The status word is
+ * sticky (never cleared by the library): the trainer passes it to ctclip_adam as its skip guard, so a
+ * step with a timed-out exchange is never applied, and checks it on the host once per step
+ * (ctclip_mi355x.trainer: the step raises).  debug != 0 (tests only): the second tile of row block 0
+ * never publishes, so its partner times out. */
 typedef struct {
   int32_t mode;
   const float* gamma; const float* beta; float eps;
@@ -124,6 +129,8 @@ typedef struct {
   float* part_gamma; float* part_beta;
   void* xchg; uint32_t epoch;
   int32_t* status;
+  uint32_t spin_limit;
+  int32_t debug;
 } ctclip_ln_epilogue;
 int ctclip_gemm_ln(const ctclip_gemm_args* a, const ctclip_ln_epilogue* ln, void* stream);
 
@@ -384,11 +391,15 @@ int ctclip_embed_bwd(const int64_t* ids, int64_t B, int32_t L, int32_t Hd, const
  * grad norm -> out[0] = norm, out[1] = clip coef (torch clip_grad_norm_ semantics);
  * Adam over a flat arena (optimizer.py:24), grads scaled by coef[1], bf16 copy refreshed;
  * zero_grad != 0 also zeroes g in the same pass (the trainer's zero_grad, CTCLIPTrainer.py:353).
+ * skip (optional device int32): when *skip != 0 the step is dropped: p, m, v unchanged, g zeroed if
+ * zero_grad (the step's guard word:
+ * the LayerNorm-fused GEMM status of ctclip_gemm_ln).
  * p, g, m, v must share one alignment modulo 16 B (slices of arenas with one layout): CT_EALIGN. */
 int ctclip_grad_norm(const float* g, int64_t n, float max_norm, float* part, int32_t nblk, float* out, void* stream);
 int ctclip_adam(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
                 float wd, int32_t step, const float* coef, void* p_bf16, void* p_bf16_lo, int32_t zero_grad,
-                void* stream);   /* p_bf16_lo (needs p_bf16): bf16(p - bf16(p)), the split-weight lo image */
+                const int32_t* skip, void* stream);   /* p_bf16_lo (needs p_bf16): bf16(p - bf16(p)), the
+                                                       * split-weight lo image */
 
 /* ---------------------------------------------------------------- volume preprocessing
  * Replaces the host-side per-sample loader arithmetic:

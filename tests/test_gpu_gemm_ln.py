@@ -150,8 +150,9 @@ def test_transformer_layer_fused_vs_unfused(K):
         for p in tr.parameters():
             p.grad = None
         xf = xf0.clone().requires_grad_(True)
-        yf, yb = tr.run(xf, xb0, geo)
-        yf.backward(dy)
+        with K.ln_guard():        # the model uses the fused forms only under a status reader
+            yf, yb = tr.run(xf, xb0, geo)
+            yf.backward(dy)
         torch.cuda.synchronize()
         return yf.detach(), xf.grad, [p.grad.clone() for p in tr.parameters() if p.grad is not None]
 
@@ -167,3 +168,60 @@ def test_transformer_layer_fused_vs_unfused(K):
     for a, b, c in zip(g0, g1, g2):
         assert _rel(b, a) < 2e-2 and _rel(c, a) < 2e-2
     assert K.ln_fused_status() == 0
+
+
+def test_train_step_raises_on_exchange_timeout(K):
+    """Fail loud: a partner tile that never publishes its row statistics (test knob)
+    makes the exchange time out.  The trainer's step then (1) is not applied on the device -- the
+    status word is the Adam kernel's skip guard, so parameters stay bit-identical -- and (2) raises
+    LayerNormExchangeError on the host (train_step two steps later at the latest, check() / flush()
+    at once).  A healthy step before it passes the same per-step check."""
+    import types
+    from ctclip_mi355x.bert import BertConfig
+    from ctclip_mi355x.models import build_ctclip, set_finetune_trainable
+    from ctclip_mi355x.trainer import CTClipTrainer, LayerNormExchangeError
+    torch.manual_seed(0)
+    # 2 x 40 x 320 x 320 volumes -> 2 x 4 x 16 x 16 = 2,048 tokens: the fused LayerNorm GEMM's shape
+    vit = dict(image_size=320, codebook_size=512, spatial_depth=1, temporal_depth=1)
+    bert = BertConfig(vocab_size=1000, hidden_size=768, num_hidden_layers=1, num_attention_heads=12,
+                      intermediate_size=3072, max_position_embeddings=64, hidden_dropout_prob=0.0,
+                      attention_probs_dropout_prob=0.0)
+    model = set_finetune_trainable(build_ctclip(vit, bert)).cuda()
+    g = torch.Generator(device='cuda').manual_seed(7)
+    hu = torch.randint(-1200, 1201, (2, 1, 40, 320, 320), generator=g, device='cuda', dtype=torch.int32).to(torch.int16)
+    ids = torch.randint(5, 1000, (2, 32), generator=g, device='cuda')
+    ids[:, 0], ids[:, -1] = 2, 3
+    text = types.SimpleNamespace(input_ids=ids, attention_mask=torch.ones_like(ids))
+    K.reset_ln_status()
+    calls = []
+    orig = K.linear_residual_ln
+
+    def spy(*a, **kw):
+        out = orig(*a, **kw)
+        calls.append(out is not None)
+        return out
+    K.linear_residual_ln = spy
+    tr = CTClipTrainer(model)
+    try:
+        tr.train_step(text, hu)
+        tr.check()                                    # healthy step: checked, no error
+        assert calls and all(calls), 'the fused LayerNorm GEMM did not run in the train step'
+        assert tr.ln_steps_checked == 1 and K.ln_fused_status() == 0
+        before = tr.flat.data.clone()
+        m_before = tr.m.clone()
+        old = K.set_ln_debug(True, spin_limit=1 << 12)
+        try:
+            with pytest.raises(LayerNormExchangeError):
+                for _ in range(3):                    # raises by the third call at the latest
+                    tr.train_step(text, hu)
+                tr.check()
+        finally:
+            K.set_ln_debug(**old)
+        torch.cuda.synchronize()
+        assert K.ln_fused_status() == 1
+        assert torch.equal(tr.flat.data, before) and torch.equal(tr.m, m_before), \
+            'a step with a timed-out LayerNorm exchange was applied'
+        assert float(tr.flat.grad.abs().max()) == 0.0      # the dropped step's gradients were cleared
+    finally:
+        K.linear_residual_ln = orig
+        K.reset_ln_status()
