@@ -43,6 +43,8 @@ def parse():
                     help='configs[3]: the 3D-ViT forward linears as MX-fp8 GEMMs (default batch 16 per GPU)')
     ap.add_argument('--text-len', type=int, default=128)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-precise', action='store_true',
+                    help='skip the f32-image-tower mode measurement (precise_f32_tower entry)')
     ap.add_argument('--cpu-batch', type=int, default=2)
     ap.add_argument('--dist-backend', default='nccl', choices=['nccl', 'gloo'],
                     help='gloo: rehearse the N>1 path with several ranks sharing one GPU (not a bench number)')
@@ -258,6 +260,40 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     K.TIMER.stop()
+    loss_v = float(loss.item())
+    precise_entry = None
+    if not args.no_precise and not args.fp8:
+        # the trainable f32 image-tower mode (precise.py: exact-f32 forward, bf16 backward; the SURVEY
+        # 8(c) contract on the loss the step differentiates): same workload, after the timed region
+        from ctclip_mi355x import precise
+        with precise.vit_precision_scope('f32'):
+            for _ in range(2):
+                trainer.train_step(text, hu)
+            trainer.flush()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            n_p = 5
+            t1 = time.perf_counter()
+            for _ in range(n_p):
+                lp = trainer.train_step(text, hu)
+            trainer.flush()
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            el_p = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([el_p], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el_p = t.item()
+        precise_entry = {'value': round(world * args.batch * n_p / el_p, 3), 'unit': 'pairs/s', 'steps': n_p,
+                         'warmup': 2, 'ms_per_step': round(1000 * el_p / n_p, 3),
+                         'vs_bf16_step': round(el_p / n_p / (elapsed / args.steps), 3),
+                         'loss': round(float(lp.item()), 5),
+                         'mode': "precise.set_vit_precision('f32'): exact-f32 image-tower forward (f32 MFMA GEMMs, "
+                                 "f32 PEG / LayerNorm / cosine attention), bf16 backward; same workload"}
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -273,7 +309,6 @@ def main():
     ff1 = K.TIMER.summary('ff1')
     dw = K.TIMER.summary('dw')
     vit_ms = sum(s.elapsed_time(e) for s, e in vit_events) / max(1, len(vit_events))
-    loss_v = float(loss.item())
 
     pairs = world * args.batch * args.steps
     value = pairs / elapsed
@@ -305,6 +340,8 @@ def main():
     # train_step / flush and its step's Adam update is skipped on the device)
     result['ln_exchange_ok'] = trainer.ln_steps_checked == args.warmup + args.steps
     result['ln_exchange_steps_checked'] = trainer.ln_steps_checked
+    if precise_entry is not None:
+        result['precise_f32_tower'] = precise_entry
     if in_sync is not None:
         result['ranks_in_sync'] = in_sync
         result['dist'] = {'backend': dist.get_backend(), 'world_size': dist.get_world_size(),

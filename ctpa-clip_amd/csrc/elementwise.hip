@@ -45,10 +45,11 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(const u16* __restrict__ d
 }
 
 // dst[r][c] (bf16, ld_dst) = src[map[r]][c] * (colscale ? colscale[c] : 1), zero if map[r] < 0 or c >= cols
+template <typename OUT>
 __global__ __launch_bounds__(256) void pack_rows_kernel(const float* __restrict__ src, int64_t ld_src,
                                                         const int32_t* __restrict__ map, int64_t rows_dst,
                                                         int cols, int cols_dst, const float* __restrict__ colscale,
-                                                        u16* __restrict__ dst, int64_t ld_dst) {
+                                                        OUT* __restrict__ dst, int64_t ld_dst) {
   const int64_t total = rows_dst * cols_dst;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = i / cols_dst;
@@ -59,7 +60,8 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const float* __restrict_
       v = src[sr * ld_src + c];
       if (colscale) v *= colscale[c];
     }
-    dst[r * ld_dst + c] = f2bf(v);
+    if constexpr (sizeof(OUT) == 2) dst[r * ld_dst + c] = f2bf(v);
+    else dst[r * ld_dst + c] = v;
   }
 }
 
@@ -133,8 +135,17 @@ extern "C" int ctclip_gelu_bwd(const void* dy, const void* pre, void* dx, int64_
 
 extern "C" int ctclip_pack_rows(const float* src, int64_t ld_src, const int32_t* map, int64_t rows_dst, int32_t cols,
                                 int32_t cols_dst, const float* colscale, void* dst, int64_t ld_dst, void* stream) {
-  hipLaunchKernelGGL(pack_rows_kernel, dim3(grid_for(rows_dst * cols_dst)), dim3(256), 0, (hipStream_t)stream, src,
-                     ld_src, map, rows_dst, cols, cols_dst, colscale, (u16*)dst, ld_dst);
+  hipLaunchKernelGGL(pack_rows_kernel<u16>, dim3(grid_for(rows_dst * cols_dst)), dim3(256), 0, (hipStream_t)stream,
+                     src, ld_src, map, rows_dst, cols, cols_dst, colscale, (u16*)dst, ld_dst);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_pack_rows_f32(const float* src, int64_t ld_src, const int32_t* map, int64_t rows_dst,
+                                    int32_t cols, int32_t cols_dst, const float* colscale, float* dst, int64_t ld_dst,
+                                    void* stream) {
+  hipLaunchKernelGGL(pack_rows_kernel<float>, dim3(grid_for(rows_dst * cols_dst)), dim3(256), 0, (hipStream_t)stream,
+                     src, ld_src, map, rows_dst, cols, cols_dst, colscale, dst, ld_dst);
   CT_CHECK_LAUNCH();
   return 0;
 }

@@ -89,6 +89,22 @@ class AttnArgs(ctypes.Structure):
     ]
 
 
+class SgemmTnArgs(ctypes.Structure):
+    """ctclip_sgemm_tn_args (include/ctclip_hip.h): the f32 image tower's exact-f32 GEMM."""
+    _fields_ = [
+        ('M', c_i64), ('N', c_i64), ('K', c_i64),
+        ('A', c_vp), ('lda', c_i64),
+        ('B', c_vp), ('ldb', c_i64),
+        ('C', c_vp), ('ldc', c_i64),
+        ('C2', c_vp), ('ldc2', c_i64),
+        ('C3', c_vp), ('ldc3', c_i64),
+        ('bias', c_vp),
+        ('R', c_vp), ('ldr', c_i64),
+        ('alpha', c_f32),
+        ('act', c_i32),
+    ]
+
+
 class ResampleArgs(ctypes.Structure):
     _fields_ = [
         ('src', c_vp), ('src_dtype', c_i32),
@@ -131,6 +147,8 @@ _SIGS = {
     'ctclip_geglu_bwd': [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
     'ctclip_gelu_bwd': [c_vp, c_vp, c_vp, c_i64, c_vp],
     'ctclip_pack_rows': [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp],
+    'ctclip_pack_rows_f32': [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp],
+    'ctclip_sgemm_tn': [ctypes.POINTER(SgemmTnArgs), c_vp],
     'ctclip_unpack_rows': [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp],
     'ctclip_gelu_f32': [c_vp, c_vp, c_i64, c_vp],
     'ctclip_cast_f32_bf16': [c_vp, c_vp, c_i64, c_vp],

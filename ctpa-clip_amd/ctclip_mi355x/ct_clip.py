@@ -110,9 +110,7 @@ class CTCLIP(nn.Module):
         return self._wvis[1]
 
     def _project(self, W, Wb, pooled, pooled_b):
-        from . import precise
-        if precise.vit_precision() == 'f32' and not (torch.is_grad_enabled() and W.requires_grad):
-            return precise.project_f32(W, pooled)       # the opt-in f32 image tower, exact f32
+        # (in the f32 image-tower mode ImageProjFn's forward is the exact-f32 product, precise.py)
         return Fn.ImageProjFn.apply(pooled, pooled_b, W, Wb)
 
     def encode(self, text, image, gather=False):

@@ -12,7 +12,6 @@ from . import dist_sync
 from . import streams
 from . import functional as Fn
 from . import kernels as K
-from . import precise
 from .attention import ContinuousPositionBias, Transformer
 from .layers import patch_offsets
 
@@ -106,8 +105,7 @@ class CTViT(nn.Module):
         """Patch-embed + spatial + temporal transformers.  video: (B, C, F, H, W) float in [-1, 1]
         or int16 HU (normalised in-kernel).  Returns (z f32 [M, D], z bf16, geometry); ``trace``
         (a dict, tests) receives the f32 token rows after patch-embed / spatial / temporal stacks."""
-        if precise.vit_precision() == 'f32':          # opt-in exact-f32 forward (precise.py)
-            return precise.encode_tokens_f32(self, video, trace)
+        # (the f32 image-tower mode, precise.py, runs inside the same Functions: functional.precise_f32)
         if video.ndim == 4:
             video = video.unsqueeze(2)
         assert video.ndim == 5

@@ -68,6 +68,14 @@ def take_shadow(gf):
     return None
 
 
+def precise_f32():
+    """True in the f32 image-tower mode (precise.set_vit_precision('f32')): the 3D-ViT Functions
+    below then run their forward in exact f32 and save the bf16 tensors their backward kernels read,
+    so the mode trains (f32 forward, bf16 backward)."""
+    from . import precise
+    return precise.vit_precision() == 'f32'
+
+
 # ----------------------------------------------------------------------------- geometry
 @dataclass(frozen=True)
 class Geo:
@@ -267,9 +275,16 @@ class PatchEmbedFn(torch.autograd.Function):
         kp = (pd + 63) // 64 * 64                                      # K padded to the 64-deep GEMM step
         xhat_p = K.patch_ln(video, is_hu, PT, P, offs, ld=kp)          # [M, kp] bf16, zero pad columns
         xhat = xhat_p[:, :pd]
-        Wp = K.pack_rows(W, W.shape[0], kp, colscale=ln1_w)            # bf16 [D, kp], zero pad columns
-        bp = K.slinear(ln1_b.view(1, -1), W, bias=b).view(-1)          # f32 [D]
-        y1 = K.linear(xhat_p, Wp, bias=bp, out_dtype=F32)               # [M, D]
+        if precise_f32():
+            # f32 tower: LayerNorm(4000) with its affine, then the Linear, both exact f32
+            # (ct_clip/ctvit.py:170-172); xhat (bf16) above is what the backward reads
+            xn0 = K.patch_ln_f32(video, is_hu, PT, P, offs, ln1_w.detach(), ln1_b.detach())
+            y1, _ = K.linear_f32(xn0, W.detach(), bias=b.detach())
+            del xn0
+        else:
+            Wp = K.pack_rows(W, W.shape[0], kp, colscale=ln1_w)        # bf16 [D, kp], zero pad columns
+            bp = K.slinear(ln1_b.view(1, -1), W, bias=b).view(-1)      # f32 [D]
+            y1 = K.linear(xhat_p, Wp, bias=bp, out_dtype=F32)           # [M, D]
         yb, yf, mean, rstd = K.layernorm_fwd(y1, ln2_w, ln2_b, 1e-5, out_bf16=True, out_f32=True)
         ctx.save_for_backward(xhat, y1, mean, rstd, ln1_w, ln1_b, W, ln2_w)
         ctx.b, ctx.ln2_w, ctx.ln2_b = b, ln2_w, ln2_b
@@ -394,6 +409,9 @@ class ViTLayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xf, xb, bias_u, geo, peg_w, peg_b, norm_g, q_scale, k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1,
                 W2):
+        if precise_f32():
+            return _vit_layer_forward_f32(ctx, xf, xb, bias_u, geo, peg_w, peg_b, norm_g, q_scale, k_scale, Wq,
+                                          Wkv, Wo, ff_w, ff_b, W1, W2)
         H, dh = geo.heads, geo.dim_head
         inner = H * dh
         x1f, x1b = K.peg_fwd(xb, xf, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, peg_b, geo.mode)
@@ -526,6 +544,53 @@ class ViTLayerFn(torch.autograd.Function):
                 None, None, None)
 
 
+def _vit_layer_forward_f32(ctx, xf, xb, bias_u, geo, peg_w, peg_b, norm_g, q_scale, k_scale, Wq, Wkv, Wo, ff_w,
+                           ff_b, W1, W2):
+    """ViTLayerFn.forward of the f32 image tower: the layer (ct_clip/attention.py:322-331) with f32
+    activations and exact-f32 products (every Linear on the f32 MFMA GEMM, PEG / LayerNorm / l2norm /
+    cosine attention with the CPB bias / GEGLU in f32 with libm transcendentals), saving exactly the
+    tensors ViTLayerFn.backward reads, as the bf16 forward saves them (bf16 copies of the f32
+    activations; the attention's o / lse from the bf16 attention kernel on the bf16 q / k / v, so the
+    backward's recomputed probabilities are those of its own operands)."""
+    H, dh = geo.heads, geo.dim_head
+    inner = H * dh
+    d = lambda t: t.detach()    # noqa: E731
+    x1f = K.peg_fwd_f32(xf.detach().contiguous(), geo.B, geo.T, geo.Hg, geo.Wg, d(peg_w), d(peg_b), geo.mode)
+    x1b = K.cast_bf16(x1f)
+    xn, xnf, m1, r1 = K.layernorm_fwd(x1f, norm_g, None, 1e-5, out_bf16=True, out_f32=True)   # q side only
+    q32, q = K.linear_f32(xnf, d(Wq), want_bf16=True)
+    kv32, kv = K.linear_f32(x1f, d(Wkv), want_bf16=True)          # K / V from the un-normalised x
+    del xnf
+    qn32 = K.l2norm_scale_fwd_f32(q32, H, dh, d(q_scale))
+    kn32 = K.l2norm_scale_fwd_f32(kv32[:, :inner], H, dh, d(k_scale))
+    L, nseq, seq = geo.seq()
+    use_bias = bias_u is not None
+    grid = (geo.Hg, geo.Wg) if use_bias else (0, 0)
+    o32 = K.attn_fwd_f32(qn32, kn32, kv32[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
+                         bias_u=bias_u if use_bias else None, grid=grid)
+    qn, kn = K.cast_bf16(qn32), K.cast_bf16(kn32)
+    del q32, qn32, kn32
+    o, lse = K.attn_fwd(qn, kn, kv[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
+                        bias_u=bias_u if use_bias else None, grid=grid)
+    x2f, x2b = K.linear_f32(o32, d(Wo), residual=x1f, want_bf16=True)
+    del o32, kv32, x1f
+    xn2, xn2f, m2, r2 = K.layernorm_fwd(x2f, ff_w, ff_b, 1e-5, out_bf16=True, out_f32=True)
+    inner_ff = W1.shape[0] // 2
+    W1p32 = K.pack_rows_f32(d(W1), 2 * ff_pad(inner_ff), W1.shape[1], rowmap=ff1_rowmap(inner_ff, W1.device))
+    h, g32, g = K.linear_f32_geglu(xn2f, W1p32)
+    del xn2f
+    W2p32 = K.pack_rows_f32(d(W2), W2.shape[0], ff_pad(W2.shape[1]))
+    x3f, x3b = K.linear_f32(g32, W2p32, residual=x2f, want_bf16=True)
+    del g32
+    ctx.geo = geo
+    ctx.use_bias = use_bias
+    ctx.params = (peg_w, peg_b, norm_g, q_scale, k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1, W2)
+    ctx.save_for_backward(xb, x1b, m1, r1, xn, q, kv, qn, kn, o, lse, x2b, m2, r2, xn2, h, g,
+                          bias_u if use_bias else torch.empty(0), bf(Wq), bf(Wkv), bf(Wo), pack_ff1(W1), pack_ff2(W2))
+    ctx.mark_non_differentiable(x3b)
+    return x3f, x3b
+
+
 class NormFn(torch.autograd.Function):
     """Bias-less LayerNorm ``norm_out`` (ct_clip/attention.py:309,333) -> (f32, bf16)."""
 
@@ -654,6 +719,10 @@ class ImageProjFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, pooled, pooled_b, W, Wb):
+        ctx.save_for_backward(pooled_b, Wb)
+        ctx.W = W
+        if precise_f32():      # the f32 image tower's projection: exact f32 (split-K f32 MFMA)
+            return K.slinear(pooled.detach().contiguous(), W.detach())
         B, Kd = pooled_b.shape
         N = Wb.shape[0]
         split = max(1, min(512, Kd // 1024))
@@ -661,8 +730,6 @@ class ImageProjFn(torch.autograd.Function):
         K.gemm_raw(B, N, Kd, pooled_b, Kd, True, Wb, Kd, True, slabs, N, split_k=split)
         out = torch.empty(B, N, device=pooled.device, dtype=F32)
         K.reduce_slabs(slabs, out)
-        ctx.save_for_backward(pooled_b, Wb)
-        ctx.W = W
         return out
 
     @staticmethod

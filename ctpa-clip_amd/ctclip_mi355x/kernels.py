@@ -634,6 +634,16 @@ def pack_rows(src, rows_dst, cols_dst, rowmap=None, colscale=None, out=None):
     return out
 
 
+def pack_rows_f32(src, rows_dst, cols_dst, rowmap=None, colscale=None, out=None):
+    """f32 working weight: out[r][c] = src[rowmap[r]][c] * colscale[c] (zero padding), as pack_rows."""
+    rows, cols = src.shape
+    if out is None:
+        out = torch.empty(rows_dst, cols_dst, device=src.device, dtype=F32)
+    call('ctclip_pack_rows_f32', ptr(src), src.stride(0), ptr(rowmap), rows_dst, cols, cols_dst, ptr(colscale),
+         ptr(out), out.stride(0), stream_ptr())
+    return out
+
+
 def unpack_rows(src, dst, rowmap=None, cols=None, accumulate=True):
     rows_src = src.shape[0]
     cols = dst.shape[1] if cols is None else cols
@@ -1046,6 +1056,37 @@ def l2norm_scale_fwd_f32(x, H, D, scale):
     call('ctclip_l2norm_scale_fwd_f32', ptr(x), x.stride(0), x.shape[0], H, D, ptr(scale), ptr(out), out.stride(0),
          stream_ptr())
     return out
+
+
+def linear_f32(x, w, *, bias=None, residual=None, want_bf16=False, alpha=1.0):
+    """Exact-f32 y[M, N] = alpha x[M, K] @ w[N, K]^T (+ bias) (+ residual f32) on the f32 MFMA GEMM
+    (ctclip_sgemm_tn; one ascending-k fma chain per output).  Returns (y f32, bf16 copy or None)."""
+    M, Kd = x.shape
+    N = w.shape[0]
+    assert w.shape[1] == Kd and x.dtype == F32 and w.dtype == F32 and x.stride(1) == 1 and w.stride(1) == 1
+    y = torch.empty(M, N, device=x.device, dtype=F32)
+    yb = torch.empty(M, N, device=x.device, dtype=BF16) if want_bf16 else None
+    a = _lib.SgemmTnArgs(M=M, N=N, K=Kd, A=ptr(x), lda=x.stride(0), B=ptr(w), ldb=w.stride(0), C=ptr(y), ldc=N,
+                         C2=ptr(yb), ldc2=N, C3=None, ldc3=0, bias=ptr(bias), R=ptr(residual),
+                         ldr=residual.stride(0) if residual is not None else 0, alpha=float(alpha), act=0)
+    call('ctclip_sgemm_tn', _lib.ctypes.byref(a), stream_ptr())
+    return y, yb
+
+
+def linear_f32_geglu(x, w1p):
+    """FF1 + GEGLU in exact f32 on the packed [32 x | 32 gate] weight (functional.pack_ff1 order, f32):
+    returns (h bf16 [M, N], g f32 [M, N/2], g bf16 [M, N/2])."""
+    M, Kd = x.shape
+    N = w1p.shape[0]
+    assert w1p.shape[1] == Kd and N % 64 == 0 and x.dtype == F32 and w1p.dtype == F32
+    h = torch.empty(M, N, device=x.device, dtype=BF16)
+    g = torch.empty(M, N // 2, device=x.device, dtype=F32)
+    gb = torch.empty(M, N // 2, device=x.device, dtype=BF16)
+    a = _lib.SgemmTnArgs(M=M, N=N, K=Kd, A=ptr(x), lda=x.stride(0), B=ptr(w1p), ldb=w1p.stride(0), C=ptr(g),
+                         ldc=N // 2, C2=ptr(h), ldc2=N, C3=ptr(gb), ldc3=N // 2, bias=None, R=None, ldr=0, alpha=1.0,
+                         act=ACT_GEGLU)
+    call('ctclip_sgemm_tn', _lib.ctypes.byref(a), stream_ptr())
+    return h, g, gb
 
 
 def geglu_f32(h):

@@ -326,6 +326,27 @@ int ctclip_l2norm_scale_fwd_f32(const float* x, int64_t ldx, int64_t rows, int32
                                 const float* scale, float* y, int64_t ldy, void* stream);
 int ctclip_geglu_f32(const float* h, int64_t ldh, int64_t rows, int32_t inner, float* g, int64_t ldg,
                      void* stream);
+/* Round 4: the f32 tower trains (its forward feeds the bf16 backward kernels) and its Linears run on
+ * a dedicated f32 MFMA GEMM (csrc/sgemm_tn.hip): C[M][N] = alpha A[M][K] . B[N][K]^T, each output one
+ * f32 fma chain in ascending k (bit-identical to ctclip_sgemm).  act 0: C f32 (+ bias[N]) (+ R f32),
+ * optional bf16 copy C2; act 2: GEGLU over the packed [32 x | 32 gate] pairs (N % 64 == 0): C2 = h
+ * bf16 [M][N], C = g f32 [M][N/2], optional C3 = g bf16.  K, N, ld* % 4 == 0; A, B, C 16-B aligned. */
+typedef struct {
+  int64_t M, N, K;
+  const float* A; int64_t lda;
+  const float* B; int64_t ldb;
+  float* C; int64_t ldc;
+  void* C2; int64_t ldc2;
+  void* C3; int64_t ldc3;
+  const float* bias;
+  const float* R; int64_t ldr;
+  float alpha;
+  int32_t act;
+} ctclip_sgemm_tn_args;
+int ctclip_sgemm_tn(const ctclip_sgemm_tn_args* a, void* stream);
+/* f32 working weights: dst[r][c] = src[map[r]][c] * colscale[c] (zero pads), as ctclip_pack_rows */
+int ctclip_pack_rows_f32(const float* src, int64_t ld_src, const int32_t* map, int64_t rows_dst, int32_t cols,
+                         int32_t cols_dst, const float* colscale, float* dst, int64_t ld_dst, void* stream);
 
 /* ---------------------------------------------------------------- vector quantiser
  * vector_quantize_pytorch==1.1.2 cosine codebook (ct_clip/ctvit.py:187,421-427).

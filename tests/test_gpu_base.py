@@ -286,6 +286,65 @@ def test_f32_image_mode_vq_contract(base):
     model.train()
 
 
+def test_f32_mode_forward_backward_full_size(base):
+    """The trainable f32 mode at configs[1] size (B = 2, train mode, autograd through the tower):
+    the loss the step differentiates meets the north-star 1e-3 against the reference's output
+    free-running, every VQ index agrees with the reference's except f32 ties (margin < 1e-6), and
+    the (bf16) backward produces finite gradients for both towers.  Reports the f32-mode forward +
+    backward time against the default mode's."""
+    from ctclip_mi355x import precise
+    g, sd, model, text = base['g'], base['sd'], base['model'], base['text']
+    hu = base['hu'].cuda()
+    cbk = model.visual_transformer.vq._codebook
+    saved = cbk.embed.clone(), cbk.cluster_size.clone()
+    model.train()
+
+    def fwd_bwd():
+        model.zero_grad(set_to_none=True)
+        loss = model(text, hu, return_loss=True)
+        loss.backward()
+        return loss
+
+    try:
+        times = {}
+        for mode in ('bf16', 'f32', 'f32'):          # second f32 run: warm timing
+            with precise.vit_precision_scope(mode):
+                with torch.no_grad():
+                    cbk.embed.copy_(saved[0])
+                    cbk.cluster_size.copy_(saved[1])
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                loss = fwd_bwd()
+                e.record()
+                torch.cuda.synchronize()
+                times[mode] = s.elapsed_time(e)
+        idx = model.visual_transformer.vq.state.last_indices.cpu().long()
+        p_img = model.visual_transformer.enc_spatial_transformer.layers[0][1].to_q.weight
+        p_txt = model.text_transformer.encoder.layer[11].output.dense.weight
+        gi_img, gi_txt = p_img.grad.norm().item(), p_txt.grad.norm().item()
+    finally:
+        with torch.no_grad():
+            cbk.embed.copy_(saved[0])
+            cbk.cluster_size.copy_(saved[1])
+        model.zero_grad(set_to_none=True)
+    zo = _oracle_tokens(base)
+    E = sd['visual_transformer.vq._codebook.embed'][0]
+    so = F.normalize(zo, dim=-1) @ E.t()
+    top2 = so.topk(2, dim=1)
+    margin = top2.values[:, 0] - top2.values[:, 1]
+    gi = g['out.vq_indices'].reshape(-1).long()
+    diff = idx != gi
+    above = (diff & (margin >= 1e-6)).sum().item()
+    dl = abs(loss.item() - g['out.loss'].item())
+    print(f'f32 mode, train-mode forward + backward at B=2: loss {loss.item():.6f} vs reference '
+          f'{g["out.loss"].item():.6f} (|d| {dl:.2e}); VQ {diff.sum().item()} of {gi.numel()} differ '
+          f'({above} above the 1e-6 margin); grad norms image {gi_img:.3e} text {gi_txt:.3e}; '
+          f'fwd+bwd ms: bf16 {times["bf16"]:.1f}, f32 {times["f32"]:.1f}')
+    assert above == 0
+    assert dl < 1e-3
+    assert math.isfinite(gi_img) and gi_img > 0 and math.isfinite(gi_txt) and gi_txt > 0
+
+
 def test_train_step_batch8_full_size(base):
     """configs[1] itself (B = 8): one full train step -- finite loss near ln 8 at init, finite
     non-zero gradient norm, parameters of both towers updated."""
