@@ -202,14 +202,14 @@ __host__ __device__ inline int plane_bytes(int W) { return (HT + 2) * (W + 2) * 
 // 107 -> 126 us there, while the conv kernels gain 174 -> 156 us)
 template <int NT, bool BF = true>
 __device__ __forceinline__ unsigned plane_load(const u16* __restrict__ x, const Geo& g, int D, int b, int h0, int c0,
-                                               int tp, u32x4 (&reg)[nld<NT>()]) {
+                                               int tp, u32x4 (&reg)[nld<NT>()], int hoff = 1) {
   const int nl = (HT + 2) * (g.W + 2) * 8;
   unsigned valid = BF ? 0u : ~0u;
 #pragma unroll
   for (int m = 0; m < nld<NT>(); ++m) {
     const int i = threadIdx.x + m * NT;
     const int k = i & 7, cw = (i >> 3) % (g.W + 2), hr = (i >> 3) / (g.W + 2);
-    const int h = h0 - 1 + hr, w = cw - 1;
+    const int h = h0 - hoff + hr, w = cw - 1;
     const bool ok = i < nl && h >= 0 && h < g.H && w >= 0 && w < g.W;
     if constexpr (BF) {
       const int64_t row = ok ? (int64_t)canon(g, b, (tp * g.H + h) * g.W + w) : 0;
@@ -239,6 +239,14 @@ __device__ __forceinline__ void plane_store(char* ring, int W, int tp, const u32
 // GK > 0: the geometry is the compile-time cube T = H = W = GK with index map MD (the 3D-ViT's
 // 24^3 token grid in both transformers), so every division of the plane / row index maps is by
 // a constant (the runtime form spends most of its issue slots on integer divisions)
+// MD = 2: the temporal transformer's raw-reshape view (mode 1) on a cube T = H = W, walked in
+// CANONICAL order.  For T = H = W the view is a pure axis permutation of the canonical (t, h, w)
+// rows -- view (t_v, h_v, w_v) = (h, w, t) (attention.py:69-70: flat f = (h W + w) T + t =
+// (t_v H + h_v) W + w_v) -- so the view's conv is a canonical-space conv with the causal offsets
+// {-2, -1, 0} on canonical h, {-1, 0, 1} on canonical t and w, and tap (kt, kh, kw) of the view
+// applied at canonical offset (dt, dh, dw) = (kw - 1, kt - 2, kh - 1).  Walking canonical t with
+// planes of canonical (h, w) rows makes every plane a contiguous run of rows (the view walk gathered
+// rows 576 apart: 217 vs 159 us per forward launch, r03).  Same outputs up to f32 summation order.
 template <int GK, int MD>
 __device__ __forceinline__ void fix_geo(Geo& g) {
   if constexpr (GK > 0) {
@@ -246,9 +254,20 @@ __device__ __forceinline__ void fix_geo(Geo& g) {
     g.H = GK;
     g.W = GK;
     g.thw = GK * GK * GK;
-    g.mode = MD;
+    g.mode = MD == 2 ? 0 : MD;    // MD 2 addresses rows canonically
   }
 }
+
+// loop index (a = walk plane, b = plane row, c = plane column) -> offsets and the tap they use; TR =
+// the transposed conv (input gradient): every offset negated
+template <int MD, int TR>
+struct Taps {
+  static constexpr int dt(int a) { return MD == 2 ? (TR ? 1 - a : a - 1) : (TR ? 2 - a : a - 2); }
+  static constexpr int dh(int b) { return MD == 2 ? (TR ? 2 - b : b - 2) : (TR ? 1 - b : b - 1); }
+  static constexpr int tap(int a, int b, int c) { return MD == 2 ? (b * 3 + c) * 3 + a : (a * 3 + b) * 3 + c; }
+  static constexpr int hoff = MD == 2 ? (TR ? 0 : 2) : 1;   // plane row 0 = h0 - hoff
+  static constexpr int lead = MD == 2 ? 1 : (TR ? 2 : 0);    // planes needed ahead of t
+};
 
 template <int TR, int GK = 0, int MD = 0>
 __global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ xin, int D,
@@ -268,11 +287,12 @@ __global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ 
     ws[tap * 64 + c] = w[(int64_t)(c0 + c) * 27 + tap];
   }
   if (threadIdx.x < 64) bs[threadIdx.x] = bias ? bias[c0 + threadIdx.x] : 0.f;
-  const int lead = TR ? 2 : 0;
+  using TP = Taps<MD, TR>;
+  constexpr int lead = TP::lead, hoff = TP::hoff;
   u32x4 reg[nld<TNTH>()];
   unsigned rvalid = 0;
   for (int tp = 0; tp <= lead && tp < g.T; ++tp) {
-    rvalid = plane_load<TNTH>(xin, g, D, b, h0, c0, tp, reg);
+    rvalid = plane_load<TNTH>(xin, g, D, b, h0, c0, tp, reg, hoff);
     plane_store<TNTH>(ring, g.W, tp, reg, rvalid);
   }
   __syncthreads();
@@ -299,7 +319,7 @@ __global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ 
   for (int t = 0; t < g.T; ++t) {
     const int tn = t + lead + 1;
     // always issued (the last steps re-read plane T-1, never stored) so no branch merges `reg`
-    const unsigned nvalid = plane_load<TNTH>(xin, g, D, b, h0, c0, min(tn, g.T - 1), reg);
+    const unsigned nvalid = plane_load<TNTH>(xin, g, D, b, h0, c0, min(tn, g.T - 1), reg, hoff);
     f32x4 rn[SEG][2];
     res_load(min(t + 1, g.T - 1), rn);
     if (active) {
@@ -311,13 +331,13 @@ __global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ 
       // rolled (kt, kh) loops: one (SEG+2) x 8 window live at a time (unrolled, hipcc hoists all
       // nine windows and the kernel runs at 1 wave/SIMD)
 #pragma unroll 1
-      for (int kt = 0; kt < 3; ++kt) {
-        const int tp = TR ? t + 2 - kt : t + kt - 2;
+      for (int kt = 0; kt < 3; ++kt) {           // (a, b, c) = (kt, kh, kw) loop indices, see Taps
+        const int tp = t + TP::dt(kt);
         if (tp < 0 || tp >= g.T) continue;
         const char* pl = ring + (tp % NSLOT) * pb;
 #pragma unroll 1
         for (int kh = 0; kh < 3; ++kh) {
-          const int lr = TR ? r + 2 - kh : r + kh;
+          const int lr = r + TP::dh(kh) + hoff;
           float xv[SEG + 2][8];
 #pragma unroll
           for (int q = 0; q < SEG + 2; ++q) {
@@ -327,7 +347,7 @@ __global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ 
           }
 #pragma unroll
           for (int kw = 0; kw < 3; ++kw) {
-            const float* wp = ws + ((kt * 3 + kh) * 3 + kw) * 64 + ch * 8;
+            const float* wp = ws + TP::tap(kt, kh, kw) * 64 + ch * 8;
             const f32x4 wa = *(const f32x4*)wp, wb = *(const f32x4*)(wp + 4);
             const float wv[8] = {wa[0], wa[1], wa[2], wa[3], wb[0], wb[1], wb[2], wb[3]};
 #pragma unroll
@@ -383,10 +403,16 @@ __global__ __launch_bounds__(WNTH, 3) void peg_wgrad_tile_kernel(const u16* __re
   for (int i = 0; i < 27; ++i) acc[i][0] = acc[i][1] = 0.f;
   // planes two steps ahead (regA = plane t+1, regB = plane t+2), this thread's dout one step
   // ahead (one (row, segment) item per thread: wgrad_ok)
+  // (planes L + 1 and L + 2 ahead, L = the forward conv's lead: 0, or 1 for the canonical walk MD 2)
+  using TP = Taps<MD, 0>;
+  constexpr int L = TP::lead, hoff = TP::hoff;
   u32x4 regA[nld<WNTH>()], regB[nld<WNTH>()];
-  unsigned va = plane_load<WNTH, false>(xin, g, D, b, h0, c0, 0, regA), vb = ~0u;
-  plane_store<WNTH>(ring, g.W, 0, regA, va);
-  if (g.T > 1) va = plane_load<WNTH, false>(xin, g, D, b, h0, c0, 1, regA);
+  unsigned va = ~0u, vb = ~0u;
+  for (int tp = 0; tp <= L && tp < g.T; ++tp) {
+    va = plane_load<WNTH, false>(xin, g, D, b, h0, c0, tp, regA, hoff);
+    plane_store<WNTH>(ring, g.W, tp, regA, va);
+  }
+  if (g.T > L + 1) va = plane_load<WNTH, false>(xin, g, D, b, h0, c0, L + 1, regA, hoff);
   const int ns = (g.W + SEGW - 1) / SEGW;
   const int items = HT * ns * 32;
   const int o = threadIdx.x;
@@ -408,8 +434,8 @@ __global__ __launch_bounds__(WNTH, 3) void peg_wgrad_tile_kernel(const u16* __re
   dload(0, du);
   __syncthreads();
   for (int t = 0; t < g.T; ++t) {
-    const int tn = t + 1;
-    if (tn + 1 < g.T) vb = plane_load<WNTH, false>(xin, g, D, b, h0, c0, tn + 1, regB);
+    const int tn = t + 1, tq = t + L + 1;     // tq: the plane stored at the end of this step
+    if (tq + 1 < g.T) vb = plane_load<WNTH, false>(xin, g, D, b, h0, c0, tq + 1, regB, hoff);
     if (tn < g.T) dload(tn, dn);
     if (act) {
       float dv[SEGW][2];
@@ -422,12 +448,12 @@ __global__ __launch_bounds__(WNTH, 3) void peg_wgrad_tile_kernel(const u16* __re
       }
 #pragma unroll
       for (int kt = 0; kt < 3; ++kt) {
-        const int tp = t + kt - 2;
+        const int tp = t + TP::dt(kt);     // <= T: plane T is stored as zeros (the causal tail, L > 0)
         if (tp < 0) continue;
         const char* pl = ring + (tp % NSLOT) * pb;
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh) {
-          const int lr = r + kh;
+          const int lr = r + TP::dh(kh) + hoff;
           float xv[SEGW + 2][2];
 #pragma unroll
           for (int q = 0; q < SEGW + 2; ++q) {
@@ -440,14 +466,16 @@ __global__ __launch_bounds__(WNTH, 3) void peg_wgrad_tile_kernel(const u16* __re
           for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
             for (int j = 0; j < SEGW; ++j) {
-              acc[(kt * 3 + kh) * 3 + kw][0] += dv[j][0] * xv[j + kw][0];
-              acc[(kt * 3 + kh) * 3 + kw][1] += dv[j][1] * xv[j + kw][1];
+              acc[TP::tap(kt, kh, kw)][0] += dv[j][0] * xv[j + kw][0];
+              acc[TP::tap(kt, kh, kw)][1] += dv[j][1] * xv[j + kw][1];
             }
         }
       }
     }
-    __syncthreads();   // slot of plane tn held plane tn - 3, read in this step
-    if (tn < g.T) plane_store<WNTH>(ring, g.W, tn, regA, va);
+    __syncthreads();   // slot of plane tq held plane tq - 3, read in this step
+    // (with L > 0 the plane past the end, tq == T, is stored as zeros: no upper-bound branch above,
+    // which kept values live across it and spilled)
+    if (tq < g.T || (L > 0 && tq == g.T)) plane_store<WNTH>(ring, g.W, tq, regA, tq < g.T ? va : 0u);
 #pragma unroll
     for (int m = 0; m < nld<WNTH>(); ++m) regA[m] = regB[m];
     va = vb;
@@ -491,8 +519,9 @@ void tile_attrs() {
   const void* ks[] = {(const void*)peg_tile_kernel<0>,         (const void*)peg_tile_kernel<1>,
                       (const void*)peg_tile_kernel<0, 24, 0>,  (const void*)peg_tile_kernel<0, 24, 1>,
                       (const void*)peg_tile_kernel<1, 24, 0>,  (const void*)peg_tile_kernel<1, 24, 1>,
+                      (const void*)peg_tile_kernel<0, 24, 2>,  (const void*)peg_tile_kernel<1, 24, 2>,
                       (const void*)peg_wgrad_tile_kernel<>,    (const void*)peg_wgrad_tile_kernel<24, 0>,
-                      (const void*)peg_wgrad_tile_kernel<24, 1>};
+                      (const void*)peg_wgrad_tile_kernel<24, 1>, (const void*)peg_wgrad_tile_kernel<24, 2>};
   for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
   s_tile_attr = true;
 }
@@ -504,12 +533,22 @@ bool fixed24(const Geo& g) {
   return on && g.T == 24 && g.H == 24 && g.W == 24 && (g.mode == 0 || g.mode == 1);
 }
 
+// mode 1 on the 24^3 cube through the canonical walk (MD 2); CTCLIP_PEG_CANON1=0 or
+// ctclip_peg_set_canon1(0): the view walk (A/B)
+int g_canon1 = -1;
+bool canon1() {
+  if (g_canon1 < 0) { const char* e = getenv("CTCLIP_PEG_CANON1"); g_canon1 = e ? atoi(e) != 0 : 1; }
+  return g_canon1 != 0;
+}
+
 template <int TR>
 void launch_tile(dim3 grid, size_t smem, hipStream_t st, const u16* x, int D, const float* w, const float* bias,
                  const float* res, const Geo& g, float* out, u16* outb) {
   if (fixed24(g)) {
     if (g.mode == 0)
       hipLaunchKernelGGL((peg_tile_kernel<TR, 24, 0>), grid, dim3(TNTH), smem, st, x, D, w, bias, res, g, out, outb);
+    else if (canon1())
+      hipLaunchKernelGGL((peg_tile_kernel<TR, 24, 2>), grid, dim3(TNTH), smem, st, x, D, w, bias, res, g, out, outb);
     else
       hipLaunchKernelGGL((peg_tile_kernel<TR, 24, 1>), grid, dim3(TNTH), smem, st, x, D, w, bias, res, g, out, outb);
     return;
@@ -518,6 +557,12 @@ void launch_tile(dim3 grid, size_t smem, hipStream_t st, const u16* x, int D, co
 }
 
 }  // namespace
+
+extern "C" int ctclip_peg_set_canon1(int on) {
+  const int old = canon1();
+  g_canon1 = on != 0;
+  return old;
+}
 
 extern "C" int ctclip_peg_wgrad_slabs(int64_t B, int32_t T, int32_t H, int32_t W, int32_t D) {
   (void)T;
@@ -580,6 +625,9 @@ extern "C" int ctclip_peg_bwd_weight(const void* dout_bf16, const void* x_bf16, 
     const hipStream_t st = (hipStream_t)stream;
     if (fixed24(g) && g.mode == 0)
       hipLaunchKernelGGL((peg_wgrad_tile_kernel<24, 0>), grid, dim3(WNTH), wgrad_smem(W), st, (const u16*)dout_bf16,
+                         (const u16*)x_bf16, D, g, part);
+    else if (fixed24(g) && canon1())
+      hipLaunchKernelGGL((peg_wgrad_tile_kernel<24, 2>), grid, dim3(WNTH), wgrad_smem(W), st, (const u16*)dout_bf16,
                          (const u16*)x_bf16, D, g, part);
     else if (fixed24(g))
       hipLaunchKernelGGL((peg_wgrad_tile_kernel<24, 1>), grid, dim3(WNTH), wgrad_smem(W), st, (const u16*)dout_bf16,

@@ -263,6 +263,9 @@ int ctclip_peg_bwd_data(const void* dout_bf16, const float* dout_f32, int64_t B,
 int ctclip_peg_bwd_weight(const void* dout_bf16, const void* x_bf16, int64_t B, int32_t T, int32_t H,
                           int32_t W, int32_t D, int32_t mode, float* part, int32_t nblk, void* stream);
 int ctclip_peg_wgrad_slabs(int64_t B, int32_t T, int32_t H, int32_t W, int32_t D);
+/* mode 1 on a T = H = W = 24 cube runs as a canonical-order walk (the view is an axis permutation
+ * there; same outputs up to f32 summation order); 0 = the view-order walk (A/B).  Returns the previous. */
+int ctclip_peg_set_canon1(int32_t on);
 
 /* ---------------------------------------------------------------- attention (attention.py:127-181)
  * softmax(scale * q.k^T + bias + mask) v per (sequence, head); q/k already l2-normalised and

@@ -79,9 +79,32 @@ def _peg_ref(x, w, b, shape, mode):
     return y.reshape(B, H, W, T, D).permute(0, 3, 1, 2, 4).reshape(-1, D)
 
 
+def test_peg_canonical_walk_matches_view_walk(K):
+    """Mode 1 on the 24^3 cube: the canonical-order walk (default) against the view-order walk."""
+    from ctclip_mi355x import _lib
+    torch.manual_seed(9)
+    shape, D = (2, 24, 24, 24), 128
+    M = 2 * 24 ** 3
+    xb = torch.randn(M, D, device=dev).bfloat16()
+    w = torch.randn(D, 1, 3, 3, 3, device=dev) * 0.2
+    b = torch.randn(D, device=dev) * 0.1
+    dy = torch.randn(M, D, device=dev).bfloat16()
+    outs = []
+    for on in (1, 0):
+        old = _lib.lib().ctclip_peg_set_canon1(on)
+        try:
+            outs.append((K.peg_fwd(xb, xb.float(), *shape, w, b, 1), K.peg_bwd(dy, dy.float(), xb, *shape, w, 1)))
+        finally:
+            _lib.lib().ctclip_peg_set_canon1(old)
+    (f1, b1), (f0, b0) = outs
+    assert rel(f1[0], f0[0]) < 1e-6 and rel(b1[0], b0[0]) < 1e-6
+    assert rel(b1[2], b0[2]) < 1e-5 and rel(b1[3], b0[3]) < 1e-5
+
+
 @pytest.mark.parametrize('mode', [0, 1])
 @pytest.mark.parametrize('shape,D', [((2, 6, 5, 7), 128),      # plane-streaming path, ragged h tile / w segment
                                      ((1, 24, 24, 24), 512),   # base token grid (480^2 x 240 volume)
+                                     ((2, 24, 24, 24), 128),   # two volumes (mode 1: canonical walk)
                                      ((1, 3, 4, 40), 64),      # W > 30: general path
                                      ((2, 2, 3, 4), 24)])      # D % 64 != 0: general path
 def test_peg(K, mode, shape, D):
