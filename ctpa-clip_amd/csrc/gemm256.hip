@@ -1287,8 +1287,11 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
   // desynchronise the CUs: half of the first dispatch round (every other workgroup within each
   // XCD) starts p.stagger x ~2k cycles late, so later rounds' store-heavy epilogues on those CUs
   // fall under the other half's MFMA main loops instead of all CUs storing at once
-  if (p.stagger > 0 && lin < 256 && ((lin >> 3) & 1))
-    for (int s = 0; s < p.stagger; ++s) __builtin_amdgcn_s_sleep(32);
+  // (stagger >= 1000: four groups delayed 0, 1, 2, 3 x (stagger - 1000) units -- A/B sweeps)
+  if (p.stagger > 0 && lin < 256) {
+    const int ng = p.stagger >= 1000 ? 4 : 2, u = p.stagger % 1000, grp = (lin >> 3) & (ng - 1);
+    for (int s = 0; s < grp * u; ++s) __builtin_amdgcn_s_sleep(32);
+  }
 
   f32x4 acc[8][4];
 #pragma unroll
