@@ -43,6 +43,8 @@ def parse():
                     help='configs[3]: the 3D-ViT forward linears as MX-fp8 GEMMs (default batch 16 per GPU)')
     ap.add_argument('--text-len', type=int, default=128)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--f32-tower', action='store_true',
+                    help="run the whole bench in the f32 image-tower mode (precise.set_vit_precision('f32'))")
     ap.add_argument('--no-precise', action='store_true',
                     help='skip the f32-image-tower mode measurement (precise_f32_tower entry)')
     ap.add_argument('--cpu-batch', type=int, default=2)
@@ -217,6 +219,10 @@ def main():
     if args.fp8:
         from ctclip_mi355x import functional as Fn
         Fn.set_vit_fp8(True)
+    if args.f32_tower:
+        from ctclip_mi355x import precise
+        precise.set_vit_precision('f32')
+        args.no_precise = True
     torch.manual_seed(0)   # identical random-init weights on every rank
     model = set_finetune_trainable(build_ctclip()).to(dev)
     model.train()
@@ -261,6 +267,9 @@ def main():
     elapsed = time.perf_counter() - t0
     K.TIMER.stop()
     loss_v = float(loss.item())
+    # every warm-up and timed step's LayerNorm-exchange status was checked by the trainer (before
+    # the f32-mode steps below add theirs)
+    ln_checked = trainer.ln_steps_checked
     precise_entry = None
     if not args.no_precise and not args.fp8:
         # the trainable f32 image-tower mode (precise.py: exact-f32 forward, bf16 backward; the SURVEY
@@ -323,7 +332,8 @@ def main():
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
-        'dtype': 'mx-fp8 e4m3 (3D-ViT forward linears) + bf16' if args.fp8 else 'bf16',
+        'dtype': 'mx-fp8 e4m3 (3D-ViT forward linears) + bf16' if args.fp8 else
+                 ('f32 image-tower forward + bf16 backward' if args.f32_tower else 'bf16'),
         'data': 'synthetic: int16 HU volumes 1x240x480x480 (randint -1200..1200) + 128-token reports; '
                 'random-init CT-CLIP base weights',
         'config': {'workload': 'CT-CLIP base contrastive train step: BERT-base(128 tok, train-mode dropout '
@@ -338,8 +348,8 @@ def main():
     # the LayerNorm-fused GEMMs' in-launch tile-pair exchange never timed out: the trainer's own
     # per-step check of ctclip_gemm_ln's status word (a timeout raises LayerNormExchangeError in
     # train_step / flush and its step's Adam update is skipped on the device)
-    result['ln_exchange_ok'] = trainer.ln_steps_checked == args.warmup + args.steps
-    result['ln_exchange_steps_checked'] = trainer.ln_steps_checked
+    result['ln_exchange_ok'] = ln_checked == args.warmup + args.steps
+    result['ln_exchange_steps_checked'] = ln_checked
     if precise_entry is not None:
         result['precise_f32_tower'] = precise_entry
     if in_sync is not None:

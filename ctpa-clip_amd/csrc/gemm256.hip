@@ -1588,7 +1588,9 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   static int ggx = -1;
   if (ggx < 0) { const char* e = getenv("CTCLIP_GEMM_GROUP_GX"); ggx = e ? atoi(e) : 8; }   // r02: FF1 (11 tiles) -2%, VQ (32) -17%; N <= 6 tiles: neutral to +4% (not grouped)
   p.group_gx = ggx;
-  p.stagger = variant() == 8 ? (g_stagger8 >= 0 ? g_stagger8 : (a->act == 2 ? 4 : 0)) : (tile_rows() == 1 ? stag : 0);
+  // (round 4 sweep, profiles/r04a_stagger.log, interleaved rounds: no start stagger is best for the
+  // GEGLU GEMM now -- 0.4229 vs 0.4289 ms at the old default 4; the GEGLU backward gains ~1.5 % at 8)
+  p.stagger = variant() == 8 ? (g_stagger8 >= 0 ? g_stagger8 : (a->act == 4 ? 8 : 0)) : (tile_rows() == 1 ? stag : 0);
   hipStream_t st = (hipStream_t)stream;
   if (variant() == 8 || a->act == 4 || a->act == 5)
     return a->a_kcontig ? launch8_any<true>(p, a->b_kcontig, batch, st) : launch8_any<false>(p, a->b_kcontig, batch, st);

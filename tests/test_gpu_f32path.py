@@ -137,9 +137,9 @@ def test_sgemm_tn_exact(K, M, N, Kd):
     assert torch.equal(y, K.slinear(x, w))
     assert torch.equal(yb, y.bfloat16())
     ref = x.double() @ w.double().t()
-    assert rel(y, ref) < 1e-6
+    assert rel(y, ref) < 5e-6          # f32 accumulation over K (4,000: ~sqrt(K) 2^-24)
     y2, _ = K.linear_f32(x, w, bias=b, residual=r)
-    assert rel(y2, ref + b.double() + r.double()) < 1e-6
+    assert rel(y2, ref + b.double() + r.double()) < 5e-6
 
 
 def test_sgemm_tn_geglu(K):
@@ -208,7 +208,7 @@ def test_f32_tower_trains_small(K):
                  'visual_transformer.enc_spatial_transformer.layers.1.3.1.weight',
                  'visual_transformer.enc_temporal_transformer.layers.1.1.to_out.weight',
                  'visual_transformer.enc_temporal_transformer.norm_out.gamma'):
-        r = rel(named[name].grad, sd[name].grad)
+        r = rel(named[name].grad.cpu(), sd[name].grad)
         print(f'f32 mode {name}: grad rel err {r:.2e}')
         worst = max(worst, r)
     print(f'f32 mode: loss {loss.item():.7f} vs oracle (same indices) {out["loss"].item():.7f} (|d| {dl:.2e})')
