@@ -66,45 +66,157 @@ __global__ __launch_bounds__(256) void patch_ln_f32_kernel(const void* __restric
   }
 }
 
-// one thread per (token, 4 channels); out = x + bias + sum of the 27 taps in the reference's view
+// the same with each lane on 4 consecutive patch elements (P % 4 == 0: one 4-voxel run of a patch
+// row, an 8-B int16 / 16-B f32 read; 16-B f32 stores): one wave per token, quads lane + 64 i
+__global__ __launch_bounds__(256) void patch_ln_f32_q_kernel(const void* __restrict__ video, int is_f32, int is_hu,
+                                                             int64_t ntok, int T, int Hg, int Wg, int64_t vol_stride,
+                                                             int64_t frame_elems, int W, int PT, int P,
+                                                             const int32_t* __restrict__ offs, int pd, float eps,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, float* __restrict__ out,
+                                                             int64_t ldo) {
+  constexpr int NQ = MAXC / 4;
+  const int lane = threadIdx.x & 63;
+  const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tok >= ntok) return;
+  int64_t r = tok;
+  const int wg = (int)(r % Wg); r /= Wg;
+  const int hg = (int)(r % Hg); r /= Hg;
+  const int t = (int)(r % T);
+  const int64_t b = r / T;
+  const int64_t base = b * vol_stride + (int64_t)t * PT * frame_elems + (int64_t)hg * P * W + (int64_t)wg * P;
+  const int nq = pd / 4;
+  f32x4 v[NQ];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int qd = lane + 64 * i;
+    f32x4 x = {0.f, 0.f, 0.f, 0.f};
+    if (qd < nq) {
+      const int64_t a = base + offs[4 * qd];
+      if (is_f32) {
+        x = *(const f32x4*)((const float*)video + a);
+      } else {
+        const short4 h = *(const short4*)((const short*)video + a);
+        x = f32x4{(float)h.x, (float)h.y, (float)h.z, (float)h.w};
+      }
+      if (is_hu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = fminf(fmaxf(x[e], -1000.f), 1000.f) / 1000.f;   // data.py:150-152
+      }
+    }
+    v[i] = x;
+    s += (x[0] + x[1]) + (x[2] + x[3]);
+  }
+  const float mean = warp_sum(s) / (float)pd;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    if (lane + 64 * i < nq) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { const float d = v[i][e] - mean; q += d * d; }
+    }
+  }
+  const float rstd = 1.f / sqrtf(warp_sum(q) / (float)pd + eps);
+  float* o = out + tok * ldo;
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int qd = lane + 64 * i;
+    if (qd < nq) {
+      const f32x4 gm = *(const f32x4*)(gamma + 4 * qd), bt = *(const f32x4*)(beta + 4 * qd);
+      f32x4 y;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[e] = (v[i][e] - mean) * rstd * gm[e] + bt[e];
+      *(f32x4*)(o + 4 * qd) = y;
+    }
+  }
+}
+
+// out = x + bias + sum of the 27 taps in the reference's view.  Thread = one 4-channel quad, its
+// 4 x 27 weights held in registers (one contiguous 432-B read per thread, not a stride-27 gather
+// per tap); a block = 256 / (D / 4) token slots x PEG_NT consecutive tokens, lanes of a token
+// on consecutive quads (coalesced 16-B reads of each tap's row).
+constexpr int PEG_NT = 16;
+
 __global__ __launch_bounds__(256) void peg_f32_kernel(const float* __restrict__ x, int64_t ntok, int D,
                                                       const float* __restrict__ w, const float* __restrict__ bias,
                                                       int T, int H, int W, int mode, float* __restrict__ out) {
-  const int dq = D / 4;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= ntok * dq) return;
-  const int64_t v = i / dq;
-  const int c = (int)(i - v * dq) * 4;
-  const int hw = H * W, thw = T * hw;
-  const int64_t b = v / thw;
-  const int r = (int)(v - b * thw);
-  // mode 1: canonical row r = (t, hw) sits at the reference's physical row hw*T + t of '(b h w) t d',
-  // raw-reshaped to (b, t, h, w) (attention.py:69-70)
-  const int pv = mode == 0 ? r : (r % hw) * T + r / hw;
-  const int tv = pv / hw, hv = (pv / W) % H, wv = pv % W;
-  float acc[4];
+  const int dq = D / 4, slots = 256 / dq;
+  if ((int)threadIdx.x >= slots * dq) return;
+  const int slot = threadIdx.x / dq, c = (threadIdx.x - slot * dq) * 4;
+  float wr[27][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = bias ? bias[c + j] : 0.f;
-  for (int kt = 0; kt < 3; ++kt) {
-    const int tt = tv + kt - 2;
-    if (tt < 0) continue;
-    for (int kh = 0; kh < 3; ++kh) {
-      const int hh = hv + kh - 1;
-      if (hh < 0 || hh >= H) continue;
-      for (int kw = 0; kw < 3; ++kw) {
-        const int ww = wv + kw - 1;
-        if (ww < 0 || ww >= W) continue;
-        const int p2 = (tt * H + hh) * W + ww;
-        const int r2 = mode == 0 ? p2 : (p2 % T) * hw + p2 / T;
-        const f32x4 xv = *(const f32x4*)(x + (b * thw + r2) * (int64_t)D + c);
-        const int tap = (kt * 3 + kh) * 3 + kw;
+  for (int i = 0; i < 27; ++i) {
+    const f32x4 t = *(const f32x4*)(w + (int64_t)c * 27 + 4 * i);   // weights of channels c..c+3, taps in order
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] = fmaf(w[(int64_t)(c + j) * 27 + tap], xv[j], acc[j]);
-      }
+    for (int e = 0; e < 4; ++e) {
+      const int f = 4 * i + e;                                      // flat index (c + f / 27) * 27 + f % 27
+      wr[f % 27][f / 27] = t[e];
     }
   }
-  const f32x4 xr = *(const f32x4*)(x + v * (int64_t)D + c);
-  *(f32x4*)(out + v * (int64_t)D + c) = f32x4{acc[0] + xr[0], acc[1] + xr[1], acc[2] + xr[2], acc[3] + xr[3]};
+  float bs[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bs[j] = bias ? bias[c + j] : 0.f;
+  const int hw = H * W, thw = T * hw;
+  const int64_t v0 = (int64_t)blockIdx.x * slots * PEG_NT;
+  for (int it = 0; it < PEG_NT; ++it) {
+    const int64_t v = v0 + (int64_t)it * slots + slot;
+    if (v >= ntok) return;
+    const int64_t b = v / thw;
+    const int r = (int)(v - b * thw);
+    // mode 1: canonical row r = (t, hw) sits at the reference's physical row hw*T + t of
+    // '(b h w) t d', raw-reshaped to (b, t, h, w) (attention.py:69-70)
+    const int pv = mode == 0 ? r : (r % hw) * T + r / hw;
+    const int tv = pv / hw, hv = (pv / W) % H, wv = pv % W;
+    const float* xb = x + b * thw * (int64_t)D + c;
+    float acc[4] = {bs[0], bs[1], bs[2], bs[3]};
+#pragma unroll
+    for (int kt = 0; kt < 3; ++kt) {
+      const int tt = tv + kt - 2;
+      if (tt < 0) continue;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int hh = hv + kh - 1;
+        if (hh < 0 || hh >= H) continue;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int ww = wv + kw - 1;
+          if (ww < 0 || ww >= W) continue;
+          const int p2 = (tt * H + hh) * W + ww;
+          const int r2 = mode == 0 ? p2 : (p2 % T) * hw + p2 / T;
+          const f32x4 xv = *(const f32x4*)(xb + (int64_t)r2 * D);
+          const int tap = (kt * 3 + kh) * 3 + kw;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j] = fmaf(wr[tap][j], xv[j], acc[j]);
+        }
+      }
+    }
+    const f32x4 xr = *(const f32x4*)(x + v * (int64_t)D + c);
+    *(f32x4*)(out + v * (int64_t)D + c) = f32x4{acc[0] + xr[0], acc[1] + xr[1], acc[2] + xr[2], acc[3] + xr[3]};
+  }
+}
+
+// G = D / 4 lanes per (row, head), a 16-B quad each: y = x / max(||x||, 1e-12) * scale (F.normalize)
+template <int G>
+__global__ __launch_bounds__(256) void l2norm_f32_vec_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows,
+                                                             int H, const float* __restrict__ scale,
+                                                             float* __restrict__ y, int64_t ldy) {
+  const int64_t i = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G;
+  const int q = threadIdx.x % G;
+  const bool ok = i < rows * H;
+  const int64_t row = ok ? i / H : 0;
+  const int h = ok ? (int)(i - row * H) : 0;
+  const int D = 4 * G;
+  f32x4 v = ok ? *(const f32x4*)(x + row * ldx + h * D + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
+  float s = v[0] * v[0];
+#pragma unroll
+  for (int e = 1; e < 4; ++e) s = fmaf(v[e], v[e], s);
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) s += __shfl_xor(s, o, 64);
+  if (!ok) return;
+  const float n = fmaxf(sqrtf(s), 1e-12f);
+  const f32x4 sc = *(const f32x4*)(scale + 4 * q);
+  *(f32x4*)(y + row * ldy + h * D + 4 * q) = f32x4{v[0] / n * sc[0], v[1] / n * sc[1], v[2] / n * sc[2], v[3] / n * sc[3]};
 }
 
 // one thread per (row, head): y = x / max(||x||, 1e-12) * scale  (F.normalize semantics)
@@ -206,6 +318,124 @@ __global__ __launch_bounds__(64) void attn_f32_kernel(ctclip_attn_args a) {
   for (int d = 0; d < D; ++d) O[d] = o[d] / l;
 }
 
+// D = 32 on the f32 matrix pipe (v_mfma_f32_16x16x4_f32, exact f32 products): one block of 4 waves
+// per (64 queries, head, sequence), each wave 16 queries; keys / values in chunks of 64 through LDS.
+// QK^T is computed transposed (first MFMA operand = K rows) so a lane ends with 4 keys of ONE query
+// (keys 16 j + 4 g + r of sub-block j, query lane & 15): the softmax needs only cross-lane max /
+// sum over the 4 lane groups g.  PV reuses that layout with the keys of MFMA step s taken as
+// {16 j + 4 g + s : g} -- the probability a lane holds in register s is exactly its B operand, and
+// V is staged [key / 4][d][key % 4] so the matching A fragment is one 16-B LDS read.  K is staged
+// with its head dims permuted (d = 4 s + g at g * 8 + s) so a lane's 8 QK fragments are 2 reads.
+// The CPB bias row of the head and a key -> (h_k * (2 W - 1) + w_k) table sit in LDS.
+constexpr int FA_KLD = 36, FA_MAXNB = 2304, FA_MAXL = 1024;
+
+__global__ __launch_bounds__(256) void attn_f32_mfma_kernel(ctclip_attn_args a) {
+  __shared__ __attribute__((aligned(16))) float Ks[64 * FA_KLD];
+  __shared__ __attribute__((aligned(16))) float Vt[16 * 32 * 4];
+  __shared__ float Bs[FA_MAXNB];
+  __shared__ __attribute__((aligned(16))) int Kx[FA_MAXL + 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
+  const int h = blockIdx.y;
+  const int64_t sq = blockIdx.z;
+  const int L = a.L;
+  const int64_t rbase = (sq / a.n_inner) * a.s_outer + (sq % a.n_inner) * a.s_inner;
+  const float* Q = (const float*)a.q;
+  const float* Kp = (const float*)a.k;
+  const float* Vp = (const float*)a.v;
+  const bool bias = a.bias_u != nullptr;
+  const int Wg = bias ? a.grid_w : 1;
+  const int nb = bias ? (2 * a.grid_h - 1) * (2 * Wg - 1) : 0;
+  if (bias) {
+    for (int i = tid; i < nb; i += 256) Bs[i] = a.bias_u[(int64_t)h * nb + i];
+    for (int i = tid; i < L + 64; i += 256) Kx[i] = i < L ? (i / Wg) * (2 * Wg - 1) + i % Wg : 0;
+  }
+  const int qi = blockIdx.x * 64 + w * 16 + r16;
+  const bool qv = qi < L;
+  const int64_t qrow = rbase + (int64_t)min(qi, L - 1) * a.s_pos;
+  float qf[8];
+#pragma unroll
+  for (int s = 0; s < 8; ++s) qf[s] = qv ? Q[qrow * a.ldq + h * 32 + 4 * s + g] : 0.f;
+  int qbase = 0;
+  if (bias) qbase = (qi / Wg + a.grid_h - 1) * (2 * Wg - 1) + qi % Wg + Wg - 1;
+  float m = -INFINITY, l = 0.f;
+  f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const int kk = tid >> 2, c = tid & 3;   // staging: key kk of the chunk, head dims 8 c .. 8 c + 7
+  for (int k0 = 0; k0 < L; k0 += 64) {
+    __syncthreads();
+    {
+      const int64_t krow = rbase + (int64_t)min(k0 + kk, L - 1) * a.s_pos;
+      const f32x4 k_lo = *(const f32x4*)(Kp + krow * a.ldk + h * 32 + 8 * c);
+      const f32x4 k_hi = *(const f32x4*)(Kp + krow * a.ldk + h * 32 + 8 * c + 4);
+      const f32x4 v_lo = *(const f32x4*)(Vp + krow * a.ldv + h * 32 + 8 * c);
+      const f32x4 v_hi = *(const f32x4*)(Vp + krow * a.ldv + h * 32 + 8 * c + 4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int d = 8 * c + j;
+        const float kv = j < 4 ? k_lo[j] : k_hi[j - 4];
+        const float vv = j < 4 ? v_lo[j] : v_hi[j - 4];
+        Ks[kk * FA_KLD + (d & 3) * 8 + (d >> 2)] = kv;
+        Vt[(kk >> 2) * 128 + d * 4 + (kk & 3)] = vv;
+      }
+    }
+    __syncthreads();
+    float x[4][4];
+    float cm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x4 ka = *(const f32x4*)(Ks + (16 * j + r16) * FA_KLD + g * 8);
+      const f32x4 kb = *(const f32x4*)(Ks + (16 * j + r16) * FA_KLD + g * 8 + 4);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ka[s], qf[s], acc, 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kb[s], qf[4 + s], acc, 0, 0, 0);
+      const int key0 = k0 + 16 * j + 4 * g;
+      int kx[4] = {0, 0, 0, 0};
+      if (bias) {
+        const int4 t4 = *(const int4*)(Kx + key0);
+        kx[0] = t4.x; kx[1] = t4.y; kx[2] = t4.z; kx[3] = t4.w;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[r] * a.scale;
+        if (bias) v += qv ? Bs[qbase - kx[r]] : 0.f;
+        x[j][r] = key0 + r < L ? v : -INFINITY;
+        cm = fmaxf(cm, x[j][r]);
+      }
+    }
+    cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+    cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+    const float mn = fmaxf(m, cm);
+    const float corr = expf(m - mn);   // m = -inf on the first chunk -> 0
+    l *= corr;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { o[0][r] *= corr; o[1][r] *= corr; }
+    m = mn;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float p[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        p[r] = expf(x[j][r] - mn);
+        l += p[r];
+      }
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const f32x4 vf = *(const f32x4*)(Vt + (4 * j + g) * 128 + (db * 16 + r16) * 4);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) o[db] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf[s], p[s], o[db], 0, 0, 0);
+      }
+    }
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (!qv) return;
+  float* O = (float*)a.o + qrow * a.ldo + h * 32;
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+    *(f32x4*)(O + db * 16 + 4 * g) = f32x4{o[db][0] / l, o[db][1] / l, o[db][2] / l, o[db][3] / l};
+}
+
 inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 }  // namespace
@@ -220,6 +450,15 @@ extern "C" int ctclip_patch_ln_f32(const void* video, int32_t is_f32, int32_t is
   const int T = F / PT, Hg = H / P, Wg = W / P;
   const int64_t ntok = B * T * Hg * Wg;
   if (ntok == 0) return 0;
+  const bool quad = P % 4 == 0 && W % 4 == 0 && ldo % 4 == 0 && aligned16(out) && aligned16(gamma) &&
+                    aligned16(beta) && ((uintptr_t)video & (is_f32 ? 15 : 7)) == 0;
+  if (quad) {
+    hipLaunchKernelGGL(patch_ln_f32_q_kernel, dim3((unsigned)cdiv(ntok, 4)), dim3(256), 0, (hipStream_t)stream, video,
+                       is_f32, is_hu, ntok, T, Hg, Wg, (int64_t)C * F * H * W, (int64_t)H * W, W, PT, P, offs, pd, eps,
+                       gamma, beta, out, ldo);
+    CT_CHECK_LAUNCH();
+    return 0;
+  }
   hipLaunchKernelGGL(patch_ln_f32_kernel, dim3((unsigned)cdiv(ntok, 4)), dim3(256), 0, (hipStream_t)stream, video,
                      is_f32, is_hu, ntok, T, Hg, Wg, (int64_t)C * F * H * W, (int64_t)H * W, W, PT, P, offs, pd, eps,
                      gamma, beta, out, ldo);
@@ -232,8 +471,10 @@ extern "C" int ctclip_peg_fwd_f32(const float* x, int64_t B, int32_t T, int32_t 
   CT_REQUIRE(D % 4 == 0 && aligned16(x) && aligned16(out) && (mode == 0 || mode == 1), CT_EINVAL);
   const int64_t ntok = B * T * H * W;
   if (ntok == 0) return 0;
-  hipLaunchKernelGGL(peg_f32_kernel, dim3(blocks_for(ntok * (D / 4))), dim3(256), 0, (hipStream_t)stream, x, ntok, D,
-                     weight, bias, T, H, W, mode, out);
+  CT_REQUIRE(D / 4 <= 256 && aligned16(weight), CT_EALIGN);
+  const int64_t per_block = (int64_t)(256 / (D / 4)) * PEG_NT;
+  hipLaunchKernelGGL(peg_f32_kernel, dim3((unsigned)cdiv(ntok, per_block)), dim3(256), 0, (hipStream_t)stream, x,
+                     ntok, D, weight, bias, T, H, W, mode, out);
   CT_CHECK_LAUNCH();
   return 0;
 }
@@ -241,6 +482,20 @@ extern "C" int ctclip_peg_fwd_f32(const float* x, int64_t B, int32_t T, int32_t 
 extern "C" int ctclip_l2norm_scale_fwd_f32(const float* x, int64_t ldx, int64_t rows, int32_t H, int32_t D,
                                            const float* scale, float* y, int64_t ldy, void* stream) {
   if (rows == 0) return 0;
+  const bool vec = (D == 32 || D == 64) && aligned16(x) && aligned16(y) && aligned16(scale) && ldx % 4 == 0 &&
+                   ldy % 4 == 0;
+  if (vec) {
+    const int G = D / 4;
+    const unsigned nb = (unsigned)cdiv(rows * H, 256 / G);
+    if (G == 8)
+      hipLaunchKernelGGL(l2norm_f32_vec_kernel<8>, dim3(nb), dim3(256), 0, (hipStream_t)stream, x, ldx, rows, H, scale,
+                         y, ldy);
+    else
+      hipLaunchKernelGGL(l2norm_f32_vec_kernel<16>, dim3(nb), dim3(256), 0, (hipStream_t)stream, x, ldx, rows, H,
+                         scale, y, ldy);
+    CT_CHECK_LAUNCH();
+    return 0;
+  }
   hipLaunchKernelGGL(l2norm_f32_kernel, dim3(blocks_for(rows * H)), dim3(256), 0, (hipStream_t)stream, x, ldx, rows,
                      H, D, scale, y, ldy);
   CT_CHECK_LAUNCH();
@@ -262,7 +517,14 @@ extern "C" int ctclip_attn_fwd_f32(const ctclip_attn_args* a, void* stream) {
   if (a->bias_u) CT_REQUIRE(a->grid_h > 0 && a->grid_w > 0 && a->grid_h * a->grid_w == a->L, CT_ESHAPE);
   if (a->nseq == 0) return 0;
   dim3 grid((unsigned)cdiv(a->L, 64), (unsigned)a->H, (unsigned)a->nseq);
-  if (a->D == 32)
+  static const bool valu = [] { const char* e = getenv("CTCLIP_F32_ATTN_VALU"); return e && e[0] == '1'; }();
+  const bool mfma_ok = a->D == 32 && (!a->bias_u || ((2 * a->grid_h - 1) * (2 * a->grid_w - 1) <= FA_MAXNB &&
+                                                     a->L <= FA_MAXL));
+  if (mfma_ok && !valu) {
+    CT_REQUIRE(aligned16(a->k) && aligned16(a->v) && aligned16(a->o) && a->ldk % 4 == 0 && a->ldv % 4 == 0 &&
+                   a->ldo % 4 == 0, CT_EALIGN);
+    hipLaunchKernelGGL(attn_f32_mfma_kernel, grid, dim3(256), 0, (hipStream_t)stream, *a);
+  } else if (a->D == 32)
     hipLaunchKernelGGL(attn_f32_kernel<32>, grid, dim3(64), 0, (hipStream_t)stream, *a);
   else if (a->D == 64)
     hipLaunchKernelGGL(attn_f32_kernel<64>, grid, dim3(64), 0, (hipStream_t)stream, *a);

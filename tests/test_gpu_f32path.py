@@ -32,11 +32,13 @@ def test_peg_f32(K, mode, shape, D):
     assert rel(out, ref) < 2e-7, rel(out, ref)
 
 
-@pytest.mark.parametrize('case', ['spatial', 'spatial_6x6', 'temporal'])
+@pytest.mark.parametrize('case', ['spatial', 'spatial_6x6', 'spatial_5x7', 'spatial_20x30', 'temporal'])
 def test_attention_f32(K, case):
+    """D = 32 runs the f32-MFMA kernel (ragged 16-query / 64-key chunks in the 5x7, 20x30 and
+    temporal L = 24 cases)."""
     torch.manual_seed(3)
     if case.startswith('spatial'):
-        gh = gw = 24 if case == 'spatial' else 6
+        gh, gw = {'spatial': (24, 24), 'spatial_6x6': (6, 6), 'spatial_5x7': (5, 7), 'spatial_20x30': (20, 30)}[case]
         L, H, D, nseq = gh * gw, 8, 32, 3
         M, seq, grid = nseq * L, (1, L, 0, 1), (gh, gw)
         u, bins = _cpb_table(H, gh, gw)

@@ -5,6 +5,9 @@
 //   1: 8 rows x 128 B (full cache lines per row)
 //   2: 4 rows x 256 B
 //   3: 1 KB contiguous
+//   4: 8 rows x 128 B, consecutive lanes on consecutive 16 B of a row (row = lane / 8)
+//   5: 16 rows x 64 B, lane-contiguous (row = lane / 4)
+//   6: 4 rows x 256 B, lane-contiguous (row = lane / 16)
 // Grid: `active` workgroups store, one per CU (256 = every CU at once; fewer = a partial burst),
 // each `reps` tiles back to back into disjoint memory.  Reports device time, GB/s and the per-CU
 // bytes per cycle (s_memtime, median over workgroups).
@@ -39,8 +42,17 @@ __global__ __launch_bounds__(NTH, 1) void probe(uint4* out, int pattern, int rep
       } else if (pattern == 2) { // 4 rows x 256 B
         const int row = (inst / 2) * 4 + (lane & 3), cb = (inst % 2) * 256 + (lane >> 2) * 16;
         off = (size_t)row * 512 + cb;
-      } else {                   // 1 KB contiguous
+      } else if (pattern == 3) { // 1 KB contiguous
         off = (size_t)inst * 1024 + lane * 16;
+      } else if (pattern == 4) {
+        const int row = (inst / 4) * 8 + (lane >> 3), cb = (inst % 4) * 128 + (lane & 7) * 16;
+        off = (size_t)row * 512 + cb;
+      } else if (pattern == 5) {
+        const int row = (inst / 8) * 16 + (lane >> 2), cb = (inst % 8) * 64 + (lane & 3) * 16;
+        off = (size_t)row * 512 + cb;
+      } else {
+        const int row = (inst / 2) * 4 + (lane >> 4), cb = (inst % 2) * 256 + (lane & 15) * 16;
+        off = (size_t)row * 512 + cb;
       }
       *(uint4*)(tb + off) = v;
     }
@@ -60,8 +72,8 @@ int main() {
   hipEventCreate(&a);
   hipEventCreate(&b);
   printf("pattern active  ms      GB/s   B/cyc/CU(median)\n");
-  for (int active : {256, 128, 64, 32, 8}) {
-    for (int pat = 0; pat < 4; ++pat) {
+  for (int active : {256, 128, 32}) {
+    for (int pat = 0; pat < 7; ++pat) {
       for (int it = 0; it < 2; ++it) {
         hipEventRecord(a);
         hipLaunchKernelGGL(probe, dim3(active), dim3(NTH), 0, 0, out, pat, reps, cyc);
