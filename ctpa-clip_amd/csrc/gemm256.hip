@@ -59,6 +59,7 @@ struct P {
   int* status;
   unsigned spin_limit;               // polls before giving up on the partner (status = 1)
   int ln_debug;                      // test knob: tile 1 of row block 0 never publishes
+  int epi_lds;                       // transposed bf16 / GEGLU epilogues: lane-contiguous stores via LDS
 };
 
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
@@ -640,6 +641,27 @@ __device__ __forceinline__ void store_row_bf16(u16* rowp, const float (&v)[4][4]
   }
 }
 
+// The same 16-row block of 64 bf16 columns (rows gm0 .. gm0 + 15, C at (gm0, c0)) through the
+// wave's LDS scratch: a lane of the transposed layout holds one row (lane & 15), so its 16-B stores
+// are 16 rows x 64 B per instruction with consecutive lanes on different rows -- the per-CU store
+// path drains that at ~16 B/cycle, against ~57 B/cycle when consecutive lanes write consecutive
+// 16 B of a row (tools/store_probe.hip, profiles/r04c_store_probe.log).  Rows are staged at a
+// 144-B pitch (16 distinct bank quads for the b128 writes) and read back row-major, 8 lanes per
+// 128-B row.  Wave-private scratch: LDS order within the wave is program order, no barrier.
+constexpr int SCR_H = 144, SCR_G = 80, SCR_GOFF = 16 * SCR_H;   // h block 2304 B + g block 1280 B
+__device__ __forceinline__ void store_blk_bf16_lds(char* scr, u16* C, int64_t ldc, int64_t gm0, int64_t M, int64_t c0,
+                                                   int64_t N, const float (&v)[4][4], int g, int m, int lane) {
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp)
+    *(u32x4*)(scr + m * SCR_H + (32 * jp + pair_coff(g)) * 2) = pair_swap(v[2 * jp], v[2 * jp + 1]);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = 8 * h + (lane >> 3), c = (lane & 7) * 8;
+    const u32x4 d = *(const u32x4*)(scr + r * SCR_H + c * 2);
+    if (gm0 + r < M && c0 + c < N) st16(C + r * ldc + c, d);
+  }
+}
+
 // MODE (compile time, so each variant's row loop stays small enough to unroll fully and the
 // accumulator never leaves registers): 0 = general (bias / residual / GELU / f32 or bf16 /
 // accumulate / shadow), 2 = GEGLU, 3 = argmax, 4 = GEGLU backward, 5 = split-K slab.
@@ -650,9 +672,9 @@ __device__ __forceinline__ void store_row_bf16(u16* rowp, const float (&v)[4][4]
 // ds_bpermute on the VQ argmax GEMM (1.193 vs 1.171-1.176 ms, profiles/r02aw_*), so off
 constexpr bool GEMM_PERMLANE = CTCLIP_GEMM_PERMLANE;
 
-template <int MODE>
+template <int MODE, bool LDS = false>
 __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int wr, int wc, int lane, int64_t m0,
-                                           int64_t n0, int split, int bidx) {
+                                           int64_t n0, int split, int bidx, char* scr) {
   const int m = lane & 15, g = lane >> 4;
   const int64_t wrow0 = m0 + wr * 128, wcol0 = n0 + wc * 64;
   const int64_t cl = wcol0 + 4 * g;          // this lane's column in block j: cl + 16 j
@@ -768,6 +790,21 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
     }
     if constexpr (MODE == 2) {
       // GEGLU in 32-column pairs: blocks 0,1 = x, blocks 2,3 = gate; h keeps both halves
+      if constexpr (LDS) {
+        const int64_t gm0 = wrow0 + i * 16;
+        store_blk_bf16_lds(scr, (u16*)p.C + bidx * p.sC + gm0 * p.ldc + wcol0, p.ldc, gm0, p.M, wcol0, p.N, v, g, m,
+                           lane);
+        float gg[2][4];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) gg[j][r] = gelu_erf(bf2f(f2bf(v[j + 2][r]))) * bf2f(f2bf(v[j][r]));
+        *(u32x4*)(scr + SCR_GOFF + m * SCR_G + pair_coff(g) * 2) = pair_swap(gg[0], gg[1]);
+        const int r = lane >> 2, c = (lane & 3) * 8;
+        const u32x4 d = *(const u32x4*)(scr + SCR_GOFF + r * SCR_G + c * 2);
+        if (gm0 + r < p.M && wcol0 < p.N) st16(p.C2 + bidx * p.sC2 + (gm0 + r) * p.ldc2 + (wcol0 >> 1) + c, d);
+        continue;
+      }
       store_row_bf16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N);
       float gg[2][4];
 #pragma unroll
@@ -839,9 +876,23 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
             for (int r = 0; r < 4; ++r) v[j][r] += rr[r];
           }
       }
-      store_row_bf16(Cb, v, g, rok, wcol0, p.N);
+      if constexpr (LDS) {
+        const int64_t gm0 = wrow0 + i * 16;
+        store_blk_bf16_lds(scr, (u16*)p.C + bidx * p.sC + gm0 * p.ldc + wcol0, p.ldc, gm0, p.M, wcol0, p.N, v, g, m,
+                           lane);
+      } else {
+        store_row_bf16(Cb, v, g, rok, wcol0, p.N);
+      }
     }
-    if (p.C2 && p.act == 0) store_row_bf16(p.C2 + bidx * p.sC2 + gm * p.ldc2 + wcol0, v, g, rok, wcol0, p.N);
+    if (p.C2 && p.act == 0) {
+      if constexpr (LDS) {
+        const int64_t gm0 = wrow0 + i * 16;
+        store_blk_bf16_lds(scr, p.C2 + bidx * p.sC2 + gm0 * p.ldc2 + wcol0, p.ldc2, gm0, p.M, wcol0, p.N, v, g, m,
+                           lane);
+      } else {
+        store_row_bf16(p.C2 + bidx * p.sC2 + gm * p.ldc2 + wcol0, v, g, rok, wcol0, p.N);
+      }
+    }
   }
 }
 
@@ -1298,6 +1349,10 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // TR epilogue scratch (p.epi_lds): 4 KB per wave in buffer O's A1 / B1 halves, which nothing
+  // loads while the epilogue runs (the next tile's prologue fills E and O's A0 / B0)
+  const int wu = __builtin_amdgcn_readfirstlane(w);   // wave-uniform: the scratch base stays scalar
+  char* scr = smem + TILEB + (wu < 4 ? A1 : B1) * HALF + (wu & 3) * 4096;
 
   auto stage_of = [&](const Tile& tl, int which, int t) {
     if (t >= tl.nk) return;
@@ -1417,16 +1472,16 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
       for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
-    } else if constexpr (EP == 2) {
-      epilogue_t<2>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
+    } else if constexpr (EP == 2 || EP == 12) {
+      epilogue_t<2, EP == 12>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx, scr);
     } else if constexpr (EP == 4) {
       epilogue_geglu_bwd(p, acc, wr, wc, lane, T.m0, T.n0, T.bidx);
-    } else if constexpr (EP == 0) {
-      epilogue_t<0>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
+    } else if constexpr (EP == 0 || EP == 10) {
+      epilogue_t<0, EP == 10>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx, scr);
     } else if constexpr (EP == 3) {
-      epilogue_t<3>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
+      epilogue_t<3>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx, scr);
     } else if constexpr (EP == 6) {
-      epilogue_t<6>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
+      epilogue_t<6>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx, scr);
     } else if constexpr (EP == -6 || EP == -7) {
       epilogue_ln<EP == -6 ? 6 : 7>(p, acc, smem, w, wr, wc, lane, T.m0, T.n0);
     } else {
@@ -1509,6 +1564,7 @@ int launch_any(const P& p, bool ak, bool bk, int batch, hipStream_t st) {
 static int g_variant = -1;
 static int g_stagger8 = -1;   // 8-phase start stagger (units of s_sleep(32)); -1 = default
 static int g_persist = -1;    // 8-phase persistent tile loop (CTCLIP_GEMM_PERSIST, default on)
+static int g_epi_lds = -1;    // transposed bf16 / GEGLU epilogues through LDS (CTCLIP_EPI_LDS)
 int variant() {
   if (g_variant < 0) {
     const char* e = getenv("CTCLIP_GEMM_VARIANT");
@@ -1521,7 +1577,8 @@ int tile_rows() { return variant() == 2 ? 2 : 1; }
 
 // epilogue kind, one kernel instantiation each (so the accumulator registers never share a
 // kernel with another epilogue's live ranges): -1 = LDS-staged rows (f32 / residual / argmax /
-// split-K slabs), 0 = transposed bf16, 2 = transposed GEGLU, 4 = transposed GEGLU backward
+// split-K slabs), 0 = transposed bf16, 2 = transposed GEGLU, 4 = transposed GEGLU backward,
+// 10 / 12 = 0 / 2 with their bf16 stores re-laid through LDS (store_blk_bf16_lds)
 template <bool AK, bool BKC>
 int launch8_ep(const P& p, int batch, hipStream_t st) {
   if (p.act == 4) return launch8<AK, BKC, 4>(p, batch, st);
@@ -1541,8 +1598,9 @@ int launch8_ep(const P& p, int batch, hipStream_t st) {
     if (p.R && p.r_f32 && p.c_f32 && p.act == 0 && !p.accumulate) return launch8<AK, BKC, -2>(p, batch, st);
     return launch8<AK, BKC, -1>(p, batch, st);
   }
-  if (p.act == 2) return launch8<AK, BKC, 2>(p, batch, st);
-  return launch8<AK, BKC, 0>(p, batch, st);
+  // 10 / 12: the same epilogues with lane-contiguous stores through LDS (p.epi_lds)
+  if (p.act == 2) return p.epi_lds ? launch8<AK, BKC, 12>(p, batch, st) : launch8<AK, BKC, 2>(p, batch, st);
+  return p.epi_lds ? launch8<AK, BKC, 10>(p, batch, st) : launch8<AK, BKC, 0>(p, batch, st);
 }
 
 template <bool AK>
@@ -1582,6 +1640,11 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   }
   p.gz = batch * split;
   p.persist = g_persist;
+  if (g_epi_lds < 0) {
+    const char* e = getenv("CTCLIP_EPI_LDS");
+    g_epi_lds = e ? (atoi(e) != 0) : 0;
+  }
+  p.epi_lds = g_epi_lds;
   // 8-phase default: stagger only the GEGLU GEMM, whose epilogue (h + g stores + erf) is long
   // enough that desynchronised CUs pay off (r01 sweep: 0.52 -> 0.48 ms at B = 8; neutral to
   // slightly negative on the plain / residual epilogues)
@@ -1657,6 +1720,14 @@ extern "C" int ctclip_gemm_ln(const ctclip_gemm_args* a, const ctclip_ln_epilogu
   if (!a->a_kcontig) return CT_EINVAL;
   if (ln->mode == 1) return a->b_kcontig ? launch8<true, true, -6>(p, 1, st) : launch8<true, false, -6>(p, 1, st);
   return a->b_kcontig ? launch8<true, true, -7>(p, 1, st) : launch8<true, false, -7>(p, 1, st);
+}
+
+// A/B switch: the transposed bf16 / GEGLU epilogues' stores through the wave's LDS scratch
+// (lane-contiguous 16-B stores); returns the previous value
+extern "C" int ctclip_gemm_set_epi_lds(int v) {
+  const int old = g256::g_epi_lds;
+  g256::g_epi_lds = v ? 1 : 0;
+  return old;
 }
 
 // diagnostic: 8-phase kernel start stagger (see gemm8p_kernel); returns the previous value

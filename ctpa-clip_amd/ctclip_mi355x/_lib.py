@@ -128,6 +128,7 @@ _SIGS = {
     'ctclip_dropout': [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, ctypes.c_uint64, c_vp],
     'ctclip_gemm_set_variant': [c_i32],
     'ctclip_gemm_set_stagger': [c_i32],
+    'ctclip_gemm_set_epi_lds': [c_i32],
     'ctclip_gemm_set_persist': [c_i32],
     'ctclip_gemm_set_grid_cap': [c_i32],
     'ctclip_reduce_slabs_ep': [c_vp, c_i64, c_i64, c_i64, c_i64, ctypes.POINTER(GemmArgs), c_vp],

@@ -19,14 +19,20 @@ def _rel(a, b):
 
 def _variants(K, fn):
     """Outputs of the 8-phase kernel (persistent, key 8) and the 128x256x32 kernel (key 1); the
-    8-phase kernel with one workgroup per tile, and persistent on a grid capped at 92 workgroups,
-    must match the persistent one bit for bit."""
+    8-phase kernel with one workgroup per tile, persistent on a grid capped at 92 workgroups, and
+    with its bf16 / GEGLU epilogue stores re-laid through LDS (ctclip_gemm_set_epi_lds), must match
+    the persistent one bit for bit."""
     from ctclip_mi355x import _lib
     outs = {}
     lib = _lib.lib()
     prev, prev_p = lib.ctclip_gemm_set_variant(8), lib.ctclip_gemm_set_persist(1)
+    prev_l = lib.ctclip_gemm_set_epi_lds(0)
     snap = lambda o: o.clone() if torch.is_tensor(o) else o  # noqa: E731
     try:
+        lib.ctclip_gemm_set_epi_lds(1)
+        lds = snap(fn())
+        torch.cuda.synchronize()
+        lib.ctclip_gemm_set_epi_lds(0)
         for v in (8, 1):
             lib.ctclip_gemm_set_variant(v)
             outs[v] = snap(fn())
@@ -43,7 +49,9 @@ def _variants(K, fn):
         lib.ctclip_gemm_set_grid_cap(0)
         lib.ctclip_gemm_set_variant(prev)
         lib.ctclip_gemm_set_persist(prev_p if prev_p >= 0 else 1)
+        lib.ctclip_gemm_set_epi_lds(max(prev_l, 0))
     if torch.is_tensor(single):
+        assert torch.equal(lds, outs[8]), 'LDS-relaid epilogue stores differ'
         assert torch.equal(single, outs[8]), 'persistent 8-phase GEMM differs from one workgroup per tile'
         assert torch.equal(capped, outs[8]), 'persistent 8-phase GEMM on a capped grid differs'
     return outs
