@@ -185,18 +185,32 @@ template <bool F32>
 __global__ __launch_bounds__(256) void patch_ln_strip20_kernel(const void* __restrict__ video, int is_hu, int T,
                                                                int Hg, int Wg, int64_t vol_stride, int H, int W,
                                                                int PT, float eps, u16* __restrict__ out,
-                                                               int64_t ldo) {
+                                                               int64_t ldo, int g_remap) {
   using E = typename std::conditional<F32, float, short>::type;
   constexpr int P = 20, VEC = F32 ? 4 : 8;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   E* sx = (E*)smem_raw;   // [PT * P][ntk * P]
   constexpr int NCH = PW * 4096 / VEC / 256;
   const int pd = PT * P * P;
-  int r = blockIdx.y;
+  // XCD-aware block order: the gridDim.x strips of one (b, t, hg) row group share partial 128-B
+  // lines at their edges (a 4-patch strip row is 160 B of int16); consecutive dispatch goes round
+  // robin over the 8 XCDs, so remap the linear index to give each XCD a contiguous range and let
+  // its L2 merge those lines instead of each XCD fetching them from HBM
+  int bx = blockIdx.x, by = blockIdx.y;
+  {
+    const int nb = gridDim.x * gridDim.y, lin = by * gridDim.x + bx;
+    if (nb >= 64 && g_remap) {
+      const int xcd = lin & 7, q = nb >> 3, rm = nb & 7;
+      const int id = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + (lin >> 3);
+      by = id / gridDim.x;
+      bx = id - by * gridDim.x;
+    }
+  }
+  int r = by;
   const int hg = r % Hg; r /= Hg;
   const int t = r % T;
   const int b = r / T;
-  const int wg0 = blockIdx.x * PW;
+  const int wg0 = bx * PW;
   const int ntk = min(PW, Wg - wg0);
   const int sw = ntk * P, cpr = sw / VEC;
   const int nchunk = PT * P * cpr;
@@ -269,6 +283,8 @@ __global__ __launch_bounds__(256) void patch_ln_strip20_kernel(const void* __res
 }
 
 bool s_strip_attr = false;
+// A/B switch of the strip20 kernel's XCD-aware block order (CTCLIP_PATCH_XCD=0: dispatch order)
+int s_patch_remap = [] { const char* e = getenv("CTCLIP_PATCH_XCD"); return e ? atoi(e) != 0 : 1; }();
 bool s_strip20_attr = false;
 
 // Given G = dy^T . xhat  [N][K] (f32) and colsum(dy) cs[N], produce the grads of the folded
@@ -420,10 +436,10 @@ extern "C" int ctclip_patch_ln(const void* video, int32_t is_f32, int32_t is_hu,
       }
       if (is_f32)
         hipLaunchKernelGGL(patch_ln_strip20_kernel<true>, grid, dim3(256), sm, (hipStream_t)stream, video, is_hu, T,
-                           Hg, Wg, vol, H, W, PT, eps, (u16*)out, ldo);
+                           Hg, Wg, vol, H, W, PT, eps, (u16*)out, ldo, s_patch_remap);
       else
         hipLaunchKernelGGL(patch_ln_strip20_kernel<false>, grid, dim3(256), sm, (hipStream_t)stream, video, is_hu, T,
-                           Hg, Wg, vol, H, W, PT, eps, (u16*)out, ldo);
+                           Hg, Wg, vol, H, W, PT, eps, (u16*)out, ldo, s_patch_remap);
     } else if (is_f32)
       hipLaunchKernelGGL(patch_ln_strip_kernel<true>, grid, dim3(256), sm, (hipStream_t)stream, video, is_hu, T, Hg,
                          Wg, vol, H, W, PT, P, eps, (u16*)out, ldo);
