@@ -60,6 +60,7 @@ struct AP {
   float drop_p, drop_scale;
   unsigned thresh;
   uint64_t seed;
+  float lazy;                     // forward: lazy-rescale threshold (log2 units), <= 0 = every chunk
 };
 
 constexpr int NW = 8;             // waves per workgroup
@@ -372,6 +373,7 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
         }
       bf16x8 pb[QB];
       float alpha[QB];
+      bool rescale[QB];
 #pragma unroll
       for (int u = 0; u < QB; ++u) {
         float cmax = -INFINITY;
@@ -401,9 +403,21 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
         }
         cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
         cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
-        const float mnew = fmaxf(m[u], cmax);
-        const float msafe = mnew == -INFINITY ? 0.f : mnew;
-        alpha[u] = fexp2(m[u] - msafe);
+        // lazy rescale (p.lazy > 0, CTCLIP_ATTN_LAZY, default 8): the running max only moves when
+        // some lane's chunk max exceeds it by more than p.lazy (log2 units), so after the first
+        // chunks the wave skips the alpha exp2, the lsum and the o rescale; probabilities stay <= 2^p.lazy (f32 sums,
+        // bf16 P operands: no range issue), and lse = m + log2(lsum) is exact either way
+        rescale[u] = p.lazy <= 0.f || __any(cmax > m[u] + p.lazy);
+        float msafe;
+        if (rescale[u]) {
+          const float mnew = fmaxf(m[u], cmax);
+          msafe = mnew == -INFINITY ? 0.f : mnew;
+          alpha[u] = fexp2(m[u] - msafe);
+          m[u] = mnew;
+        } else {
+          msafe = m[u];        // finite: some earlier chunk set it
+          alpha[u] = 1.f;
+        }
         float psum = 0.f;
 #pragma unroll
         for (int bi = 0; bi < 2; ++bi)
@@ -413,8 +427,7 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
             sa[u][bi][r] = e;
             psum += e;
           }
-        lsum[u] = lsum[u] * alpha[u] + psum;
-        m[u] = mnew;
+        lsum[u] = rescale[u] ? lsum[u] * alpha[u] + psum : lsum[u] + psum;
         if constexpr (!BIAS) {
           if (p.drop_p > 0.f) {
 #pragma unroll
@@ -430,7 +443,7 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
         const bf16x8 vf = trfrag<D>(Vimg, kc, d * 16, lane);
 #pragma unroll
         for (int u = 0; u < QB; ++u) {
-          o[u][d] *= alpha[u];
+          if (rescale[u]) o[u][d] *= alpha[u];
           o[u][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[u], o[u][d], 0, 0, 0);
         }
       }
@@ -1310,6 +1323,8 @@ int fill(AP& p, const ctclip_attn_args* a) {
   p.drop_scale = p.drop_p > 0.f ? 1.f / (1.f - p.drop_p) : 1.f;
   p.thresh = (unsigned)std::min(4294967295.0, (double)p.drop_p * 4294967296.0);
   p.seed = a->dropout_seed;
+  static const float lazy = [] { const char* e = getenv("CTCLIP_ATTN_LAZY"); return e ? (float)atof(e) : 8.f; }();
+  p.lazy = lazy;
   p.L = a->L; p.H = a->H; p.nseq = a->nseq; p.M = a->M;
   p.Hg = a->grid_h; p.Wg = a->grid_w;
   p.nbins = (2 * a->grid_h - 1) * (2 * a->grid_w - 1);
