@@ -630,6 +630,13 @@ __device__ __forceinline__ void st16(void* p, u32x4 d) {
 #endif
 }
 
+// 16-B store that drops its line from the XCD's L2 (sc1; MI355X_MICROARCH.md, store flavours)
+__device__ __forceinline__ void st16_sc1(void* p, u32x4 d) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const v4u dv = {d.x, d.y, d.z, d.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(dv) : "memory");
+}
+
 // store one row's 4 j-blocks x 4 cols as bf16; rowp = row base at the wave's first column c0
 __device__ __forceinline__ void store_row_bf16(u16* rowp, const float (&v)[4][4], int g, bool ok, int64_t c0,
                                                int64_t N) {
@@ -650,7 +657,8 @@ __device__ __forceinline__ void store_row_bf16(u16* rowp, const float (&v)[4][4]
 // 128-B row.  Wave-private scratch: LDS order within the wave is program order, no barrier.
 constexpr int SCR_H = 144, SCR_G = 80, SCR_GOFF = 16 * SCR_H;   // h block 2304 B + g block 1280 B
 __device__ __forceinline__ void store_blk_bf16_lds(char* scr, u16* C, int64_t ldc, int64_t gm0, int64_t M, int64_t c0,
-                                                   int64_t N, const float (&v)[4][4], int g, int m, int lane) {
+                                                   int64_t N, const float (&v)[4][4], int g, int m, int lane,
+                                                   bool sc1) {
 #pragma unroll
   for (int jp = 0; jp < 2; ++jp)
     *(u32x4*)(scr + m * SCR_H + (32 * jp + pair_coff(g)) * 2) = pair_swap(v[2 * jp], v[2 * jp + 1]);
@@ -658,7 +666,10 @@ __device__ __forceinline__ void store_blk_bf16_lds(char* scr, u16* C, int64_t ld
   for (int h = 0; h < 2; ++h) {
     const int r = 8 * h + (lane >> 3), c = (lane & 7) * 8;
     const u32x4 d = *(const u32x4*)(scr + r * SCR_H + c * 2);
-    if (gm0 + r < M && c0 + c < N) st16(C + r * ldc + c, d);
+    if (gm0 + r < M && c0 + c < N) {
+      if (sc1) st16_sc1(C + r * ldc + c, d);
+      else st16(C + r * ldc + c, d);
+    }
   }
 }
 
@@ -793,7 +804,7 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
       if constexpr (LDS) {
         const int64_t gm0 = wrow0 + i * 16;
         store_blk_bf16_lds(scr, (u16*)p.C + bidx * p.sC + gm0 * p.ldc + wcol0, p.ldc, gm0, p.M, wcol0, p.N, v, g, m,
-                           lane);
+                           lane, p.epi_lds == 2);
         float gg[2][4];
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -802,7 +813,10 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
         *(u32x4*)(scr + SCR_GOFF + m * SCR_G + pair_coff(g) * 2) = pair_swap(gg[0], gg[1]);
         const int r = lane >> 2, c = (lane & 3) * 8;
         const u32x4 d = *(const u32x4*)(scr + SCR_GOFF + r * SCR_G + c * 2);
-        if (gm0 + r < p.M && wcol0 < p.N) st16(p.C2 + bidx * p.sC2 + (gm0 + r) * p.ldc2 + (wcol0 >> 1) + c, d);
+        if (gm0 + r < p.M && wcol0 < p.N) {
+          if (p.epi_lds == 2) st16_sc1(p.C2 + bidx * p.sC2 + (gm0 + r) * p.ldc2 + (wcol0 >> 1) + c, d);
+          else st16(p.C2 + bidx * p.sC2 + (gm0 + r) * p.ldc2 + (wcol0 >> 1) + c, d);
+        }
         continue;
       }
       store_row_bf16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N);
@@ -879,7 +893,7 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
       if constexpr (LDS) {
         const int64_t gm0 = wrow0 + i * 16;
         store_blk_bf16_lds(scr, (u16*)p.C + bidx * p.sC + gm0 * p.ldc + wcol0, p.ldc, gm0, p.M, wcol0, p.N, v, g, m,
-                           lane);
+                           lane, p.epi_lds == 2);
       } else {
         store_row_bf16(Cb, v, g, rok, wcol0, p.N);
       }
@@ -888,7 +902,7 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
       if constexpr (LDS) {
         const int64_t gm0 = wrow0 + i * 16;
         store_blk_bf16_lds(scr, p.C2 + bidx * p.sC2 + gm0 * p.ldc2 + wcol0, p.ldc2, gm0, p.M, wcol0, p.N, v, g, m,
-                           lane);
+                           lane, p.epi_lds == 2);
       } else {
         store_row_bf16(p.C2 + bidx * p.sC2 + gm * p.ldc2 + wcol0, v, g, rok, wcol0, p.N);
       }
@@ -1642,7 +1656,7 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   p.persist = g_persist;
   if (g_epi_lds < 0) {
     const char* e = getenv("CTCLIP_EPI_LDS");
-    g_epi_lds = e ? (atoi(e) != 0) : 0;
+    g_epi_lds = e ? std::min(2, std::max(0, atoi(e))) : 0;
   }
   p.epi_lds = g_epi_lds;
   // 8-phase default: stagger only the GEGLU GEMM, whose epilogue (h + g stores + erf) is long
@@ -1726,7 +1740,7 @@ extern "C" int ctclip_gemm_ln(const ctclip_gemm_args* a, const ctclip_ln_epilogu
 // (lane-contiguous 16-B stores); returns the previous value
 extern "C" int ctclip_gemm_set_epi_lds(int v) {
   const int old = g256::g_epi_lds;
-  g256::g_epi_lds = v ? 1 : 0;
+  g256::g_epi_lds = v == 2 ? 2 : (v ? 1 : 0);
   return old;
 }
 

@@ -75,8 +75,9 @@ int ctclip_gemm_set_variant(int variant);
 /* diagnostic: start stagger of the 8-phase kernel (units of ~2k cycles); returns the previous */
 int ctclip_gemm_set_stagger(int units);
 /* A/B switch: the 8-phase kernel's transposed bf16 / GEGLU epilogues store through a wave-private
- * LDS scratch so consecutive lanes write consecutive 16 B of a row (1) or straight from the
- * transposed accumulator layout (0); returns the previous setting.  Results are identical. */
+ * LDS scratch so consecutive lanes write consecutive 16 B of a row (1; 2 = the same with sc1
+ * stores, which drop their lines from the XCD's L2) or straight from the transposed accumulator
+ * layout (0, default); returns the previous setting.  Results are identical. */
 int ctclip_gemm_set_epi_lds(int on);
 /* diagnostic: 8-phase kernel as persistent workgroups walking the tile sequence (1, default) or
  * one workgroup per tile (0); returns the previous setting.  Results are identical. */

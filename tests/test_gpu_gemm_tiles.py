@@ -32,6 +32,9 @@ def _variants(K, fn):
         lib.ctclip_gemm_set_epi_lds(1)
         lds = snap(fn())
         torch.cuda.synchronize()
+        lib.ctclip_gemm_set_epi_lds(2)      # the same with L2-dropping (sc1) stores
+        lds_sc1 = snap(fn())
+        torch.cuda.synchronize()
         lib.ctclip_gemm_set_epi_lds(0)
         for v in (8, 1):
             lib.ctclip_gemm_set_variant(v)
@@ -52,6 +55,7 @@ def _variants(K, fn):
         lib.ctclip_gemm_set_epi_lds(max(prev_l, 0))
     if torch.is_tensor(single):
         assert torch.equal(lds, outs[8]), 'LDS-relaid epilogue stores differ'
+        assert torch.equal(lds_sc1, outs[8]), 'LDS-relaid sc1 epilogue stores differ'
         assert torch.equal(single, outs[8]), 'persistent 8-phase GEMM differs from one workgroup per tile'
         assert torch.equal(capped, outs[8]), 'persistent 8-phase GEMM on a capped grid differs'
     return outs
