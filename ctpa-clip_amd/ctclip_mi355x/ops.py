@@ -14,12 +14,15 @@ are the same kernels exposed one operation at a time, for callers that compose t
     torch.ops.ctclip.vq_cos_argmax(x, codebook)                 # (idx int32, l2norm(x))
     torch.ops.ctclip.peg_dwconv3d(x, weight, bias, shape, mode)  # x + PEG(x), canonical rows
     torch.ops.ctclip.cpb_mlp(rel, w0, b0, w1, b1, w2, b2)        # CPB table [heads, bins]
+    torch.ops.ctclip.patch_embed_i16(video, ln1_w, ln1_b, w, b, ln2_w, ln2_b, pt, p)   # to_patch_emb
+    torch.ops.ctclip.bert_layer(x, attention_mask, heads, eps, wq, bq, ..., ln2_w, ln2_b)  # eval
 
 Device tensors only (the ops are registered for the "cuda" device type, which is HIP on ROCm):
 a CPU tensor raises, and with the library missing every op raises (``_lib.lib``).  Reference
 call sites: ct_clip/attention.py:44-52,88-181 (linears, LayerNorm, cosine attention), :56-84
 (PEG), :229-276 (continuous position bias),
-ct_clip/ct_clip.py:796-812 (InfoNCE), ct_clip/ctvit.py:421-427 (VQ cosine argmax)."""
+ct_clip/ct_clip.py:796-812 (InfoNCE), ct_clip/ctvit.py:421-427 (VQ cosine argmax), :169-174
+(patch embedding), ct_clip/ct_clip.py:685-686 (the BERT text tower's layers)."""
 from __future__ import annotations
 
 from typing import List, Optional, Tuple
@@ -347,3 +350,104 @@ def cpb_mlp(rel: Tensor, w0: Tensor, b0: Tensor, w1: Tensor, b1: Tensor, w2: Ten
     (functional.cpb_table: sign(x) log(|x| + 1) of the (dh, dw) offsets of an h x w grid).
     Returns the bias table [heads, bins] that cos_attn(bias=..., grid=(h, w)) consumes."""
     return _cpb_mlp(rel, w0, b0, w1, b1, w2, b2)[0]
+
+
+# ------------------------------------------------------------------------ patch_embed_i16
+@torch.library.custom_op('ctclip::patch_embed_i16', mutates_args=(), device_types='cuda')
+def _patch_embed_i16(video: Tensor, ln1_w: Tensor, ln1_b: Tensor, w: Tensor, b: Tensor, ln2_w: Tensor,
+                     ln2_b: Tensor, temporal_patch: int, patch: int) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+    from .layers import patch_offsets
+    _need(video.dim() == 5 and video.dtype in (torch.int16, F32), 'patch_embed_i16: video [B, C, F, H, W] int16 / f32')
+    Bv, C, Fr, H, W = video.shape
+    PT, P = temporal_patch, patch
+    _need(Fr % PT == 0 and H % P == 0 and W % P == 0, 'patch_embed_i16: frames / sides divisible by the patch')
+    pd, dim = C * PT * P * P, w.shape[0]
+    _need(w.dtype == F32 and w.shape == (dim, pd) and b.shape == (dim,) and ln1_w.shape == (pd,) == ln1_b.shape
+          and ln2_w.shape == (dim,) == ln2_b.shape, 'patch_embed_i16: w [dim, c*pt*p*p], b / ln2 [dim], ln1 [pd]')
+    video = video.contiguous()
+    offs = patch_offsets(C, PT, P, P, H, W).to(video.device)
+    kp = (pd + 63) // 64 * 64
+    xhat_p = K.patch_ln(video, video.dtype == torch.int16, PT, P, offs, ld=kp)   # [M, kp] bf16
+    Wp = K.pack_rows(w.contiguous(), dim, kp, colscale=ln1_w.contiguous())         # W diag(g1), bf16
+    bp = K.slinear(ln1_b.view(1, -1), w, bias=b).view(-1)                          # b + W beta1
+    y1 = K.linear(xhat_p, Wp, bias=bp, out_dtype=F32)
+    _, yf, mean, rstd = K.layernorm_fwd(y1, ln2_w.contiguous(), ln2_b.contiguous(), 1e-5, out_bf16=False,
+                                        out_f32=True)
+    return yf, xhat_p, y1, mean, rstd
+
+
+@_patch_embed_i16.register_fake
+def _(video, ln1_w, ln1_b, w, b, ln2_w, ln2_b, temporal_patch, patch):
+    Bv, C, Fr, H, W = video.shape
+    M = Bv * (Fr // temporal_patch) * (H // patch) * (W // patch)
+    kp = (w.shape[1] + 63) // 64 * 64
+    return (w.new_empty(M, w.shape[0]), w.new_empty(M, kp, dtype=BF16), w.new_empty(M, w.shape[0]),
+            w.new_empty(M), w.new_empty(M))
+
+
+def _pe_setup(ctx, inputs, output):
+    _, ln1_w, ln1_b, w, _, ln2_w, _, _, _ = inputs
+    _, xhat_p, y1, mean, rstd = output
+    ctx.save_for_backward(xhat_p, y1, mean, rstd, ln1_w, ln1_b, w, ln2_w)
+
+
+def _pe_bwd(ctx, dy, *_):
+    xhat_p, y1, mean, rstd, ln1_w, ln1_b, w, ln2_w = ctx.saved_tensors
+    pd = w.shape[1]
+    _, dy1b, dg2, db2 = K.layernorm_bwd(dy.contiguous(), y1, mean, rstd, ln2_w, dx_f32=False)
+    G = K.matmul_tn(dy1b, xhat_p[:, :pd])                   # dy1^T xhat [dim, pd]
+    cs = K.colsum(dy1b)                                      # d bias
+    dw, dg1, db1 = torch.zeros_like(w), torch.zeros_like(ln1_w), torch.zeros_like(ln1_b)
+    K.patch_wgrad(G, cs, w.contiguous(), ln1_w.contiguous(), ln1_b.contiguous(), dw, dg1, db1, accumulate=True)
+    return None, dg1, db1, dw, cs, dg2, db2, None, None
+
+
+_patch_embed_i16.register_autograd(_pe_bwd, setup_context=_pe_setup)
+
+
+def patch_embed_i16(video: Tensor, ln1_w: Tensor, ln1_b: Tensor, w: Tensor, b: Tensor, ln2_w: Tensor,
+                    ln2_b: Tensor, temporal_patch: int = 10, patch: int = 20) -> Tensor:
+    """CTViT.to_patch_emb (ct_clip/ctvit.py:169-174: Rearrange 'b c (t pt) (h p1) (w p2) -> b t h w
+    (c pt p1 p2)', LayerNorm(pd), Linear(pd, dim), LayerNorm(dim)) on the raw int16 HU volume, the
+    input normalisation of ct_clip/data.py:150-152 fused (an f32 volume in [-1, 1] is taken as is).
+    Returns the tokens [B*T*Hg*Wg, dim] f32 in canonical (b, t, h, w) order; differentiable in the
+    weights (the volume is data)."""
+    return _patch_embed_i16(video, ln1_w, ln1_b, w, b, ln2_w, ln2_b, temporal_patch, patch)[0]
+
+
+# ----------------------------------------------------------------------------- bert_layer
+class _NoCtx:
+    """Stand-in autograd context for running a fused Function's forward as a plain op."""
+
+    def save_for_backward(self, *_):
+        pass
+
+    def mark_non_differentiable(self, *_):
+        pass
+
+
+@torch.library.custom_op('ctclip::bert_layer', mutates_args=(), device_types='cuda')
+def bert_layer(x: Tensor, attention_mask: Tensor, heads: int, eps: float, wq: Tensor, bq: Tensor, wk: Tensor,
+               bk: Tensor, wv: Tensor, bv: Tensor, wo: Tensor, bo: Tensor, ln1_w: Tensor, ln1_b: Tensor, wi: Tensor,
+               bi: Tensor, wout: Tensor, bout: Tensor, ln2_w: Tensor, ln2_b: Tensor) -> Tensor:
+    """transformers' BertLayer forward in eval mode (ct_clip/ct_clip.py:685-686 runs BERT-base; no
+    dropout): x [B, L, hidden] f32, attention_mask [B, L] (1 = attend); the fused QKV GEMM (hi / lo
+    split weights), the MFMA attention with the additive key mask, dense + residual + LayerNorm, GELU
+    MLP, dense + residual + LayerNorm -- the kernels of functional.BertLayerFn, whose autograd form
+    the model trains with.  Returns [B, L, hidden] f32."""
+    from . import functional as Fn
+    _need(x.dim() == 3 and x.dtype == F32, 'bert_layer: x [B, L, hidden] f32')
+    B, L, Hd = x.shape
+    _need(attention_mask.shape == (B, L), 'bert_layer: attention_mask [B, L]')
+    _need(Hd % heads == 0 and Hd // heads in (32, 64), 'bert_layer: head dim 32 or 64')
+    xf = x.reshape(B * L, Hd).contiguous()
+    kmask = attention_mask.to(torch.int32).contiguous()
+    ps = [t.detach().contiguous() for t in (wq, bq, wk, bk, wv, bv, wo, bo, ln1_w, ln1_b, wi, bi, wout, bout,
+                                              ln2_w, ln2_b)]
+    x2f, _ = Fn.BertLayerFn.forward(_NoCtx(), xf, K.cast_bf16(xf), kmask, B, L, heads, eps, *ps)
+    return x2f.view(B, L, Hd)
+
+
+@bert_layer.register_fake
+def _(x, attention_mask, heads, eps, *ws):
+    return torch.empty_like(x)

@@ -11,7 +11,8 @@ from torch._subclasses.fake_tensor import FakeTensorMode
 from ctclip_mi355x import ops  # noqa: F401  (registers torch.ops.ctclip)
 
 BF, F32 = torch.bfloat16, torch.float32
-OPS = ('gemm_bf16', 'layernorm', 'cos_attn', 'clip_infonce', 'vq_cos_argmax', 'peg_dwconv3d', 'cpb_mlp')
+OPS = ('gemm_bf16', 'layernorm', 'cos_attn', 'clip_infonce', 'vq_cos_argmax', 'peg_dwconv3d', 'cpb_mlp',
+       'patch_embed_i16', 'bert_layer')
 
 
 def rel(a, b):
@@ -51,6 +52,18 @@ def test_ops_registered_with_fake_shapes():
         u, _, _ = torch.ops.ctclip.cpb_mlp(rel_, torch.empty(512, 2, device='cuda'), g, torch.empty(512, 512, device='cuda'),
                                            g, torch.empty(8, 512, device='cuda'), torch.empty(8, device='cuda'))
         assert u.shape == (8, 2209)
+        vol = torch.empty(2, 1, 20, 80, 80, dtype=torch.int16, device='cuda')
+        pw = torch.empty(512, 4000, device='cuda')
+        p1 = torch.empty(4000, device='cuda')
+        ye = torch.ops.ctclip.patch_embed_i16(vol, p1, p1, pw, g, g, g, 10, 20)
+        assert ye[0].shape == (64, 512) and ye[1].shape == (64, 4032) and ye[1].dtype == BF
+        xb_ = torch.empty(2, 16, 256, device='cuda')
+        wl = [torch.empty(256, 256, device='cuda'), torch.empty(256, device='cuda')]
+        bl = torch.ops.ctclip.bert_layer(xb_, torch.empty(2, 16, dtype=torch.int64, device='cuda'), 4, 1e-12,
+                                         *(wl * 4), wl[1], wl[1], torch.empty(1024, 256, device='cuda'),
+                                         torch.empty(1024, device='cuda'), torch.empty(256, 1024, device='cuda'),
+                                         wl[1], wl[1], wl[1])
+        assert bl.shape == xb_.shape
 
 
 def test_ops_refuse_host_tensors():
@@ -280,3 +293,62 @@ def test_opcheck_registrations():
     t = torch.randn(8, 512, device=dev, generator=g)
     torch.library.opcheck(torch.ops.ctclip.clip_infonce, (t, t.flip(0), torch.ones(1, device=dev)),
                           test_utils=utils)
+
+
+@pytest.mark.gpu
+def test_patch_embed_i16_fwd_bwd():
+    """to_patch_emb on a raw int16 HU volume (ct_clip/data.py:150-152 + ctvit.py:169-174) against the
+    fp32 torch restatement; weight gradients through the op's registered backward."""
+    g = torch.Generator(device=dev).manual_seed(9)
+    B, Fr, S, PT, P, dim = 2, 20, 80, 10, 20, 512
+    pd = PT * P * P
+    hu = torch.randint(-1200, 1200, (B, 1, Fr, S, S), device=dev, dtype=torch.int16, generator=g)
+    ws = [torch.randn(pd, device=dev, generator=g) * 0.1 + 1, torch.randn(pd, device=dev, generator=g) * 0.1,
+          torch.randn(dim, pd, device=dev, generator=g) / pd ** 0.5, torch.randn(dim, device=dev, generator=g) * 0.1,
+          torch.randn(dim, device=dev, generator=g) * 0.1 + 1, torch.randn(dim, device=dev, generator=g) * 0.1]
+    ws = [t.requires_grad_(True) for t in ws]
+    y = ops.patch_embed_i16(hu, *ws, PT, P)
+    wr = [t.detach().clone().requires_grad_(True) for t in ws]
+    v = hu.float().clamp(-1000, 1000) / 1000
+    T, Hg, Wg = Fr // PT, S // P, S // P
+    p = v.reshape(B, 1, T, PT, Hg, P, Wg, P).permute(0, 2, 4, 6, 1, 3, 5, 7).reshape(-1, pd)
+    yr = F.layer_norm(F.linear(F.layer_norm(p, (pd,), wr[0], wr[1], 1e-5), wr[2], wr[3]), (dim,), wr[4], wr[5], 1e-5)
+    assert y.shape == (B * T * Hg * Wg, dim)
+    assert rel(y, yr) < 1e-2, rel(y, yr)
+    dy = torch.randn_like(yr)
+    y.backward(dy)
+    yr.backward(dy)
+    errs = [rel(a.grad, b_.grad) for a, b_ in zip(ws, wr)]
+    assert max(errs) < 3e-2, errs
+
+
+def _bert_layer_ref(x, mask, heads, eps, wq, bq, wk, bk, wv, bv, wo, bo, g1, b1, wi, bi, wout, bout, g2, b2):
+    """HF BertLayer (eval, post-LN, exact GELU) in fp32 torch."""
+    B, L, Hd = x.shape
+    dh = Hd // heads
+    sp = lambda t: t.view(B, L, heads, dh).transpose(1, 2)  # noqa: E731
+    q, k, v = sp(F.linear(x, wq, bq)), sp(F.linear(x, wk, bk)), sp(F.linear(x, wv, bv))
+    s = q @ k.transpose(-1, -2) / math.sqrt(dh) + (1 - mask.float())[:, None, None, :] * -1e30
+    c = (s.softmax(-1) @ v).transpose(1, 2).reshape(B, L, Hd)
+    a = F.layer_norm(F.linear(c, wo, bo) + x, (Hd,), g1, b1, eps)
+    return F.layer_norm(F.linear(F.gelu(F.linear(a, wi, bi)), wout, bout) + a, (Hd,), g2, b2, eps)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('Hd,heads,inter', [(768, 12, 3072), (256, 8, 1024)])
+def test_bert_layer(Hd, heads, inter):
+    """One BertLayer forward (the text tower's unit, ct_clip/ct_clip.py:685-686) with a padded key mask
+    against the fp32 restatement: the hi / lo split-weight GEMMs keep it at the 1e-3 level."""
+    g = torch.Generator(device=dev).manual_seed(10)
+    B, L = 4, 128
+    r = lambda *s, sc=0.02: torch.randn(*s, device=dev, generator=g) * sc  # noqa: E731
+    ws = [r(Hd, Hd), r(Hd), r(Hd, Hd), r(Hd), r(Hd, Hd), r(Hd), r(Hd, Hd), r(Hd), 1 + r(Hd, sc=0.1), r(Hd),
+          r(inter, Hd), r(inter), r(Hd, inter), r(Hd), 1 + r(Hd, sc=0.1), r(Hd)]
+    x = torch.randn(B, L, Hd, device=dev, generator=g)
+    mask = torch.ones(B, L, device=dev, dtype=torch.int64)
+    mask[1, 90:] = 0
+    mask[3, 17:] = 0
+    y = torch.ops.ctclip.bert_layer(x, mask, heads, 1e-12, *ws)
+    yr = _bert_layer_ref(x, mask, heads, 1e-12, *ws)
+    assert y.shape == x.shape
+    assert rel(y, yr) < 3e-3, rel(y, yr)

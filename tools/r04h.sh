@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 t=r04h
-timeout -k 10 300 python -u -m pytest tests/test_gpu_gemm_tiles.py -v --timeout 300 --timeout-method thread \
+timeout -k 10 300 python -u -m pytest tests/test_gpu_gemm_tiles.py tests/test_torch_ops.py -v --timeout 300 --timeout-method thread \
   > gpurun_out/${t}_gemm_tests.log 2>&1 || { rc=$?; echo "gemm tests rc=$rc"; tail -20 gpurun_out/${t}_gemm_tests.log; exit $rc; }
 tail -1 gpurun_out/${t}_gemm_tests.log
 timeout -k 10 400 python -u tools/epi_lds_ab.py > gpurun_out/${t}_epi_lds_ab.log 2>&1 || exit $?
