@@ -158,6 +158,54 @@ __device__ __forceinline__ bf16x8 trfrag(const char* img, int r0, int c0, int la
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// Swizzled 64-B-row images (head dim 32): the 16-B chunk of row r sits at chunk ^ kv_swz(r), which
+// keeps the ds_read_b128 row fragments and the ds_read_b64_tr_b16 transposed ones conflict-free
+// under gfx950's lane groups (searched); the padded 80-B rows above conflict (r02 / r03 PMC:
+// 23-35 % of LDS-active cycles).
+__device__ __forceinline__ int kv_swz(int row) { return (row >> 1) & 3; }
+__device__ __forceinline__ bf16x8 rowfrag_sw(const char* img, int r0, int lane) {
+  const int row = r0 + (lane & 15);
+  return *(const bf16x8*)(img + row * 64 + (((lane >> 4) ^ kv_swz(row)) << 4));
+}
+__device__ __forceinline__ bf16x8 trfrag_sw(const char* img, int r0, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
+  const int row = r0 + 4 * g + q, colb = 2 * c0 + 8 * pp;
+  const char* a1 = img + row * 64 + (((colb >> 4) ^ kv_swz(row)) << 4) + (colb & 15);
+  const char* a2 = a1 + 16 * 64;   // row + 16: same swizzle
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a1));
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a2));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// stage2 into swizzled 64-B-row images (head dim 32)
+template <int U>
+__device__ __forceinline__ void stage2_sw(char* imgA, const u16* a, int64_t lda, char* imgB, const u16* b, int64_t ldb,
+                                          const AP& p, int s, int h, int Lp, int tid, int nth) {
+  constexpr int D = 32, CH = 4;
+  const int n1 = Lp * CH, n = 2 * n1;
+  for (int i0 = tid; i0 < n; i0 += U * nth) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = i0 + u * nth, isb = idx >= n1, id = isb ? idx - n1 : idx;
+      const int r = id / CH, c = id - r * CH;
+      v[u] = make_uint4(0, 0, 0, 0);
+      if (idx < n && r < p.L) {
+        const int64_t row = seq_row(p, s, r);
+        v[u] = isb ? *(const u32x4*)(b + row * ldb + h * D + c * 8) : *(const u32x4*)(a + row * lda + h * D + c * 8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = i0 + u * nth, isb = idx >= n1, id = isb ? idx - n1 : idx;
+      const int r = id / CH, c = id - r * CH;
+      if (idx < n) *(u32x4*)((isb ? imgB : imgA) + r * 64 + ((c ^ kv_swz(r)) << 4)) = v[u];
+    }
+  }
+}
+
 __device__ __forceinline__ bf16x8 pack_perm(const f32x4& a, const f32x4& b) {
   bf16x8 r;
   r[0] = (bf16)a[0]; r[1] = (bf16)a[1]; r[2] = (bf16)a[2]; r[3] = (bf16)a[3];
@@ -218,7 +266,9 @@ __device__ __forceinline__ void load_tables(const AP& p, char* tab, int Lp, int 
 template <int D, bool BIAS, int W = (BIAS ? 12 : NW), bool RUN = false, int QB = 1, bool SMAX = false>
 __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int KK = D / 32, DB = D / 16, RS = Img<D>::RS, NTH = W * 64;
+  // head dim 32: swizzled 64-B-row K / V images (kv_swz); 64: the padded rows
+  constexpr bool SWZ = D == 32;
+  constexpr int KK = D / 32, DB = D / 16, RS = SWZ ? 64 : Img<D>::RS, NTH = W * 64;
   const int L = p.L, Lp = (L + 31) & ~31;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wpp = W / p.pp;                          // waves per pair
@@ -228,9 +278,21 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
     const int pair = blockIdx.x * p.pp + pl;
     if (pair >= p.nseq * p.H) break;
     const int s = pair / p.H, h = pair - s * p.H;
-    stage2<D, SU>(smem + pl * pair_bytes, p.k, p.ldk, smem + pl * pair_bytes + Lp * RS, p.v, p.ldv, p, s, h, Lp,
-                  tid, NTH);
+    if constexpr (SWZ)
+      stage2_sw<SU>(smem + pl * pair_bytes, p.k, p.ldk, smem + pl * pair_bytes + Lp * RS, p.v, p.ldv, p, s, h, Lp,
+                    tid, NTH);
+    else
+      stage2<D, SU>(smem + pl * pair_bytes, p.k, p.ldk, smem + pl * pair_bytes + Lp * RS, p.v, p.ldv, p, s, h, Lp,
+                    tid, NTH);
   }
+  auto kfrag = [&](const char* img, int r0, int kk) {
+    if constexpr (SWZ) return rowfrag_sw(img, r0, lane);
+    else return rowfrag<D>(img, r0, kk, lane);
+  };
+  auto vfrag = [&](const char* img, int r0, int c0) {
+    if constexpr (SWZ) return trfrag_sw(img, r0, c0, lane);
+    else return trfrag<D>(img, r0, c0, lane);
+  };
   float* ub = nullptr;
   int* kb = nullptr;
   float* madd = nullptr;
@@ -320,7 +382,7 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
 #pragma unroll
           for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-            for (int kk = 0; kk < KK; ++kk) kf[bi][kk] = rowfrag<D>(Kimg, kc + 16 * bi, kk, lane);
+            for (int kk = 0; kk < KK; ++kk) kf[bi][kk] = kfrag(Kimg, kc + 16 * bi, kk);
           bf16x8 pb[QB];
 #pragma unroll
           for (int u = 0; u < QB; ++u) {
@@ -346,7 +408,7 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
           }
 #pragma unroll
           for (int d = 0; d < DB; ++d) {
-            const bf16x8 vf = trfrag<D>(Vimg, kc, d * 16, lane);
+            const bf16x8 vf = vfrag(Vimg, kc, d * 16);
 #pragma unroll
             for (int u = 0; u < QB; ++u) o[u][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[u], o[u][d], 0, 0, 0);
           }
@@ -360,7 +422,7 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
 #pragma unroll
       for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-        for (int kk = 0; kk < KK; ++kk) kf[bi][kk] = rowfrag<D>(Kimg, kc + 16 * bi, kk, lane);
+        for (int kk = 0; kk < KK; ++kk) kf[bi][kk] = kfrag(Kimg, kc + 16 * bi, kk);
       f32x4 sa[QB][2];
 #pragma unroll
       for (int u = 0; u < QB; ++u)
@@ -440,7 +502,7 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
       }
 #pragma unroll
       for (int d = 0; d < DB; ++d) {
-        const bf16x8 vf = trfrag<D>(Vimg, kc, d * 16, lane);
+        const bf16x8 vf = vfrag(Vimg, kc, d * 16);
 #pragma unroll
         for (int u = 0; u < QB; ++u) {
           if (rescale[u]) o[u][d] *= alpha[u];
@@ -902,23 +964,6 @@ constexpr int DQD_W = 8, DQD_NT = DQD_W * 64, DQD_KP = 2;
 #ifndef CTCLIP_ATTN_DIAG_BIN
 #define CTCLIP_ATTN_DIAG_BIN 1
 #endif
-__device__ __forceinline__ int kv_swz(int row) { return (row >> 1) & 3; }
-__device__ __forceinline__ bf16x8 rowfrag_sw(const char* img, int r0, int lane) {
-  const int row = r0 + (lane & 15);
-  return *(const bf16x8*)(img + row * 64 + (((lane >> 4) ^ kv_swz(row)) << 4));
-}
-__device__ __forceinline__ bf16x8 trfrag_sw(const char* img, int r0, int c0, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
-  const int row = r0 + 4 * g + q, colb = 2 * c0 + 8 * pp;
-  const char* a1 = img + row * 64 + (((colb >> 4) ^ kv_swz(row)) << 4) + (colb & 15);
-  const char* a2 = a1 + 16 * 64;   // row + 16: same swizzle
-  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a1));
-  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4, a2));
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
-  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
 template <int LF>
 __global__ __launch_bounds__(DQD_NT) void attn_bwd_dq_bias_dma_kernel(AP p, int nfc) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
