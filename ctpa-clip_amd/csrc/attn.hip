@@ -263,11 +263,14 @@ __device__ __forceinline__ void load_tables(const AP& p, char* tab, int Lp, int 
 // span (2 scale ||q|| max||k|| + bias range) stays <= 64, so no probability can underflow more
 // than exp2(-64) below the row's largest; otherwise that group runs the online-max code.  Same
 // softmax in exact arithmetic, f32-level differences in rounding.
+#ifndef CTCLIP_ATTN_FWD_SWZ
+#define CTCLIP_ATTN_FWD_SWZ 1   // A/B build switch (tools/attn_lazy_ab.py): 0 = padded 80-B rows
+#endif
 template <int D, bool BIAS, int W = (BIAS ? 12 : NW), bool RUN = false, int QB = 1, bool SMAX = false>
 __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // head dim 32: swizzled 64-B-row K / V images (kv_swz); 64: the padded rows
-  constexpr bool SWZ = D == 32;
+  constexpr bool SWZ = D == 32 && CTCLIP_ATTN_FWD_SWZ;
   constexpr int KK = D / 32, DB = D / 16, RS = SWZ ? 64 : Img<D>::RS, NTH = W * 64;
   const int L = p.L, Lp = (L + 31) & ~31;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;

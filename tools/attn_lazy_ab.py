@@ -63,13 +63,22 @@ if __name__ == '__main__':
     else:
         import torch
         outs = {}
-        for v in ('0', '8', '0', '8', '4', '16'):
+        # the padded-row (unswizzled) forward as an A/B library, when built:
+        #   make -C ctpa-clip_amd/csrc OUT=../../tools/ab/libctclip_noswz.so OBJDIR=build_noswz EXTRA=-DCTCLIP_ATTN_FWD_SWZ=0
+        noswz = os.path.join(REPO, 'tools', 'ab', 'libctclip_noswz.so')
+        runs = [('0', {}), ('8', {}), ('8-noswz', {'CTCLIP_HIP_LIB': noswz}), ('0', {}), ('8', {}),
+                ('8-noswz', {'CTCLIP_HIP_LIB': noswz}), ('4', {}), ('16', {})]
+        for v, extra in runs:
+            if 'CTCLIP_HIP_LIB' in extra and not os.path.exists(noswz):
+                continue
             path = f'/tmp/attn_lazy_{v}.pt'
-            r = subprocess.run([sys.executable, __file__, 'child', path], env=dict(os.environ, CTCLIP_ATTN_LAZY=v))
+            env = dict(os.environ, CTCLIP_ATTN_LAZY=v.split('-')[0], **extra)
+            print(f'[{v}]', end=' ', flush=True)
+            r = subprocess.run([sys.executable, __file__, 'child', path], env=env)
             if r.returncode != 0:
                 sys.exit(r.returncode)
             outs[v] = torch.load(path, weights_only=True)
-        for v in ('8', '4', '16'):
+        for v in [x for x in ('8', '8-noswz', '4', '16') if x in outs]:
             for k in ('spatial', 'bert'):
                 do = (outs[v][k][1] - outs['0'][k][1]).abs().max().item()
                 dl = (outs[v][k][2] - outs['0'][k][2]).abs().max().item()
