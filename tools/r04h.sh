@@ -16,3 +16,5 @@ timeout -k 10 400 python -u tools/epi_lds_ab.py > gpurun_out/${t}_epi_lds_ab.log
 tail -7 gpurun_out/${t}_epi_lds_ab.log
 CTCLIP_EPI_LDS=2 bash tools/pmc_gemm.sh ff1 ${t}lds2 || exit $?
 python -c "import json; d=json.load(open('gpurun_out/pmc_${t}lds2_ff1.json')); print({k: d[k] for k in ('duration_us_profiled','fetch_bytes_per_launch','write_bytes_per_launch','mfma_busy','l2_hit_rate')})"
+timeout -k 10 300 python -u tools/variant_ab.py > gpurun_out/${t}_variant_ab.log 2>&1 || exit $?
+tail -8 gpurun_out/${t}_variant_ab.log
