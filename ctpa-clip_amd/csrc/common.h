@@ -109,12 +109,19 @@ __device__ __forceinline__ float erf_fast(float x) {
   const float r = fmaf(-y, __expf(-a * a), 1.0f);
   return copysignf(r, x);
 }
+#ifdef CTCLIP_DIAG_CHEAP_GELU
+// diagnostic A/B build only (tools/gelu_cost_ab.py): WRONG activations, to time what the erf costs
+// inside the GEGLU / GELU GEMM epilogues
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x; }
+__device__ __forceinline__ float gelu_erf_grad(float x) { return 0.5f + 0.1f * x; }
+#else
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float gelu_erf_grad(float x) {
   const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752f));
   const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
   return cdf + x * pdf;
 }
+#endif
 
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
