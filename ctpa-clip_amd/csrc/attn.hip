@@ -263,8 +263,11 @@ __device__ __forceinline__ void load_tables(const AP& p, char* tab, int Lp, int 
 // span (2 scale ||q|| max||k|| + bias range) stays <= 64, so no probability can underflow more
 // than exp2(-64) below the row's largest; otherwise that group runs the online-max code.  Same
 // softmax in exact arithmetic, f32-level differences in rounding.
+// A/B build switch (tools/attn_lazy_ab.py): 1 = the swizzled 64-B-row K / V images for head dim 32.
+// Measured 1.2 % SLOWER in this VALU-bound kernel (profiles/r04h_attn_lazy_ab.log: 252.4 vs 249.5 us),
+// so the padded 80-B rows stay the default
 #ifndef CTCLIP_ATTN_FWD_SWZ
-#define CTCLIP_ATTN_FWD_SWZ 1   // A/B build switch (tools/attn_lazy_ab.py): 0 = padded 80-B rows
+#define CTCLIP_ATTN_FWD_SWZ 0
 #endif
 template <int D, bool BIAS, int W = (BIAS ? 12 : NW), bool RUN = false, int QB = 1, bool SMAX = false>
 __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
@@ -468,7 +471,7 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
         }
         cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
         cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
-        // lazy rescale (p.lazy > 0, CTCLIP_ATTN_LAZY, default 8): the running max only moves when
+        // lazy rescale (p.lazy > 0, CTCLIP_ATTN_LAZY, default 16): the running max only moves when
         // some lane's chunk max exceeds it by more than p.lazy (log2 units), so after the first
         // chunks the wave skips the alpha exp2, the lsum and the o rescale; probabilities stay <= 2^p.lazy (f32 sums,
         // bf16 P operands: no range issue), and lse = m + log2(lsum) is exact either way
@@ -1371,7 +1374,7 @@ int fill(AP& p, const ctclip_attn_args* a) {
   p.drop_scale = p.drop_p > 0.f ? 1.f / (1.f - p.drop_p) : 1.f;
   p.thresh = (unsigned)std::min(4294967295.0, (double)p.drop_p * 4294967296.0);
   p.seed = a->dropout_seed;
-  static const float lazy = [] { const char* e = getenv("CTCLIP_ATTN_LAZY"); return e ? (float)atof(e) : 8.f; }();
+  static const float lazy = [] { const char* e = getenv("CTCLIP_ATTN_LAZY"); return e ? (float)atof(e) : 16.f; }();
   p.lazy = lazy;
   p.L = a->L; p.H = a->H; p.nseq = a->nseq; p.M = a->M;
   p.Hg = a->grid_h; p.Wg = a->grid_w;

@@ -639,12 +639,15 @@ __device__ __forceinline__ void st16_sc1(void* p, u32x4 d) {
 
 // store one row's 4 j-blocks x 4 cols as bf16; rowp = row base at the wave's first column c0
 __device__ __forceinline__ void store_row_bf16(u16* rowp, const float (&v)[4][4], int g, bool ok, int64_t c0,
-                                               int64_t N) {
+                                               int64_t N, bool sc1 = false) {
 #pragma unroll
   for (int jp = 0; jp < 2; ++jp) {
     const u32x4 d = pair_swap(v[2 * jp], v[2 * jp + 1]);
     const int coff = 32 * jp + pair_coff(g);
-    if (ok && c0 + coff < N) st16(rowp + coff, d);
+    if (ok && c0 + coff < N) {
+      if (sc1) st16_sc1(rowp + coff, d);
+      else st16(rowp + coff, d);
+    }
   }
 }
 
@@ -819,7 +822,7 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
         }
         continue;
       }
-      store_row_bf16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N);
+      store_row_bf16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N, p.epi_lds == 3);
       float gg[2][4];
 #pragma unroll
       for (int j = 0; j < 2; ++j)
@@ -829,7 +832,10 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
           gg[j][r] = gelu_erf(gb) * xb;
         }
       const u32x4 d = pair_swap(gg[0], gg[1]);
-      if (rok && wcol0 < p.N) st16(p.C2 + bidx * p.sC2 + gm * p.ldc2 + (wcol0 >> 1) + pair_coff(g), d);
+      if (rok && wcol0 < p.N) {
+        if (p.epi_lds == 3) st16_sc1(p.C2 + bidx * p.sC2 + gm * p.ldc2 + (wcol0 >> 1) + pair_coff(g), d);
+        else st16(p.C2 + bidx * p.sC2 + gm * p.ldc2 + (wcol0 >> 1) + pair_coff(g), d);
+      }
       continue;
     }
     if constexpr (MODE != 0) continue;
@@ -895,7 +901,7 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
         store_blk_bf16_lds(scr, (u16*)p.C + bidx * p.sC + gm0 * p.ldc + wcol0, p.ldc, gm0, p.M, wcol0, p.N, v, g, m,
                            lane, p.epi_lds == 2);
       } else {
-        store_row_bf16(Cb, v, g, rok, wcol0, p.N);
+        store_row_bf16(Cb, v, g, rok, wcol0, p.N, p.epi_lds == 3);
       }
     }
     if (p.C2 && p.act == 0) {
@@ -904,7 +910,7 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
         store_blk_bf16_lds(scr, p.C2 + bidx * p.sC2 + gm0 * p.ldc2 + wcol0, p.ldc2, gm0, p.M, wcol0, p.N, v, g, m,
                            lane, p.epi_lds == 2);
       } else {
-        store_row_bf16(p.C2 + bidx * p.sC2 + gm * p.ldc2 + wcol0, v, g, rok, wcol0, p.N);
+        store_row_bf16(p.C2 + bidx * p.sC2 + gm * p.ldc2 + wcol0, v, g, rok, wcol0, p.N, p.epi_lds == 3);
       }
     }
   }
@@ -1613,8 +1619,9 @@ int launch8_ep(const P& p, int batch, hipStream_t st) {
     return launch8<AK, BKC, -1>(p, batch, st);
   }
   // 10 / 12: the same epilogues with lane-contiguous stores through LDS (p.epi_lds)
-  if (p.act == 2) return p.epi_lds ? launch8<AK, BKC, 12>(p, batch, st) : launch8<AK, BKC, 2>(p, batch, st);
-  return p.epi_lds ? launch8<AK, BKC, 10>(p, batch, st) : launch8<AK, BKC, 0>(p, batch, st);
+  const bool relay = p.epi_lds == 1 || p.epi_lds == 2;   // 3: direct stores with sc1 (EP 0 / 2)
+  if (p.act == 2) return relay ? launch8<AK, BKC, 12>(p, batch, st) : launch8<AK, BKC, 2>(p, batch, st);
+  return relay ? launch8<AK, BKC, 10>(p, batch, st) : launch8<AK, BKC, 0>(p, batch, st);
 }
 
 template <bool AK>
@@ -1656,7 +1663,7 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   p.persist = g_persist;
   if (g_epi_lds < 0) {
     const char* e = getenv("CTCLIP_EPI_LDS");
-    g_epi_lds = e ? std::min(2, std::max(0, atoi(e))) : 0;
+    g_epi_lds = e ? std::min(3, std::max(0, atoi(e))) : 0;
   }
   p.epi_lds = g_epi_lds;
   // 8-phase default: stagger only the GEGLU GEMM, whose epilogue (h + g stores + erf) is long
@@ -1740,7 +1747,7 @@ extern "C" int ctclip_gemm_ln(const ctclip_gemm_args* a, const ctclip_ln_epilogu
 // (lane-contiguous 16-B stores); returns the previous value
 extern "C" int ctclip_gemm_set_epi_lds(int v) {
   const int old = g256::g_epi_lds;
-  g256::g_epi_lds = v == 2 ? 2 : (v ? 1 : 0);
+  g256::g_epi_lds = v >= 0 && v <= 3 ? v : 0;
   return old;
 }
 

@@ -77,7 +77,8 @@ int ctclip_gemm_set_stagger(int units);
 /* A/B switch: the 8-phase kernel's transposed bf16 / GEGLU epilogues store through a wave-private
  * LDS scratch so consecutive lanes write consecutive 16 B of a row (1; 2 = the same with sc1
  * stores, which drop their lines from the XCD's L2) or straight from the transposed accumulator
- * layout (0, default); returns the previous setting.  Results are identical. */
+ * layout (0, default; 3 = those direct stores with sc1); returns the previous setting.  Results
+ * are identical. */
 int ctclip_gemm_set_epi_lds(int on);
 /* diagnostic: 8-phase kernel as persistent workgroups walking the tile sequence (1, default) or
  * one workgroup per tile (0); returns the previous setting.  Results are identical. */

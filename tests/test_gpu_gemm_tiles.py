@@ -35,6 +35,9 @@ def _variants(K, fn):
         lib.ctclip_gemm_set_epi_lds(2)      # the same with L2-dropping (sc1) stores
         lds_sc1 = snap(fn())
         torch.cuda.synchronize()
+        lib.ctclip_gemm_set_epi_lds(3)      # direct stores, sc1
+        sc1 = snap(fn())
+        torch.cuda.synchronize()
         lib.ctclip_gemm_set_epi_lds(0)
         for v in (8, 1):
             lib.ctclip_gemm_set_variant(v)
@@ -56,6 +59,7 @@ def _variants(K, fn):
     if torch.is_tensor(single):
         assert torch.equal(lds, outs[8]), 'LDS-relaid epilogue stores differ'
         assert torch.equal(lds_sc1, outs[8]), 'LDS-relaid sc1 epilogue stores differ'
+        assert torch.equal(sc1, outs[8]), 'sc1 epilogue stores differ'
         assert torch.equal(single, outs[8]), 'persistent 8-phase GEMM differs from one workgroup per tile'
         assert torch.equal(capped, outs[8]), 'persistent 8-phase GEMM on a capped grid differs'
     return outs

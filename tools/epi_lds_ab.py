@@ -41,7 +41,7 @@ def main():
         'dX K=2816': lambda: K.matmul_nn(dh, w1),
     }
     L = _lib.lib()
-    confs = [(lds, st) for lds in (0, 1, 2) for st in (0, 8)]
+    confs = [(lds, st) for lds in (0, 3, 2) for st in (0, 8)]
     res_ms = {(c, cf): [] for c in cases for cf in confs}
     for rnd in range(4):
         for cf in confs:
