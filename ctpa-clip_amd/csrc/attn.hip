@@ -469,15 +469,19 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
             cmax = fmaxf(cmax, x);
           }
         }
-        cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
-        cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
         // lazy rescale (p.lazy > 0, CTCLIP_ATTN_LAZY, default 16): the running max only moves when
         // some lane's chunk max exceeds it by more than p.lazy (log2 units), so after the first
         // chunks the wave skips the alpha exp2, the lsum and the o rescale; probabilities stay <= 2^p.lazy (f32 sums,
-        // bf16 P operands: no range issue), and lse = m + log2(lsum) is exact either way
+        // bf16 P operands: no range issue), and lse = m + log2(lsum) is exact either way.
+        // The test needs no cross-lane max: m[u] is equal on the 4 lanes of a query, so some
+        // lane's PARTIAL max exceeds m + lazy iff the query's full chunk max does.  The two
+        // lane ^ 16 / ^ 32 exchanges (LDS permutes on the chunk's critical path) run only on the
+        // chunks that rescale; the rescaled max is the same full max as before (bit-identical).
         rescale[u] = p.lazy <= 0.f || __any(cmax > m[u] + p.lazy);
         float msafe;
         if (rescale[u]) {
+          cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+          cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
           const float mnew = fmaxf(m[u], cmax);
           msafe = mnew == -INFINITY ? 0.f : mnew;
           alpha[u] = fexp2(m[u] - msafe);
