@@ -90,6 +90,20 @@ __device__ __forceinline__ float drop_keep(const AP& p, int s, int h, int q, int
 // bias table constants: bin(q, k) = kb[q] + boff - kb[k]
 __device__ __forceinline__ int kb_of(const AP& p, int i) { return (i / p.Wg) * (2 * p.Wg - 1) + i % p.Wg; }
 __device__ __forceinline__ int boff(const AP& p) { return (p.Hg - 1) * (2 * p.Wg - 1) + p.Wg - 1; }
+// the same position in two VALU ops instead of an LDS table read inside the chunk loops (whose
+// result the bias read's address waits on: a two-deep LDS chain per chunk becomes one):
+// kb(i) = (i / Wg)(2 Wg - 1) + i % Wg = i + (i / Wg)(Wg - 1), with i / Wg = umulhi(i, mg),
+// mg = floor((2^32 - 1) / Wg) + 1 (= ceil(2^32 / Wg), exact division for i < 2^29 / Wg * Wg)
+struct KbFast {
+  unsigned mg;
+  int wg1;
+};
+__device__ __forceinline__ KbFast kb_fast_init(const AP& p) {
+  return p.Wg > 0 ? KbFast{0xFFFFFFFFu / (unsigned)p.Wg + 1u, p.Wg - 1} : KbFast{0u, 0};
+}
+__device__ __forceinline__ int kb_fast(const KbFast& f, int i) {
+  return i + (int)__umulhi((unsigned)i, f.mg) * f.wg1;
+}
 
 template <int D>
 struct Img {
@@ -313,6 +327,8 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
   const int g = lane >> 4, li = lane & 15;
   const int nqb = (L + 15) >> 4;
   const float sc2 = p.scale * LOG2E;
+  const KbFast kbf = kb_fast_init(p);
+  (void)kbf;
   float kmax2 = 0.f, bhi = 0.f, blo = 0.f;
   if constexpr (SMAX) {
     // max_k ||k||^2 of this pair's keys and the bias table's range (log2 units): one block reduction
@@ -449,7 +465,7 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
         for (int bi = 0; bi < 2; ++bi) {
           const int k0 = kc + 16 * bi + 4 * g;
           if constexpr (RUN) {
-            const float* up = ub + (cq[u] - kb[k0] - 3);   // up[3 - r] = ub[bin(q, k0 + r)]
+            const float* up = ub + (cq[u] - kb_fast(kbf, k0) - 3);   // up[3 - r] = ub[bin(q, k0 + r)]
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const float x = sa[u][bi][r] * sc2 + up[3 - r];
@@ -1211,6 +1227,7 @@ __global__ __launch_bounds__(DKP_NT) void attn_bwd_dkv_persist_kernel(AP p) {
   for (int i = tid; i < L; i += NTH) kb[i] = kb_of(p, i);
   const int g = lane >> 4, li = lane & 15;
   const float sc2 = p.scale * LOG2E;
+  const KbFast kbf = kb_fast_init(p);
   // staging map: chunk u of a thread is row R = tid / CH + RPU u of the stacked [Q; dO] image
   // (dO when R >= L: wave-uniform as 64 / CH rows per wave divide L), 16-B column tid % CH
   const int r0 = tid / CH, c0 = tid % CH;
@@ -1280,7 +1297,7 @@ __global__ __launch_bounds__(DKP_NT) void attn_bwd_dkv_persist_kernel(AP p) {
           const int q0 = qc + 16 * bi + 4 * g;
           const f32x4 lv = *(const f32x4*)(ls + q0);
           const f32x4 dlq = *(const f32x4*)(dls + q0);
-          const float* up = ub + (kb[q0] - ck);   // up[r] = ub[bin(q0 + r, key)]
+          const float* up = ub + (kb_fast(kbf, q0) - ck);   // up[r] = ub[bin(q0 + r, key)]
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float x = sa[bi][r] * sc2 + up[r];

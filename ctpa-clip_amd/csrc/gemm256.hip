@@ -60,6 +60,10 @@ struct P {
   unsigned spin_limit;               // polls before giving up on the partner (status = 1)
   int ln_debug;                      // test knob: tile 1 of row block 0 never publishes
   int epi_lds;                       // transposed bf16 / GEGLU epilogues: lane-contiguous stores via LDS
+  // EP 8 (ctclip_gemm_qkv_lnfold): columns < nfold carry the LayerNorm fold
+  //   C = rstd[row] * (acc - mean[row] * fold_cs[col])   (ln_mean / ln_rstd read)
+  const float* fold_cs;
+  int nfold;
 };
 
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
@@ -214,11 +218,13 @@ __device__ __forceinline__ void epilogue(const P& p, f32x4 (&acc)[8][4], char* s
       const int64_t gn = wcol0 + (lane & 7) * 8;
       const int cc = (lane & 7) * 8;
       const bool pre_acc = LM == -1 && !p.R && p.accumulate;
-      if constexpr (LM == -2) {
+      if constexpr (LM == -2 || LM == -8) {
         // residual mode: C (f32) = alpha acc + bias + R (f32), bf16 shadow into C2 when given
         // unconditional loads (rows / columns clamped into the matrix, results of clamped
         // chunks unused): a load under a branch must complete before its phi copy, which put a
         // vmcnt(0) behind every pair
+        // LM -8 (ctclip_gemm_lnfold_bwd): also - c1[row] - beta[row] * X[row][col] (X bf16 in
+        // ln_x, c1 / beta in ln_mean / ln_rstd): the folded LayerNorm backward
         f32x4 ra[4], rb[4];
         const int64_t gnc = min(gn, p.N - 8);
 #pragma unroll
@@ -227,6 +233,20 @@ __device__ __forceinline__ void epilogue(const P& p, f32x4 (&acc)[8][4], char* s
           const float* Rp = (const float*)p.R + bidx * p.sR + gm * p.ldr + gnc;
           ra[it] = *(const f32x4*)Rp;
           rb[it] = *(const f32x4*)(Rp + 4);
+        }
+        if constexpr (LM == -8) {
+#pragma unroll
+          for (int it = 0; it < 4; ++it) {
+            const int64_t gm = min(rbase + ((lane + 64 * it) >> 3), p.M - 1);
+            float xv[8];
+            unpack8(*(const u32x4*)(p.ln_x + gm * p.ln_ldx + gnc), xv);
+            const float c1 = p.ln_mean[gm], be = p.ln_rstd[gm];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              ra[it][j] -= fmaf(be, xv[j], c1);
+              rb[it][j] -= fmaf(be, xv[4 + j], c1);
+            }
+          }
         }
         f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
         if (p.bias) {
@@ -693,10 +713,14 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
   const int64_t wrow0 = m0 + wr * 128, wcol0 = n0 + wc * 64;
   const int64_t cl = wcol0 + 4 * g;          // this lane's column in block j: cl + 16 j
   float bias[4][4];
+  // EP 8: this wave's columns are LayerNorm-folded (wave-uniform); bias[][] then holds fold_cs
+  const bool fold = MODE == 8 && wcol0 < p.nfold;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     f32x4 b = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (p.bias && p.split_k <= 1 && p.act != 3 && p.act != 5 && cl + 16 * j < p.N) b = *(const f32x4*)(p.bias + cl + 16 * j);
+    if (MODE == 8) {
+      if (fold) b = *(const f32x4*)(p.fold_cs + cl + 16 * j);
+    } else if (p.bias && p.split_k <= 1 && p.act != 3 && p.act != 5 && cl + 16 * j < p.N) b = *(const f32x4*)(p.bias + cl + 16 * j);
 #pragma unroll
     for (int r = 0; r < 4; ++r) bias[j][r] = b[r];
   }
@@ -750,9 +774,22 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
       }
       continue;
     }
-    if constexpr (MODE == 6) {
+    if constexpr (MODE == 8) {
+      // LayerNorm folded into the projection (ctclip_gemm_qkv_lnfold): LN(x) W^T =
+      // rstd (x (gamma o W)^T - mean (W gamma)), gamma o W pre-packed, W gamma = fold_cs
+      if (fold) {
+        const int64_t gr = rok ? gm : p.M - 1;
+        const float mu = p.ln_mean[gr], rs = p.ln_rstd[gr];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[j][r] = rs * (v[j][r] - mu * bias[j][r]);
+      }
+    }
+    if constexpr (MODE == 6 || MODE == 8) {
       // C = bf16 result; C2 = its l2norm over each 32-column head (the wave's 64 columns are two
-      // heads) times the head-dim scale p.bias[c % 32], bit-identical to ctclip_l2norm_scale_fwd:
+      // heads) times the head-dim scale p.bias[c % 32], bit-identical to ctclip_l2norm_scale_fwd
+      // (EP 8: p.bias holds two 32-scales, the folded columns' then the rest's):
       // the permlane16 pair swap leaves each lane 8 consecutive columns (a chunk: offset
       // pair_coff(g)), summed in that kernel's order, then combined chunk 0+1, 2+3 (lanes g ^ 2)
       // and the two pairs (g ^ 1), as its xor-1 / xor-2 shuffles over the 4 lanes of a head
@@ -764,7 +801,8 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
       store_row_bf16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N);
       if (wcol0 < p.n2) {
         const int d0 = pair_coff(g);
-        const f32x4 s0v = *(const f32x4*)(p.bias + d0), s1v = *(const f32x4*)(p.bias + d0 + 4);
+        const float* sp = p.bias + d0 + (MODE == 8 && !fold ? 32 : 0);   // EP 8: the second scale set
+        const f32x4 s0v = *(const f32x4*)sp, s1v = *(const f32x4*)(sp + 4);
 #pragma unroll
         for (int jp = 0; jp < 2; ++jp) {
           float c8[8];
@@ -1502,6 +1540,10 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
       epilogue_t<3>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx, scr);
     } else if constexpr (EP == 6) {
       epilogue_t<6>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx, scr);
+    } else if constexpr (EP == 8) {
+      epilogue_t<8>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx, scr);
+    } else if constexpr (EP == -8) {
+      epilogue<-8>(p, acc, smem + TILEB, w, wr, wc, lane, T.m0, T.n0, T.split, T.bidx);
     } else if constexpr (EP == -6 || EP == -7) {
       epilogue_ln<EP == -6 ? 6 : 7>(p, acc, smem, w, wr, wc, lane, T.m0, T.n0);
     } else {
@@ -1645,6 +1687,8 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   p.alpha = a->alpha; p.act = a->act; p.accumulate = a->accumulate; p.split_k = split;
   p.sA = a->sA; p.sB = a->sB; p.sC = a->sC; p.sC2 = a->sC2; p.sR = a->sR;
   p.n2 = a->n2;
+  p.fold_cs = nullptr;
+  p.nfold = 0;
   const int kstep = (variant() == 8 || a->act == 4 || a->act == 5) ? p8::BKK : BK;
   p.kper = (a->K / kstep + split - 1) / split * kstep;
   static int dbg = -1, stag = 0;
@@ -1741,6 +1785,95 @@ extern "C" int ctclip_gemm_ln(const ctclip_gemm_args* a, const ctclip_ln_epilogu
   if (!a->a_kcontig) return CT_EINVAL;
   if (ln->mode == 1) return a->b_kcontig ? launch8<true, true, -6>(p, 1, st) : launch8<true, false, -6>(p, 1, st);
   return a->b_kcontig ? launch8<true, true, -7>(p, 1, st) : launch8<true, false, -7>(p, 1, st);
+}
+
+// Q | K | V projection of one transformer layer as ONE GEMM over the raw residual rows, with the
+// attention's LayerNorm folded into the Q columns (include/ctclip_hip.h).  Q uses LN(x) and K / V
+// use x (ct_clip/attention.py:139-141,152-154), so with B = [gamma o Wq ; Wkv] (bf16, K-contiguous)
+// the Q columns are LN(x) Wq^T = rstd (x (gamma o Wq)^T - mean (Wq gamma)) and the LayerNorm
+// output never exists; both l2norms ride in the epilogue as in act 5.
+extern "C" int ctclip_gemm_qkv_lnfold(const ctclip_gemm_args* a, const float* mean, const float* rstd,
+                                      const float* fold_cs, int32_t nfold, void* stream) {
+  using namespace g256;
+  if (!a || !mean || !rstd || !fold_cs) return CT_EINVAL;
+  if (a->M == 0) return 0;
+  CT_REQUIRE(a->M > 0 && a->N % 256 == 0 && a->K > 0 && a->K % 64 == 0, CT_ESHAPE);
+  CT_REQUIRE(nfold > 0 && nfold % 256 == 0 && nfold < a->N && a->n2 > nfold && a->n2 % 64 == 0 && a->n2 <= a->N,
+             CT_EINVAL);
+  CT_REQUIRE(a->a_kcontig && a->b_kcontig && !a->c_f32 && a->C2 && a->bias && !a->R && !a->B2 && a->act == 5 &&
+                 a->split_k <= 1 && a->batch <= 1 && !a->accumulate,
+             CT_EINVAL);
+  CT_REQUIRE(variant() == 8, CT_EINVAL);
+  CT_REQUIRE(aligned16(a->A) && aligned16(a->B) && aligned16(a->C) && aligned16(a->C2) && aligned16(a->bias) &&
+                 aligned16(fold_cs) && a->lda % 8 == 0 && a->ldb % 8 == 0 && a->ldc % 8 == 0 && a->ldc2 % 8 == 0,
+             CT_EALIGN);
+  P p;
+  memset(&p, 0, sizeof(p));
+  p.M = a->M; p.N = a->N; p.K = a->K;
+  p.A = (const u16*)a->A; p.lda = a->lda;
+  p.B = (const u16*)a->B; p.ldb = a->ldb;
+  p.C = a->C; p.ldc = a->ldc; p.c_f32 = 0;
+  p.C2 = (u16*)a->C2; p.ldc2 = a->ldc2;
+  p.bias = a->bias;
+  p.alpha = a->alpha; p.act = 5; p.split_k = 1;
+  p.n2 = a->n2;
+  p.kper = a->K;
+  p.gz = 1;
+  if (g_persist < 0) {
+    const char* e = getenv("CTCLIP_GEMM_PERSIST");
+    g_persist = e ? (atoi(e) != 0) : 1;
+  }
+  p.persist = g_persist;
+  p.group_gx = 8;
+  p.ln_mean = (float*)mean;
+  p.ln_rstd = (float*)rstd;
+  p.fold_cs = fold_cs;
+  p.nfold = nfold;
+  return launch8<true, true, 8>(p, 1, (hipStream_t)stream);
+}
+
+// Backward of the folded LayerNorm + Q | K | V projections (include/ctclip_hip.h): with A = [dq o rstd |
+// dk | dv] and B = [gamma o Wq ; Wkv] (the forward's packed operand, row-major [K][N]),
+//   C = A B + R - c1[m] - beta[m] X[m][n] = LN'(dq Wq) + dkv Wkv + R
+// (c1, beta from ctclip_l2norm_scale_bwd_fold, X the LayerNorm's bf16 input).  Replaces the dX GEMM
+// of the Q projection, the LayerNorm backward and the K / V dX GEMM with its residual.
+extern "C" int ctclip_gemm_lnfold_bwd(const ctclip_gemm_args* a, const void* X, int64_t ldx, const float* c1,
+                                      const float* beta, void* stream) {
+  using namespace g256;
+  if (!a || !X || !c1 || !beta) return CT_EINVAL;
+  if (a->M == 0) return 0;
+  CT_REQUIRE(a->M > 0 && a->N > 0 && a->N % 8 == 0 && a->K > 0 && a->K % 64 == 0, CT_ESHAPE);
+  CT_REQUIRE(a->a_kcontig && a->c_f32 && a->R && a->r_f32 && !a->bias && !a->B2 && a->act == 0 && a->split_k <= 1 &&
+                 a->batch <= 1 && !a->accumulate,
+             CT_EINVAL);
+  CT_REQUIRE(variant() == 8, CT_EINVAL);
+  CT_REQUIRE(aligned16(a->A) && aligned16(a->B) && aligned16(a->C) && aligned16(a->R) && aligned16(X) &&
+                 a->lda % 8 == 0 && a->ldb % 8 == 0 && a->ldc % 8 == 0 && a->ldr % 8 == 0 && ldx % 8 == 0,
+             CT_EALIGN);
+  if (a->C2) CT_REQUIRE(aligned16(a->C2) && a->ldc2 % 8 == 0, CT_EALIGN);
+  P p;
+  memset(&p, 0, sizeof(p));
+  p.M = a->M; p.N = a->N; p.K = a->K;
+  p.A = (const u16*)a->A; p.lda = a->lda;
+  p.B = (const u16*)a->B; p.ldb = a->ldb;
+  p.C = a->C; p.ldc = a->ldc; p.c_f32 = 1;
+  p.C2 = (u16*)a->C2; p.ldc2 = a->ldc2;
+  p.R = a->R; p.ldr = a->ldr; p.r_f32 = 1;
+  p.alpha = a->alpha; p.split_k = 1;
+  p.kper = a->K;
+  p.gz = 1;
+  if (g_persist < 0) {
+    const char* e = getenv("CTCLIP_GEMM_PERSIST");
+    g_persist = e ? (atoi(e) != 0) : 1;
+  }
+  p.persist = g_persist;
+  p.group_gx = 8;
+  p.ln_x = (const u16*)X;
+  p.ln_ldx = ldx;
+  p.ln_mean = (float*)c1;
+  p.ln_rstd = (float*)beta;
+  hipStream_t st = (hipStream_t)stream;
+  return a->b_kcontig ? launch8<true, true, -8>(p, 1, st) : launch8<true, false, -8>(p, 1, st);
 }
 
 // A/B switch: the transposed bf16 / GEGLU epilogues' stores through the wave's LDS scratch

@@ -255,11 +255,22 @@ __global__ __launch_bounds__(256) void l2n_fwd_kernel(const u16* __restrict__ x,
 }
 
 // backward of the above: dx = (du - u (u.du)) / max(||x||,eps), du = dy*scale; dscale partial[d] += dy * u
+// FOLD (the LayerNorm folded into the Q projection, ctclip_gemm_qkv_lnfold): also dx2 =
+// bf16(dx * rstd[row]) and part_u [nblocks][H * D] = per-block column sums of dx2 * mean[row] --
+// the operands of the Q weight gradient without the LayerNorm output (ctclip_lnfold_wgrad)
+template <bool FOLD>
 __global__ __launch_bounds__(256) void l2n_bwd_kernel(const u16* __restrict__ x, int64_t ldx, const u16* __restrict__ dy,
                                                       int64_t lddy, int64_t rows, int H, int D,
                                                       const float* __restrict__ scale, u16* __restrict__ dx,
-                                                      int64_t lddx, float* __restrict__ part) {
+                                                      int64_t lddx, float* __restrict__ part,
+                                                      const float* __restrict__ row_rstd,
+                                                      const float* __restrict__ row_mean, u16* __restrict__ dx2,
+                                                      int64_t lddx2, float* __restrict__ part_u,
+                                                      const float* __restrict__ fold_cs, float inv_dm,
+                                                      float* __restrict__ c1_out, float* __restrict__ beta_out) {
   __shared__ float red[256][8];
+  __shared__ float redu[FOLD ? 256 : 1][8];
+  float accu[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int lpr = H * D / 8;
   const int64_t nthreads = (int64_t)gridDim.x * 256;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -267,6 +278,12 @@ __global__ __launch_bounds__(256) void l2n_bwd_kernel(const u16* __restrict__ x,
   const int64_t gid0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int c = (int)(gid0 % lpr);
   const int col = c * 8, d0 = col % D;
+  float csv[8];
+  if constexpr (FOLD) {
+    const f32x4 a = *(const f32x4*)(fold_cs + col), b = *(const f32x4*)(fold_cs + col + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { csv[j] = a[j]; csv[4 + j] = b[j]; }
+  }
   float sc[8];
   {
     const f32x4 a = *(const f32x4*)(scale + d0), b = *(const f32x4*)(scale + d0 + 4);
@@ -298,11 +315,56 @@ __global__ __launch_bounds__(256) void l2n_bwd_kernel(const u16* __restrict__ x,
       const float u = v[j] * inv;
       o8[j] = n > 1e-12f ? (du[j] - u * ud) * inv : du[j] * inv;
     }
-    *(u32x4*)(dx + row * lddx + col) = pack8(o8);
+    if (!FOLD || dx) *(u32x4*)(dx + row * lddx + col) = pack8(o8);
+    if constexpr (FOLD) {
+      const float rs = row_rstd[row], mu = row_mean[row];
+      float s8[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s8[j] = o8[j] * rs;
+      const u32x4 pk = pack8(s8);
+      *(u32x4*)(dx2 + row * lddx2 + col) = pk;
+      float r8[8];
+      unpack8(pk, r8);   // the rounded values the GEMMs read
+      float pa = 0.f, pb = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        accu[j] = fmaf(r8[j], mu, accu[j]);
+        pa = fmaf(r8[j], csv[j], pa);
+        pb = fmaf(r8[j], v[j], pb);
+      }
+      if (c1_out) {
+        // the LayerNorm backward's two row means, through the fold (ctclip_gemm_lnfold_bwd):
+        // alpha = mean_k(gamma dy) rstd = (dq2 . cs) / Dm, beta = rstd^2 mean_k(gamma dy xhat) =
+        // rstd (dq2 . q) / Dm (q = xhat (gamma o Wq)^T, the forward's projection); the row's lpr
+        // chunks sit in lpr consecutive lanes
+        for (int o = 1; o < lpr; o <<= 1) {
+          pa += __shfl_xor(pa, o, 64);
+          pb += __shfl_xor(pb, o, 64);
+        }
+        if (c == 0) {
+          const float al = pa * inv_dm, be = rs * pb * inv_dm;
+          c1_out[row] = al - be * mu;
+          beta_out[row] = be;
+        }
+      }
+    }
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = acc[j];
+  if constexpr (FOLD) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) redu[threadIdx.x][j] = accu[j];
+  }
   __syncthreads();
+  if constexpr (FOLD) {
+    // column col of the H * D row: chunk c = col / 8 is held by threads t = c (mod lpr)
+    for (int cc = threadIdx.x; cc < H * D; cc += 256) {
+      const int c = cc >> 3, j = cc & 7;
+      float su = 0.f;
+      for (int t = c; t < 256; t += lpr) su += redu[t][j];
+      part_u[(int64_t)blockIdx.x * H * D + cc] = su;
+    }
+  }
   // fold threads with the same d-chunk: chunk = (gid % lpr) % (D/8) = tid % (D/8), since
   // D/8 divides both lpr and 256 (checked by the launcher)
   if (threadIdx.x < D) {
@@ -463,8 +525,164 @@ extern "C" int ctclip_l2norm_scale_bwd(const void* x, int64_t ldx, const void* d
   CT_REQUIRE((256 % lpr == 0) || (lpr % 256 == 0), CT_ESHAPE);
   CT_REQUIRE(D % 8 == 0 && D <= 512 && 256 % (D / 8) == 0, CT_ESHAPE);
   CT_REQUIRE(((int64_t)nblocks * 256) % lpr == 0, CT_ESHAPE);
-  hipLaunchKernelGGL(l2n_bwd_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, (const u16*)x, ldx,
-                     (const u16*)dy, lddy, rows, H, D, scale, (u16*)dx, lddx, part_scale);
+  hipLaunchKernelGGL(l2n_bwd_kernel<false>, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, (const u16*)x, ldx,
+                     (const u16*)dy, lddy, rows, H, D, scale, (u16*)dx, lddx, part_scale, (const float*)nullptr,
+                     (const float*)nullptr, (u16*)nullptr, (int64_t)0, (float*)nullptr, (const float*)nullptr, 0.f,
+                     (float*)nullptr, (float*)nullptr);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_l2norm_scale_bwd_fold(const void* x, int64_t ldx, const void* dy, int64_t lddy, int64_t rows,
+                                            int32_t H, int32_t D, const float* scale, void* dx, int64_t lddx,
+                                            float* part_scale, int32_t nblocks, const float* row_rstd,
+                                            const float* row_mean, void* dx2, int64_t lddx2, float* part_u,
+                                            const float* fold_cs, int32_t Dm, float* c1_out, float* beta_out,
+                                            void* stream) {
+  if (rows == 0) return 0;
+  const int lpr = H * D / 8;
+  CT_REQUIRE(256 % lpr == 0 && lpr <= 64, CT_ESHAPE);   // part_u fold / row shuffles inside one block / wave
+  CT_REQUIRE(D % 8 == 0 && D <= 512 && 256 % (D / 8) == 0, CT_ESHAPE);
+  CT_REQUIRE(((int64_t)nblocks * 256) % lpr == 0, CT_ESHAPE);
+  CT_REQUIRE(row_rstd && row_mean && dx2 && part_u && lddx2 % 8 == 0, CT_EINVAL);
+  CT_REQUIRE(!c1_out || (beta_out && fold_cs && Dm > 0 && aligned16(fold_cs)), CT_EINVAL);
+  hipLaunchKernelGGL(l2n_bwd_kernel<true>, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, (const u16*)x, ldx,
+                     (const u16*)dy, lddy, rows, H, D, scale, (u16*)dx, lddx, part_scale, row_rstd, row_mean,
+                     (u16*)dx2, lddx2, part_u, fold_cs, Dm > 0 ? 1.f / Dm : 0.f, c1_out, beta_out);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+namespace {
+// LayerNorm statistics of rows whose (mean, M2) arrive as ng partial groups of D / ng columns each
+// (the PEG forward's per-64-channel groups): Chan's pairwise merge, then the biased variance
+// (torch LayerNorm).  part: [ng][rows] float2.
+__global__ __launch_bounds__(256) void ln_stats_merge_kernel(const float2* __restrict__ part, int ng, int64_t rows,
+                                                             int D, float eps, float* __restrict__ mean,
+                                                             float* __restrict__ rstd) {
+  const int64_t row = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (row >= rows) return;
+  float m2 = 0.f, mu = 0.f;
+  for (int gi = 0; gi < ng; ++gi) {
+    const float2 v = part[(int64_t)gi * rows + row];
+    mu += v.x;
+    m2 += v.y;
+  }
+  mu *= 1.f / ng;
+  const float n_g = (float)(D / ng);
+  for (int gi = 0; gi < ng; ++gi) {   // second (cached) pass over the group means
+    const float d = part[(int64_t)gi * rows + row].x - mu;
+    m2 = fmaf(n_g * d, d, m2);
+  }
+  mean[row] = mu;
+  rstd[row] = rsqrtf(m2 * (1.f / D) + eps);
+}
+
+// Weight gradients of the folded LayerNorm + projections, from G = [dq2 | dkv]^T x (one GEMM over
+// the Q | K | V rows) and u = dq2^T mean (ctclip_l2norm_scale_bwd_fold), dq2 = dq o rstd:
+//   rows n < nq:  grad_q[n][k] += gamma[k] (G[n][k] - u[n])        (dWq = dq^T LN(x))
+//   rows n >= nq: grad_rest[n - nq][k] += G[n][k]                   (dWkv = dkv^T x)
+__global__ __launch_bounds__(256) void lnfold_wgrad_kernel(const float* __restrict__ G, int64_t ldg,
+                                                           const float* __restrict__ u, const float* __restrict__ gamma,
+                                                           int64_t nq, int64_t nrest, int64_t K,
+                                                           float* __restrict__ out, int64_t ldo,
+                                                           float* __restrict__ rest, int64_t ldr) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (nq + nrest) * K) return;
+  const int64_t n = i / K, k = i - n * K;
+  if (n < nq) out[n * ldo + k] += gamma[k] * (G[n * ldg + k] - u[n]);
+  else rest[(n - nq) * ldr + k] += G[n * ldg + k];
+}
+
+// the LayerNorm gamma gradient of the fold: dgamma[k] += sum_n Wq[n][k] (G[n][k] - u[n]) (= sum over
+// rows of dy xhat with dy = dq Wq), one thread per column, n in increasing order
+__global__ __launch_bounds__(256) void lnfold_dgamma_kernel(const float* __restrict__ G, int64_t ldg,
+                                                            const float* __restrict__ u, const float* __restrict__ Wq,
+                                                            int64_t ldw, int64_t nq, int64_t K,
+                                                            float* __restrict__ dgamma) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  float s = 0.f;
+  for (int64_t n = 0; n < nq; ++n) s = fmaf(Wq[n * ldw + k], G[n * ldg + k] - u[n], s);
+  dgamma[k] += s;
+}
+
+// B operand of ctclip_gemm_qkv_lnfold: rows [0, nq) = bf16(Wq o gamma) (f32 master Wq [nq][K]),
+// rows [nq, nq + nrest) = the bf16 rows of Wrest; cs[n] = sum_k of the bf16 folded row (f32, the
+// values the GEMM multiplies).  One wave per row, K % 8 == 0, K <= 512 * 8.
+__global__ __launch_bounds__(64) void pack_qkv_fold_kernel(const float* __restrict__ Wq, int64_t ldq,
+                                                           const float* __restrict__ gamma, int64_t K, int64_t nq,
+                                                           const u16* __restrict__ Wr, int64_t ldr,
+                                                           u16* __restrict__ out, int64_t ldo, float* __restrict__ cs,
+                                                           const float* __restrict__ s_fold,
+                                                           const float* __restrict__ s_rest, int ns,
+                                                           float* __restrict__ s_out) {
+  const int64_t n = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (n == 0 && s_out && lane < ns) {   // the epilogue's two l2norm scales, concatenated
+    s_out[lane] = s_fold[lane];
+    s_out[ns + lane] = s_rest[lane];
+  }
+  if (n >= nq) {
+    for (int64_t c = lane * 8; c < K; c += 512) *(u32x4*)(out + n * ldo + c) = *(const u32x4*)(Wr + (n - nq) * ldr + c);
+    return;
+  }
+  float s = 0.f;
+  for (int64_t c = lane * 8; c < K; c += 512) {
+    float w[8];
+    const f32x4 a = *(const f32x4*)(Wq + n * ldq + c), b = *(const f32x4*)(Wq + n * ldq + c + 4);
+    const f32x4 ga = *(const f32x4*)(gamma + c), gb = *(const f32x4*)(gamma + c + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { w[j] = a[j] * ga[j]; w[4 + j] = b[j] * gb[j]; }
+    const u32x4 pk = pack8(w);
+    *(u32x4*)(out + n * ldo + c) = pk;
+    float r[8];
+    unpack8(pk, r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += r[j];
+  }
+  s = warp_sum(s);
+  if (lane == 0) cs[n] = s;
+}
+}  // namespace
+
+extern "C" int ctclip_ln_stats_merge(const float* part, int32_t ngroups, int64_t rows, int32_t D, float eps,
+                                     float* mean, float* rstd, void* stream) {
+  if (rows == 0) return 0;
+  CT_REQUIRE(ngroups >= 1 && ngroups <= 16 && D % ngroups == 0 && part && mean && rstd, CT_EINVAL);
+  hipLaunchKernelGGL(ln_stats_merge_kernel, dim3(cdiv(rows, 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const float2*)part, ngroups, rows, D, eps, mean, rstd);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_lnfold_wgrad(const float* G, int64_t ldg, const float* u, const float* gamma, const float* Wq,
+                                   int64_t ldw, int64_t nq, int64_t nrest, int64_t K, float* grad_q, int64_t ldgq,
+                                   float* grad_gamma, float* grad_rest, int64_t ldgr, void* stream) {
+  if (nq + nrest == 0 || K == 0) return 0;
+  CT_REQUIRE(G && u && gamma && grad_q && (nrest == 0 || grad_rest) && (!grad_gamma || Wq), CT_EINVAL);
+  hipLaunchKernelGGL(lnfold_wgrad_kernel, dim3(cdiv((nq + nrest) * K, 256)), dim3(256), 0, (hipStream_t)stream, G, ldg,
+                     u, gamma, nq, nrest, K, grad_q, ldgq, grad_rest, ldgr);
+  CT_CHECK_LAUNCH();
+  if (grad_gamma) {
+    hipLaunchKernelGGL(lnfold_dgamma_kernel, dim3(cdiv(K, 256)), dim3(256), 0, (hipStream_t)stream, G, ldg, u, Wq,
+                       ldw, nq, K, grad_gamma);
+    CT_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+extern "C" int ctclip_pack_qkv_fold(const float* Wq, int64_t ldq, const float* gamma, int64_t nq, int64_t K,
+                                    const void* Wrest, int64_t ldr, int64_t nrest, void* out, int64_t ldo, float* cs,
+                                    const float* s_fold, const float* s_rest, int32_t ns, float* s_out,
+                                    void* stream) {
+  if (nq + nrest == 0) return 0;
+  CT_REQUIRE(K % 8 == 0 && ldq % 4 == 0 && ldr % 8 == 0 && ldo % 8 == 0 && aligned16(Wq) && aligned16(gamma) &&
+                 aligned16(out) && (nrest == 0 || aligned16(Wrest)),
+             CT_EALIGN);
+  CT_REQUIRE(!s_out || (s_fold && s_rest && ns > 0 && ns <= 64), CT_EINVAL);
+  hipLaunchKernelGGL(pack_qkv_fold_kernel, dim3(nq + nrest), dim3(64), 0, (hipStream_t)stream, Wq, ldq, gamma, K, nq,
+                     (const u16*)Wrest, ldr, (u16*)out, ldo, cs, s_fold, s_rest, ns, s_out);
   CT_CHECK_LAUNCH();
   return 0;
 }

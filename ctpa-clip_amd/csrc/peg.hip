@@ -273,7 +273,8 @@ template <int TR, int GK = 0, int MD = 0>
 __global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ xin, int D,
                                                         const float* __restrict__ w, const float* __restrict__ bias,
                                                         const float* __restrict__ res, Geo g,
-                                                        float* __restrict__ out, u16* __restrict__ outb) {
+                                                        float* __restrict__ out, u16* __restrict__ outb,
+                                                        float* __restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   fix_geo<GK, MD>(g);
   const int nht = (g.H + HT - 1) / HT;
@@ -363,7 +364,8 @@ __global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ 
       for (int j = 0; j < SEG; ++j) {
         const int wq = w0 + j;
         if (wq >= g.W) break;
-        const int64_t co = (int64_t)canon(g, b, (t * g.H + h) * g.W + wq) * D + c0 + ch * 8;
+        const int64_t orow = canon(g, b, (t * g.H + h) * g.W + wq);
+        const int64_t co = orow * D + c0 + ch * 8;
         if (has_res) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) { acc[j][e] += rv[j][0][e]; acc[j][4 + e] += rv[j][1][e]; }
@@ -373,6 +375,31 @@ __global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ 
           *(f32x4*)(out + co + 4) = f32x4{acc[j][4], acc[j][5], acc[j][6], acc[j][7]};
         }
         if (outb) *(u32x4*)(outb + co) = pack8(acc[j]);
+        if (!TR && stats) {
+          // the output row's (mean, M2) over this workgroup's 64 channels (two-pass over the 8 lanes
+          // ch = 0..7 of the token, which sit in 8 consecutive lanes), for the LayerNorm that reads
+          // this output (attention.py:139-141): ctclip_ln_stats_merge combines the D / 64 groups
+          float sm = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sm += acc[j][e];
+          sm += __shfl_xor(sm, 1, 64);
+          sm += __shfl_xor(sm, 2, 64);
+          sm += __shfl_xor(sm, 4, 64);
+          const float mu = sm * (1.f / 64.f);
+          float m2 = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = acc[j][e] - mu;
+            m2 = fmaf(d, d, m2);
+          }
+          m2 += __shfl_xor(m2, 1, 64);
+          m2 += __shfl_xor(m2, 2, 64);
+          m2 += __shfl_xor(m2, 4, 64);
+          if (ch == 0) {
+            const int64_t ntok = (int64_t)(gridDim.x / nht) * g.thw;
+            *(float2*)(stats + ((int64_t)blockIdx.y * ntok + orow) * 2) = make_float2(mu, m2);
+          }
+        }
       }
     }
     // the slot of plane tn held plane tn - 3, read in this step: write it after a barrier
@@ -543,17 +570,20 @@ bool canon1() {
 
 template <int TR>
 void launch_tile(dim3 grid, size_t smem, hipStream_t st, const u16* x, int D, const float* w, const float* bias,
-                 const float* res, const Geo& g, float* out, u16* outb) {
+                 const float* res, const Geo& g, float* out, u16* outb, float* stats = nullptr) {
   if (fixed24(g)) {
     if (g.mode == 0)
-      hipLaunchKernelGGL((peg_tile_kernel<TR, 24, 0>), grid, dim3(TNTH), smem, st, x, D, w, bias, res, g, out, outb);
+      hipLaunchKernelGGL((peg_tile_kernel<TR, 24, 0>), grid, dim3(TNTH), smem, st, x, D, w, bias, res, g, out, outb,
+                         stats);
     else if (canon1())
-      hipLaunchKernelGGL((peg_tile_kernel<TR, 24, 2>), grid, dim3(TNTH), smem, st, x, D, w, bias, res, g, out, outb);
+      hipLaunchKernelGGL((peg_tile_kernel<TR, 24, 2>), grid, dim3(TNTH), smem, st, x, D, w, bias, res, g, out, outb,
+                         stats);
     else
-      hipLaunchKernelGGL((peg_tile_kernel<TR, 24, 1>), grid, dim3(TNTH), smem, st, x, D, w, bias, res, g, out, outb);
+      hipLaunchKernelGGL((peg_tile_kernel<TR, 24, 1>), grid, dim3(TNTH), smem, st, x, D, w, bias, res, g, out, outb,
+                         stats);
     return;
   }
-  hipLaunchKernelGGL((peg_tile_kernel<TR>), grid, dim3(TNTH), smem, st, x, D, w, bias, res, g, out, outb);
+  hipLaunchKernelGGL((peg_tile_kernel<TR>), grid, dim3(TNTH), smem, st, x, D, w, bias, res, g, out, outb, stats);
 }
 
 }  // namespace
@@ -572,15 +602,22 @@ extern "C" int ctclip_peg_wgrad_slabs(int64_t B, int32_t T, int32_t H, int32_t W
 extern "C" int ctclip_peg_fwd(const void* x_bf16, const float* x_f32, int64_t B, int32_t T, int32_t H, int32_t W,
                               int32_t D, const float* weight, const float* bias, int32_t mode, float* out_f32,
                               void* out_bf16, void* stream) {
+  return ctclip_peg_fwd_stats(x_bf16, x_f32, B, T, H, W, D, weight, bias, mode, out_f32, out_bf16, nullptr, stream);
+}
+
+extern "C" int ctclip_peg_fwd_stats(const void* x_bf16, const float* x_f32, int64_t B, int32_t T, int32_t H,
+                                    int32_t W, int32_t D, const float* weight, const float* bias, int32_t mode,
+                                    float* out_f32, void* out_bf16, float* stats, void* stream) {
   CT_REQUIRE(D % 8 == 0, CT_EALIGN);
   Geo g{T, H, W, T * H * W, mode};
   const int64_t ntok = B * g.thw;
   if (ntok == 0) return 0;
+  if (stats) CT_REQUIRE(tiled_ok(W, D) && D % 64 == 0 && (((uintptr_t)stats) & 7) == 0, CT_EINVAL);
   if (tiled_ok(W, D)) {
     tile_attrs();
     dim3 grid(B * ((H + HT - 1) / HT), D / 64);
     launch_tile<0>(grid, tile_smem(W), (hipStream_t)stream, (const u16*)x_bf16, D, weight, bias, x_f32, g, out_f32,
-                   (u16*)out_bf16);
+                   (u16*)out_bf16, stats);
   } else {
     dim3 grid(cdiv(ntok, 32), cdiv(D, 64));
     hipLaunchKernelGGL(peg_kernel<0>, grid, dim3(256), 0, (hipStream_t)stream, (const u16*)x_bf16, ntok, D, weight,

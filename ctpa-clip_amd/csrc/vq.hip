@@ -94,7 +94,9 @@ __global__ __launch_bounds__(256) void vq_select_kernel(const float2* __restrict
       }
     }
   }
-  if (lane == 0) idx_out[row] = bi;
+  // a row without any finite score (NaN / inf tokens) keeps bi = INT_MAX: clamp it into the
+  // codebook so no consumer (pool, gather, EMA statistics) reads outside it
+  if (lane == 0) idx_out[row] = (unsigned)bi < (unsigned)C ? bi : 0;
 }
 
 // pooled[b][hw][d] = (1/T) sum_t cb[idx[b][t*HW + hw]][d]

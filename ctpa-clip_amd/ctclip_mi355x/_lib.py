@@ -122,6 +122,13 @@ _SIGS = {
     'ctclip_device_arch': [ctypes.c_char_p, c_i32],
     'ctclip_gemm': [ctypes.POINTER(GemmArgs), c_vp],
     'ctclip_gemm_ln': [ctypes.POINTER(GemmArgs), ctypes.POINTER(LnEpilogueArgs), c_vp],
+    'ctclip_gemm_qkv_lnfold': [ctypes.POINTER(GemmArgs), c_vp, c_vp, c_vp, c_i32, c_vp],
+    'ctclip_pack_qkv_fold': [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp,
+                             c_i32, c_vp, c_vp],
+    'ctclip_ln_stats_merge': [c_vp, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp],
+    'ctclip_lnfold_wgrad': [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp,
+                            c_i64, c_vp],
+    'ctclip_gemm_lnfold_bwd': [ctypes.POINTER(GemmArgs), c_vp, c_i64, c_vp, c_vp, c_vp],
     'ctclip_quant_mxfp8': [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp],
     'ctclip_gemm_mxfp8': [ctypes.POINTER(MxGemmArgs), c_vp],
     'ctclip_gemm_mxfp8_set_tile': [c_i32],
@@ -144,6 +151,8 @@ _SIGS = {
                              c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp],
     'ctclip_l2norm_scale_fwd': [c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp],
     'ctclip_l2norm_scale_bwd': [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],
+    'ctclip_l2norm_scale_bwd_fold': [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp, c_i32,
+                                     c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp],
     'ctclip_colsum': [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_i32, c_vp],
     'ctclip_geglu_bwd': [c_vp, c_i64, c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
     'ctclip_gelu_bwd': [c_vp, c_vp, c_vp, c_i64, c_vp],
@@ -161,6 +170,8 @@ _SIGS = {
     'ctclip_unpatch_mse': [c_vp, c_i64, c_vp, c_i32, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp,
                            c_vp, c_i64, c_vp, c_vp, c_vp, c_vp],
     'ctclip_peg_fwd': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp],
+    'ctclip_peg_fwd_stats': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp,
+                             c_vp],
     'ctclip_peg_bwd_data': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp],
     'ctclip_peg_bwd_weight': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp],
     'ctclip_peg_wgrad_slabs': [c_i64, c_i32, c_i32, c_i32, c_i32],

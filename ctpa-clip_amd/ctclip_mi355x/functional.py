@@ -207,6 +207,12 @@ def _adjacent(ts, arena_of):
 # activations and weights.  SURVEY 8(c): compared to the build's own bf16 path, tolerance per test.
 _FP8 = {'on': False}
 _L2N_FUSED = os.environ.get('CTCLIP_L2N_FUSED', '1') != '0'   # A/B switch of the act-5 projections
+# The attention's pre-norm LayerNorm folded into ONE Q | K | V projection over the PEG output
+# (gemm256.hip EP 8, ctclip_gemm_qkv_lnfold): PEG leaves the LayerNorm statistics, the Q columns
+# compute LN(x) Wq^T = rstd (x (gamma o Wq)^T - mean Wq gamma), so neither the LayerNorm kernel
+# nor its output exists; the Q weight gradient uses the same fold (ctclip_lnfold_wgrad).
+# CTCLIP_LN1_FOLD=0: the LayerNorm kernel and the two projections (A/B switch).
+_LN1_FOLD = os.environ.get('CTCLIP_LN1_FOLD', '1') != '0'
 _QKV_WGRAD = os.environ.get('CTCLIP_QKV_WGRAD', '1') != '0'   # A/B switch of BERT's merged q/k/v wgrad
 
 
@@ -414,11 +420,23 @@ class ViTLayerFn(torch.autograd.Function):
                                           Wkv, Wo, ff_w, ff_b, W1, W2)
         H, dh = geo.heads, geo.dim_head
         inner = H * dh
-        x1f, x1b = K.peg_fwd(xb, xf, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, peg_b, geo.mode)
-        xn, _, m1, r1 = K.layernorm_fwd(x1f, norm_g, None, 1e-5)
         Wq_b, Wkv_b, Wo_b = bf(Wq), bf(Wkv), bf(Wo)
         fp8 = vit_fp8()
-        if fp8:
+        dim = xb.shape[1]
+        fold = (_LN1_FOLD and not fp8 and _L2N_FUSED and dh == 32 and inner % 256 == 0 and dim % 64 == 0
+                and geo.Wg <= 24 and Wkv.shape[0] == 2 * inner)
+        if fold:
+            x1f, x1b, m1, r1 = K.peg_fwd_stats(xb, xf, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, peg_b, geo.mode)
+            xn = None
+        else:
+            x1f, x1b = K.peg_fwd(xb, xf, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, peg_b, geo.mode)
+            xn, _, m1, r1 = K.layernorm_fwd(x1f, norm_g, None, 1e-5)
+        if fold:
+            Wp, cs, scales = K.pack_qkv_fold(Wq.detach(), norm_g, Wkv_b, q_scale.detach(), k_scale.detach())
+            qkv, qkn = K.linear_qkv_lnfold(x1b, Wp, cs, m1, r1, scales, inner, 2 * inner)
+            q, kv = qkv[:, :inner], qkv[:, inner:]
+            qn, kn = qkn[:, :inner], qkn[:, inner:]
+        elif fp8:
             q = fp8_linear(xn, Wq, 'q', Wq_b)
             kv = fp8_linear(x1b, Wkv, 'kv', Wkv_b)
             qn = K.l2norm_scale_fwd(q, H, dh, q_scale)
@@ -464,6 +482,8 @@ class ViTLayerFn(torch.autograd.Function):
             x3f = K.linear(g, W2p, residual=x2f, out_dtype=F32, out2=x3b)
         ctx.geo = geo
         ctx.use_bias = use_bias
+        ctx.fold = fold
+        ctx.fold_w = (Wp, cs) if fold else None
         ctx.params = (peg_w, peg_b, norm_g, q_scale, k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1, W2)
         ctx.save_for_backward(xb, x1b, m1, r1, xn, q, kv, qn, kn, o, lse, x2b, m2, r2, xn2, h, g,
                               bias_u if use_bias else torch.empty(0), Wq_b, Wkv_b, Wo_b, W1p, W2p)
@@ -508,31 +528,54 @@ class ViTLayerFn(torch.autograd.Function):
         K.matmul_tn(dx2b, o, out=gsink(Wo), accumulate=True, tag='dw')
         dqn = torch.empty_like(qn)
         dkn = torch.empty_like(kn)
-        dkv = torch.empty_like(kv)
         L, nseq, seq = geo.seq()
         du = torch.zeros_like(bias_u) if ctx.use_bias else None
-        K.attn_bwd(qn, kn, kv[:, inner:], o, lse, do, dqn, dkn, dkv[:, inner:], L=L, H=H, D=dh, nseq=nseq,
-                   scale=8.0, seq=seq, bias_u=bias_u if ctx.use_bias else None, dbias_u=du,
-                   grid=(geo.Hg, geo.Wg) if ctx.use_bias else (0, 0))
-        dq = torch.empty_like(q)
-        K.l2norm_scale_bwd(q, dqn, H, dh, q_scale, dq, ds_out=gsink(q_scale))
-        K.l2norm_scale_bwd(kv[:, :inner], dkn, H, dh, k_scale, dkv[:, :inner], ds_out=gsink(k_scale))
-        fusable = K.ln_guarded() and K.ln_fusable(dq.shape[0], Wq_b.shape[1], bwd=True)
-        if not fusable:
-            dxn = K.matmul_nn(dq, Wq_b)
-        K.matmul_tn(dq, xn, out=gsink(Wq), accumulate=True, tag='dw')
-        K.matmul_tn(dkv, x1b, out=gsink(Wkv), accumulate=True, tag='dw')
-        dx1kv = K.matmul_nn(dkv, Wkv_b, residual=dx2f, out_dtype=F32)
-        # dx1 = LN'(dq . Wq) + (dkv . Wkv + dx2) in one launch where the shape allows (EP -7)
-        fused = K.matmul_nn_ln_bwd(dq, Wq_b, x1b, m1, r1, norm_g, dx1kv, dgamma_out=gsink(norm_g)) \
-            if fusable else None
-        if fused is not None:
-            dx1f, dx1b = fused
+        fold = getattr(ctx, 'fold', False)
+        if fold:
+            # the folded LayerNorm (ctx.fold, forward above) backward through the Q | K | V
+            # projections without the LayerNorm output or its backward kernel:
+            #   dqkv = [dq o rstd | dk | dv] (one buffer: the Q | K | V weight gradients are ONE GEMM)
+            #   dWq = gamma o ((dq o rstd)^T x - u), dgamma = sum_n Wq o (...), dWkv = dkv^T x
+            #   dx1 = LN'(dq Wq) + dkv Wkv + dx2 = dqkv [gamma o Wq ; Wkv] + dx2 - c1 - beta o x
+            Wp, cs = ctx.fold_w
+            M_ = qn.shape[0]
+            dqkv = torch.empty(M_, 3 * inner, device=dev, dtype=BF16)
+            K.attn_bwd(qn, kn, kv[:, inner:], o, lse, do, dqn, dkn, dqkv[:, 2 * inner:], L=L, H=H, D=dh,
+                       nseq=nseq, scale=8.0, seq=seq, bias_u=bias_u if ctx.use_bias else None, dbias_u=du,
+                       grid=(geo.Hg, geo.Wg) if ctx.use_bias else (0, 0))
+            _, _, u1, c1, be1 = K.l2norm_scale_bwd_fold(q, dqn, H, dh, q_scale, r1, m1, dx2=dqkv[:, :inner],
+                                                        fold_cs=cs, Dm=x1b.shape[1], ds_out=gsink(q_scale))
+            K.l2norm_scale_bwd(kv[:, :inner], dkn, H, dh, k_scale, dqkv[:, inner:2 * inner], ds_out=gsink(k_scale))
+            Gqkv = K.matmul_tn(dqkv, x1b, tag='dw')
+            gq, gkv = gsink(Wq), gsink(Wkv)      # (frozen projections: scratch sinks)
+            K.lnfold_wgrad(Gqkv, u1, norm_g, gq if gq is not None else torch.empty(Wq.shape, device=dev),
+                           wq=Wq.detach(), grad_gamma=gsink(norm_g),
+                           grad_rest=gkv if gkv is not None else torch.empty(Wkv.shape, device=dev))
+            dx1f, dx1b = K.matmul_lnfold_bwd(dqkv, Wp, dx2f, x1b, c1, be1)
         else:
-            if fusable:
+            dkv = torch.empty_like(kv)
+            K.attn_bwd(qn, kn, kv[:, inner:], o, lse, do, dqn, dkn, dkv[:, inner:], L=L, H=H, D=dh, nseq=nseq,
+                       scale=8.0, seq=seq, bias_u=bias_u if ctx.use_bias else None, dbias_u=du,
+                       grid=(geo.Hg, geo.Wg) if ctx.use_bias else (0, 0))
+            dq = torch.empty(q.shape, device=dev, dtype=q.dtype)
+            K.l2norm_scale_bwd(q, dqn, H, dh, q_scale, dq, ds_out=gsink(q_scale))
+            K.l2norm_scale_bwd(kv[:, :inner], dkn, H, dh, k_scale, dkv[:, :inner], ds_out=gsink(k_scale))
+            fusable = K.ln_guarded() and K.ln_fusable(dq.shape[0], Wq_b.shape[1], bwd=True)
+            if not fusable:
                 dxn = K.matmul_nn(dq, Wq_b)
-            dx1f, dx1b, _, _ = K.layernorm_bwd(dxn, x1b, m1, r1, norm_g, dres=dx1kv, want_beta=False,
-                                               dgamma_out=gsink(norm_g))
+            K.matmul_tn(dq, xn, out=gsink(Wq), accumulate=True, tag='dw')
+            K.matmul_tn(dkv, x1b, out=gsink(Wkv), accumulate=True, tag='dw')
+            dx1kv = K.matmul_nn(dkv, Wkv_b, residual=dx2f, out_dtype=F32)
+            # dx1 = LN'(dq . Wq) + (dkv . Wkv + dx2) in one launch where the shape allows (EP -7)
+            fused = K.matmul_nn_ln_bwd(dq, Wq_b, x1b, m1, r1, norm_g, dx1kv, dgamma_out=gsink(norm_g)) \
+                if fusable else None
+            if fused is not None:
+                dx1f, dx1b = fused
+            else:
+                if fusable:
+                    dxn = K.matmul_nn(dq, Wq_b)
+                dx1f, dx1b, _, _ = K.layernorm_bwd(dxn, x1b, m1, r1, norm_g, dres=dx1kv, want_beta=False,
+                                                   dgamma_out=gsink(norm_g))
         # PEG
         dxf, dxb, dpw, dpb = K.peg_bwd(dx1b, dx1f, xb, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, geo.mode)
         put_shadow(dxf, dxb)

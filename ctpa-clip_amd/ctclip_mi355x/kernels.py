@@ -717,6 +717,132 @@ def peg_fwd(xb, xf, B, T, H, W, weight, bias, mode):
     return outf, outb
 
 
+def peg_fwd_stats(xb, xf, B, T, H, W, weight, bias, mode, eps=1e-5):
+    """peg_fwd plus the LayerNorm statistics of its output rows (the attention's pre-norm,
+    ct_clip/attention.py:139-141): the conv kernel leaves (mean, M2) per 64-channel group and one
+    light pass merges them.  Returns (out_f32, out_bf16, mean [M], rstd [M])."""
+    M, D = xb.shape
+    outf = torch.empty_like(xf)
+    outb = torch.empty_like(xb)
+    part = torch.empty(D // 64, M, 2, device=xb.device, dtype=F32)
+    call('ctclip_peg_fwd_stats', ptr(xb), ptr(xf), B, T, H, W, D, ptr(weight), ptr(bias), mode, ptr(outf),
+         ptr(outb), ptr(part), stream_ptr())
+    mean = torch.empty(M, device=xb.device, dtype=F32)
+    rstd = torch.empty(M, device=xb.device, dtype=F32)
+    call('ctclip_ln_stats_merge', ptr(part), D // 64, M, D, float(eps), ptr(mean), ptr(rstd), stream_ptr())
+    return outf, outb, mean, rstd
+
+
+def pack_qkv_fold(wq, gamma, wkv_b, s_fold, s_rest):
+    """[bf16(Wq o gamma) ; Wkv], the f32 row sums of the folded rows and the concatenated
+    l2norm scales [s_fold ; s_rest] (ctclip_pack_qkv_fold, one launch)."""
+    nq, K = wq.shape
+    nr = wkv_b.shape[0]
+    assert wq.dtype == F32 and wq.stride(1) == 1 and gamma.numel() == K and wkv_b.dtype == BF16
+    assert s_fold.numel() == s_rest.numel() and s_fold.is_contiguous() and s_rest.is_contiguous()
+    out = torch.empty(nq + nr, K, device=wq.device, dtype=BF16)
+    cs = torch.empty(nq, device=wq.device, dtype=F32)
+    ns = s_fold.numel()
+    scales = torch.empty(2 * ns, device=wq.device, dtype=F32)
+    g = gamma.detach().contiguous()
+    call('ctclip_pack_qkv_fold', ptr(wq), wq.stride(0), ptr(g), nq, K, ptr(wkv_b), wkv_b.stride(0), nr, ptr(out),
+         out.stride(0), ptr(cs), ptr(s_fold), ptr(s_rest), ns, ptr(scales), stream_ptr())
+    return out, cs, scales
+
+
+def linear_qkv_lnfold(x, wp, cs, mean, rstd, scales, nfold, n2, out=None, out2=None):
+    """C = x @ wp^T with the LayerNorm folded into columns < nfold and the per-head l2norm * scale
+    of columns < n2 in C2 (ctclip_gemm_qkv_lnfold); scales = [64] f32 (folded columns' 32, then
+    the rest's).  Returns (C [M, N] bf16, C2 [M, n2] bf16)."""
+    M, K = x.shape
+    N = wp.shape[0]
+    assert wp.shape[1] == K and x.stride(1) == 1 and wp.stride(1) == 1 and scales.numel() == 64
+    if out is None:
+        out = torch.empty(M, N, device=x.device, dtype=BF16)
+    if out2 is None:
+        out2 = torch.empty(M, n2, device=x.device, dtype=BF16)
+    a = GemmArgs()
+    a.M, a.N, a.K = M, N, K
+    a.A, a.lda, a.a_kcontig = ptr(x), x.stride(0), 1
+    a.B, a.ldb, a.b_kcontig = ptr(wp), wp.stride(0), 1
+    a.C, a.ldc, a.c_f32 = ptr(out), out.stride(0), 0
+    a.C2, a.ldc2 = ptr(out2), out2.stride(0)
+    a.bias = ptr(scales)
+    a.alpha, a.act, a.split_k, a.batch = 1.0, ACT_L2N, 1, 1
+    a.n2 = n2
+    call('ctclip_gemm_qkv_lnfold', _lib.ctypes.byref(a), ptr(mean), ptr(rstd), ptr(cs), nfold, stream_ptr())
+    return out, out2
+
+
+def l2norm_scale_bwd_fold(x, dy, H, D, scale, row_rstd, row_mean, *, out=None, dx2=None, fold_cs=None, Dm=0,
+                          ds_out=None):
+    """l2norm_scale_bwd for the folded-LayerNorm Q (x = the forward's q): dx into `out` (optional),
+    dx2 = bf16(dx o rstd) (written into `dx2` when given, e.g. a column slice of the [dq2 | dk | dv]
+    buffer), u = dx2^T mean [H D]; with fold_cs / Dm also the LayerNorm backward's row terms (c1,
+    beta) of ctclip_gemm_lnfold_bwd.  Returns (dscale or ds_out, dx2, u, c1, beta)."""
+    rows = x.shape[0]
+    lpr = H * D // 8
+    nb = 2048
+    while (nb * 256) % lpr:
+        nb += 1
+    part = torch.empty(nb, D, device=x.device, dtype=F32)
+    if dx2 is None:
+        dx2 = torch.empty(rows, H * D, device=x.device, dtype=BF16)
+    part_u = torch.empty(nb, H * D, device=x.device, dtype=F32)
+    c1 = beta = None
+    if fold_cs is not None:
+        c1 = torch.empty(rows, device=x.device, dtype=F32)
+        beta = torch.empty(rows, device=x.device, dtype=F32)
+    call('ctclip_l2norm_scale_bwd_fold', ptr(x), x.stride(0), ptr(dy), dy.stride(0), rows, H, D, ptr(scale),
+         ptr(out), out.stride(0) if out is not None else 0, ptr(part), nb, ptr(row_rstd), ptr(row_mean), ptr(dx2),
+         dx2.stride(0), ptr(part_u), ptr(fold_cs), int(Dm), ptr(c1), ptr(beta), stream_ptr())
+    u = torch.empty(H * D, device=x.device, dtype=F32)
+    reduce_slabs(part_u.view(nb, 1, H * D), u.view(1, H * D))
+    if ds_out is not None:
+        ds = reduce_param_partials(part, ds_out, True)
+    else:
+        ds = torch.empty(D, device=x.device, dtype=F32)
+        reduce_slabs(part.view(nb, 1, D), ds.view(1, D))
+    return ds, dx2, u, c1, beta
+
+
+def lnfold_wgrad(G, u, gamma, grad_q, *, wq=None, grad_gamma=None, grad_rest=None):
+    """Weight gradients of the fold from G = [dq o rstd | dkv]^T x ([nq + nrest, K] f32):
+    grad_q += gamma o (G[:nq] - u), grad_gamma += sum_n wq o (G[:nq] - u) (optional),
+    grad_rest += G[nq:] (ctclip_lnfold_wgrad)."""
+    nq = grad_q.shape[0]
+    Kd = G.shape[1]
+    nrest = G.shape[0] - nq
+    assert nrest == 0 or grad_rest is not None
+    g = gamma.detach().contiguous()
+    call('ctclip_lnfold_wgrad', ptr(G), G.stride(0), ptr(u), ptr(g), ptr(wq), wq.stride(0) if wq is not None else 0,
+         nq, nrest, Kd, ptr(grad_q), grad_q.stride(0), ptr(grad_gamma), ptr(grad_rest),
+         grad_rest.stride(0) if grad_rest is not None else 0, stream_ptr())
+    return grad_q
+
+
+def matmul_lnfold_bwd(dqkv, wp, res, x, c1, beta, out=None, out2=None):
+    """dx = [dq o rstd | dk | dv] @ [gamma o Wq ; Wkv] + res - c1 - beta o x (f32) and its bf16 copy:
+    the folded LayerNorm's backward through the Q | K | V projections (ctclip_gemm_lnfold_bwd)."""
+    M, Kq = dqkv.shape
+    N = wp.shape[1]
+    assert wp.shape[0] == Kq and dqkv.stride(1) == 1 and wp.stride(1) == 1
+    if out is None:
+        out = torch.empty(M, N, device=dqkv.device, dtype=F32)
+    if out2 is None:
+        out2 = torch.empty(M, N, device=dqkv.device, dtype=BF16)
+    a = GemmArgs()
+    a.M, a.N, a.K = M, N, Kq
+    a.A, a.lda, a.a_kcontig = ptr(dqkv), dqkv.stride(0), 1
+    a.B, a.ldb, a.b_kcontig = ptr(wp), wp.stride(0), 0
+    a.C, a.ldc, a.c_f32 = ptr(out), out.stride(0), 1
+    a.C2, a.ldc2 = ptr(out2), out2.stride(0)
+    a.R, a.ldr, a.r_f32 = ptr(res), res.stride(0), 1
+    a.alpha, a.act, a.split_k, a.batch = 1.0, ACT_NONE, 1, 1
+    call('ctclip_gemm_lnfold_bwd', _lib.ctypes.byref(a), ptr(x), x.stride(0), ptr(c1), ptr(beta), stream_ptr())
+    return out, out2
+
+
 def peg_bwd(doutb, doutf, xb, B, T, H, W, weight, mode):
     """Returns (dx_f32, dx_bf16, dweight [D,27], dbias [D])."""
     D = xb.shape[1]

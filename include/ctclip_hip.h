@@ -140,6 +140,44 @@ typedef struct {
 } ctclip_ln_epilogue;
 int ctclip_gemm_ln(const ctclip_gemm_args* a, const ctclip_ln_epilogue* ln, void* stream);
 
+/* Q | K | V projections of one transformer layer as ONE GEMM over the raw residual rows x, with
+ * the attention's pre-norm LayerNorm (bias-free, gamma) folded into the Q columns
+ * (ct_clip/attention.py:139-141 norm -> to_q; 119-125 to_q / to_kv; 152-154 l2norm * scale):
+ *   B = [gamma o Wq ; Wkv] bf16 K-contiguous (ctclip_pack_qkv_fold), N % 256 == 0;
+ *   C (bf16 [M][N]) columns < nfold: rstd[m] * (x_m . B_n - mean[m] * fold_cs[n]) = LN(x) Wq^T,
+ *   the rest x . B_n; C2 (bf16 [M][n2]) = per 32-column head l2norm(C) * scale, scale = bias[0:32]
+ *   for columns < nfold (q_scale) and bias[32:64] after them (k_scale); act must be 5, A / B
+ *   K-contiguous, nfold % 256 == 0, nfold < n2 <= N, no R / split-K / batch / accumulate / B2.
+ * mean / rstd: the LayerNorm statistics of x (ctclip_ln_stats_merge).  Replaces ctclip_layernorm_fwd
+ * + two act-5 GEMMs. */
+int ctclip_gemm_qkv_lnfold(const ctclip_gemm_args* a, const float* mean, const float* rstd, const float* fold_cs,
+                           int32_t nfold, void* stream);
+/* B operand of ctclip_gemm_qkv_lnfold: out rows [0, nq) = bf16(Wq o gamma) (Wq f32 [nq][K]), rows
+ * [nq, nq + nrest) = the bf16 rows of Wrest; cs [nq] = row sums of the bf16 folded rows (f32);
+ * s_out (optional) [2 ns] = s_fold ++ s_rest (the epilogue's two l2norm scales). */
+int ctclip_pack_qkv_fold(const float* Wq, int64_t ldq, const float* gamma, int64_t nq, int64_t K,
+                         const void* Wrest, int64_t ldr, int64_t nrest, void* out, int64_t ldo, float* cs,
+                         const float* s_fold, const float* s_rest, int32_t ns, float* s_out, void* stream);
+/* LayerNorm statistics from ngroups partial (mean, M2) groups of D / ngroups columns each
+ * (part [ngroups][rows] float2, e.g. ctclip_peg_fwd_stats): mean, rstd = 1 / sqrt(var + eps). */
+int ctclip_ln_stats_merge(const float* part, int32_t ngroups, int64_t rows, int32_t D, float eps, float* mean,
+                          float* rstd, void* stream);
+/* Backward of ctclip_gemm_qkv_lnfold's layer input: with A = [dq o rstd | dk | dv] (bf16, K-contiguous)
+ * and B = the forward's packed [gamma o Wq ; Wkv] read as [K][N] (b_kcontig = 0),
+ *   C (f32) = A B + R - c1[m] - beta[m] X[m][n]  (= LN'(dq Wq) + dkv Wkv + R),  C2 = bf16(C) if given;
+ * X = the LayerNorm's bf16 input, c1 / beta from ctclip_l2norm_scale_bwd_fold.  act 0, R f32 required,
+ * no bias / split-K / batch / accumulate / B2.  Replaces two dX GEMMs and ctclip_layernorm_bwd. */
+int ctclip_gemm_lnfold_bwd(const ctclip_gemm_args* a, const void* X, int64_t ldx, const float* c1, const float* beta,
+                           void* stream);
+/* Weight gradients of the fold from G = [dq o rstd | dkv]^T X ([nq + nrest][K] f32) and
+ * u = (dq o rstd)^T mean (ctclip_l2norm_scale_bwd_fold):
+ *   grad_q[n][k] += gamma[k] (G[n][k] - u[n])            (n < nq: dWq = dq^T LN(X))
+ *   grad_gamma[k] += sum_n Wq[n][k] (G[n][k] - u[n])    (optional: the LayerNorm gamma gradient)
+ *   grad_rest[n - nq][k] += G[n][k]                     (n >= nq: dWkv = dkv^T X) */
+int ctclip_lnfold_wgrad(const float* G, int64_t ldg, const float* u, const float* gamma, const float* Wq, int64_t ldw,
+                        int64_t nq, int64_t nrest, int64_t K, float* grad_q, int64_t ldgq, float* grad_gamma,
+                        float* grad_rest, int64_t ldgr, void* stream);
+
 /* sum f32 slabs [s][rows][ld] -> out (f32 or bf16), optional accumulate into f32 out */
 int ctclip_reduce_slabs(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,
                         void* out, int64_t ldo, int32_t out_f32, int32_t accumulate, void* stream);
@@ -208,6 +246,16 @@ int ctclip_l2norm_scale_fwd(const void* x, int64_t ldx, int64_t rows, int32_t H,
 int ctclip_l2norm_scale_bwd(const void* x, int64_t ldx, const void* dy, int64_t lddy, int64_t rows,
                             int32_t H, int32_t D, const float* scale, void* dx, int64_t lddx,
                             float* part_scale, int32_t nblocks, void* stream);
+/* the same for the folded-LayerNorm Q (ctclip_gemm_qkv_lnfold; x = the forward's q): dx (optional)
+ * as above, dx2 = bf16(dx * row_rstd[row]), part_u [nblocks][H * D] = per-block column sums of
+ * dx2 * row_mean[row]; with c1_out / beta_out (and fold_cs [H * D], the LayerNorm width Dm) the
+ * LayerNorm backward's row terms for ctclip_gemm_lnfold_bwd: alpha = (dx2 . fold_cs) / Dm,
+ * beta = row_rstd (dx2 . x) / Dm, c1 = alpha - beta * row_mean.  H * D / 8 divides 256, <= 64. */
+int ctclip_l2norm_scale_bwd_fold(const void* x, int64_t ldx, const void* dy, int64_t lddy, int64_t rows,
+                                 int32_t H, int32_t D, const float* scale, void* dx, int64_t lddx,
+                                 float* part_scale, int32_t nblocks, const float* row_rstd, const float* row_mean,
+                                 void* dx2, int64_t lddx2, float* part_u, const float* fold_cs, int32_t Dm,
+                                 float* c1_out, float* beta_out, void* stream);
 /* per-block column-sum partials [nblocks][cols] (bias gradients) */
 int ctclip_colsum(const void* x, int32_t x_f32, int64_t ld, int64_t rows, int32_t cols, float* part,
                   int32_t nblocks, void* stream);
@@ -261,6 +309,11 @@ int ctclip_unpatch_mse(const float* pix, int64_t ldp, const void* video, int32_t
 int ctclip_peg_fwd(const void* x_bf16, const float* x_f32, int64_t B, int32_t T, int32_t H, int32_t W,
                    int32_t D, const float* weight, const float* bias, int32_t mode, float* out_f32,
                    void* out_bf16, void* stream);
+/* the same, plus the LayerNorm statistics of every output row over each 64-channel group:
+ * stats [D / 64][B T H W] float2 (mean, M2) for ctclip_ln_stats_merge (plane-streaming shapes) */
+int ctclip_peg_fwd_stats(const void* x_bf16, const float* x_f32, int64_t B, int32_t T, int32_t H, int32_t W,
+                         int32_t D, const float* weight, const float* bias, int32_t mode, float* out_f32,
+                         void* out_bf16, float* stats, void* stream);
 int ctclip_peg_bwd_data(const void* dout_bf16, const float* dout_f32, int64_t B, int32_t T, int32_t H,
                         int32_t W, int32_t D, const float* weight, int32_t mode, float* dx_f32,
                         void* dx_bf16, void* stream);
