@@ -554,6 +554,104 @@ extern "C" int ctclip_l2norm_scale_bwd_fold(const void* x, int64_t ldx, const vo
 }
 
 namespace {
+// The q AND k l2norm backwards of the folded-LayerNorm layer in one pass (head dim 32, 256 q then
+// 256 k columns: x = the forward's [q | k], dy = [dq_n | dk_n], one wave per row, chunk c = lane):
+// q lanes (c < 32) write dq o rstd and the fold's row / column terms as l2n_bwd_kernel<true>, k lanes
+// write dk; both into the [dq o rstd | dk | dv] buffer (out).  part_s [2][nblocks][32] = the q / k
+// scale-gradient partials; part_u [nblocks][256] as in l2n_bwd_kernel<true>.
+constexpr int QK_D = 32, QK_COLS = 512, QK_LPR = QK_COLS / 8, QK_NQ = 256;
+__global__ __launch_bounds__(256) void l2n_qk_bwd_fold_kernel(
+    const u16* __restrict__ x, int64_t ldx, const u16* __restrict__ dy, int64_t lddy, int64_t rows,
+    const float* __restrict__ scale_q, const float* __restrict__ scale_k, u16* __restrict__ out, int64_t ldo,
+    float* __restrict__ part_s, const float* __restrict__ row_rstd, const float* __restrict__ row_mean,
+    float* __restrict__ part_u, const float* __restrict__ fold_cs, float inv_dm, float* __restrict__ c1_out,
+    float* __restrict__ beta_out) {
+  __shared__ float red[256][8];
+  __shared__ float redu[256][8];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool isq = lane < QK_LPR / 2;
+  const int col = lane * 8, d0 = col % QK_D;
+  float sc[8], csv[8], acc[8], accu[8];
+  {
+    const float* sp = (isq ? scale_q : scale_k) + d0;
+    const f32x4 a = *(const f32x4*)sp, b = *(const f32x4*)(sp + 4);
+    const float* cp = fold_cs + (isq ? col : 0);
+    const f32x4 ca = *(const f32x4*)cp, cb = *(const f32x4*)(cp + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { sc[j] = a[j]; sc[4 + j] = b[j]; csv[j] = ca[j]; csv[4 + j] = cb[j]; }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = accu[j] = 0.f;
+  const int64_t wstride = (int64_t)gridDim.x * 4;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < rows; row += wstride) {
+    float v[8], g[8];
+    unpack8(*(const u32x4*)(x + row * ldx + col), v);
+    unpack8(*(const u32x4*)(dy + row * lddy + col), g);
+    const float rs = row_rstd[row], mu = row_mean[row];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[j] * v[j];
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    const float n = sqrtf(s);
+    const float inv = 1.f / fmaxf(n, 1e-12f);
+    float du[8], ud = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float u = v[j] * inv;
+      acc[j] += g[j] * u;
+      du[j] = g[j] * sc[j];
+      ud += du[j] * u;
+    }
+    ud += __shfl_xor(ud, 1, 64);
+    ud += __shfl_xor(ud, 2, 64);
+    float o8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float u = v[j] * inv;
+      o8[j] = (n > 1e-12f ? (du[j] - u * ud) * inv : du[j] * inv) * (isq ? rs : 1.f);
+    }
+    const u32x4 pk = pack8(o8);
+    *(u32x4*)(out + row * ldo + col) = pk;
+    float r8[8];
+    unpack8(pk, r8);   // the rounded values the GEMMs read
+    float pa = 0.f, pb = 0.f;
+    if (isq) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        accu[j] = fmaf(r8[j], mu, accu[j]);
+        pa = fmaf(r8[j], csv[j], pa);
+        pb = fmaf(r8[j], v[j], pb);
+      }
+    }
+    // the q half's row sums (lanes 0..31; the k half reduces zeros alongside)
+#pragma unroll
+    for (int o = 1; o < QK_LPR / 2; o <<= 1) {
+      pa += __shfl_xor(pa, o, 64);
+      pb += __shfl_xor(pb, o, 64);
+    }
+    if (lane == 0) {
+      const float al = pa * inv_dm, be = rs * pb * inv_dm;
+      c1_out[row] = al - be * mu;
+      beta_out[row] = be;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { red[threadIdx.x][j] = acc[j]; redu[threadIdx.x][j] = accu[j]; }
+  __syncthreads();
+  // scale partials: head dim d of q (k): lanes c < 32 (>= 32) with c % 4 == d / 8, over the 4 waves
+  if (threadIdx.x < 2 * QK_D) {
+    const int half = threadIdx.x / QK_D, d = threadIdx.x % QK_D, j = d & 7;
+    float su = 0.f;
+    for (int wv = 0; wv < 4; ++wv)
+      for (int c = half * 32 + (d >> 3); c < half * 32 + 32; c += 4) su += red[wv * 64 + c][j];
+    part_s[((int64_t)half * gridDim.x + blockIdx.x) * QK_D + d] = su;
+  }
+  for (int cc = threadIdx.x; cc < QK_NQ; cc += 256) {
+    const int c = cc >> 3, j = cc & 7;
+    part_u[(int64_t)blockIdx.x * QK_NQ + cc] = ((redu[c][j] + redu[64 + c][j]) + redu[128 + c][j]) + redu[192 + c][j];
+  }
+}
 // LayerNorm statistics of rows whose (mean, M2) arrive as ng partial groups of D / ng columns each
 // (the PEG forward's per-64-channel groups): Chan's pairwise merge, then the biased variance
 // (torch LayerNorm).  part: [ng][rows] float2.
@@ -595,16 +693,24 @@ __global__ __launch_bounds__(256) void lnfold_wgrad_kernel(const float* __restri
 }
 
 // the LayerNorm gamma gradient of the fold: dgamma[k] += sum_n Wq[n][k] (G[n][k] - u[n]) (= sum over
-// rows of dy xhat with dy = dq Wq), one thread per column, n in increasing order
+// rows of dy xhat with dy = dq Wq).  A workgroup owns 64 columns; its 4 waves sum rows n = w, w + 4,
+// ... (coalesced 256-B row reads), then the 4 partials are added in wave order (deterministic).
+// (One thread per column walking all nq rows was a 100 us dependent-load chain per launch.)
 __global__ __launch_bounds__(256) void lnfold_dgamma_kernel(const float* __restrict__ G, int64_t ldg,
                                                             const float* __restrict__ u, const float* __restrict__ Wq,
                                                             int64_t ldw, int64_t nq, int64_t K,
                                                             float* __restrict__ dgamma) {
-  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (k >= K) return;
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t k = (int64_t)blockIdx.x * 64 + lane;
   float s = 0.f;
-  for (int64_t n = 0; n < nq; ++n) s = fmaf(Wq[n * ldw + k], G[n * ldg + k] - u[n], s);
-  dgamma[k] += s;
+  if (k < K) {
+#pragma unroll 8
+    for (int64_t n = w; n < nq; n += 4) s = fmaf(Wq[n * ldw + k], G[n * ldg + k] - u[n], s);
+  }
+  part[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && k < K) dgamma[k] += ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
 }
 
 // B operand of ctclip_gemm_qkv_lnfold: rows [0, nq) = bf16(Wq o gamma) (f32 master Wq [nq][K]),
@@ -646,6 +752,25 @@ __global__ __launch_bounds__(64) void pack_qkv_fold_kernel(const float* __restri
 }
 }  // namespace
 
+extern "C" int ctclip_l2norm_qk_bwd_fold(const void* x, int64_t ldx, const void* dy, int64_t lddy, int64_t rows,
+                                         const float* scale_q, const float* scale_k, void* out, int64_t ldo,
+                                         float* part_s, int32_t nblocks, const float* row_rstd, const float* row_mean,
+                                         float* part_u, const float* fold_cs, int32_t Dm, float* c1_out,
+                                         float* beta_out, void* stream) {
+  if (rows == 0) return 0;
+  CT_REQUIRE(x && dy && scale_q && scale_k && out && part_s && row_rstd && row_mean && part_u && fold_cs && c1_out &&
+                 beta_out && Dm > 0 && nblocks > 0,
+             CT_EINVAL);
+  CT_REQUIRE(aligned16(x) && aligned16(dy) && aligned16(out) && aligned16(fold_cs) && aligned16(scale_q) &&
+                 aligned16(scale_k) && ldx % 8 == 0 && lddy % 8 == 0 && ldo % 8 == 0,
+             CT_EALIGN);
+  hipLaunchKernelGGL(l2n_qk_bwd_fold_kernel, dim3(nblocks), dim3(256), 0, (hipStream_t)stream, (const u16*)x, ldx,
+                     (const u16*)dy, lddy, rows, scale_q, scale_k, (u16*)out, ldo, part_s, row_rstd, row_mean, part_u,
+                     fold_cs, 1.f / Dm, c1_out, beta_out);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int ctclip_ln_stats_merge(const float* part, int32_t ngroups, int64_t rows, int32_t D, float eps,
                                      float* mean, float* rstd, void* stream) {
   if (rows == 0) return 0;
@@ -665,7 +790,7 @@ extern "C" int ctclip_lnfold_wgrad(const float* G, int64_t ldg, const float* u, 
                      u, gamma, nq, nrest, K, grad_q, ldgq, grad_rest, ldgr);
   CT_CHECK_LAUNCH();
   if (grad_gamma) {
-    hipLaunchKernelGGL(lnfold_dgamma_kernel, dim3(cdiv(K, 256)), dim3(256), 0, (hipStream_t)stream, G, ldg, u, Wq,
+    hipLaunchKernelGGL(lnfold_dgamma_kernel, dim3(cdiv(K, 64)), dim3(256), 0, (hipStream_t)stream, G, ldg, u, Wq,
                        ldw, nq, K, grad_gamma);
     CT_CHECK_LAUNCH();
   }

@@ -129,6 +129,8 @@ _SIGS = {
     'ctclip_lnfold_wgrad': [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp,
                             c_i64, c_vp],
     'ctclip_gemm_lnfold_bwd': [ctypes.POINTER(GemmArgs), c_vp, c_i64, c_vp, c_vp, c_vp],
+    'ctclip_l2norm_qk_bwd_fold': [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp,
+                                  c_vp, c_vp, c_i32, c_vp, c_vp, c_vp],
     'ctclip_quant_mxfp8': [c_vp, c_i32, c_i64, c_i64, c_i64, c_vp, c_i64, c_vp, c_i64, c_vp],
     'ctclip_gemm_mxfp8': [ctypes.POINTER(MxGemmArgs), c_vp],
     'ctclip_gemm_mxfp8_set_tile': [c_i32],

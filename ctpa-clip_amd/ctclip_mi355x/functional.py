@@ -213,6 +213,8 @@ _L2N_FUSED = os.environ.get('CTCLIP_L2N_FUSED', '1') != '0'   # A/B switch of th
 # nor its output exists; the Q weight gradient uses the same fold (ctclip_lnfold_wgrad).
 # CTCLIP_LN1_FOLD=0: the LayerNorm kernel and the two projections (A/B switch).
 _LN1_FOLD = os.environ.get('CTCLIP_LN1_FOLD', '1') != '0'
+# fold backward: the q and k l2norm backwards as one pass (ctclip_l2norm_qk_bwd_fold); 0 = two (A/B)
+_QK_BWD_MERGED = os.environ.get('CTCLIP_QK_BWD_MERGED', '1') != '0'
 _QKV_WGRAD = os.environ.get('CTCLIP_QKV_WGRAD', '1') != '0'   # A/B switch of BERT's merged q/k/v wgrad
 
 
@@ -540,12 +542,22 @@ class ViTLayerFn(torch.autograd.Function):
             Wp, cs = ctx.fold_w
             M_ = qn.shape[0]
             dqkv = torch.empty(M_, 3 * inner, device=dev, dtype=BF16)
-            K.attn_bwd(qn, kn, kv[:, inner:], o, lse, do, dqn, dkn, dqkv[:, 2 * inner:], L=L, H=H, D=dh,
-                       nseq=nseq, scale=8.0, seq=seq, bias_u=bias_u if ctx.use_bias else None, dbias_u=du,
-                       grid=(geo.Hg, geo.Wg) if ctx.use_bias else (0, 0))
-            _, _, u1, c1, be1 = K.l2norm_scale_bwd_fold(q, dqn, H, dh, q_scale, r1, m1, dx2=dqkv[:, :inner],
-                                                        fold_cs=cs, Dm=x1b.shape[1], ds_out=gsink(q_scale))
-            K.l2norm_scale_bwd(kv[:, :inner], dkn, H, dh, k_scale, dqkv[:, inner:2 * inner], ds_out=gsink(k_scale))
+            dqkn = torch.empty(M_, 2 * inner, device=dev, dtype=BF16)       # [dq_n | dk_n]
+            K.attn_bwd(qn, kn, kv[:, inner:], o, lse, do, dqkn[:, :inner], dqkn[:, inner:], dqkv[:, 2 * inner:],
+                       L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq, bias_u=bias_u if ctx.use_bias else None,
+                       dbias_u=du, grid=(geo.Hg, geo.Wg) if ctx.use_bias else (0, 0))
+            if _QK_BWD_MERGED:
+                # both l2norm backwards in one pass over the forward's [q | k] (one wave per row)
+                qk = q.as_strided((M_, 2 * inner), q.stride())
+                _, _, u1, c1, be1 = K.l2norm_qk_bwd_fold(qk, dqkn, q_scale, k_scale, r1, m1, dqkv[:, :2 * inner], cs,
+                                                         x1b.shape[1], ds_q_out=gsink(q_scale),
+                                                         ds_k_out=gsink(k_scale))
+            else:
+                _, _, u1, c1, be1 = K.l2norm_scale_bwd_fold(q, dqkn[:, :inner], H, dh, q_scale, r1, m1,
+                                                            dx2=dqkv[:, :inner], fold_cs=cs, Dm=x1b.shape[1],
+                                                            ds_out=gsink(q_scale))
+                K.l2norm_scale_bwd(kv[:, :inner], dqkn[:, inner:], H, dh, k_scale, dqkv[:, inner:2 * inner],
+                                   ds_out=gsink(k_scale))
             Gqkv = K.matmul_tn(dqkv, x1b, tag='dw')
             gq, gkv = gsink(Wq), gsink(Wkv)      # (frozen projections: scratch sinks)
             K.lnfold_wgrad(Gqkv, u1, norm_g, gq if gq is not None else torch.empty(Wq.shape, device=dev),

@@ -806,6 +806,35 @@ def l2norm_scale_bwd_fold(x, dy, H, D, scale, row_rstd, row_mean, *, out=None, d
     return ds, dx2, u, c1, beta
 
 
+def l2norm_qk_bwd_fold(qk, dqk, q_scale, k_scale, row_rstd, row_mean, out, fold_cs, Dm, ds_q_out=None,
+                       ds_k_out=None):
+    """Both l2norm backwards of the folded layer (ctclip_l2norm_qk_bwd_fold): qk = the forward's
+    [q | k] (256 + 256 columns), dqk = [dq_n | dk_n]; writes [dq o rstd | dk] into `out`.  Returns
+    (ds_q, ds_k, u, c1, beta); ds_* accumulate into the given sinks (deferred in a backward)."""
+    rows = qk.shape[0]
+    assert qk.shape[1] == 512 and dqk.shape[1] == 512 and out.shape[1] == 512
+    nb = 2048
+    dev = qk.device
+    part_s = torch.empty(2, nb, 32, device=dev, dtype=F32)
+    part_u = torch.empty(nb, 256, device=dev, dtype=F32)
+    c1 = torch.empty(rows, device=dev, dtype=F32)
+    beta = torch.empty(rows, device=dev, dtype=F32)
+    call('ctclip_l2norm_qk_bwd_fold', ptr(qk), qk.stride(0), ptr(dqk), dqk.stride(0), rows, ptr(q_scale),
+         ptr(k_scale), ptr(out), out.stride(0), ptr(part_s), nb, ptr(row_rstd), ptr(row_mean), ptr(part_u),
+         ptr(fold_cs), int(Dm), ptr(c1), ptr(beta), stream_ptr())
+    u = torch.empty(256, device=dev, dtype=F32)
+    reduce_slabs(part_u.view(nb, 1, 256), u.view(1, 256))
+    ds = []
+    for i, sink in ((0, ds_q_out), (1, ds_k_out)):
+        if sink is not None:
+            ds.append(reduce_param_partials(part_s[i], sink, True))
+        else:
+            d = torch.empty(32, device=dev, dtype=F32)
+            reduce_slabs(part_s[i].view(nb, 1, 32), d.view(1, 32))
+            ds.append(d)
+    return ds[0], ds[1], u, c1, beta
+
+
 def lnfold_wgrad(G, u, gamma, grad_q, *, wq=None, grad_gamma=None, grad_rest=None):
     """Weight gradients of the fold from G = [dq o rstd | dkv]^T x ([nq + nrest, K] f32):
     grad_q += gamma o (G[:nq] - u), grad_gamma += sum_n wq o (G[:nq] - u) (optional),

@@ -256,6 +256,14 @@ int ctclip_l2norm_scale_bwd_fold(const void* x, int64_t ldx, const void* dy, int
                                  float* part_scale, int32_t nblocks, const float* row_rstd, const float* row_mean,
                                  void* dx2, int64_t lddx2, float* part_u, const float* fold_cs, int32_t Dm,
                                  float* c1_out, float* beta_out, void* stream);
+/* both l2norm backwards of the folded layer in one pass (head dim 32; x = the forward's [q | k],
+ * 256 + 256 columns; dy = [dq_n | dk_n]): out[:, :256] = dq o row_rstd, out[:, 256:] = dk (the
+ * [dq o rstd | dk | dv] buffer), part_s [2][nblocks][32] = q / k scale-gradient partials, part_u /
+ * c1 / beta as ctclip_l2norm_scale_bwd_fold.  Replaces that call + ctclip_l2norm_scale_bwd for k. */
+int ctclip_l2norm_qk_bwd_fold(const void* x, int64_t ldx, const void* dy, int64_t lddy, int64_t rows,
+                              const float* scale_q, const float* scale_k, void* out, int64_t ldo, float* part_s,
+                              int32_t nblocks, const float* row_rstd, const float* row_mean, float* part_u,
+                              const float* fold_cs, int32_t Dm, float* c1_out, float* beta_out, void* stream);
 /* per-block column-sum partials [nblocks][cols] (bias gradients) */
 int ctclip_colsum(const void* x, int32_t x_f32, int64_t ld, int64_t rows, int32_t cols, float* part,
                   int32_t nblocks, void* stream);

@@ -177,3 +177,24 @@ def test_layer_fold_vs_unfolded(K, mode):
     assert [n for n, _ in g0] == [n for n, _ in g1]
     for (n, a), (_, b) in zip(g0, g1):
         assert _rel(b, a) < 3e-2, (n, _rel(b, a))
+
+
+def test_l2norm_qk_bwd_fold_matches_two_passes(K):
+    """The merged q | k l2norm backward (one wave per row) against the q fold pass + the k pass."""
+    M = 8192
+    x1f, x1b, Wq, Wkv, gamma, qs, ks = _fold_case(M, 9)
+    _, _, mean, rstd = K.layernorm_fwd(x1f, gamma, None, 1e-5)
+    _, cs, _ = K.pack_qkv_fold(Wq, gamma, Wkv, qs, ks)
+    g = torch.Generator(device='cuda').manual_seed(10)
+    qkv = (torch.randn(M, 768, device='cuda', generator=g) * 0.5).bfloat16()
+    dqk = (torch.randn(M, 512, device='cuda', generator=g) * 0.1).bfloat16()
+    out1 = torch.zeros(M, 768, device='cuda', dtype=torch.bfloat16)
+    dsq1, dsk1, u1, c11, be1 = K.l2norm_qk_bwd_fold(qkv[:, :512], dqk, qs, ks, rstd, mean, out1[:, :512], cs, 512)
+    out0 = torch.zeros(M, 768, device='cuda', dtype=torch.bfloat16)
+    dsq0, _, u0, c10, be0 = K.l2norm_scale_bwd_fold(qkv[:, :256], dqk[:, :256], 8, 32, qs, rstd, mean,
+                                                    dx2=out0[:, :256], fold_cs=cs, Dm=512)
+    dsk0 = K.l2norm_scale_bwd(qkv[:, 256:512], dqk[:, 256:], 8, 32, ks, out0[:, 256:512])
+    torch.cuda.synchronize()
+    assert torch.equal(out1, out0)
+    assert torch.equal(c11, c10) and torch.equal(be1, be0)
+    assert _rel(u1, u0) < 1e-5 and _rel(dsq1, dsq0) < 1e-5 and _rel(dsk1, dsk0) < 1e-5
