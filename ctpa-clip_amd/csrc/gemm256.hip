@@ -740,18 +740,21 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
       // made this epilogue as long as the tile's whole main loop (r02 stamps: 31.5 k cycles).  A
       // lane scans its columns in increasing order, so the in-lane tie-break (first max) is a
       // strict >; columns past N read as -inf and never win (bi stays 0x7fffffff when all are)
+      // (best, second) as max / med3: second = med3(best, second, x) is the old best when x wins,
+      // x when it lands between, else unchanged -- the select chain's values with 2 VALU instead of
+      // 4; the column guard only on a wave whose 64 columns cross N (wave-uniform)
       float best = -INFINITY, second = -INFINITY;
       int bi = 0x7fffffff;
+      const bool cfull = wcol0 + 64 <= p.N;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = 16 * j + 4 * g + r;
-          const float x = wcol0 + c < p.N ? v[j][r] : -INFINITY;
-          const bool gt = x > best;
-          second = gt ? best : fmaxf(second, x);
-          bi = gt ? c : bi;
-          best = gt ? x : best;
+          const float x = cfull || wcol0 + c < p.N ? v[j][r] : -INFINITY;
+          bi = x > best ? c : bi;
+          second = __builtin_amdgcn_fmed3f(best, second, x);
+          best = fmaxf(best, x);
         }
       auto merge = [&](float ob, float os, int oi) {
         const bool take = ob > best || (ob == best && oi < bi);
