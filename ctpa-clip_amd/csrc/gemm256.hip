@@ -48,6 +48,7 @@ struct P {
   int stagger;   // start delay (s_sleep units of 64 cycles) for the second co-resident workgroup
   int gz;        // batch * split_k (8-phase tile count = ceil(N/256) * ceil(M/256) * gz)
   int persist;   // 8-phase: persistent workgroups (one per CU) walking the tile sequence
+  int pre1;      // 8-phase TR: the next tile's whole K-step 1 staged before the epilogue (CTCLIP_GEMM_PRE1)
   // LayerNorm epilogues (EP -6 forward, -7 backward; ctclip_gemm_ln)
   const float* ln_gamma; const float* ln_beta; float ln_eps;
   u16* ln_y; int64_t ln_ldy;         // -6: LN output (bf16)
@@ -1484,6 +1485,20 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
 
   int tcount = 0;
   (void)tcount;
+  // TR epilogues without the LDS relay (EP 10 / 12 use O's A1 / B1 halves as scratch) leave buffer O
+  // idle, so with p.pre1 the next tile's K-step 1 is staged whole before the epilogue: its A1 / B1
+  // halves get the epilogue's duration to land instead of the three MFMA phases of K-step 0 (the
+  // first two K-steps of a tile ran at ~3x the steady-state time, r02 stamps).  Older loads only
+  // complete earlier, so the vmcnt(4) waits of the loop stay exact.
+  // Enabled for the VQ argmax GEMM (EP 3), the GEGLU backward (EP 4) and the NN dX GEMMs (EP 0 with
+  // an N-contiguous B): 1.098 -> 1.013, 0.446 -> 0.436 and 0.313 -> 0.304 ms against the previous
+  // build (profiles/r04r_gemm_pre1_ab.log).  Most of the VQ gain is the compiled code rather than
+  // the prefetch (spills 18 -> 14; with p.pre1 = 0 the same build runs 1.02 ms, r04s_gemm_pre1_ab.log);
+  // end to end within noise (r04s_pre1_ab_bench.log).  Skipping the re-issue costs the NT plain /
+  // GEGLU / l2norm kernels 4-18 spilled VGPRs (FF1 +3 %, Q / KV +7 %), and re-issuing instead
+  // gains nothing, so those keep the in-loop staging.
+  constexpr bool PRE_OK = TR && (EP == 3 || EP == 4 || (EP == 0 && !BKC));
+  bool pre = false;
   while (true) {
     const int nk = T.nk;
     STAMP(0, __builtin_amdgcn_s_memtime());
@@ -1493,11 +1508,14 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
     for (int i = 0; 2 * i < nk; ++i) {
       if (i == 1) STAMP(2, __builtin_amdgcn_s_memtime());
       const int te = 2 * i, to = 2 * i + 1;
+      // K-step 1's second halves already staged before the epilogue: not re-issued here (step index
+      // nk = no load, the bound check stage_of makes anyway)
+      const int t1 = (PRE_OK && i == 0 && pre) ? nk : to;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         load_frags(0, q);
-        if (q == 0) stage(B1, to);
-        if (q == 1) stage(A1, to);
+        if (q == 0) stage(B1, t1);
+        if (q == 1) stage(A1, t1);
         if (q == 2) stage(A0, te + 2);
         if (q == 3) { stage(B0, te + 2); if (to < nk) wait_ahead(te + 2 < nk); }
         compute_phase();
@@ -1527,7 +1545,11 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
       const Tile nx = tile_at(p, lin, gx, gy, ntiles);
       stage_of(nx, A0, 0); stage_of(nx, A1, 0); stage_of(nx, B0, 0); stage_of(nx, B1, 0);
       if constexpr (TR) { stage_of(nx, A0, 1); stage_of(nx, B0, 1); }
+      if constexpr (PRE_OK) {
+        if (p.pre1) { stage_of(nx, B1, 1); stage_of(nx, A1, 1); }
+      }
     }
+    pre = PRE_OK && more && p.pre1;
     if (p.debug & 1) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -1589,10 +1611,14 @@ int launch8(const P& p, int batch, hipStream_t st) {
     if (e && g_grid_cap == 0) g_grid_cap = atoi(e);
     cap_env = true;
   }
+  static int pre1 = -1;   // CTCLIP_GEMM_PRE1=0: K-step 1's A1 / B1 halves staged inside the loop (A/B)
+  if (pre1 < 0) { const char* e = getenv("CTCLIP_GEMM_PRE1"); pre1 = e ? atoi(e) != 0 : 1; }
   if (p.persist) {
     const int64_t cap = g_grid_cap > 0 && g_grid_cap < 256 ? g_grid_cap : 256;
     dim3 grid((unsigned)(ntiles < cap ? ntiles : cap));
-    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP>), grid, dim3(p8::NTH), smem, st, p);
+    P q = p;
+    q.pre1 = pre1;
+    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP>), grid, dim3(p8::NTH), smem, st, q);
   } else {
     dim3 grid(cdiv(p.N, p8::BNN), cdiv(p.M, p8::BM), batch * p.split_k);
     hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP>), grid, dim3(p8::NTH), smem, st, p);
