@@ -583,11 +583,25 @@ __global__ __launch_bounds__(256) void l2n_qk_bwd_fold_kernel(
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = accu[j] = 0.f;
   const int64_t wstride = (int64_t)gridDim.x * 4;
-  for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < rows; row += wstride) {
+  // the next row's operands are loaded while this row computes (unconditionally: past the end the
+  // last row is re-read and dropped -- a conditional load would be merged right after it with a
+  // vmcnt(0) wait); one wave per row is otherwise a dependent load -> shuffle chain per row
+  int64_t row = (int64_t)blockIdx.x * 4 + w;
+  u32x4 xn_ = {0u, 0u, 0u, 0u}, gn_ = {0u, 0u, 0u, 0u};
+  float rsn = 0.f, mun = 0.f;
+  auto load_row = [&](int64_t r) {
+    xn_ = *(const u32x4*)(x + r * ldx + col);
+    gn_ = *(const u32x4*)(dy + r * lddy + col);
+    rsn = row_rstd[r];
+    mun = row_mean[r];
+  };
+  if (row < rows) load_row(row);
+  for (; row < rows; row += wstride) {
     float v[8], g[8];
-    unpack8(*(const u32x4*)(x + row * ldx + col), v);
-    unpack8(*(const u32x4*)(dy + row * lddy + col), g);
-    const float rs = row_rstd[row], mu = row_mean[row];
+    unpack8(xn_, v);
+    unpack8(gn_, g);
+    const float rs = rsn, mu = mun;
+    load_row(min(row + wstride, rows - 1));
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) s += v[j] * v[j];

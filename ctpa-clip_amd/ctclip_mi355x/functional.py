@@ -297,10 +297,13 @@ class PatchEmbedFn(torch.autograd.Function):
         ctx.save_for_backward(xhat, y1, mean, rstd, ln1_w, ln1_b, W, ln2_w)
         ctx.b, ctx.ln2_w, ctx.ln2_b = b, ln2_w, ln2_b
         ctx.mark_non_differentiable(yb)
+        ctx.set_materialize_grads(False)   # no zero-filled grad for the bf16 companion
         return yf, yb
 
     @staticmethod
     def backward(ctx, dyf, _dyb):
+        if dyf is None:   # the f32 output fed nothing that needs a gradient
+            return (None,) * 11
         xhat, y1, mean, rstd, ln1_w, ln1_b, W, ln2_w = ctx.saved_tensors
         take_shadow(dyf)
         _, dy1b, dg2, db2 = K.layernorm_bwd(dyf.contiguous(), y1, mean, rstd, ln2_w, dx_f32=False)
@@ -490,10 +493,13 @@ class ViTLayerFn(torch.autograd.Function):
         ctx.save_for_backward(xb, x1b, m1, r1, xn, q, kv, qn, kn, o, lse, x2b, m2, r2, xn2, h, g,
                               bias_u if use_bias else torch.empty(0), Wq_b, Wkv_b, Wo_b, W1p, W2p)
         ctx.mark_non_differentiable(x3b)
+        ctx.set_materialize_grads(False)   # no zero-filled grad for the bf16 companion
         return x3f, x3b
 
     @staticmethod
     def backward(ctx, dx3f, _dx3b):
+        if dx3f is None:   # the f32 output fed nothing that needs a gradient
+            return (None,) * 16
         (xb, x1b, m1, r1, xn, q, kv, qn, kn, o, lse, x2b, m2, r2, xn2, h, g, bias_u, Wq_b, Wkv_b, Wo_b, W1p,
          W2p) = ctx.saved_tensors
         peg_w, peg_b, norm_g, q_scale, k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1, W2 = ctx.params
@@ -643,6 +649,7 @@ def _vit_layer_forward_f32(ctx, xf, xb, bias_u, geo, peg_w, peg_b, norm_g, q_sca
     ctx.save_for_backward(xb, x1b, m1, r1, xn, q, kv, qn, kn, o, lse, x2b, m2, r2, xn2, h, g,
                           bias_u if use_bias else torch.empty(0), bf(Wq), bf(Wkv), bf(Wo), pack_ff1(W1), pack_ff2(W2))
     ctx.mark_non_differentiable(x3b)
+    ctx.set_materialize_grads(False)   # no zero-filled grad for the bf16 companion
     return x3f, x3b
 
 
@@ -655,10 +662,13 @@ class NormFn(torch.autograd.Function):
         ctx.save_for_backward(xb, mean, rstd, gamma)
         ctx.gamma = gamma
         ctx.mark_non_differentiable(yb)
+        ctx.set_materialize_grads(False)   # no zero-filled grad for the bf16 companion
         return yf, yb
 
     @staticmethod
     def backward(ctx, dyf, _):
+        if dyf is None:   # the f32 output fed nothing that needs a gradient
+            return None, None, None
         xb, mean, rstd, gamma = ctx.saved_tensors
         take_shadow(dyf)
         dxf, dxb, _, _ = K.layernorm_bwd(dyf.contiguous(), xb, mean, rstd, gamma, want_beta=False,
@@ -861,10 +871,13 @@ class BertEmbedFn(torch.autograd.Function):
         ctx.save_for_backward(ids, x, mean, rstd, ln_w)
         ctx.params = (word, pos, typ, ln_w, ln_b)
         ctx.mark_non_differentiable(yb)
+        ctx.set_materialize_grads(False)   # no zero-filled grad for the bf16 companion
         return yf, yb
 
     @staticmethod
     def backward(ctx, dyf, _):
+        if dyf is None:   # the f32 output fed nothing that needs a gradient
+            return (None,) * 9
         ids, x, mean, rstd, ln_w = ctx.saved_tensors
         word, pos, typ, _, ln_b = ctx.params
         dyf = dyf.contiguous()
@@ -922,10 +935,13 @@ class BertLayerFn(torch.autograd.Function):
         ctx.dims = (B, L, heads, dh)
         ctx.drop = drop
         ctx.mark_non_differentiable(x2b)
+        ctx.set_materialize_grads(False)   # no zero-filled grad for the bf16 companion
         return x2f, x2b
 
     @staticmethod
     def backward(ctx, dx2f, _):
+        if dx2f is None:   # the f32 output fed nothing that needs a gradient
+            return (None,) * 25
         (xb, kmask, qkv, ctxv, lse, a, m1, r1, x1b, hpre, hact, b2, m2, r2, Wqkv, Wo_b, Wi_b, Wout_b, ln1_w,
          ln2_w) = ctx.saved_tensors
         Wq, bq, Wk, bk, Wv, bv, Wo, bo, _, ln1_b, Wi, bi, Wout, bout, _, ln2_b = ctx.params
