@@ -5,6 +5,8 @@ Parameter / buffer layout matches the reference's ``CTViT.state_dict()`` (built 
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
@@ -14,6 +16,8 @@ from . import functional as Fn
 from . import kernels as K
 from .attention import ContinuousPositionBias, Transformer
 from .layers import patch_offsets
+
+_CPB_AUX = os.environ.get('CTCLIP_CPB_AUX', '1') != '0'
 
 
 def pair(v):
@@ -116,6 +120,22 @@ class CTViT(nn.Module):
         if not is_hu and video.dtype != torch.float32:
             video = video.float()
         video = video.contiguous()
+        hg, wg = self.patch_height_width
+        # the CPB MLP (ctvit.py:317; ~0.14 ms of latency-bound f32 GEMMs forward, ~0.28 ms backward)
+        # runs on the auxiliary stream beside the HBM-bound patch embedding; autograd runs its
+        # backward there too (the stream of its forward), beside the patch-embed backward.  Its
+        # parameter gradients are joined before the optimizer (trainer.optimizer_step: join_aux) and
+        # before the image tower's bucket all-reduce (dist_sync).  CTCLIP_CPB_AUX=0: inline.
+        dev = video.device
+        aux = streams.aux_stream(dev) if _CPB_AUX else None
+        cpb_ev = None
+        if aux is not None:
+            main = torch.cuda.current_stream(dev)
+            aux.wait_stream(main)            # the previous optimizer step's update of the MLP
+            with torch.cuda.stream(aux):
+                bias_u = self.spatial_rel_pos_bias(hg, wg)
+                cpb_ev = aux.record_event()
+            bias_u.record_stream(main)
         pe = self.to_patch_emb
         xf, xb = Fn.PatchEmbedFn.apply(video, pe[1].weight, pe[1].bias, pe[2].weight, pe[2].bias, pe[3].weight,
                                        pe[3].bias, self.temporal_patch_size, self.patch_size[0], is_hu,
@@ -124,11 +144,13 @@ class CTViT(nn.Module):
         streams.mark_image_head(video.device)   # deferred text-stream work may start (streams.py)
         if trace is not None:
             trace['patch_emb'] = xf
-        hg, wg = self.patch_height_width
         T = F // self.temporal_patch_size
         g_sp = Fn.Geo(B, T, hg, wg, self.heads, self.dim_head, 0)
         g_tm = Fn.Geo(B, T, hg, wg, self.heads, self.dim_head, 1)
-        bias_u = self.spatial_rel_pos_bias(hg, wg)                       # ctvit.py:317
+        if cpb_ev is not None:
+            torch.cuda.current_stream(dev).wait_event(cpb_ev)
+        else:
+            bias_u = self.spatial_rel_pos_bias(hg, wg)                   # ctvit.py:317
         dist_sync.mark_ready(bias_u, 'vit_rest')
         xf, xb = self.enc_spatial_transformer.run(xf, xb, g_sp, bias_u)   # ctvit.py:319
         zf, zb = self.enc_temporal_transformer.run(xf, xb, g_tm)         # ctvit.py:327

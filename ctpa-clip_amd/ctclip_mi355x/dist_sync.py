@@ -24,6 +24,7 @@ import torch
 import torch.distributed as dist
 
 from . import kernels as K
+from . import streams
 
 
 def world_rank():
@@ -151,6 +152,7 @@ class BucketedGradSync:
         self.launched = []
         self.works = []
         self.log = []
+        self.stream = None
 
     def _launch(self, tag):
         if tag in self.launched:
@@ -167,6 +169,14 @@ class BucketedGradSync:
                 for st in K.flush_reductions(lo, lo + 4 * n):
                     if st != cur:
                         cur.wait_stream(st)
+            if self.grad.is_cuda and not t.startswith('text'):
+                # an image-tower bucket may be launched from a hook on the auxiliary stream (the CPB
+                # MLP's backward, ctvit.encode_tokens) or hold gradients written there: order it after
+                # both the stream the step runs on and the auxiliary stream
+                cur = torch.cuda.current_stream()
+                if self.stream is not None and cur != self.stream:
+                    cur.wait_stream(self.stream)
+                streams.join_aux(self.grad.device)
             if self.before_launch is not None:
                 self.before_launch(t)
             self.launched.append(t)
@@ -180,6 +190,7 @@ class BucketedGradSync:
     def arm(self):
         world, _ = world_rank()
         self.launched, self.works, self.log = [], [], []
+        self.stream = torch.cuda.current_stream(self.grad.device) if self.grad.is_cuda else None
         if world > 1 or self.force:
             for t, _, _ in self.buckets:
                 _READY[t] = self._launch

@@ -353,10 +353,12 @@ def test_train_step_bit_reproducible():
     Adam moments, VQ codebook and cluster sizes, BERT dropout on, ragged reports (pad ids): no
     float atomics on the step's path (CPB bias gradient through the per-workgroup workspace,
     embedding and patch-LN gradients in fixed order, VQ statistics in fixed point).  A third run
-    with the text Adam deferred (trainer.defer_text_adam) is bit-identical too.  The spatial
-    stage runs the base shape (24 x 24 grid, L = 576: the LDS-DMA dQ kernel); smaller grids take
-    the frame-inner kernel, checked by test_deferred_text_adam_matches."""
+    with the text Adam deferred (trainer.defer_text_adam) is bit-identical too, and so is a fourth
+    with the CPB MLP inline on the main stream instead of the auxiliary one (ctvit._CPB_AUX).  The
+    spatial stage runs the base shape (24 x 24 grid, L = 576: the LDS-DMA dQ kernel); smaller grids
+    take the frame-inner kernel, checked by test_deferred_text_adam_matches."""
     from ctclip_mi355x.trainer import CTClipTrainer
+    from ctclip_mi355x import ctvit
     vit = O.ViTConfig(dim=512, codebook_size=8192, image_size=480, patch_size=20, temporal_patch_size=10,
                       spatial_depth=1, temporal_depth=1, dim_head=32, heads=8, frames=20)
     bert = O.BertConfig(vocab_size=1000, hidden=768, layers=2, heads=12, intermediate=3072, max_position=64)
@@ -367,12 +369,17 @@ def test_train_step_bit_reproducible():
     assert (ids == 0).any()
     text = types.SimpleNamespace(input_ids=ids.cuda(), attention_mask=mask.cuda())
     runs = []
-    for defer in (False, False, True):
+    cpb_aux = ctvit._CPB_AUX
+    for defer, aux in ((False, cpb_aux), (False, cpb_aux), (True, cpb_aux), (False, not cpb_aux)):
         torch.manual_seed(0)
+        ctvit._CPB_AUX = aux
         model = build(cfg, dropout=0.1)
         tr = CTClipTrainer(model, lr=1e-4, defer_text_adam=defer)
-        losses = torch.stack([tr.train_step(text, hu) for _ in range(3)])
-        tr.flush()
+        try:
+            losses = torch.stack([tr.train_step(text, hu) for _ in range(3)])
+            tr.flush()
+        finally:
+            ctvit._CPB_AUX = cpb_aux
         torch.cuda.synchronize()
         cbk = model.visual_transformer.vq._codebook
         runs.append([losses, tr.flat.data.clone(), tr.m.clone(), tr.v.clone(), cbk.embed.clone(),
