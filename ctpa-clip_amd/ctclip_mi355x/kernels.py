@@ -813,7 +813,7 @@ def l2norm_qk_bwd_fold(qk, dqk, q_scale, k_scale, row_rstd, row_mean, out, fold_
     (ds_q, ds_k, u, c1, beta); ds_* accumulate into the given sinks (deferred in a backward)."""
     rows = qk.shape[0]
     assert qk.shape[1] == 512 and dqk.shape[1] == 512 and out.shape[1] == 512
-    nb = 2048
+    nb = 1024    # the u partials are summed right away (lnfold_wgrad reads u): fewer, longer blocks
     dev = qk.device
     part_s = torch.empty(2, nb, 32, device=dev, dtype=F32)
     part_u = torch.empty(nb, 256, device=dev, dtype=F32)

@@ -11,7 +11,8 @@ the text bucket's Adam here too, so the next step's image tower does not wait fo
 BertModel.forward, on this stream, does).
 ``CTCLIP_TEXT_STREAM=0`` keeps everything on the current stream.
 
-A third, auxiliary stream takes the vector quantiser's EMA codebook update (statistics, their
+A third, auxiliary stream takes the CPB MLP (forward and, through autograd, backward: ctvit.py) and
+the vector quantiser's EMA codebook update (statistics, their
 all-reduce at N > 1, finalize): nothing reads the updated codebook before the next step's VQ,
 which waits for it (``join_aux``)."""
 from __future__ import annotations
