@@ -10,18 +10,21 @@ namespace {
 
 constexpr int MAXB = 128;
 
-__global__ __launch_bounds__(256) void clip_loss_kernel(const float* __restrict__ t_raw, const float* __restrict__ i_raw,
+// 1,024 threads: the per-row passes (2 Bg rows) and the Bg^2 dot products spread over 16 waves
+// (with 4 waves each walked 4 rows / 16 dots in sequence: ~110 us in the step, on its critical path)
+constexpr int CL_NT = 1024, CL_NW = CL_NT / 64;
+__global__ __launch_bounds__(CL_NT) void clip_loss_kernel(const float* __restrict__ t_raw, const float* __restrict__ i_raw,
                                                         int Bg, int Dl, const float* __restrict__ log_temp,
                                                         float* __restrict__ tn, float* __restrict__ in_,
                                                         float* __restrict__ loss_out, float* __restrict__ dt_raw,
                                                         float* __restrict__ di_raw, float* __restrict__ dlogtemp,
                                                         float* __restrict__ sim_out) {
   __shared__ float S[MAXB][MAXB + 1];
-  __shared__ float tnorm[MAXB], inorm[MAXB], rs[MAXB], cs[MAXB], red[8];
+  __shared__ float tnorm[MAXB], inorm[MAXB], rs[MAXB], cs[MAXB], red[CL_NW];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const float temp = __expf(log_temp[0]);
   // 1. norms (one wave per row)
-  for (int r = w; r < 2 * Bg; r += 4) {
+  for (int r = w; r < 2 * Bg; r += CL_NW) {
     const float* src = r < Bg ? t_raw + (int64_t)r * Dl : i_raw + (int64_t)(r - Bg) * Dl;
     float s = 0.f;
     for (int k = lane; k < Dl; k += 64) s += src[k] * src[k];
@@ -34,7 +37,7 @@ __global__ __launch_bounds__(256) void clip_loss_kernel(const float* __restrict_
   }
   __syncthreads();
   // 2. S = temp * tn . in^T
-  for (int e = w; e < Bg * Bg; e += 4) {
+  for (int e = w; e < Bg * Bg; e += CL_NW) {
     const int i = e / Bg, j = e - i * Bg;
     float s = 0.f;
     for (int k = lane; k < Dl; k += 64) s += tn[(int64_t)i * Dl + k] * in_[(int64_t)j * Dl + k];
@@ -43,12 +46,12 @@ __global__ __launch_bounds__(256) void clip_loss_kernel(const float* __restrict_
   }
   __syncthreads();
   // 3. exp, row / column sums
-  for (int e = tid; e < Bg * Bg; e += 256) {
+  for (int e = tid; e < Bg * Bg; e += CL_NT) {
     const int i = e / Bg, j = e - i * Bg;
     if (sim_out) sim_out[e] = S[i][j];
   }
   __syncthreads();
-  for (int e = tid; e < Bg * Bg; e += 256) {
+  for (int e = tid; e < Bg * Bg; e += CL_NT) {
     const int i = e / Bg, j = e - i * Bg;
     S[i][j] = __expf(S[i][j]);
   }
@@ -71,7 +74,7 @@ __global__ __launch_bounds__(256) void clip_loss_kernel(const float* __restrict_
   // 4. dS (stored in place over exp(S)); dlogtemp = sum dS * S  (S = log(E))
   const float c0 = 0.5f / Bg;
   float dlt = 0.f;
-  for (int e = tid; e < Bg * Bg; e += 256) {
+  for (int e = tid; e < Bg * Bg; e += CL_NT) {
     const int i = e / Bg, j = e - i * Bg;
     const float E = S[i][j];
     float d = E / (rs[i] + 1e-20f) + E / (cs[j] + 1e-20f);
@@ -84,7 +87,7 @@ __global__ __launch_bounds__(256) void clip_loss_kernel(const float* __restrict_
   if (tid == 0 && dlogtemp) dlogtemp[0] = dltot;
   __syncthreads();
   // 5. d tn_i = temp * sum_j dS_ij in_j ; d in_j = temp * sum_i dS_ij tn_i ; then through l2norm
-  for (int r = w; r < 2 * Bg; r += 4) {
+  for (int r = w; r < 2 * Bg; r += CL_NW) {
     const bool is_t = r < Bg;
     const int a = is_t ? r : r - Bg;
     const float* self = is_t ? tn + (int64_t)a * Dl : in_ + (int64_t)a * Dl;
@@ -184,7 +187,7 @@ extern "C" int ctclip_clip_loss(const float* t_raw, const float* i_raw, int32_t 
                                 float* t_norm, float* i_norm, float* loss, float* dt_raw, float* di_raw,
                                 float* dlogtemp, float* sim, void* stream) {
   CT_REQUIRE(Bg > 0 && Bg <= MAXB, CT_ESHAPE);
-  hipLaunchKernelGGL(clip_loss_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, t_raw, i_raw, Bg, Dl, log_temp,
+  hipLaunchKernelGGL(clip_loss_kernel, dim3(1), dim3(CL_NT), 0, (hipStream_t)stream, t_raw, i_raw, Bg, Dl, log_temp,
                      t_norm, i_norm, loss, dt_raw, di_raw, dlogtemp, sim);
   CT_CHECK_LAUNCH();
   return 0;
