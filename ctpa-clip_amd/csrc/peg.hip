@@ -531,6 +531,21 @@ __global__ __launch_bounds__(WNTH, 3) void peg_wgrad_tile_kernel(const u16* __re
   }
 }
 
+// one thread per (channel, tap-or-bias) output, the nblk slabs summed in order
+__global__ __launch_bounds__(256) void peg_wgrad_reduce_kernel(const float* __restrict__ part, int nblk, int D,
+                                                               float* __restrict__ dw, float* __restrict__ db,
+                                                               int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= D * 28) return;
+  const int64_t stride = (int64_t)D * 28;
+  float s = 0.f;
+#pragma unroll 8
+  for (int b = 0; b < nblk; ++b) s += part[b * stride + i];
+  const int c = i / 28, k = i - c * 28;
+  float* o = k < 27 ? (dw ? dw + c * 27 + k : nullptr) : (db ? db + c : nullptr);
+  if (o) *o = accumulate ? *o + s : s;
+}
+
 bool tiled_ok(int W, int D) {
   return D % 64 == 0 && HT * ((W + SEG - 1) / SEG) * 8 <= TNTH && (HT + 2) * (W + 2) * 8 <= PLANE_CH &&
          HT * ((W + SEGW - 1) / SEGW) * 32 <= WNTH;   // wgrad: one item per thread
@@ -645,6 +660,15 @@ extern "C" int ctclip_peg_bwd_data(const void* dout_bf16, const float* dout_f32,
     hipLaunchKernelGGL(peg_kernel<1>, grid, dim3(256), 0, (hipStream_t)stream, (const u16*)dout_bf16, ntok, D,
                        weight, (const float*)nullptr, dout_f32, g, dx_f32, (u16*)dx_bf16);
   }
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_peg_wgrad_reduce(const float* part, int32_t nblk, int32_t D, float* dweight, float* dbias,
+                                       int32_t accumulate, void* stream) {
+  CT_REQUIRE(part && nblk > 0 && D > 0, CT_EINVAL);
+  hipLaunchKernelGGL(peg_wgrad_reduce_kernel, dim3(cdiv((int64_t)D * 28, 256)), dim3(256), 0, (hipStream_t)stream, part,
+                     nblk, D, dweight, dbias, accumulate);
   CT_CHECK_LAUNCH();
   return 0;
 }

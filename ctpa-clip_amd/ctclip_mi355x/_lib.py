@@ -176,6 +176,7 @@ _SIGS = {
                              c_vp],
     'ctclip_peg_bwd_data': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp],
     'ctclip_peg_bwd_weight': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp],
+    'ctclip_peg_wgrad_reduce': [c_vp, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp],
     'ctclip_peg_wgrad_slabs': [c_i64, c_i32, c_i32, c_i32, c_i32],
     'ctclip_peg_set_canon1': [c_i32],
     'ctclip_attn_fwd': [ctypes.POINTER(AttnArgs), c_vp],

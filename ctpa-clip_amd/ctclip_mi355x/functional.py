@@ -595,12 +595,11 @@ class ViTLayerFn(torch.autograd.Function):
                 dx1f, dx1b, _, _ = K.layernorm_bwd(dxn, x1b, m1, r1, norm_g, dres=dx1kv, want_beta=False,
                                                    dgamma_out=gsink(norm_g))
         # PEG
-        dxf, dxb, dpw, dpb = K.peg_bwd(dx1b, dx1f, xb, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, geo.mode)
+        # the weight / bias gradients accumulate into .grad in the slab-reduction launch itself, so the
+        # layer's grads are final when its node returns (dist_sync buckets)
+        dxf, dxb, _, _ = K.peg_bwd(dx1b, dx1f, xb, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, geo.mode,
+                                   dweight_out=gsink(peg_w), dbias_out=gsink(peg_b))
         put_shadow(dxf, dxb)
-        if peg_w.requires_grad:          # into .grad here too, so the layer's grads are final when
-            gsink(peg_w).add_(dpw.reshape(peg_w.shape))   # its node returns (dist_sync buckets)
-        if peg_b.requires_grad:
-            gsink(peg_b).add_(dpb)
         return (dxf, None, du, None, None, None, None, None, None, None, None, None, None,
                 None, None, None)
 

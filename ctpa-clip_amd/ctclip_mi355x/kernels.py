@@ -872,8 +872,11 @@ def matmul_lnfold_bwd(dqkv, wp, res, x, c1, beta, out=None, out2=None):
     return out, out2
 
 
-def peg_bwd(doutb, doutf, xb, B, T, H, W, weight, mode):
-    """Returns (dx_f32, dx_bf16, dweight [D,27], dbias [D])."""
+def peg_bwd(doutb, doutf, xb, B, T, H, W, weight, mode, dweight_out=None, dbias_out=None):
+    """Returns (dx_f32, dx_bf16, dweight [D,27], dbias [D]).  dweight_out / dbias_out (the
+    parameters' .grad, [D, 27]-contiguous / [D]): the weight gradient accumulates into them in the
+    same launch that sums the partial slabs (ctclip_peg_wgrad_reduce) and the returned dweight /
+    dbias are those sinks."""
     D = xb.shape[1]
     dxf = torch.empty_like(doutf)
     dxb = torch.empty_like(doutb)
@@ -882,10 +885,15 @@ def peg_bwd(doutb, doutf, xb, B, T, H, W, weight, mode):
     nblk = _lib.lib().ctclip_peg_wgrad_slabs(B, T, H, W, D)
     part = torch.empty(nblk, D * 28, device=xb.device, dtype=F32)
     call('ctclip_peg_bwd_weight', ptr(doutb), ptr(xb), B, T, H, W, D, mode, ptr(part), nblk, stream_ptr())
-    red = torch.empty(D * 28, device=xb.device, dtype=F32)
-    reduce_slabs(part.view(nblk, 1, D * 28), red.view(1, D * 28))
-    red = red.view(D, 28)
-    return dxf, dxb, red[:, :27], red[:, 27]
+    if dweight_out is not None or dbias_out is not None:
+        assert dweight_out is None or (dweight_out.is_contiguous() and dweight_out.numel() == D * 27)
+        assert dbias_out is None or (dbias_out.is_contiguous() and dbias_out.numel() == D)
+        call('ctclip_peg_wgrad_reduce', ptr(part), nblk, D, ptr(dweight_out), ptr(dbias_out), 1, stream_ptr())
+        return dxf, dxb, dweight_out, dbias_out
+    dw = torch.empty(D, 27, device=xb.device, dtype=F32)
+    db = torch.empty(D, device=xb.device, dtype=F32)
+    call('ctclip_peg_wgrad_reduce', ptr(part), nblk, D, ptr(dw), ptr(db), 0, stream_ptr())
+    return dxf, dxb, dw, db
 
 
 # ----------------------------------------------------------------------------- attention

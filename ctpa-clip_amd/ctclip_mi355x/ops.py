@@ -425,6 +425,9 @@ class _NoCtx:
     def mark_non_differentiable(self, *_):
         pass
 
+    def set_materialize_grads(self, *_):
+        pass
+
 
 @torch.library.custom_op('ctclip::bert_layer', mutates_args=(), device_types='cuda')
 def bert_layer(x: Tensor, attention_mask: Tensor, heads: int, eps: float, wq: Tensor, bq: Tensor, wk: Tensor,

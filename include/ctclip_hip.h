@@ -330,6 +330,12 @@ int ctclip_peg_bwd_data(const void* dout_bf16, const float* dout_f32, int64_t B,
 int ctclip_peg_bwd_weight(const void* dout_bf16, const void* x_bf16, int64_t B, int32_t T, int32_t H,
                           int32_t W, int32_t D, int32_t mode, float* part, int32_t nblk, void* stream);
 int ctclip_peg_wgrad_slabs(int64_t B, int32_t T, int32_t H, int32_t W, int32_t D);
+/* Sum of the nblk [D][28] partial slabs of ctclip_peg_bwd_weight straight into the parameters'
+   gradients: dweight[c][27] (+)= sum_b part[b][c][0..26], dbias[c] (+)= sum_b part[b][c][27], slabs
+   summed in order (deterministic); either output may be null.  Replaces a slab reduction + two
+   strided adds per layer (round 4). */
+int ctclip_peg_wgrad_reduce(const float* part, int32_t nblk, int32_t D, float* dweight, float* dbias,
+                            int32_t accumulate, void* stream);
 /* mode 1 on a T = H = W = 24 cube runs as a canonical-order walk (the view is an axis permutation
  * there; same outputs up to f32 summation order); 0 = the view-order walk (A/B).  Returns the previous. */
 int ctclip_peg_set_canon1(int32_t on);
