@@ -420,6 +420,14 @@ class ViTLayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xf, xb, bias_u, geo, peg_w, peg_b, norm_g, q_scale, k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1,
                 W2):
+        # the layers sharing one CPB table accumulate its gradient in ONE buffer (the attention's
+        # slab reduction adds into it) and only the first layer of the forward -- the last backward
+        # -- hands it to autograd: no per-layer gradient tensors for autograd to add up on the CPB
+        # node's (auxiliary) stream
+        if bias_u is not None:
+            acc = bias_u.__dict__.setdefault('_ctclip_bias_acc', {'n': 0, 'du': None})
+            ctx.bias_acc, ctx.bias_first = acc, acc['n'] == 0
+            acc['n'] += 1
         if precise_f32():
             return _vit_layer_forward_f32(ctx, xf, xb, bias_u, geo, peg_w, peg_b, norm_g, q_scale, k_scale, Wq,
                                           Wkv, Wo, ff_w, ff_b, W1, W2)
@@ -537,7 +545,12 @@ class ViTLayerFn(torch.autograd.Function):
         dqn = torch.empty_like(qn)
         dkn = torch.empty_like(kn)
         L, nseq, seq = geo.seq()
-        du = torch.zeros_like(bias_u) if ctx.use_bias else None
+        du = None
+        if ctx.use_bias:
+            acc = ctx.bias_acc
+            if acc['du'] is None:
+                acc['du'] = torch.zeros_like(bias_u)
+            du = acc['du']
         fold = getattr(ctx, 'fold', False)
         if fold:
             # the folded LayerNorm (ctx.fold, forward above) backward through the Q | K | V
@@ -600,6 +613,11 @@ class ViTLayerFn(torch.autograd.Function):
         dxf, dxb, _, _ = K.peg_bwd(dx1b, dx1f, xb, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, geo.mode,
                                    dweight_out=gsink(peg_w), dbias_out=gsink(peg_b))
         put_shadow(dxf, dxb)
+        if du is not None:
+            if ctx.bias_first:       # every layer's share is in: release the buffer to autograd
+                ctx.bias_acc['du'] = None
+            else:
+                du = None
         return (dxf, None, du, None, None, None, None, None, None, None, None, None, None,
                 None, None, None)
 
