@@ -136,6 +136,17 @@ class CTViT(nn.Module):
                 bias_u = self.spatial_rel_pos_bias(hg, wg)
                 cpb_ev = aux.record_event()
             bias_u.record_stream(main)
+            node = bias_u.grad_fn
+            if node is not None:
+                def cpb_ready(du, node=node, aux=aux):
+                    # called by the last spatial layer's backward right after its attention backward
+                    # (functional._bias_grad_ready): the CPB MLP's backward starts there, on aux
+                    aux.wait_stream(torch.cuda.current_stream(du.device))
+                    with torch.cuda.stream(aux):
+                        Fn.CPBFn.backward(node, du)
+                    du.record_stream(aux)
+                    node._ctclip_done = True
+                bias_u.__dict__['_ctclip_bias_acc'] = {'n': 0, 'du': None, 'ready': cpb_ready}
         pe = self.to_patch_emb
         xf, xb = Fn.PatchEmbedFn.apply(video, pe[1].weight, pe[1].bias, pe[2].weight, pe[2].bias, pe[3].weight,
                                        pe[3].bias, self.temporal_patch_size, self.patch_size[0], is_hu,

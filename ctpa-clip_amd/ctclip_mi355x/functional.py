@@ -386,6 +386,9 @@ class CPBFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, du):
+        if getattr(ctx, '_ctclip_done', False):   # already run from the last layer's backward
+            ctx._ctclip_done = False                 # (ctvit.encode_tokens: cpb_ready)
+            return None, None, None, None, None, None, None
         rel, w0, w1, w2, h1, h2 = ctx.saved_tensors
         pw0, pb0, pw1, pb1, pw2, pb2 = ctx.params
         du = du.contiguous()
@@ -413,6 +416,18 @@ class CPBFn(torch.autograd.Function):
 
 
 # ----------------------------------------------------------------------------- transformer layer
+def _bias_grad_ready(ctx, du):
+    """The CPB table's gradient is complete once the first layer of the forward (the last backward)
+    has run its attention backward: hand it to the owner's 'ready' callback right there (ctvit
+    registers one that runs the CPB MLP's backward on the auxiliary stream), instead of when this
+    layer's whole backward node returns."""
+    if du is None or not ctx.bias_first:
+        return
+    cb = ctx.bias_acc.get('ready')
+    if cb is not None:
+        cb(du)
+
+
 class ViTLayerFn(torch.autograd.Function):
     """One CTViT transformer layer (ct_clip/attention.py:322-331):
     x = PEG(x) + x; x = Attention(x, bias) + x; x = FeedForward(x) + x."""
@@ -565,6 +580,7 @@ class ViTLayerFn(torch.autograd.Function):
             K.attn_bwd(qn, kn, kv[:, inner:], o, lse, do, dqkn[:, :inner], dqkn[:, inner:], dqkv[:, 2 * inner:],
                        L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq, bias_u=bias_u if ctx.use_bias else None,
                        dbias_u=du, grid=(geo.Hg, geo.Wg) if ctx.use_bias else (0, 0))
+            _bias_grad_ready(ctx, du)
             if _QK_BWD_MERGED:
                 # both l2norm backwards in one pass over the forward's [q | k] (one wave per row)
                 qk = q.as_strided((M_, 2 * inner), q.stride())
@@ -588,6 +604,7 @@ class ViTLayerFn(torch.autograd.Function):
             K.attn_bwd(qn, kn, kv[:, inner:], o, lse, do, dqn, dkn, dkv[:, inner:], L=L, H=H, D=dh, nseq=nseq,
                        scale=8.0, seq=seq, bias_u=bias_u if ctx.use_bias else None, dbias_u=du,
                        grid=(geo.Hg, geo.Wg) if ctx.use_bias else (0, 0))
+            _bias_grad_ready(ctx, du)
             dq = torch.empty(q.shape, device=dev, dtype=q.dtype)
             K.l2norm_scale_bwd(q, dqn, H, dh, q_scale, dq, ds_out=gsink(q_scale))
             K.l2norm_scale_bwd(kv[:, :inner], dkn, H, dh, k_scale, dkv[:, :inner], ds_out=gsink(k_scale))
