@@ -306,7 +306,9 @@ class PatchEmbedFn(torch.autograd.Function):
             return (None,) * 11
         xhat, y1, mean, rstd, ln1_w, ln1_b, W, ln2_w = ctx.saved_tensors
         take_shadow(dyf)
-        _, dy1b, dg2, db2 = K.layernorm_bwd(dyf.contiguous(), y1, mean, rstd, ln2_w, dx_f32=False)
+        # LN2's gamma / beta gradients straight into their .grad (deferred partial reductions)
+        _, dy1b, _, _ = K.layernorm_bwd(dyf.contiguous(), y1, mean, rstd, ln2_w, dx_f32=False,
+                                        dgamma_out=gsink(ctx.ln2_w), dbeta_out=gsink(ctx.ln2_b))
         G = K.matmul_tn(dy1b, xhat, tag='dw')                           # [D, pd] f32
         cs = K.colsum(dy1b)                                             # d bias
         # straight into .grad (gsink), so the node's parameters are final when it returns
@@ -314,9 +316,8 @@ class PatchEmbedFn(torch.autograd.Function):
         sinks = [gsink(t) for t in (W, ln1_w, ln1_b)]
         tmp = [s_ if s_ is not None else torch.zeros_like(t) for s_, t in zip(sinks, (W, ln1_w, ln1_b))]
         K.patch_wgrad(G, cs, W, ln1_w, ln1_b, tmp[0], tmp[1], tmp[2], accumulate=True)
-        for t, g_ in ((ctx.b, cs), (ctx.ln2_w, dg2), (ctx.ln2_b, db2)):
-            if t.requires_grad:
-                gsink(t).add_(g_)
+        if ctx.b.requires_grad:
+            gsink(ctx.b).add_(cs)
         return None, None, None, None, None, None, None, None, None, None, None
 
 
