@@ -18,6 +18,7 @@ from .attention import ContinuousPositionBias, Transformer
 from .layers import patch_offsets
 
 _CPB_AUX = os.environ.get('CTCLIP_CPB_AUX', '1') != '0'
+_PREPACK_AUX = os.environ.get('CTCLIP_PREPACK_AUX', '1') != '0'
 
 
 def pair(v):
@@ -134,8 +135,12 @@ class CTViT(nn.Module):
             aux.wait_stream(main)            # the previous optimizer step's update of the MLP
             with torch.cuda.stream(aux):
                 bias_u = self.spatial_rel_pos_bias(hg, wg)
+                # the layers' packed FeedForward weights too (16 small launches off the main stream)
+                packs = Fn.prepack_ff(self._ff_weights()) if _PREPACK_AUX else []
                 cpb_ev = aux.record_event()
             bias_u.record_stream(main)
+            for t in packs:
+                t.record_stream(main)
             node = bias_u.grad_fn
             if node is not None:
                 def cpb_ready(du, node=node, aux=aux):
@@ -168,6 +173,10 @@ class CTViT(nn.Module):
         if trace is not None:
             trace['spatial_out'], trace['temporal_out'] = xf, zf
         return zf, zb, g_sp
+
+    def _ff_weights(self):
+        return [(ff[1].weight, ff[4].weight) for tr in (self.enc_spatial_transformer, self.enc_temporal_transformer)
+                for (_, _, _, ff) in tr.layers]
 
     def encode_pooled(self, video):
         """Encoder + VQ + mean over t (the CTCLIP image path, ct_clip.py:715,724,740):

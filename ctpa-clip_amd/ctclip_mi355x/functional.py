@@ -126,14 +126,42 @@ def ff1_rowmap(inner, device):
     return _MAP_CACHE[key]
 
 
+# packed FeedForward weights made ahead of the layers (prepack_ff, on the auxiliary stream at the
+# start of the image tower's forward), keyed by the weight's storage, version and optimizer epoch
+_PREPACKED = {}
+
+
+def _pack_key(kind, W):
+    return (kind, W.data_ptr(), W._version, K.weights_epoch())
+
+
 def pack_ff1(W1):
+    hit = _PREPACKED.get(_pack_key('ff1', W1))
+    if hit is not None:
+        return hit
     inner = W1.shape[0] // 2
     P = ff_pad(inner)
     return K.pack_rows(W1, 2 * P, W1.shape[1], rowmap=ff1_rowmap(inner, W1.device))
 
 
 def pack_ff2(W2):
+    hit = _PREPACKED.get(_pack_key('ff2', W2))
+    if hit is not None:
+        return hit
     return K.pack_rows(W2, W2.shape[0], ff_pad(W2.shape[1]))
+
+
+def prepack_ff(pairs):
+    """Pack every layer's FeedForward weights now (on the caller's current stream) for the layers
+    that run later (pack_ff1 / pack_ff2 then return these); returns the packed tensors."""
+    _PREPACKED.clear()
+    out = []
+    for W1, W2 in pairs:
+        a, b = pack_ff1(W1), pack_ff2(W2)
+        _PREPACKED[_pack_key('ff1', W1)] = a
+        _PREPACKED[_pack_key('ff2', W2)] = b
+        out += [a, b]
+    return out
 
 
 def shadow_bf16(W):
