@@ -13,7 +13,14 @@
 #include "common.h"
 #include "../../include/ctclip_hip.h"
 
+// diagnostic build only (timing the full-group re-score; wrong indices): treat every group as single
+#ifndef CTCLIP_VQ_DIAG_NOFULL
+#define CTCLIP_VQ_DIAG_NOFULL 0
+#endif
+
 namespace {
+
+constexpr int VQ_SB = 4;   // single-code candidates re-scored together
 
 // one wave per row; the row's f32 l2norm lives in a wave-private LDS strip (D floats) so the
 // full-group re-score can run one code per lane
@@ -52,45 +59,68 @@ __global__ __launch_bounds__(256) void vq_select_kernel(const float2* __restrict
     if (t < ntiles) {
       c = cand[row * ntiles + t];
       take = c.x >= thr;
-      full = take && cand2 && cand2[row * ntiles + t] >= thr;
+      full = !CTCLIP_VQ_DIAG_NOFULL && take && cand2 && cand2[row * ntiles + t] >= thr;
     }
-    unsigned long long mask = __ballot(take);
+    const unsigned long long mask = __ballot(take);
     const unsigned long long fmask = __ballot(full);
-    while (mask) {
-      const int src = __ffsll((long long)mask) - 1;
-      mask &= mask - 1;
-      if ((fmask >> src) & 1ull) {
-        // several codes of this group are within the margin: score all of them, one per lane
-        const int ci = (t0 + src) * 64 + lane;
-        float d = -INFINITY;
-        if (ci < C) {
-          const float* cr = cb + (int64_t)ci * D;
-          d = 0.f;
-          for (int k = 0; k < D; k += 4) {
-            const f32x4 w = *(const f32x4*)(cr + k);
-            const f32x4 xv = *(const f32x4*)(xs + k);
-            d += xv[0] * w[0];
-            d += xv[1] * w[1];
-            d += xv[2] * w[2];
-            d += xv[3] * w[3];
-          }
-        }
-        float dv = d;
-        int di = ci < C ? ci : 0x7fffffff;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-          const float ov = __shfl_xor(dv, o, 64);
-          const int oi = __shfl_xor(di, o, 64);
-          if (ov > dv || (ov == dv && oi < di)) { dv = ov; di = oi; }
-        }
-        if (dv > bv || (dv == bv && di < bi)) { bv = dv; bi = di; }
-      } else {
-        const int ci = __float_as_int(__shfl(c.y, src, 64));
+    // (bv, bi) = the max score, ties to the lowest code: independent of the order codes are scored
+    // in, so full groups go first and single codes after, VQ_SB at a time with their loads
+    // interleaved (one code per pass was a dependent load -> warp-sum chain per candidate)
+    unsigned long long gmask = mask & fmask, smask = mask & ~fmask;
+    while (gmask) {
+      const int src = __ffsll((long long)gmask) - 1;
+      gmask &= gmask - 1;
+      // several codes of this group are within the margin: score all of them, one per lane
+      const int ci = (t0 + src) * 64 + lane;
+      float d = -INFINITY;
+      if (ci < C) {
         const float* cr = cb + (int64_t)ci * D;
-        float d = 0.f;
-        for (int k = lane; k < D; k += 64) d += xs[k] * cr[k];
-        d = warp_sum(d);
-        if (d > bv || (d == bv && ci < bi)) { bv = d; bi = ci; }
+        d = 0.f;
+        for (int k = 0; k < D; k += 4) {
+          const f32x4 w = *(const f32x4*)(cr + k);
+          const f32x4 xv = *(const f32x4*)(xs + k);
+          d += xv[0] * w[0];
+          d += xv[1] * w[1];
+          d += xv[2] * w[2];
+          d += xv[3] * w[3];
+        }
+      }
+      float dv = d;
+      int di = ci < C ? ci : 0x7fffffff;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const float ov = __shfl_xor(dv, o, 64);
+        const int oi = __shfl_xor(di, o, 64);
+        if (ov > dv || (ov == dv && oi < di)) { dv = ov; di = oi; }
+      }
+      if (dv > bv || (dv == bv && di < bi)) { bv = dv; bi = di; }
+    }
+    while (smask) {
+      int ci[VQ_SB];
+#pragma unroll
+      for (int q = 0; q < VQ_SB; ++q) {
+        ci[q] = -1;
+        if (smask) {   // wave-uniform
+          const int src = __ffsll((long long)smask) - 1;
+          smask &= smask - 1;
+          ci[q] = __float_as_int(__shfl(c.y, src, 64));
+        }
+      }
+      // per code the same sum as one at a time: lane k-slice in order, then the wave sum
+      float d[VQ_SB];
+#pragma unroll
+      for (int q = 0; q < VQ_SB; ++q) d[q] = 0.f;
+      for (int k = lane; k < D; k += 64) {
+        const float xk = xs[k];
+#pragma unroll
+        for (int q = 0; q < VQ_SB; ++q)
+          if (ci[q] >= 0) d[q] += xk * cb[(int64_t)ci[q] * D + k];
+      }
+#pragma unroll
+      for (int q = 0; q < VQ_SB; ++q) {
+        if (ci[q] < 0) continue;
+        const float dq = warp_sum(d[q]);
+        if (dq > bv || (dq == bv && ci[q] < bi)) { bv = dq; bi = ci[q]; }
       }
     }
   }
