@@ -38,6 +38,7 @@ struct AP {
   const u16* v; int64_t ldv;
   const u16* o; int64_t ldo;      // forward output (read in backward for delta)
   u16* out; int64_t ldout;        // forward: O
+  u16* out16;                     // forward, optional: an fp16 copy of O (ldout), the fp16 to_out GEMM's A
   const u16* dout; int64_t lddo;  // backward: dO
   u16* dq; int64_t lddq;
   u16* dk; int64_t lddk;
@@ -493,7 +494,9 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
         // lane's PARTIAL max exceeds m + lazy iff the query's full chunk max does.  The two
         // lane ^ 16 / ^ 32 exchanges (LDS permutes on the chunk's critical path) run only on the
         // chunks that rescale; the rescaled max is the same full max as before (bit-identical).
-        rescale[u] = p.lazy <= 0.f || __any(cmax > m[u] + p.lazy);
+        // m[u] == -inf (every key so far masked, e.g. a left-padded BERT mask): rescale, so the
+        // exp2 below never sees -inf - -inf
+        rescale[u] = p.lazy <= 0.f || __any(cmax > m[u] + p.lazy || m[u] == -INFINITY);
         float msafe;
         if (rescale[u]) {
           cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
@@ -503,7 +506,7 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
           alpha[u] = fexp2(m[u] - msafe);
           m[u] = mnew;
         } else {
-          msafe = m[u];        // finite: some earlier chunk set it
+          msafe = m[u];        // finite: m == -inf always takes the rescale branch
           alpha[u] = 1.f;
         }
         float psum = 0.f;
@@ -546,10 +549,10 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
       if (qv[u]) {
 #pragma unroll
         for (int d = 0; d < DB; ++d) {
-          uint2 pk;
-          pk.x = pack2(o[u][d][0] * inv, o[u][d][1] * inv);
-          pk.y = pack2(o[u][d][2] * inv, o[u][d][3] * inv);
-          *(uint2*)(p.out + qrow[u] * p.ldout + h * D + d * 16 + 4 * g) = pk;
+          const float o4[4] = {o[u][d][0] * inv, o[u][d][1] * inv, o[u][d][2] * inv, o[u][d][3] * inv};
+          const int64_t off = qrow[u] * p.ldout + h * D + d * 16 + 4 * g;
+          *(uint2*)(p.out + off) = pack4(o4);
+          if (p.out16) *(uint2*)(p.out16 + off) = pack4h(o4);
         }
         // natural-log LSE: ln(sum exp(x)) = (m2 + log2(lsum)) * ln 2
         if (g == 0 && p.lse) p.lse[(int64_t)h * p.M + qrow[u]] = ls > 0.f ? (m[u] + __log2f(ls)) * LN2 : INFINITY;
@@ -1380,6 +1383,7 @@ int fill(AP& p, const ctclip_attn_args* a) {
   p.v = (const u16*)a->v; p.ldv = a->ldv;
   p.o = (const u16*)a->o; p.ldo = a->ldo;
   p.out = (u16*)a->o; p.ldout = a->ldo;
+  p.out16 = (u16*)a->o16;
   p.dout = (const u16*)a->dout; p.lddo = a->lddo;
   p.dq = (u16*)a->dq; p.lddq = a->lddq;
   p.dk = (u16*)a->dk; p.lddk = a->lddk;
@@ -1571,7 +1575,9 @@ __global__ __launch_bounds__(SW * 64) void attn_small_fwd_kernel(AP p) {
       const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt[db], pf, z4, 0, 0, 0);
       if (q < p.L) {
         const float o4[4] = {ot[0] * inv, ot[1] * inv, ot[2] * inv, ot[3] * inv};
-        *(uint2*)(p.out + seq_row(p, s, q) * p.ldout + h * 32 + 16 * db + 4 * g) = pack4(o4);
+        const int64_t off = seq_row(p, s, q) * p.ldout + h * 32 + 16 * db + 4 * g;
+        *(uint2*)(p.out + off) = pack4(o4);
+        if (p.out16) *(uint2*)(p.out16 + off) = pack4h(o4);
       }
     }
     if (g == 0 && q < p.L && p.lse) p.lse[(int64_t)h * p.M + seq_row(p, s, q)] = (m + __log2f(l)) * LN2;

@@ -87,6 +87,35 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   return r;
 }
 __device__ __forceinline__ uint2 pack4(const float* f) { return make_uint2(pack2(f[0], f[1]), pack2(f[2], f[3])); }
+
+// IEEE fp16 (the 3D-ViT forward's 16-bit GEMM operands since round 5: 3 more mantissa bits than
+// bf16 at the same MFMA rate).  Conversions round to nearest even.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ u16 f2h(float f) { return __builtin_bit_cast(u16, (_Float16)f); }
+__device__ __forceinline__ float h2f(u16 v) { return (float)__builtin_bit_cast(_Float16, v); }
+__device__ __forceinline__ float rh(float f) { return (float)(_Float16)f; }   // f rounded to f16
+__device__ __forceinline__ unsigned pack2h(float a, float b) { return (unsigned)f2h(a) | ((unsigned)f2h(b) << 16); }
+__device__ __forceinline__ u32x4 pack8h(const float* f) {
+  return make_uint4(pack2h(f[0], f[1]), pack2h(f[2], f[3]), pack2h(f[4], f[5]), pack2h(f[6], f[7]));
+}
+__device__ __forceinline__ uint2 pack4h(const float* f) { return make_uint2(pack2h(f[0], f[1]), pack2h(f[2], f[3])); }
+__device__ __forceinline__ void unpack8h(const u32x4& v, float* f) {
+  const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = h2f((u16)(w[i] & 0xffffu));
+    f[2 * i + 1] = h2f((u16)(w[i] >> 16));
+  }
+}
+// 16-bit A/B MFMA step: bf16 or fp16 operands (same fragment layout), f32 accumulate
+template <bool H16>
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  if constexpr (H16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0,
+                                                  0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 __device__ __forceinline__ void unpack4(const uint2& v, float* f) {
   f[0] = __uint_as_float(v.x << 16);
   f[1] = __uint_as_float(v.x & 0xffff0000u);

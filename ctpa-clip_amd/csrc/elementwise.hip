@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(const u16* __restrict__ d
 }
 
 // dst[r][c] (bf16, ld_dst) = src[map[r]][c] * (colscale ? colscale[c] : 1), zero if map[r] < 0 or c >= cols
-template <typename OUT>
+template <typename OUT, bool H16 = false>
 __global__ __launch_bounds__(256) void pack_rows_kernel(const float* __restrict__ src, int64_t ld_src,
                                                         const int32_t* __restrict__ map, int64_t rows_dst,
                                                         int cols, int cols_dst, const float* __restrict__ colscale,
@@ -60,7 +60,8 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const float* __restrict_
       v = src[sr * ld_src + c];
       if (colscale) v *= colscale[c];
     }
-    if constexpr (sizeof(OUT) == 2) dst[r * ld_dst + c] = f2bf(v);
+    if constexpr (H16) dst[r * ld_dst + c] = f2h(v);
+    else if constexpr (sizeof(OUT) == 2) dst[r * ld_dst + c] = f2bf(v);
     else dst[r * ld_dst + c] = v;
   }
 }
@@ -137,6 +138,15 @@ extern "C" int ctclip_pack_rows(const float* src, int64_t ld_src, const int32_t*
                                 int32_t cols_dst, const float* colscale, void* dst, int64_t ld_dst, void* stream) {
   hipLaunchKernelGGL(pack_rows_kernel<u16>, dim3(grid_for(rows_dst * cols_dst)), dim3(256), 0, (hipStream_t)stream,
                      src, ld_src, map, rows_dst, cols, cols_dst, colscale, (u16*)dst, ld_dst);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_pack_rows_h16(const float* src, int64_t ld_src, const int32_t* map, int64_t rows_dst,
+                                    int32_t cols, int32_t cols_dst, const float* colscale, void* dst, int64_t ld_dst,
+                                    void* stream) {
+  hipLaunchKernelGGL((pack_rows_kernel<u16, true>), dim3(grid_for(rows_dst * cols_dst)), dim3(256), 0,
+                     (hipStream_t)stream, src, ld_src, map, rows_dst, cols, cols_dst, colscale, (u16*)dst, ld_dst);
   CT_CHECK_LAUNCH();
   return 0;
 }

@@ -36,6 +36,7 @@ struct P {
   float alpha; int act; int accumulate; int split_k;
   int64_t sA, sB, sC, sC2, sR;
   int64_t kper;
+  int r_f16;                     // act 4: R (h) is fp16
 };
 
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
@@ -114,7 +115,7 @@ __device__ __forceinline__ void xcd_remap(int& tx, int& ty) {
   tx = id - ty * gx;
 }
 
-template <bool AK, bool BK>
+template <bool AK, bool BK, bool H16 = false>
 __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wr = w >> 1, wc = w & 1;
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16<H16>(af[i], bfr[j], acc[i][j]);
     }
     if (kt + 1 < nk) {
       swrite<AK>(AS(cur ^ 1), ra);
@@ -224,8 +225,13 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
       const u16* hr = (const u16*)p.R + bidx * p.sR + gm * p.ldr + tg * 64 + cw;
       u16* dr = (u16*)p.C + bidx * p.sC + gm * p.ldc + tg * 64 + cw;
       float x[8], gt[8], ox[8], og[8];
-      unpack8(*(const u32x4*)hr, x);
-      unpack8(*(const u32x4*)(hr + 32), gt);
+      if (p.r_f16) {
+        unpack8h(*(const u32x4*)hr, x);
+        unpack8h(*(const u32x4*)(hr + 32), gt);
+      } else {
+        unpack8(*(const u32x4*)hr, x);
+        unpack8(*(const u32x4*)(hr + 32), gt);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float d = bf2f(f2bf(cs[row * CS_LD + cc + j] * p.alpha));
@@ -300,7 +306,8 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += rr[j];
       }
-      *(u32x4*)Cb = pack8(v);
+      // the fp16 GEGLU GEMM (act 2) keeps h in fp16
+      *(u32x4*)Cb = (H16 && p.act == 2) ? pack8h(v) : pack8(v);
     }
     if (p.C2 && p.act == 0) *(u32x4*)(p.C2 + bidx * p.sC2 + gm * p.ldc2 + gn) = pack8(v);
   }
@@ -317,8 +324,9 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
       for (int j = 0; j < 8; ++j) {
         const float x = cs[row * CS_LD + cc + j] * p.alpha;
         const float gt = cs[row * CS_LD + 32 + cc + j] * p.alpha;
-        // round h to bf16 first so forward g == geglu(stored h) bit-for-bit in backward
-        const float xb = bf2f(f2bf(x)), gb = bf2f(f2bf(gt));
+        // round h as stored (bf16, or fp16 in the fp16 GEMM) first so forward g == geglu(stored h)
+        // bit-for-bit in backward
+        const float xb = H16 ? rh(x) : bf2f(f2bf(x)), gb = H16 ? rh(gt) : bf2f(f2bf(gt));
         v[j] = gelu_erf(gb) * xb;
       }
       *(u32x4*)(p.C2 + bidx * p.sC2 + gm * p.ldc2 + gn) = pack8(v);
@@ -326,10 +334,10 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
   }
 }
 
-template <bool AK, bool BK>
+template <bool AK, bool BK, bool H16 = false>
 int launch(const P& p, int batch, hipStream_t st) {
   dim3 grid(cdiv(p.N, BN), cdiv(p.M, BM), batch * p.split_k);
-  hipLaunchKernelGGL((gemm_kernel<AK, BK>), grid, dim3(NTH), SMEM_BYTES, st, p);
+  hipLaunchKernelGGL((gemm_kernel<AK, BK, H16>), grid, dim3(NTH), SMEM_BYTES, st, p);
   CT_CHECK_LAUNCH();
   return 0;
 }
@@ -487,6 +495,10 @@ extern "C" int ctclip_gemm(const ctclip_gemm_args* a, void* stream) {
                    (a->batch <= 1) && a->N % 64 == 0 && a->n2 > 0 && a->n2 % 64 == 0 && a->n2 <= a->N,
                CT_EINVAL);
   if (a->B2) CT_REQUIRE(aligned16(a->B2) && a->act != 3, CT_EINVAL);
+  if (a->ab_f16)   // fp16 operands: the 3D-ViT forward GEMMs (K-contiguous A and B, no split-K / B2)
+    CT_REQUIRE(a->a_kcontig && a->b_kcontig && !a->B2 && split == 1 && (a->act == 0 || a->act == 2) &&
+                   !a->accumulate && (a->batch <= 1),
+               CT_EINVAL);
   if (!a->B2 && a->act != 6) {   // act 6 (GELU backward): the 128-tile kernel only (text tower)
     const int b = a->batch > 0 ? a->batch : 1;
     const int64_t tiles256 = ((a->M + 255) / 256) * ((a->N + 255) / 256) * split * b;
@@ -509,6 +521,7 @@ extern "C" int ctclip_gemm(const ctclip_gemm_args* a, void* stream) {
     (void)hipFuncSetAttribute((const void*)gemm_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
     (void)hipFuncSetAttribute((const void*)gemm_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
+    (void)hipFuncSetAttribute((const void*)gemm_kernel<true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
     s_smem_set = true;
   }
   P p;
@@ -525,8 +538,10 @@ extern "C" int ctclip_gemm(const ctclip_gemm_args* a, void* stream) {
   int64_t kper = (a->K + split - 1) / split;
   kper = (kper + BKT - 1) / BKT * BKT;
   p.kper = kper;
+  p.r_f16 = a->r_f16;
   const int batch = a->batch > 0 ? a->batch : 1;
   hipStream_t st = (hipStream_t)stream;
+  if (a->ab_f16) return launch<true, true, true>(p, batch, st);
   if (a->a_kcontig && a->b_kcontig) return launch<true, true>(p, batch, st);
   if (a->a_kcontig && !a->b_kcontig) return launch<true, false>(p, batch, st);
   if (!a->a_kcontig && a->b_kcontig) return launch<false, true>(p, batch, st);

@@ -65,6 +65,10 @@ struct P {
   //   C = rstd[row] * (acc - mean[row] * fold_cs[col])   (ln_mean / ln_rstd read)
   const float* fold_cs;
   int nfold;
+  // fp16 (round 5): h16 = FF1's h is fp16 -- written by the GEGLU epilogue of the fp16 kernel (EP 2,
+  // H16), read by the GEGLU backward (EP 4); ln_y16 = optional fp16 copy of the -6 LayerNorm output
+  int h16;
+  u16* ln_y16;
 };
 
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
@@ -619,6 +623,13 @@ __device__ __forceinline__ u32x4 pair_swap(const float* x4, const float* y4) {
   return make_uint4(r0[0], r1[0], r0[1], r1[1]);
 }
 __device__ __forceinline__ int pair_coff(int g) { return ((g & 1) ? 16 : 0) + ((g & 2) ? 8 : 0); }
+// the same pairing for fp16 values
+__device__ __forceinline__ u32x4 pair_swap_h(const float* x4, const float* y4) {
+  const uint2 x = pack4h(x4), y = pack4h(y4);
+  const auto r0 = __builtin_amdgcn_permlane16_swap(x.x, y.x, false, false);
+  const auto r1 = __builtin_amdgcn_permlane16_swap(x.y, y.y, false, false);
+  return make_uint4(r0[0], r1[0], r0[1], r1[1]);
+}
 
 // value of lane ^ 16 / lane ^ 32 through v_permlane16_swap / v_permlane32_swap (VALU) instead of
 // ds_bpermute (the LDS crossbar, ~100+ cycles each in the argmax / l2norm epilogues).  Swapping x
@@ -672,6 +683,17 @@ __device__ __forceinline__ void store_row_bf16(u16* rowp, const float (&v)[4][4]
   }
 }
 
+// store one row's 4 j-blocks x 4 cols as fp16 (FF1's h in the fp16 GEMM)
+__device__ __forceinline__ void store_row_f16(u16* rowp, const float (&v)[4][4], int g, bool ok, int64_t c0,
+                                              int64_t N) {
+#pragma unroll
+  for (int jp = 0; jp < 2; ++jp) {
+    const u32x4 d = pair_swap_h(v[2 * jp], v[2 * jp + 1]);
+    const int coff = 32 * jp + pair_coff(g);
+    if (ok && c0 + coff < N) st16(rowp + coff, d);
+  }
+}
+
 // The same 16-row block of 64 bf16 columns (rows gm0 .. gm0 + 15, C at (gm0, c0)) through the
 // wave's LDS scratch: a lane of the transposed layout holds one row (lane & 15), so its 16-B stores
 // are 16 rows x 64 B per instruction with consecutive lanes on different rows -- the per-CU store
@@ -707,7 +729,7 @@ __device__ __forceinline__ void store_blk_bf16_lds(char* scr, u16* C, int64_t ld
 // ds_bpermute on the VQ argmax GEMM (1.193 vs 1.171-1.176 ms, profiles/r02aw_*), so off
 constexpr bool GEMM_PERMLANE = CTCLIP_GEMM_PERMLANE;
 
-template <int MODE, bool LDS = false>
+template <int MODE, bool LDS = false, bool H16 = false>
 __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int wr, int wc, int lane, int64_t m0,
                                            int64_t n0, int split, int bidx, char* scr) {
   const int m = lane & 15, g = lane >> 4;
@@ -864,13 +886,17 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
         }
         continue;
       }
-      store_row_bf16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N, p.epi_lds == 3);
+      // fp16 kernel: h stored as fp16, g from the fp16-rounded h (the backward recomputes g' from
+      // the stored h); bf16 kernel: both in bf16
+      if constexpr (H16) store_row_f16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N);
+      else store_row_bf16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N, p.epi_lds == 3);
       float gg[2][4];
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float xb = bf2f(f2bf(v[j][r])), gb = bf2f(f2bf(v[j + 2][r]));
+          const float xb = H16 ? rh(v[j][r]) : bf2f(f2bf(v[j][r]));
+          const float gb = H16 ? rh(v[j + 2][r]) : bf2f(f2bf(v[j + 2][r]));
           gg[j][r] = gelu_erf(gb) * xb;
         }
       const u32x4 d = pair_swap(gg[0], gg[1]);
@@ -1004,8 +1030,13 @@ __device__ __forceinline__ void epilogue_geglu_bwd(const P& p, f32x4 (&acc)[8][4
       for (int r = 0; r < 4; ++r) { v0[r] = acc[i][2 * jp][r] * p.alpha; v1[r] = acc[i][2 * jp + 1][r] * p.alpha; }
       float d[8], x[8], gt[8], ox[8], og[8];
       unpack8(pair_swap(v0, v1), d);
-      unpack8(hx[b][jp], x);
-      unpack8(hg[b][jp], gt);
+      if (p.h16) {   // h from the fp16 forward (wave-uniform)
+        unpack8h(hx[b][jp], x);
+        unpack8h(hg[b][jp], gt);
+      } else {
+        unpack8(hx[b][jp], x);
+        unpack8(hg[b][jp], gt);
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         ox[k] = d[k] * gelu_erf(gt[k]);
@@ -1261,6 +1292,7 @@ __device__ __forceinline__ void epilogue_ln(const P& p, f32x4 (&acc)[8][4], char
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = (keep[quarter][it][j] - f.x) * f.y * gam[j] + bet[j];
         *(u32x4*)(p.ln_y + (rbase + it * 8 + rl) * p.ln_ldy + gn) = pack8(o);
+        if (p.ln_y16) *(u32x4*)(p.ln_y16 + (rbase + it * 8 + rl) * p.ln_ldy + gn) = pack8h(o);
       }
     } else {
       // 32-bit element offsets (the host checks M * ld < 2^31); two row chunks per step (the
@@ -1385,7 +1417,7 @@ __device__ unsigned long long g_stamps[256][32][6];
 #define STAMP(k, v) do { } while (0)
 #endif
 
-template <bool AK, bool BKC, int EP>
+template <bool AK, bool BKC, int EP, bool H16 = false>
 __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
   using namespace p8;
   constexpr bool TR = EP >= 0;
@@ -1462,9 +1494,8 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
           const bf16x8 bb = ni ? b1[jj][s] : b0[jj][s];
-          acc[mi * 4 + ii][ni * 2 + jj] =
-              TR ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb, a[ii][s], acc[mi * 4 + ii][ni * 2 + jj], 0, 0, 0)
-                 : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ii][s], bb, acc[mi * 4 + ii][ni * 2 + jj], 0, 0, 0);
+          acc[mi * 4 + ii][ni * 2 + jj] = TR ? mfma16<H16>(bb, a[ii][s], acc[mi * 4 + ii][ni * 2 + jj])
+                                             : mfma16<H16>(a[ii][s], bb, acc[mi * 4 + ii][ni * 2 + jj]);
         }
     __builtin_amdgcn_s_setprio(0);
   };
@@ -1556,7 +1587,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
     } else if constexpr (EP == 2 || EP == 12) {
-      epilogue_t<2, EP == 12>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx, scr);
+      epilogue_t<2, EP == 12, H16>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx, scr);
     } else if constexpr (EP == 4) {
       epilogue_geglu_bwd(p, acc, wr, wc, lane, T.m0, T.n0, T.bidx);
     } else if constexpr (EP == 0 || EP == 10) {
@@ -1595,12 +1626,12 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
 // the chip (ctclip_gemm_set_grid_cap)
 static int g_grid_cap = 0;
 
-template <bool AK, bool BKC, int EP>
+template <bool AK, bool BKC, int EP, bool H16 = false>
 int launch8(const P& p, int batch, hipStream_t st) {
   constexpr int smem = EP == -6 || EP == -7 ? SMEM_LN : p8::SMEM_P;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<AK, BKC, EP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<AK, BKC, EP, H16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               smem);
     attr = true;
   }
@@ -1618,10 +1649,10 @@ int launch8(const P& p, int batch, hipStream_t st) {
     dim3 grid((unsigned)(ntiles < cap ? ntiles : cap));
     P q = p;
     q.pre1 = pre1;
-    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP>), grid, dim3(p8::NTH), smem, st, q);
+    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP, H16>), grid, dim3(p8::NTH), smem, st, q);
   } else {
     dim3 grid(cdiv(p.N, p8::BNN), cdiv(p.M, p8::BM), batch * p.split_k);
-    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP>), grid, dim3(p8::NTH), smem, st, p);
+    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP, H16>), grid, dim3(p8::NTH), smem, st, p);
   }
   CT_CHECK_LAUNCH();
   return 0;
@@ -1695,6 +1726,17 @@ int launch8_ep(const P& p, int batch, hipStream_t st) {
   return relay ? launch8<AK, BKC, 10>(p, batch, st) : launch8<AK, BKC, 0>(p, batch, st);
 }
 
+// fp16 operands (the 3D-ViT forward: K-contiguous A and B only): the forward epilogues -- GEGLU (h in
+// fp16), plain 16-bit / l2norm-free outputs, the LDS-staged f32 / bias / residual rows
+int launch8_h16(const P& p, int batch, hipStream_t st) {
+  if (p.split_k > 1 || p.act == 3 || p.act == 4 || p.act == 5 || p.act == 6) return CT_EINVAL;
+  const bool tr = !p.c_f32 && !p.R;
+  if (p.act == 2) return launch8<true, true, 2, true>(p, batch, st);
+  if (tr) return launch8<true, true, 0, true>(p, batch, st);
+  if (p.R && p.r_f32 && p.c_f32 && p.act == 0 && !p.accumulate) return launch8<true, true, -2, true>(p, batch, st);
+  return launch8<true, true, -1, true>(p, batch, st);
+}
+
 template <bool AK>
 int launch8_any(const P& p, bool bk, int batch, hipStream_t st) {
   return bk ? launch8_ep<AK, true>(p, batch, st) : launch8_ep<AK, false>(p, batch, st);
@@ -1718,6 +1760,8 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   p.n2 = a->n2;
   p.fold_cs = nullptr;
   p.nfold = 0;
+  p.h16 = a->ab_f16 || a->r_f16;
+  p.ln_y16 = nullptr;
   const int kstep = (variant() == 8 || a->act == 4 || a->act == 5) ? p8::BKK : BK;
   p.kper = (a->K / kstep + split - 1) / split * kstep;
   static int dbg = -1, stag = 0;
@@ -1749,6 +1793,11 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   // GEGLU GEMM now -- 0.4229 vs 0.4289 ms at the old default 4; the GEGLU backward gains ~1.5 % at 8)
   p.stagger = variant() == 8 ? (g_stagger8 >= 0 ? g_stagger8 : (a->act == 4 ? 8 : 0)) : (tile_rows() == 1 ? stag : 0);
   hipStream_t st = (hipStream_t)stream;
+  if (a->ab_f16) {
+    if (!a->a_kcontig || !a->b_kcontig) return CT_EINVAL;
+    p.stagger = 0;
+    return launch8_h16(p, batch, st);
+  }
   if (variant() == 8 || a->act == 4 || a->act == 5)
     return a->a_kcontig ? launch8_any<true>(p, a->b_kcontig, batch, st) : launch8_any<false>(p, a->b_kcontig, batch, st);
   if (tile_rows() == 2) return launch_any<2>(p, a->a_kcontig, a->b_kcontig, batch, st);
@@ -1810,8 +1859,13 @@ extern "C" int ctclip_gemm_ln(const ctclip_gemm_args* a, const ctclip_ln_epilogu
   p.status = ln->status;
   p.spin_limit = ln->spin_limit ? ln->spin_limit : LN_SPIN_LIMIT;
   p.ln_debug = ln->debug;
+  p.ln_y16 = ln->mode == 1 ? (u16*)ln->Y16 : nullptr;
   hipStream_t st = (hipStream_t)stream;
   if (!a->a_kcontig) return CT_EINVAL;
+  if (a->ab_f16) {   // fp16 operands: the forward form only, B K-contiguous
+    if (ln->mode != 1 || !a->b_kcontig) return CT_EINVAL;
+    return launch8<true, true, -6, true>(p, 1, st);
+  }
   if (ln->mode == 1) return a->b_kcontig ? launch8<true, true, -6>(p, 1, st) : launch8<true, false, -6>(p, 1, st);
   return a->b_kcontig ? launch8<true, true, -7>(p, 1, st) : launch8<true, false, -7>(p, 1, st);
 }
@@ -1858,6 +1912,7 @@ extern "C" int ctclip_gemm_qkv_lnfold(const ctclip_gemm_args* a, const float* me
   p.ln_rstd = (float*)rstd;
   p.fold_cs = fold_cs;
   p.nfold = nfold;
+  if (a->ab_f16) return launch8<true, true, 8, true>(p, 1, (hipStream_t)stream);
   return launch8<true, true, 8>(p, 1, (hipStream_t)stream);
 }
 

@@ -81,7 +81,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      float eps, u16* __restrict__ yb, int64_t ldyb,
                                                      float* __restrict__ yf, int64_t ldyf,
-                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     u16* __restrict__ yh) {
   const int lane = threadIdx.x & 63;
   const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
   float gv[CPL][8], bv[CPL][8];
@@ -121,6 +122,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (v[r][c][j] - mean) * rstd * gv[c][j] + bv[c][j];
       if (yb) *(u32x4*)(yb + row * ldyb + col) = pack8(o);
+      if (yh) *(u32x4*)(yh + row * ldyb + col) = pack8h(o);   // optional fp16 copy (ldyb)
       if (yf) {
         float* p = yf + row * ldyf + col;
         *(f32x4*)p = f32x4{o[0], o[1], o[2], o[3]};
@@ -420,13 +422,13 @@ int ln_cpl(int D) { return (D + 511) / 512; }
 template <int C, int R>
 void launch_ln_fwd(bool xf, dim3 grid, hipStream_t st, const void* x, int64_t ldx, int64_t rows, int D,
                    const float* gamma, const float* beta, float eps, u16* yb, int64_t ldyb, float* yf, int64_t ldyf,
-                   float* mean, float* rstd) {
+                   float* mean, float* rstd, u16* yh) {
   if (xf)
     hipLaunchKernelGGL((ln_fwd_kernel<C, R, true>), grid, dim3(256), 0, st, x, ldx, rows, D, gamma, beta, eps, yb,
-                       ldyb, yf, ldyf, mean, rstd);
+                       ldyb, yf, ldyf, mean, rstd, yh);
   else
     hipLaunchKernelGGL((ln_fwd_kernel<C, R, false>), grid, dim3(256), 0, st, x, ldx, rows, D, gamma, beta, eps, yb,
-                       ldyb, yf, ldyf, mean, rstd);
+                       ldyb, yf, ldyf, mean, rstd, yh);
 }
 
 template <int C>
@@ -448,19 +450,27 @@ void launch_ln_bwd(bool dyf, bool xf, dim3 grid, hipStream_t st, const void* dy,
 extern "C" int ctclip_layernorm_fwd(const void* x, int32_t x_f32, int64_t ldx, int64_t rows, int32_t D,
                                     const float* gamma, const float* beta, float eps, void* y_bf16, int64_t ldyb,
                                     float* y_f32, int64_t ldyf, float* mean, float* rstd, void* stream) {
+  return ctclip_layernorm_fwd_x2(x, x_f32, ldx, rows, D, gamma, beta, eps, y_bf16, nullptr, ldyb, y_f32, ldyf, mean,
+                                 rstd, stream);
+}
+
+extern "C" int ctclip_layernorm_fwd_x2(const void* x, int32_t x_f32, int64_t ldx, int64_t rows, int32_t D,
+                                       const float* gamma, const float* beta, float eps, void* y_bf16, void* y_f16,
+                                       int64_t ldyb, float* y_f32, int64_t ldyf, float* mean, float* rstd,
+                                       void* stream) {
   if (rows == 0) return 0;
   CT_REQUIRE(D % 8 == 0 && ldx % 8 == 0, CT_EALIGN);
   const int cpl = ln_cpl(D);
   hipStream_t st = (hipStream_t)stream;
   if (cpl == 1)
     launch_ln_fwd<1, 4>(x_f32, dim3(cdiv(rows, 16)), st, x, ldx, rows, D, gamma, beta, eps, (u16*)y_bf16, ldyb,
-                        y_f32, ldyf, mean, rstd);
+                        y_f32, ldyf, mean, rstd, (u16*)y_f16);
   else if (cpl == 2)
     launch_ln_fwd<2, 2>(x_f32, dim3(cdiv(rows, 8)), st, x, ldx, rows, D, gamma, beta, eps, (u16*)y_bf16, ldyb,
-                        y_f32, ldyf, mean, rstd);
+                        y_f32, ldyf, mean, rstd, (u16*)y_f16);
   else if (cpl <= 8)
     launch_ln_fwd<8, 1>(x_f32, dim3(cdiv(rows, 4)), st, x, ldx, rows, D, gamma, beta, eps, (u16*)y_bf16, ldyb,
-                        y_f32, ldyf, mean, rstd);
+                        y_f32, ldyf, mean, rstd, (u16*)y_f16);
   else
     return CT_ESHAPE;
   CT_CHECK_LAUNCH();
@@ -690,6 +700,42 @@ __global__ __launch_bounds__(256) void ln_stats_merge_kernel(const float2* __res
   rstd[row] = rsqrtf(m2 * (1.f / D) + eps);
 }
 
+// fp16 form of the fold's B operand (the fp16 forward GEMM, round 5): rows < nq = f16(Wq o gamma) with
+// cs[n] = the row sums of those f16 values, rows >= nq = f16 of the f32 rows of Wr.  Same summation
+// order as pack_qkv_fold_kernel.
+__global__ __launch_bounds__(64) void pack_qkv_fold_h16_kernel(const float* __restrict__ Wq, int64_t ldq,
+                                                               const float* __restrict__ gamma, int64_t K, int64_t nq,
+                                                               const float* __restrict__ Wr, int64_t ldr,
+                                                               u16* __restrict__ out, int64_t ldo,
+                                                               float* __restrict__ cs) {
+  const int64_t n = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (n >= nq) {
+    for (int64_t c = lane * 8; c < K; c += 512) {
+      const f32x4 a = *(const f32x4*)(Wr + (n - nq) * ldr + c), b = *(const f32x4*)(Wr + (n - nq) * ldr + c + 4);
+      const float w[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+      *(u32x4*)(out + n * ldo + c) = pack8h(w);
+    }
+    return;
+  }
+  float s = 0.f;
+  for (int64_t c = lane * 8; c < K; c += 512) {
+    float w[8];
+    const f32x4 a = *(const f32x4*)(Wq + n * ldq + c), b = *(const f32x4*)(Wq + n * ldq + c + 4);
+    const f32x4 ga = *(const f32x4*)(gamma + c), gb = *(const f32x4*)(gamma + c + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { w[j] = a[j] * ga[j]; w[4 + j] = b[j] * gb[j]; }
+    const u32x4 pk = pack8h(w);
+    *(u32x4*)(out + n * ldo + c) = pk;
+    float r[8];
+    unpack8h(pk, r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += r[j];
+  }
+  s = warp_sum(s);
+  if (lane == 0) cs[n] = s;
+}
+
 // Weight gradients of the folded LayerNorm + projections, from G = [dq2 | dkv]^T x (one GEMM over
 // the Q | K | V rows) and u = dq2^T mean (ctclip_l2norm_scale_bwd_fold), dq2 = dq o rstd:
 //   rows n < nq:  grad_q[n][k] += gamma[k] (G[n][k] - u[n])        (dWq = dq^T LN(x))
@@ -788,7 +834,7 @@ extern "C" int ctclip_l2norm_qk_bwd_fold(const void* x, int64_t ldx, const void*
 extern "C" int ctclip_ln_stats_merge(const float* part, int32_t ngroups, int64_t rows, int32_t D, float eps,
                                      float* mean, float* rstd, void* stream) {
   if (rows == 0) return 0;
-  CT_REQUIRE(ngroups >= 1 && ngroups <= 16 && D % ngroups == 0 && part && mean && rstd, CT_EINVAL);
+  CT_REQUIRE(ngroups >= 1 && ngroups <= 32 && D % ngroups == 0 && part && mean && rstd, CT_EINVAL);
   hipLaunchKernelGGL(ln_stats_merge_kernel, dim3(cdiv(rows, 256)), dim3(256), 0, (hipStream_t)stream,
                      (const float2*)part, ngroups, rows, D, eps, mean, rstd);
   CT_CHECK_LAUNCH();
@@ -822,6 +868,19 @@ extern "C" int ctclip_pack_qkv_fold(const float* Wq, int64_t ldq, const float* g
   CT_REQUIRE(!s_out || (s_fold && s_rest && ns > 0 && ns <= 64), CT_EINVAL);
   hipLaunchKernelGGL(pack_qkv_fold_kernel, dim3(nq + nrest), dim3(64), 0, (hipStream_t)stream, Wq, ldq, gamma, K, nq,
                      (const u16*)Wrest, ldr, (u16*)out, ldo, cs, s_fold, s_rest, ns, s_out);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_pack_qkv_fold_h16(const float* Wq, int64_t ldq, const float* gamma, int64_t nq, int64_t K,
+                                        const float* Wrest, int64_t ldr, int64_t nrest, void* out, int64_t ldo,
+                                        float* cs, void* stream) {
+  if (nq + nrest == 0) return 0;
+  CT_REQUIRE(K % 8 == 0 && ldq % 4 == 0 && ldr % 4 == 0 && ldo % 8 == 0 && aligned16(Wq) && aligned16(gamma) &&
+                 aligned16(out) && (nrest == 0 || aligned16(Wrest)),
+             CT_EALIGN);
+  hipLaunchKernelGGL(pack_qkv_fold_h16_kernel, dim3(nq + nrest), dim3(64), 0, (hipStream_t)stream, Wq, ldq, gamma, K,
+                     nq, Wrest, ldr, (u16*)out, ldo, cs);
   CT_CHECK_LAUNCH();
   return 0;
 }

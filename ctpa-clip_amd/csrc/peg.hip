@@ -8,6 +8,8 @@
 //     reference's physical row p = (h*W + w)*T + t  ->  canonical row t*H*W + h*W + w.
 //   Both index maps are integer-exact; tests/test_gpu_ops.py checks them against the oracle.
 // out(v) = x(v) + bias + sum_{kt,kh,kw} w[c][kt][kh][kw] * x(v + (kt-2, kh-1, kw-1)), zero outside.
+#include <type_traits>
+
 #include "common.h"
 #include "../../include/ctclip_hip.h"
 
@@ -411,6 +413,234 @@ __global__ __launch_bounds__(TNTH) void peg_tile_kernel(const u16* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Forward from the f32 residual stream (round 5, the default forward).  The bf16 kernel above
+// reads the conv taps from the layer input's bf16 shadow: every PEG output then carries that
+// shadow's 2^-9 rounding, ~22 % of the bf16 tower's squared pre-VQ token error
+// (tools/vit_precision.py: the 'xb' site alone 4.8e-3 of the 1.0e-2 median).  Here the LDS planes
+// hold the f32 tokens, 32 channels per workgroup (128 B per plane position, as the bf16 kernel's 64
+// channels), 4 channels per thread, and the residual is the centre tap of the plane (no separate
+// residual read: HBM reads per launch 113 + 226 MB -> 226 MB at B = 8).
+// Walk: each plane is read from LDS ONCE and scattered into the three outputs it feeds.  A plane p
+// along the walk axis contributes tap a (kt) to output t = p + 2 - lead - a, so three rolling
+// accumulator sets (t mod 3) collect an output over three steps and output p - lead is complete
+// after plane p.  Only one plane is live in LDS (plus the next one landing): a 2-slot ring, one
+// barrier per step, and a 4-row tile (halo 1.5x instead of 2x) in 43.5 KB -> 3 workgroups of 256
+// threads per CU, the base grid (8 x 6 x 16 = 768 workgroups) resident in one round.
+// Outputs: f32, bf16 shadow, optional f16 copy (a 16-bit MFMA A operand) and optional (mean, M2)
+// per 32-channel group (D / 32 groups, ctclip_ln_stats_merge).
+#ifndef CTCLIP_PEGX_WAVES
+#define CTCLIP_PEGX_WAVES 1   // launch-bounds occupancy floor (waves per SIMD): 1 = the compiler's choice
+#endif
+constexpr int XC = 32;             // channels per workgroup
+constexpr int XHT = 4;             // output rows per workgroup
+constexpr int XNT = 256;           // threads: XHT x ceil(W / SEG) x 8 chunks of 4 channels
+constexpr int XPCH = 1280;         // 16-B chunks a plane may hold: (XHT + 2) x (W + 2) x 8
+constexpr int XNLD = XPCH / XNT;   // plane loads per thread
+__host__ __device__ inline int xplane_bytes(int W) { return (XHT + 2) * (W + 2) * 128; }
+
+__device__ __forceinline__ unsigned xplane_load(const float* __restrict__ x, const Geo& g, int D, int b, int h0,
+                                                int c0, int tp, u32x4 (&reg)[XNLD], int hoff) {
+  const int nl = (XHT + 2) * (g.W + 2) * 8;
+  unsigned valid = 0u;
+#pragma unroll
+  for (int m = 0; m < XNLD; ++m) {
+    const int i = threadIdx.x + m * XNT;
+    const int k = i & 7, cw = (i >> 3) % (g.W + 2), hr = (i >> 3) / (g.W + 2);
+    const int h = h0 - hoff + hr, w = cw - 1;
+    const bool ok = i < nl && h >= 0 && h < g.H && w >= 0 && w < g.W;
+    const int64_t row = ok ? (int64_t)canon(g, b, (tp * g.H + h) * g.W + w) : 0;
+    reg[m] = *(const u32x4*)(x + row * D + c0 + k * 4);
+    valid |= (unsigned)ok << m;
+  }
+  return valid;
+}
+
+__device__ __forceinline__ void xplane_store(char* dst, int W, const u32x4 (&reg)[XNLD], unsigned valid) {
+  const int nl = (XHT + 2) * (W + 2) * 8;
+#pragma unroll
+  for (int m = 0; m < XNLD; ++m) {
+    const int i = threadIdx.x + m * XNT;
+    if (i < nl) *(u32x4*)(dst + i * 16) = ((valid >> m) & 1) ? reg[m] : u32x4{0u, 0u, 0u, 0u};
+  }
+}
+
+template <int GK = 0, int MD = 0>
+__global__ __launch_bounds__(XNT, CTCLIP_PEGX_WAVES) void peg_fwd32_kernel(const float* __restrict__ xin, int D,
+                                                        const float* __restrict__ w, const float* __restrict__ bias,
+                                                        Geo g, float* __restrict__ out, u16* __restrict__ outb,
+                                                        u16* __restrict__ outh, float* __restrict__ stats) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  fix_geo<GK, MD>(g);
+  const int nht = (g.H + XHT - 1) / XHT;
+  const int b = blockIdx.x / nht, h0 = (blockIdx.x - b * nht) * XHT, c0 = blockIdx.y * XC;
+  const int pb = xplane_bytes(g.W);
+  float* ws = (float*)(smem + 2 * pb);   // [27][XC]
+  float* bs = ws + 27 * XC;
+  for (int i = threadIdx.x; i < 27 * XC; i += XNT) {
+    const int c = i / 27, tap = i - c * 27;
+    ws[tap * XC + c] = w[(int64_t)(c0 + c) * 27 + tap];
+  }
+  if (threadIdx.x < XC) bs[threadIdx.x] = bias ? bias[c0 + threadIdx.x] : 0.f;
+  using TP = Taps<MD, 0>;
+  constexpr int lead = TP::lead, hoff = TP::hoff;
+  u32x4 reg[XNLD];
+  {
+    const unsigned v = xplane_load(xin, g, D, b, h0, c0, 0, reg, hoff);
+    xplane_store(smem, g.W, reg, v);
+  }
+  __syncthreads();
+  const int ns = (g.W + SEG - 1) / SEG;
+  const int o = threadIdx.x;
+  const int ch = o & 7, s = (o >> 3) % ns, r = (o >> 3) / ns;
+  const int h = h0 + r, w0 = s * SEG;
+  const bool active = o < XHT * ns * 8 && h < g.H;
+  // three rolling accumulator sets, indexed by t mod 3 -- compile-time indices: the walk is unrolled
+  // by three (step<P3> handles planes p = P3 mod 3), so no set is ever selected at run time (which
+  // would put the arrays in scratch).  The residual of output t is plane t's centre row, still in LDS
+  // when t completes (plane t + lead is the newest; plane t + 1 overwrites slot t & 1 only after
+  // the finalize)
+  float acc[3][SEG][4];
+#pragma unroll
+  for (int u = 0; u < 3; ++u)
+#pragma unroll
+    for (int j = 0; j < SEG; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[u][j][e] = bs[ch * 4 + e];
+  const int nsteps = g.T + lead;
+  // step p: plane p (p < T) sits in LDS slot p & 1; output p - lead completes
+  auto step = [&](auto p3c, int p) {
+    constexpr int P3 = decltype(p3c)::value;
+    const bool have = p < g.T;
+    // next plane into registers (always issued, clamped: no branch merges `reg`)
+    const unsigned nvalid = xplane_load(xin, g, D, b, h0, c0, min(p + 1, g.T - 1), reg, hoff);
+    if (active && have) {
+      const char* pl = smem + (p & 1) * pb;
+#pragma unroll 1
+      for (int kh = 0; kh < 3; ++kh) {
+        const int lr = r + TP::dh(kh) + hoff;
+        float xv[SEG + 2][4];
+#pragma unroll
+        for (int q = 0; q < SEG + 2; ++q) {
+          const int cw = min(w0 + q, g.W + 1);
+          const f32x4 v = *(const f32x4*)(pl + ((lr * (g.W + 2) + cw) * 8 + ch) * 16);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) xv[q][e] = v[e];
+        }
+#pragma unroll
+        for (int kt = 0; kt < 3; ++kt) {
+          const int t = p + 2 - lead - kt;       // the output this tap of plane p feeds
+          if (t < 0 || t >= g.T) continue;
+          const int u = (P3 + 2 - lead - kt + 3) % 3;   // compile-time after the unroll
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const f32x4 wv = *(const f32x4*)(ws + TP::tap(kt, kh, kw) * XC + ch * 4);
+#pragma unroll
+            for (int j = 0; j < SEG; ++j)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) acc[u][j][e] += wv[e] * xv[j + kw][e];
+          }
+        }
+      }
+    }
+    const int tf = p - lead;   // the output completed by plane p
+    if (active && tf >= 0) {
+      constexpr int uf = (P3 - lead + 3) % 3;   // t mod 3 of that output
+      const char* rp = smem + (tf & 1) * pb + (((r + hoff) * (g.W + 2) + w0 + 1) * 8 + ch) * 16;   // centre row
+#pragma unroll
+      for (int j = 0; j < SEG; ++j) {
+        const int wq = w0 + j;
+        const f32x4 xr = *(const f32x4*)(rp + j * 128);   // (columns past W read padding; unused)
+        float v4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v4[e] = acc[uf][j][e] + xr[e];
+          acc[uf][j][e] = bs[ch * 4 + e];
+        }
+        if (wq < g.W) {
+          const int64_t orow = canon(g, b, (tf * g.H + h) * g.W + wq);
+          const int64_t co = orow * D + c0 + ch * 4;
+          *(f32x4*)(out + co) = f32x4{v4[0], v4[1], v4[2], v4[3]};
+          if (outb) *(uint2*)(outb + co) = pack4(v4);
+          if (outh) *(uint2*)(outh + co) = make_uint2(pack2h(v4[0], v4[1]), pack2h(v4[2], v4[3]));
+        }
+        if (stats) {
+          // the output row's (mean, M2) over this workgroup's 32 channels (two-pass over the 8 lanes
+          // ch = 0..7 of the token), merged over the D / 32 groups by ctclip_ln_stats_merge
+          float sm = v4[0] + v4[1] + v4[2] + v4[3];
+          sm += __shfl_xor(sm, 1, 64);
+          sm += __shfl_xor(sm, 2, 64);
+          sm += __shfl_xor(sm, 4, 64);
+          const float mu = sm * (1.f / XC);
+          float m2 = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float d = v4[e] - mu;
+            m2 = fmaf(d, d, m2);
+          }
+          m2 += __shfl_xor(m2, 1, 64);
+          m2 += __shfl_xor(m2, 2, 64);
+          m2 += __shfl_xor(m2, 4, 64);
+          if (ch == 0 && wq < g.W) {
+            const int64_t ntok = (int64_t)(gridDim.x / nht) * g.thw;
+            const int64_t orow = canon(g, b, (tf * g.H + h) * g.W + wq);
+            *(float2*)(stats + ((int64_t)blockIdx.y * ntok + orow) * 2) = make_float2(mu, m2);
+          }
+        }
+      }
+    }
+    // slot (p + 1) & 1 was last read in step p - 1, before the barrier that ended it: one barrier
+    // per step (after the store) orders the new plane before its reads
+    if (p + 1 < g.T) xplane_store(smem + ((p + 1) & 1) * pb, g.W, reg, nvalid);
+    __syncthreads();
+  };
+  for (int p = 0; p < nsteps; p += 3) {
+    step(std::integral_constant<int, 0>{}, p);
+    if (p + 1 < nsteps) step(std::integral_constant<int, 1>{}, p + 1);
+    if (p + 2 < nsteps) step(std::integral_constant<int, 2>{}, p + 2);
+  }
+}
+
+// any geometry / width (D % 4 == 0): one thread per (token, 4 channels), taps from global memory
+__global__ __launch_bounds__(256) void peg_fwd32_naive_kernel(const float* __restrict__ xin, int64_t ntok, int D,
+                                                              const float* __restrict__ w,
+                                                              const float* __restrict__ bias, Geo g,
+                                                              float* __restrict__ out, u16* __restrict__ outb,
+                                                              u16* __restrict__ outh) {
+  const int nc = D / 4;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= ntok * nc) return;
+  const int v = (int)(i / nc), col = (int)(i - (int64_t)v * nc) * 4;
+  const int b = v / g.thw, p = v - b * g.thw;
+  const int hwq = p / g.W, wq = p - hwq * g.W, tq = hwq / g.H, hq = hwq - tq * g.H;
+  float acc[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) acc[e] = bias ? bias[col + e] : 0.f;
+  for (int kt = 0; kt < 3; ++kt) {
+    const int tt = tq + kt - 2;
+    if (tt < 0 || tt >= g.T) continue;
+    for (int kh = 0; kh < 3; ++kh) {
+      const int hh = hq + kh - 1;
+      if (hh < 0 || hh >= g.H) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int ww = wq + kw - 1;
+        if (ww < 0 || ww >= g.W) continue;
+        const f32x4 x = *(const f32x4*)(xin + (int64_t)canon(g, b, (tt * g.H + hh) * g.W + ww) * D + col);
+        const int tap = (kt * 3 + kh) * 3 + kw;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] += w[(int64_t)(col + e) * 27 + tap] * x[e];
+      }
+    }
+  }
+  const int64_t co = (int64_t)canon(g, b, p) * D + col;
+  const f32x4 rx = *(const f32x4*)(xin + co);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) acc[e] += rx[e];
+  *(f32x4*)(out + co) = f32x4{acc[0], acc[1], acc[2], acc[3]};
+  if (outb) *(uint2*)(outb + co) = pack4(acc);
+  if (outh) *(uint2*)(outh + co) = make_uint2(pack2h(acc[0], acc[1]), pack2h(acc[2], acc[3]));
+}
+
 // weight/bias gradient: grid (B * ceil(H/HT), D/64), WNTH threads; thread = (row, w-segment of
 // SEGW, channel pair); part[blockIdx.x][c][28] (27 taps in (kt,kh,kw) order, then bias).
 // Channel pairs keep the 27 x 2 accumulators + windows under 128 VGPRs (4 waves/SIMD).
@@ -637,6 +867,48 @@ extern "C" int ctclip_peg_fwd_stats(const void* x_bf16, const float* x_f32, int6
     dim3 grid(cdiv(ntok, 32), cdiv(D, 64));
     hipLaunchKernelGGL(peg_kernel<0>, grid, dim3(256), 0, (hipStream_t)stream, (const u16*)x_bf16, ntok, D, weight,
                        bias, x_f32, g, out_f32, (u16*)out_bf16);
+  }
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_peg_fwd_x32(const float* x_f32, int64_t B, int32_t T, int32_t H, int32_t W, int32_t D,
+                                  const float* weight, const float* bias, int32_t mode, float* out_f32, void* out_bf16,
+                                  void* out_f16, float* stats, void* stream) {
+  CT_REQUIRE(D % 4 == 0 && x_f32 && out_f32 && aligned16(x_f32) && aligned16(out_f32), CT_EALIGN);
+  Geo g{T, H, W, T * H * W, mode};
+  const int64_t ntok = B * g.thw;
+  if (ntok == 0) return 0;
+  const bool tiled = D % XC == 0 && XHT * ((W + SEG - 1) / SEG) * 8 <= XNT && (XHT + 2) * (W + 2) * 8 <= XPCH;
+  if (stats) CT_REQUIRE(tiled && (((uintptr_t)stats) & 7) == 0, CT_EINVAL);
+  const hipStream_t st = (hipStream_t)stream;
+  if (tiled) {
+    static bool attr = false;
+    const size_t smem = (size_t)2 * xplane_bytes(W) + (27 * XC + XC) * 4;
+    if (!attr) {
+      const void* ks[] = {(const void*)peg_fwd32_kernel<>, (const void*)peg_fwd32_kernel<24, 0>,
+                          (const void*)peg_fwd32_kernel<24, 1>, (const void*)peg_fwd32_kernel<24, 2>};
+      for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      attr = true;
+    }
+    dim3 grid(B * ((H + XHT - 1) / XHT), D / XC);
+    const auto ob = (u16*)out_bf16;
+    const auto oh = (u16*)out_f16;
+    if (fixed24(g) && g.mode == 0)
+      hipLaunchKernelGGL((peg_fwd32_kernel<24, 0>), grid, dim3(XNT), smem, st, x_f32, D, weight, bias, g, out_f32, ob,
+                         oh, stats);
+    else if (fixed24(g) && canon1())
+      hipLaunchKernelGGL((peg_fwd32_kernel<24, 2>), grid, dim3(XNT), smem, st, x_f32, D, weight, bias, g, out_f32, ob,
+                         oh, stats);
+    else if (fixed24(g))
+      hipLaunchKernelGGL((peg_fwd32_kernel<24, 1>), grid, dim3(XNT), smem, st, x_f32, D, weight, bias, g, out_f32, ob,
+                         oh, stats);
+    else
+      hipLaunchKernelGGL((peg_fwd32_kernel<>), grid, dim3(XNT), smem, st, x_f32, D, weight, bias, g, out_f32, ob, oh,
+                         stats);
+  } else {
+    hipLaunchKernelGGL(peg_fwd32_naive_kernel, dim3(cdiv(ntok * (D / 4), 256)), dim3(256), 0, st, x_f32, ntok, D,
+                       weight, bias, g, out_f32, (u16*)out_bf16, (u16*)out_f16);
   }
   CT_CHECK_LAUNCH();
   return 0;

@@ -125,8 +125,14 @@ __global__ __launch_bounds__(256) void vq_select_kernel(const float2* __restrict
     }
   }
   // a row without any finite score (NaN / inf tokens) keeps bi = INT_MAX: clamp it into the
-  // codebook so no consumer (pool, gather, EMA statistics) reads outside it
-  if (lane == 0) idx_out[row] = (unsigned)bi < (unsigned)C ? bi : 0;
+  // codebook so no consumer (pool, gather, EMA statistics) reads outside it, and zero its
+  // normalised row so the EMA statistics take no direction from it (a NaN row would otherwise
+  // reach vq_ema_accum's float -> int64 conversion and corrupt code 0's running mean for good;
+  // the non-finite loss of such a step is what surfaces the problem)
+  const bool bad = (unsigned)bi >= (unsigned)C;   // wave-uniform
+  if (lane == 0) idx_out[row] = bad ? 0 : bi;
+  if (bad && xn_out)
+    for (int c = lane; c < D; c += 64) xn_out[row * D + c] = 0.f;
 }
 
 // pooled[b][hw][d] = (1/T) sum_t cb[idx[b][t*HW + hw]][d]

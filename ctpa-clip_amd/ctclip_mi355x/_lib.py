@@ -44,6 +44,8 @@ class GemmArgs(ctypes.Structure):
         ('sA', c_i64), ('sB', c_i64), ('sC', c_i64), ('sC2', c_i64), ('sR', c_i64),
         ('n2', c_i32),
         ('B2', c_vp),
+        ('ab_f16', c_i32),
+        ('r_f16', c_i32),
     ]
 
 
@@ -59,6 +61,7 @@ class LnEpilogueArgs(ctypes.Structure):
         ('xchg', c_vp), ('epoch', ctypes.c_uint32),
         ('status', c_vp),
         ('spin_limit', ctypes.c_uint32), ('debug', c_i32),
+        ('Y16', c_vp),
     ]
 
 
@@ -86,6 +89,7 @@ class AttnArgs(ctypes.Structure):
         ('s_outer', c_i64), ('s_inner', c_i64), ('s_pos', c_i64),
         ('dropout_p', c_f32), ('dropout_seed', ctypes.c_uint64),
         ('dbias_ws', c_vp), ('dbias_ws_floats', c_i64),
+        ('o16', c_vp),
     ]
 
 
@@ -145,6 +149,14 @@ _SIGS = {
                                     c_vp],
     'ctclip_layernorm_bwd_drop': [c_vp, c_i32, c_i64, c_vp, c_i32, c_i64, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_i64,
                                   c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_f32, ctypes.c_uint64, c_vp],
+    'ctclip_patch_ln_x2': [c_vp, c_i32, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp,
+                           c_vp, c_i64, c_vp],
+    'ctclip_layernorm_fwd_x2': [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_i64, c_vp, c_i64,
+                                c_vp, c_vp, c_vp],
+    'ctclip_pack_rows_h16': [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp],
+    'ctclip_pack_qkv_fold_h16': [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp],
+    'ctclip_skinny_gemm_slices': [c_i64, c_i64, c_i64],
+    'ctclip_skinny_gemm': [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp],
     'ctclip_reduce_slabs': [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp],
     'ctclip_reduce_slabs_multi': [ctypes.POINTER(SlabJob), c_i32, c_vp],
     'ctclip_layernorm_fwd': [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_f32, c_vp, c_i64, c_vp, c_i64,
@@ -174,6 +186,7 @@ _SIGS = {
     'ctclip_peg_fwd': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp],
     'ctclip_peg_fwd_stats': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp,
                              c_vp],
+    'ctclip_peg_fwd_x32': [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
     'ctclip_peg_bwd_data': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp],
     'ctclip_peg_bwd_weight': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp],
     'ctclip_peg_wgrad_reduce': [c_vp, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp],

@@ -85,10 +85,15 @@ class CTCLIP(nn.Module):
 
     def state_dict(self, *args, **kwargs):
         """The reference key layout; a text-tower Adam the trainer deferred to the next step
-        (CTClipTrainer(defer_text_adam=True)) is queued first, so the weights read are current."""
+        (CTClipTrainer(defer_text_adam=True)) is queued first, and the caller's stream is ordered
+        after the text stream (BERT's Adam) and the auxiliary stream (the codebook EMA), so the
+        tensors returned -- and any copy of them queued on the current stream, e.g. torch.save --
+        hold the updated weights."""
         for p in self.text_transformer.parameters():
             if p.is_cuda:
                 streams.flush_text(p.device)
+                streams.join_text(p.device)
+                streams.join_aux(p.device)
             break
         return super().state_dict(*args, **kwargs)
 

@@ -136,7 +136,7 @@ class CTViT(nn.Module):
             with torch.cuda.stream(aux):
                 bias_u = self.spatial_rel_pos_bias(hg, wg)
                 # the layers' packed FeedForward weights too (16 small launches off the main stream)
-                packs = Fn.prepack_ff(self._ff_weights()) if _PREPACK_AUX else []
+                packs = Fn.prepack_ff(self._ff_weights(), self._out_weights()) if _PREPACK_AUX else []
                 cpb_ev = aux.record_event()
             bias_u.record_stream(main)
             for t in packs:
@@ -173,6 +173,10 @@ class CTViT(nn.Module):
         if trace is not None:
             trace['spatial_out'], trace['temporal_out'] = xf, zf
         return zf, zb, g_sp
+
+    def _out_weights(self):
+        return [attn.to_out.weight for tr in (self.enc_spatial_transformer, self.enc_temporal_transformer)
+                for (_, attn, _, _) in tr.layers]
 
     def _ff_weights(self):
         return [(ff[1].weight, ff[4].weight) for tr in (self.enc_spatial_transformer, self.enc_temporal_transformer)

@@ -151,9 +151,28 @@ def pack_ff2(W2):
     return K.pack_rows(W2, W2.shape[0], ff_pad(W2.shape[1]))
 
 
-def prepack_ff(pairs):
+def pack_ff1_h16(W1):
+    """fp16 image of the GEGLU-interleaved W1 (the fp16 forward FF1 GEMM; pack_ff1 layout)."""
+    hit = _PREPACKED.get(_pack_key('ff1h', W1))
+    if hit is not None:
+        return hit
+    inner = W1.shape[0] // 2
+    P = ff_pad(inner)
+    return K.pack_rows_h16(W1, 2 * P, W1.shape[1], rowmap=ff1_rowmap(inner, W1.device))
+
+
+def h16(W):
+    """fp16 copy of an f32 weight (the fp16 forward GEMMs), cached by prepack_ff."""
+    hit = _PREPACKED.get(_pack_key('h16', W))
+    if hit is not None:
+        return hit
+    return K.pack_rows_h16(W, W.shape[0], W.shape[1])
+
+
+def prepack_ff(pairs, wo=()):
     """Pack every layer's FeedForward weights now (on the caller's current stream) for the layers
-    that run later (pack_ff1 / pack_ff2 then return these); returns the packed tensors."""
+    that run later (pack_ff1 / pack_ff2 then return these) -- with the fp16 forward also the fp16 W1
+    images and the attention output weights `wo`; returns the packed tensors."""
     _PREPACKED.clear()
     out = []
     for W1, W2 in pairs:
@@ -161,6 +180,15 @@ def prepack_ff(pairs):
         _PREPACKED[_pack_key('ff1', W1)] = a
         _PREPACKED[_pack_key('ff2', W2)] = b
         out += [a, b]
+        if vit_f16():
+            c = pack_ff1_h16(W1)
+            _PREPACKED[_pack_key('ff1h', W1)] = c
+            out.append(c)
+    if vit_f16():
+        for W in wo:
+            c = h16(W)
+            _PREPACKED[_pack_key('h16', W)] = c
+            out.append(c)
     return out
 
 
@@ -244,6 +272,33 @@ _LN1_FOLD = os.environ.get('CTCLIP_LN1_FOLD', '1') != '0'
 # fold backward: the q and k l2norm backwards as one pass (ctclip_l2norm_qk_bwd_fold); 0 = two (A/B)
 _QK_BWD_MERGED = os.environ.get('CTCLIP_QK_BWD_MERGED', '1') != '0'
 _QKV_WGRAD = os.environ.get('CTCLIP_QKV_WGRAD', '1') != '0'   # A/B switch of BERT's merged q/k/v wgrad
+# PEG forward taps from the f32 residual stream instead of its bf16 shadow (ctclip_peg_fwd_x32, round 5:
+# the shadow's rounding was ~22 % of the bf16 tower's squared pre-VQ error, tools/vit_precision.py);
+# CTCLIP_PEG_X32=0: the bf16-tap kernel (A/B)
+_PEG_X32 = os.environ.get('CTCLIP_PEG_X32', '1') != '0'
+# The 3D-ViT forward GEMMs -- patch embedding, the LayerNorm-folded Q | K | V projection, to_out (+ the
+# FeedForward LayerNorm) and FF1 -- on fp16 operands (round 5): fp16 has 3 more mantissa bits than
+# bf16 at the same MFMA rate, and these operands (LayerNorm outputs, the residual stream, unit-norm
+# attention outputs, weights ~1e-2) sit well inside its range.  The producers write an fp16 copy beside
+# the bf16 tensor the backward reads (the backward stays bf16); FF1's h is stored in fp16 (the GEGLU
+# backward reads it).  tools/vit_precision.py: pre-VQ token error 1.05e-2 -> ~4e-3 with the f32-tap
+# PEG.  CTCLIP_VIT_F16=0: the bf16 forward (A/B).
+_VIT_F16 = {'on': os.environ.get('CTCLIP_VIT_F16', '1') != '0'}
+
+
+def vit_f16():
+    return _VIT_F16['on']
+
+
+def set_vit_f16(on):
+    """Switch the fp16 forward GEMMs of the 3D-ViT on / off; returns the previous setting."""
+    old = _VIT_F16['on']
+    _VIT_F16['on'] = bool(on)
+    return old
+
+
+# image projection forward on the skinny streaming GEMM (ctclip_skinny_gemm); 0 = split-K tile (A/B)
+_SKINNY_PROJ = os.environ.get('CTCLIP_SKINNY_PROJ', '1') != '0'
 
 
 def set_vit_fp8(on):
@@ -309,7 +364,10 @@ class PatchEmbedFn(torch.autograd.Function):
     def forward(ctx, video, ln1_w, ln1_b, W, b, ln2_w, ln2_b, PT, P, is_hu, offs):
         pd = W.shape[1]
         kp = (pd + 63) // 64 * 64                                      # K padded to the 64-deep GEMM step
-        xhat_p = K.patch_ln(video, is_hu, PT, P, offs, ld=kp)          # [M, kp] bf16, zero pad columns
+        f16 = vit_f16() and not precise_f32() and not vit_fp8()
+        xhat_p = K.patch_ln(video, is_hu, PT, P, offs, ld=kp, want_f16=f16)   # [M, kp], zero pad columns
+        if f16:
+            xhat_p, xhat16 = xhat_p      # bf16 (the weight gradient's operand) and fp16 (the GEMM's)
         xhat = xhat_p[:, :pd]
         if precise_f32():
             # f32 tower: LayerNorm(4000) with its affine, then the Linear, both exact f32
@@ -318,9 +376,14 @@ class PatchEmbedFn(torch.autograd.Function):
             y1, _ = K.linear_f32(xn0, W.detach(), bias=b.detach())
             del xn0
         else:
-            Wp = K.pack_rows(W, W.shape[0], kp, colscale=ln1_w)        # bf16 [D, kp], zero pad columns
             bp = K.slinear(ln1_b.view(1, -1), W, bias=b).view(-1)      # f32 [D]
-            y1 = K.linear(xhat_p, Wp, bias=bp, out_dtype=F32)           # [M, D]
+            if f16:
+                Wp = K.pack_rows_h16(W, W.shape[0], kp, colscale=ln1_w)   # fp16 [D, kp], zero pad columns
+                y1 = K.linear(xhat16, Wp, bias=bp, out_dtype=F32)
+                del xhat16
+            else:
+                Wp = K.pack_rows(W, W.shape[0], kp, colscale=ln1_w)    # bf16 [D, kp], zero pad columns
+                y1 = K.linear(xhat_p, Wp, bias=bp, out_dtype=F32)       # [M, D]
         yb, yf, mean, rstd = K.layernorm_fwd(y1, ln2_w, ln2_b, 1e-5, out_bf16=True, out_f32=True)
         ctx.save_for_backward(xhat, y1, mean, rstd, ln1_w, ln1_b, W, ln2_w)
         ctx.b, ctx.ln2_w, ctx.ln2_b = b, ln2_w, ln2_b
@@ -480,17 +543,32 @@ class ViTLayerFn(torch.autograd.Function):
         Wq_b, Wkv_b, Wo_b = bf(Wq), bf(Wkv), bf(Wo)
         fp8 = vit_fp8()
         dim = xb.shape[1]
-        fold = (_LN1_FOLD and not fp8 and _L2N_FUSED and dh == 32 and inner % 256 == 0 and dim % 64 == 0
-                and geo.Wg <= 24 and Wkv.shape[0] == 2 * inner)
-        if fold:
+        # the merged q | k l2norm backward of the fold (kernels.l2norm_qk_bwd_fold) is built for
+        # exactly 256 q columns, the statistics merge (ctclip_ln_stats_merge) for <= 16 64-channel
+        # groups: other widths run the unfolded LayerNorm + projections
+        fold = (_LN1_FOLD and not fp8 and _L2N_FUSED and dh == 32 and inner == 256 and dim % 64 == 0
+                and dim <= 1024 and geo.Wg <= 24 and Wkv.shape[0] == 2 * inner)
+        # fp16 forward GEMMs (vit_f16): the folded Q | K | V projection, to_out, FF1
+        f16 = vit_f16() and fold and _PEG_X32
+        if _PEG_X32:
+            x1f, x1b, x1h, m1, r1 = K.peg_fwd_x32(xf.detach().contiguous(), geo.B, geo.T, geo.Hg, geo.Wg, peg_w,
+                                                  peg_b, geo.mode, stats=fold, want_f16=f16)
+        elif fold:
             x1f, x1b, m1, r1 = K.peg_fwd_stats(xb, xf, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, peg_b, geo.mode)
-            xn = None
         else:
             x1f, x1b = K.peg_fwd(xb, xf, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, peg_b, geo.mode)
+        if fold:
+            xn = None
+        else:
             xn, _, m1, r1 = K.layernorm_fwd(x1f, norm_g, None, 1e-5)
         if fold:
             Wp, cs, scales = K.pack_qkv_fold(Wq.detach(), norm_g, Wkv_b, q_scale.detach(), k_scale.detach())
-            qkv, qkn = K.linear_qkv_lnfold(x1b, Wp, cs, m1, r1, scales, inner, 2 * inner)
+            if f16:
+                Wp16, cs16 = K.pack_qkv_fold_h16(Wq.detach(), norm_g, Wkv.detach())
+                qkv, qkn = K.linear_qkv_lnfold(x1h, Wp16, cs16, m1, r1, scales, inner, 2 * inner)
+                del x1h, Wp16
+            else:
+                qkv, qkn = K.linear_qkv_lnfold(x1b, Wp, cs, m1, r1, scales, inner, 2 * inner)
             q, kv = qkv[:, :inner], qkv[:, inner:]
             qn, kn = qkn[:, :inner], qkn[:, inner:]
         elif fp8:
@@ -512,26 +590,43 @@ class ViTLayerFn(torch.autograd.Function):
         L, nseq, seq = geo.seq()
         use_bias = bias_u is not None
         streams.mark_image_head(xf.device, 'attn')   # deferred text-stream work may start (streams.py)
-        o, lse = K.attn_fwd(qn, kn, kv[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
-                            bias_u=bias_u if use_bias else None, grid=(geo.Hg, geo.Wg) if use_bias else (0, 0))
+        att = K.attn_fwd(qn, kn, kv[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
+                         bias_u=bias_u if use_bias else None, grid=(geo.Hg, geo.Wg) if use_bias else (0, 0),
+                         want_o16=f16)
+        o, lse = att[0], att[1]
+        o_in, Wo_in = (att[2], h16(Wo)) if f16 else (o, Wo_b)   # to_out's operands
         # to_out + residual + the FeedForward's LayerNorm in one launch (gemm256.hip, EP -6) -- only
         # where a caller checks the launch's status word every step (kernels.ln_guard: the trainer)
-        fused = None if fp8 or not K.ln_guarded() else K.linear_residual_ln(o, Wo_b, x1f, ff_w, ff_b, 1e-5)
+        fused = None if fp8 or not K.ln_guarded() else K.linear_residual_ln(o_in, Wo_in, x1f, ff_w, ff_b, 1e-5,
+                                                                            y16=f16)
+        xn2h = None
         if fused is not None:
-            x2f, x2b, xn2, m2, r2 = fused
+            x2f, x2b, xn2, m2, r2 = fused[:5]
+            if f16:
+                xn2h = fused[5]
         else:
             x2b = torch.empty_like(xb)
             if fp8:
                 x2f = fp8_linear(o, Wo, 'o', Wo_b, residual=x1f, out_f32=True, out2=x2b)
             else:
-                x2f = K.linear(o, Wo_b, residual=x1f, out_dtype=F32, out2=x2b)
-            xn2, _, m2, r2 = K.layernorm_fwd(x2f, ff_w, ff_b, 1e-5)
+                x2f = K.linear(o_in, Wo_in, residual=x1f, out_dtype=F32, out2=x2b)
+            lnr = K.layernorm_fwd(x2f, ff_w, ff_b, 1e-5, out_f16=f16)
+            xn2, _, m2, r2 = lnr[:4]
+            if f16:
+                xn2h = lnr[4]
+        del o_in, Wo_in
         W1p, W2p = pack_ff1(W1), pack_ff2(W2)
         g = torch.empty(xf.shape[0], W2p.shape[1], device=xf.device, dtype=BF16)
         x3b = torch.empty_like(xb)
         if fp8:
             h = fp8_linear(xn2, W1, 'ff1', W1p, act=K.ACT_GEGLU, out2=g)
             x3f = fp8_linear(g, W2, 'ff2', W2p, residual=x2f, out_f32=True, out2=x3b)
+        elif f16:
+            # fp16 FF1: h stored in fp16 (read by the GEGLU backward), g (bf16) from the fp16 h
+            h = K.linear(xn2h, pack_ff1_h16(W1), act=K.ACT_GEGLU, out2=g, out_dtype=K.F16, tag='ff1',
+                         flops=2.0 * xf.shape[0] * W1.shape[0] * W1.shape[1])
+            del xn2h
+            x3f = K.linear(g, W2p, residual=x2f, out_dtype=F32, out2=x3b)
         else:
             # tagged for bench.py's live roofline: algorithmic flops exclude the zero padding rows
             h = K.linear(xn2, W1p, act=K.ACT_GEGLU, out2=g, tag='ff1',
@@ -851,6 +946,12 @@ class ImageProjFn(torch.autograd.Function):
         ctx.W = W
         if precise_f32():      # the f32 image tower's projection: exact f32 (split-K f32 MFMA)
             return K.slinear(pooled.detach().contiguous(), W.detach())
+        # the HBM-streaming skinny GEMM (csrc/proj.hip): the 302 MB weight read once at ~HBM speed
+        # (the generic split-K 128-row MFMA tile ran at 0.85 TB/s at M = 8, round 4)
+        if _SKINNY_PROJ:
+            out = K.skinny_linear(pooled_b, Wb)
+            if out is not None:
+                return out
         B, Kd = pooled_b.shape
         N = Wb.shape[0]
         split = max(1, min(512, Kd // 1024))

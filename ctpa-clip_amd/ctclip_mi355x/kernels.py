@@ -11,6 +11,7 @@ from ._lib import GemmArgs, LnEpilogueArgs, call, ptr, stream_ptr
 
 BF16 = torch.bfloat16
 F32 = torch.float32
+F16 = torch.float16
 
 ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_ARGMAX, ACT_GEGLU_BWD, ACT_L2N, ACT_GELU_BWD = 0, 1, 2, 3, 4, 5, 6
 
@@ -75,7 +76,9 @@ def _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, *, C2=None,
     """drop = (p, seed): BERT hidden dropout on (A.B + bias) before the residual R (f32 C, act 0)."""
     if B2 is not None:
         assert B2.dtype == B.dtype and B2.shape == B.shape and B2.stride() == B.stride()
-    s = _auto_split(M, N, K, act, split_k, batch, accumulate, C)
+    h16 = A.dtype == F16       # fp16 operands (the 3D-ViT forward GEMMs): both, no split-K
+    assert B.dtype == A.dtype, (A.dtype, B.dtype)
+    s = 1 if h16 else _auto_split(M, N, K, act, split_k, batch, accumulate, C)
     if drop is not None:
         assert act == ACT_NONE and not accumulate and C.dtype == F32 and batch == 1 and ldc == N
         if s <= 1:     # no split-K combine to fold it into: GEMM (+ bias), then the dropout kernel
@@ -118,6 +121,8 @@ def _gemm_raw(M, N, K, A, lda, a_kcontig, B, ldb, b_kcontig, C, ldc, *, C2=None,
     a.sA, a.sB, a.sC, a.sC2, a.sR = sA, sB, sC, sC2, sR
     a.n2 = n2
     a.B2 = ptr(B2)
+    a.ab_f16 = int(h16)
+    a.r_f16 = int(R is not None and R.dtype == F16)
     call('ctclip_gemm', _lib.ctypes.byref(a), stream_ptr())
 
 
@@ -261,7 +266,9 @@ def ln_fusable(M, N, bwd=False):
 
 def _gemm_ln(M, K, A, B, b_kcontig, C, C2, R, ln, tag=None, flops=None):
     """Returns False (nothing launched) when the library refuses the configuration."""
+    assert A.dtype == B.dtype
     a = GemmArgs()
+    a.ab_f16 = int(A.dtype == F16)
     a.M, a.N, a.K = M, 512, K
     a.A, a.lda, a.a_kcontig = ptr(A), A.stride(0), 1
     a.B, a.ldb, a.b_kcontig = ptr(B), B.stride(0), int(b_kcontig)
@@ -284,10 +291,11 @@ def _gemm_ln(M, K, A, B, b_kcontig, C, C2, R, ln, tag=None, flops=None):
     return True
 
 
-def linear_residual_ln(x, w, residual, gamma, beta, eps, *, tag=None):
+def linear_residual_ln(x, w, residual, gamma, beta, eps, *, tag=None, y16=False):
     """x1 = residual + x @ w^T (w [512, K] nn.Linear weight) and y = LayerNorm(x1) (gamma, beta;
-    bf16) in ONE launch (ctclip_gemm_ln mode 1).  Returns (x1 f32, x1 bf16, y bf16, mean, rstd),
-    or None when the shape / configuration does not allow the fused form."""
+    bf16) in ONE launch (ctclip_gemm_ln mode 1).  Returns (x1 f32, x1 bf16, y bf16, mean, rstd) --
+    plus y's fp16 copy when y16 -- or None when the shape / configuration does not allow the fused
+    form.  x, w fp16: the fp16 GEMM."""
     M, K = x.shape
     if not ln_fusable(M, w.shape[0]) or K % 64 or residual.dtype != F32:
         return None
@@ -300,8 +308,12 @@ def linear_residual_ln(x, w, residual, gamma, beta, eps, *, tag=None):
     ln = LnEpilogueArgs()
     ln.mode, ln.gamma, ln.beta, ln.eps = 1, ptr(gamma), ptr(beta), eps
     ln.Y, ln.ldy, ln.mean, ln.rstd = ptr(y), 512, ptr(mean), ptr(rstd)
+    yh = torch.empty(M, 512, device=dev, dtype=F16) if y16 else None
+    ln.Y16 = ptr(yh)
     if not _gemm_ln(M, K, x, w, True, x1f, x1b, residual, ln, tag=tag):
         return None
+    if y16:
+        return x1f, x1b, y, mean, rstd, yh
     return x1f, x1b, y, mean, rstd
 
 
@@ -508,14 +520,18 @@ def colsum(x, out=None, accumulate=False):
 
 
 # ----------------------------------------------------------------------------- LayerNorm
-def layernorm_fwd(x, gamma, beta, eps, *, out_bf16=True, out_f32=False):
+def layernorm_fwd(x, gamma, beta, eps, *, out_bf16=True, out_f32=False, out_f16=False):
+    """Returns (y bf16, y f32, mean, rstd), plus y's fp16 copy when out_f16 (requires out_bf16)."""
     rows, D = x.shape
     yb = torch.empty(rows, D, device=x.device, dtype=BF16) if out_bf16 else None
     yf = torch.empty(rows, D, device=x.device, dtype=F32) if out_f32 else None
+    yh = torch.empty(rows, D, device=x.device, dtype=F16) if out_f16 else None
     mean = torch.empty(rows, device=x.device, dtype=F32)
     rstd = torch.empty(rows, device=x.device, dtype=F32)
-    call('ctclip_layernorm_fwd', ptr(x), int(x.dtype == F32), x.stride(0), rows, D, ptr(gamma), ptr(beta), eps,
-         ptr(yb), D, ptr(yf), D, ptr(mean), ptr(rstd), stream_ptr())
+    call('ctclip_layernorm_fwd_x2', ptr(x), int(x.dtype == F32), x.stride(0), rows, D, ptr(gamma), ptr(beta), eps,
+         ptr(yb), ptr(yh), D, ptr(yf), D, ptr(mean), ptr(rstd), stream_ptr())
+    if out_f16:
+        return yb, yf, mean, rstd, yh
     return yb, yf, mean, rstd
 
 
@@ -634,6 +650,16 @@ def pack_rows(src, rows_dst, cols_dst, rowmap=None, colscale=None, out=None):
     return out
 
 
+def pack_rows_h16(src, rows_dst, cols_dst, rowmap=None, colscale=None, out=None):
+    """fp16 working weight (the fp16 forward GEMMs), as pack_rows."""
+    rows, cols = src.shape
+    if out is None:
+        out = torch.empty(rows_dst, cols_dst, device=src.device, dtype=F16)
+    call('ctclip_pack_rows_h16', ptr(src), src.stride(0), ptr(rowmap), rows_dst, cols, cols_dst, ptr(colscale),
+         ptr(out), out.stride(0), stream_ptr())
+    return out
+
+
 def pack_rows_f32(src, rows_dst, cols_dst, rowmap=None, colscale=None, out=None):
     """f32 working weight: out[r][c] = src[rowmap[r]][c] * colscale[c] (zero padding), as pack_rows."""
     rows, cols = src.shape
@@ -674,16 +700,18 @@ def add_f32(a, b, out=None, out_bf16=None):
 
 
 # ----------------------------------------------------------------------------- patch embed
-def patch_ln(video, is_hu, PT, P, offs, eps=1e-5, ld=None):
-    """LayerNorm'd patch rows [tokens, ld] bf16 (columns pd..ld-1 zero: K padding for the GEMM)."""
+def patch_ln(video, is_hu, PT, P, offs, eps=1e-5, ld=None, want_f16=False):
+    """LayerNorm'd patch rows [tokens, ld] bf16 (columns pd..ld-1 zero: K padding for the GEMM);
+    with want_f16 also their fp16 copy (returns (bf16, f16))."""
     B, C, Fr, H, W = video.shape
     T, Hg, Wg = Fr // PT, H // P, W // P
     pd = C * PT * P * P
     ld = pd if ld is None else ld
     out = torch.empty(B * T * Hg * Wg, ld, device=video.device, dtype=BF16)
-    call('ctclip_patch_ln', ptr(video), int(video.dtype == F32), int(is_hu), B, C, Fr, H, W, PT, P, ptr(offs), eps,
-         ptr(out), ld, stream_ptr())
-    return out
+    out16 = torch.empty(B * T * Hg * Wg, ld, device=video.device, dtype=F16) if want_f16 else None
+    call('ctclip_patch_ln_x2', ptr(video), int(video.dtype == F32), int(is_hu), B, C, Fr, H, W, PT, P, ptr(offs), eps,
+         ptr(out), ptr(out16), ld, stream_ptr())
+    return (out, out16) if want_f16 else out
 
 
 def unpatch_mse(pix, video, is_hu, PT, P, offs, want_grad=True, want_recon=False):
@@ -733,6 +761,45 @@ def peg_fwd_stats(xb, xf, B, T, H, W, weight, bias, mode, eps=1e-5):
     return outf, outb, mean, rstd
 
 
+def skinny_linear(x, w):
+    """y[M, N] f32 = x[M, K] @ w[N, K]^T for M <= 16 rows, both bf16 K-contiguous, through the
+    HBM-streaming skinny GEMM (ctclip_skinny_gemm: w read once, partial sums per k-slice reduced in
+    a fixed order).  Returns None when the shape does not qualify."""
+    M, Kd = x.shape
+    N = w.shape[0]
+    if x.dtype != BF16 or w.dtype != BF16 or x.stride(1) != 1 or w.stride(1) != 1 or w.shape[1] != Kd:
+        return None
+    ns = _lib.lib().ctclip_skinny_gemm_slices(M, N, Kd)
+    if ns <= 0:
+        return None
+    slabs = torch.empty(ns, M, N, device=x.device, dtype=F32)
+    call('ctclip_skinny_gemm', ptr(x), x.stride(0), ptr(w), w.stride(0), M, N, Kd, ptr(slabs), ns, stream_ptr())
+    out = torch.empty(M, N, device=x.device, dtype=F32)
+    reduce_slabs(slabs, out)
+    return out
+
+
+def peg_fwd_x32(xf, B, T, H, W, weight, bias, mode, stats=False, want_f16=False, eps=1e-5):
+    """PEG forward with the taps read from the f32 residual stream (ctclip_peg_fwd_x32; the bf16
+    shadow's rounding never enters the conv).  Returns (out_f32, out_bf16, out_f16 or None, mean,
+    rstd) -- mean / rstd the LayerNorm statistics of the output rows when stats (merged from the
+    kernel's 32-channel groups), else None."""
+    M, D = xf.shape
+    assert xf.dtype == F32 and xf.is_contiguous()
+    outf = torch.empty_like(xf)
+    outb = torch.empty(M, D, device=xf.device, dtype=BF16)
+    outh = torch.empty(M, D, device=xf.device, dtype=torch.float16) if want_f16 else None
+    part = torch.empty(D // 32, M, 2, device=xf.device, dtype=F32) if stats else None
+    call('ctclip_peg_fwd_x32', ptr(xf), B, T, H, W, D, ptr(weight), ptr(bias), mode, ptr(outf), ptr(outb), ptr(outh),
+         ptr(part), stream_ptr())
+    if not stats:
+        return outf, outb, outh, None, None
+    mean = torch.empty(M, device=xf.device, dtype=F32)
+    rstd = torch.empty(M, device=xf.device, dtype=F32)
+    call('ctclip_ln_stats_merge', ptr(part), D // 32, M, D, float(eps), ptr(mean), ptr(rstd), stream_ptr())
+    return outf, outb, outh, mean, rstd
+
+
 def pack_qkv_fold(wq, gamma, wkv_b, s_fold, s_rest):
     """[bf16(Wq o gamma) ; Wkv], the f32 row sums of the folded rows and the concatenated
     l2norm scales [s_fold ; s_rest] (ctclip_pack_qkv_fold, one launch)."""
@@ -748,6 +815,20 @@ def pack_qkv_fold(wq, gamma, wkv_b, s_fold, s_rest):
     call('ctclip_pack_qkv_fold', ptr(wq), wq.stride(0), ptr(g), nq, K, ptr(wkv_b), wkv_b.stride(0), nr, ptr(out),
          out.stride(0), ptr(cs), ptr(s_fold), ptr(s_rest), ns, ptr(scales), stream_ptr())
     return out, cs, scales
+
+
+def pack_qkv_fold_h16(wq, gamma, wkv):
+    """fp16 [f16(Wq o gamma) ; f16(Wkv)] and the f32 row sums of its folded rows (the fp16 GEMM's fold
+    constants; ctclip_pack_qkv_fold_h16).  wq, wkv f32."""
+    nq, K = wq.shape
+    nr = wkv.shape[0]
+    assert wq.dtype == F32 and wkv.dtype == F32 and wq.stride(1) == 1 and wkv.stride(1) == 1
+    out = torch.empty(nq + nr, K, device=wq.device, dtype=F16)
+    cs = torch.empty(nq, device=wq.device, dtype=F32)
+    g = gamma.detach().contiguous()
+    call('ctclip_pack_qkv_fold_h16', ptr(wq), wq.stride(0), ptr(g), nq, K, ptr(wkv), wkv.stride(0), nr, ptr(out),
+         out.stride(0), ptr(cs), stream_ptr())
+    return out, cs
 
 
 def linear_qkv_lnfold(x, wp, cs, mean, rstd, scales, nfold, n2, out=None, out2=None):
@@ -770,6 +851,8 @@ def linear_qkv_lnfold(x, wp, cs, mean, rstd, scales, nfold, n2, out=None, out2=N
     a.bias = ptr(scales)
     a.alpha, a.act, a.split_k, a.batch = 1.0, ACT_L2N, 1, 1
     a.n2 = n2
+    assert wp.dtype == x.dtype
+    a.ab_f16 = int(x.dtype == F16)     # fp16 x and packed weight (pack_qkv_fold_h16)
     call('ctclip_gemm_qkv_lnfold', _lib.ctypes.byref(a), ptr(mean), ptr(rstd), ptr(cs), nfold, stream_ptr())
     return out, out2
 
@@ -917,15 +1000,19 @@ def _attn_args(q, k, v, o, *, L, H, D, nseq, M, scale, seq, bias_u=None, grid=(0
     return a
 
 
-def attn_fwd(q, k, v, *, L, H, D, nseq, scale, seq, bias_u=None, grid=(0, 0), kmask=None, dropout=(0.0, 0)):
-    """q/k/v: 2D views [M, ...] whose head h occupies columns h*D:(h+1)*D.  Returns (o [M, H*D], lse [H, M])."""
+def attn_fwd(q, k, v, *, L, H, D, nseq, scale, seq, bias_u=None, grid=(0, 0), kmask=None, dropout=(0.0, 0),
+             want_o16=False):
+    """q/k/v: 2D views [M, ...] whose head h occupies columns h*D:(h+1)*D.  Returns (o [M, H*D], lse [H, M]),
+    plus o's fp16 copy when want_o16."""
     M = q.shape[0]
     o = torch.empty(M, H * D, device=q.device, dtype=BF16)
+    o16 = torch.empty(M, H * D, device=q.device, dtype=F16) if want_o16 else None
     lse = torch.empty(H, M, device=q.device, dtype=F32)
     a = _attn_args(q, k, v, o, L=L, H=H, D=D, nseq=nseq, M=M, scale=scale, seq=seq, bias_u=bias_u, grid=grid,
                    kmask=kmask, lse=lse, dropout=dropout)
+    a.o16 = ptr(o16)
     call('ctclip_attn_fwd', _lib.ctypes.byref(a), stream_ptr())
-    return o, lse
+    return (o, lse, o16) if want_o16 else (o, lse)
 
 
 def attn_bwd(q, k, v, o, lse, dout, dq, dk, dv, *, L, H, D, nseq, scale, seq, bias_u=None, dbias_u=None,

@@ -255,7 +255,7 @@ def peg_dwconv3d(x: Tensor, weight: Tensor, bias: Tensor, shape: List[int], mode
     (1, 1, 1, 1, 2, 0)), on token rows x [B*T*H*W, D] f32 in canonical (b, t, h, w) order.  mode 0:
     the spatial transformer's view; mode 1: the temporal transformer's raw-reshape view of its
     '(b h w) t d' tensor (attention.py:69-70).  weight [D, 1, 3, 3, 3] f32, bias [D] f32.  The
-    conv reads the bf16 rounding of x (as in the model); the residual is the f32 x."""
+    conv reads the f32 x (as the model does since round 5, ctclip_peg_fwd_x32)."""
     B, T, H, W = shape
     D = x.shape[1]
     _need(x.dtype == F32 and x.dim() == 2 and x.shape[0] == B * T * H * W, 'peg_dwconv3d: x [B*T*H*W, D] f32')
@@ -263,7 +263,7 @@ def peg_dwconv3d(x: Tensor, weight: Tensor, bias: Tensor, shape: List[int], mode
           'peg_dwconv3d: weight [D, 1, 3, 3, 3], bias [D] f32')
     _need(mode in (0, 1), 'peg_dwconv3d: mode 0 (spatial) or 1 (temporal)')
     x = x.contiguous()
-    outf, _ = K.peg_fwd(K.cast_bf16(x), x, B, T, H, W, weight.contiguous(), bias.contiguous(), mode)
+    outf, _, _, _, _ = K.peg_fwd_x32(x, B, T, H, W, weight.contiguous(), bias.contiguous(), mode)
     return outf
 
 

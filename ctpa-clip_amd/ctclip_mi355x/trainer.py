@@ -247,6 +247,10 @@ class CTClipTrainer:
         LayerNorm-exchange status (synchronises): call after the last ``train_step`` before reading
         the parameters."""
         streams.flush_text(self.device)
+        # the text-bucket Adam runs on the text stream, the codebook EMA on the auxiliary one: order
+        # the caller's stream after both, so parameters read (or saved) on it are the updated ones
+        streams.join_text(self.device)
+        streams.join_aux(self.device)
         self.check()
 
     def check(self):

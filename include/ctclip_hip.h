@@ -67,6 +67,11 @@ typedef struct {
                                      * B2 = bf16(W - bf16(W)) the GEMM sees W to ~16 mantissa bits
                                      * (the text tower's hi / lo split weights); 128-tile kernel only,
                                      * not with act 3 */
+  int32_t ab_f16;                   /* A and B are IEEE fp16 (both K-contiguous; no B2, split-K,
+                                     * act 3-6): the 3D-ViT forward GEMMs (3 more mantissa bits
+                                     * than bf16 at the same MFMA rate).  With act 2 the h output
+                                     * C is fp16 too and g is computed from the fp16-rounded h */
+  int32_t r_f16;                    /* act 4: R (h) is fp16 (written by an ab_f16 act-2 GEMM) */
 } ctclip_gemm_args;
 int ctclip_gemm(const ctclip_gemm_args* a, void* stream);
 /* diagnostic: large-tile kernel variant (8 = 8-phase 256x256x64 default, 1 = 128x256x32,
@@ -137,6 +142,8 @@ typedef struct {
   int32_t* status;
   uint32_t spin_limit;
   int32_t debug;
+  void* Y16;                        /* mode 1, optional: an fp16 copy of Y (same ldy) -- the next
+                                     * fp16 GEMM's A operand */
 } ctclip_ln_epilogue;
 int ctclip_gemm_ln(const ctclip_gemm_args* a, const ctclip_ln_epilogue* ln, void* stream);
 
@@ -158,6 +165,11 @@ int ctclip_gemm_qkv_lnfold(const ctclip_gemm_args* a, const float* mean, const f
 int ctclip_pack_qkv_fold(const float* Wq, int64_t ldq, const float* gamma, int64_t nq, int64_t K,
                          const void* Wrest, int64_t ldr, int64_t nrest, void* out, int64_t ldo, float* cs,
                          const float* s_fold, const float* s_rest, int32_t ns, float* s_out, void* stream);
+/* fp16 B operand of the fp16 ctclip_gemm_qkv_lnfold (ab_f16): rows [0, nq) = f16(Wq o gamma), cs [nq] =
+ * their row sums (of the f16 values), rows [nq, nq + nrest) = f16 of the f32 rows of Wrest */
+int ctclip_pack_qkv_fold_h16(const float* Wq, int64_t ldq, const float* gamma, int64_t nq, int64_t K,
+                             const float* Wrest, int64_t ldr, int64_t nrest, void* out, int64_t ldo, float* cs,
+                             void* stream);
 /* LayerNorm statistics from ngroups partial (mean, M2) groups of D / ngroups columns each
  * (part [ngroups][rows] float2, e.g. ctclip_peg_fwd_stats): mean, rstd = 1 / sqrt(var + eps). */
 int ctclip_ln_stats_merge(const float* part, int32_t ngroups, int64_t rows, int32_t D, float eps, float* mean,
@@ -178,6 +190,15 @@ int ctclip_lnfold_wgrad(const float* G, int64_t ldg, const float* u, const float
                         int64_t nq, int64_t nrest, int64_t K, float* grad_q, int64_t ldgq, float* grad_gamma,
                         float* grad_rest, int64_t ldgr, void* stream);
 
+/* Skinny-M streaming GEMM: slabs[s][m][n] = sum over k-slice s of A[m][k] B[n][k], A [M][K] and B
+ * [N][K] bf16 K-contiguous, 1 <= M <= 16, N % 64 == 0, K % 64 == 0; nslices must equal
+ * ctclip_skinny_gemm_slices(M, N, K) (> 0); reduce the [nslices][M][N] f32 workspace with
+ * ctclip_reduce_slabs.  The forward of CTCLIP's image projection to_visual_latent
+ * (ct_clip/ct_clip.py:564,767: Linear(294,912 -> 512) on the pooled tokens of the local batch),
+ * which streams its 302 MB bf16 weight once per step. */
+int ctclip_skinny_gemm_slices(int64_t M, int64_t N, int64_t K);
+int ctclip_skinny_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
+                       float* slabs, int32_t nslices, void* stream);
 /* sum f32 slabs [s][rows][ld] -> out (f32 or bf16), optional accumulate into f32 out */
 int ctclip_reduce_slabs(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,
                         void* out, int64_t ldo, int32_t out_f32, int32_t accumulate, void* stream);
@@ -229,6 +250,11 @@ int ctclip_gemm_mxfp8_set_tile(int bm);
  * ct_clip/attention.py:28-35 (bias-less LayerNorm: gamma, beta = 0 buffer, eps 1e-5),
  * nn.LayerNorm in FeedForward / to_patch_emb (attention.py:47, ctvit.py:171,173), BERT LayerNorms.
  * x, y row-major with leading dims; f32 statistics; y in bf16 and/or f32.  D % 8 == 0. */
+/* ctclip_layernorm_fwd plus an optional fp16 copy y_f16 of the output (stride ldyb): the A operand of
+ * the fp16 FeedForward GEMM (round 5) */
+int ctclip_layernorm_fwd_x2(const void* x, int32_t x_f32, int64_t ldx, int64_t rows, int32_t D, const float* gamma,
+                            const float* beta, float eps, void* y_bf16, void* y_f16, int64_t ldyb, float* y_f32,
+                            int64_t ldyf, float* mean, float* rstd, void* stream);
 int ctclip_layernorm_fwd(const void* x, int32_t x_f32, int64_t ldx, int64_t rows, int32_t D,
                          const float* gamma, const float* beta, float eps,
                          void* y_bf16, int64_t ldyb, float* y_f32, int64_t ldyf,
@@ -298,6 +324,11 @@ int ctclip_add_f32(const float* a, const float* b, float* y, void* y_bf16, int64
 int ctclip_patch_ln(const void* video, int32_t is_f32, int32_t is_hu, int64_t B, int32_t C, int32_t F,
                     int32_t H, int32_t W, int32_t PT, int32_t P, const int32_t* offs, float eps,
                     void* xhat, int64_t ldo, void* stream);
+/* the same, plus an optional fp16 copy xhat16 (same ldo): the fp16 patch-embed GEMM's A operand
+ * (round 5; the bf16 xhat stays the weight gradient's operand) */
+int ctclip_patch_ln_x2(const void* video, int32_t is_f32, int32_t is_hu, int64_t B, int32_t C, int32_t F,
+                       int32_t H, int32_t W, int32_t PT, int32_t P, const int32_t* offs, float eps,
+                       void* xhat, void* xhat16, int64_t ldo, void* stream);
 int ctclip_patch_wgrad(const float* G, const float* colsum_dy, const float* W, const float* gamma,
                        const float* beta, int32_t N, int32_t K, float* dW, float* dgamma, float* dbeta,
                        int32_t accumulate, void* stream);
@@ -322,6 +353,14 @@ int ctclip_peg_fwd(const void* x_bf16, const float* x_f32, int64_t B, int32_t T,
 int ctclip_peg_fwd_stats(const void* x_bf16, const float* x_f32, int64_t B, int32_t T, int32_t H, int32_t W,
                          int32_t D, const float* weight, const float* bias, int32_t mode, float* out_f32,
                          void* out_bf16, float* stats, void* stream);
+/* PEG forward with the conv taps read from the f32 residual stream x (not its bf16 shadow; the
+ * residual is the centre tap): out_f32 = x + bias + conv(x) (ct_clip/attention.py:56-84,324),
+ * out_bf16 / out_f16 (optional) its 16-bit copies, stats (optional, plane-streaming shapes:
+ * D % 32 == 0, W <= 24) [D / 32][B T H W] float2 (mean, M2) per 32-channel group for
+ * ctclip_ln_stats_merge.  Any D % 4 == 0 otherwise (one thread per token x 4 channels). */
+int ctclip_peg_fwd_x32(const float* x_f32, int64_t B, int32_t T, int32_t H, int32_t W, int32_t D,
+                       const float* weight, const float* bias, int32_t mode, float* out_f32, void* out_bf16,
+                       void* out_f16, float* stats, void* stream);
 int ctclip_peg_bwd_data(const void* dout_bf16, const float* dout_f32, int64_t B, int32_t T, int32_t H,
                         int32_t W, int32_t D, const float* weight, int32_t mode, float* dx_f32,
                         void* dx_bf16, void* stream);
@@ -373,6 +412,7 @@ typedef struct {
    * atomics.  Its size in floats is ctclip_attn_bwd_ws_floats(a) (0: this shape does not use it). */
   float* dbias_ws;
   int64_t dbias_ws_floats;
+  void* o16;   /* fwd, optional: an fp16 copy of O (ldo) -- the fp16 to_out GEMM's A operand */
 } ctclip_attn_args;
 int ctclip_attn_fwd(const ctclip_attn_args* a, void* stream);
 int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream);
@@ -420,6 +460,9 @@ typedef struct {
   int32_t act;
 } ctclip_sgemm_tn_args;
 int ctclip_sgemm_tn(const ctclip_sgemm_tn_args* a, void* stream);
+/* fp16 working weights of the fp16 forward GEMMs, as ctclip_pack_rows (round 5) */
+int ctclip_pack_rows_h16(const float* src, int64_t ld_src, const int32_t* map, int64_t rows_dst, int32_t cols,
+                         int32_t cols_dst, const float* colscale, void* dst, int64_t ld_dst, void* stream);
 /* f32 working weights: dst[r][c] = src[map[r]][c] * colscale[c] (zero pads), as ctclip_pack_rows */
 int ctclip_pack_rows_f32(const float* src, int64_t ld_src, const int32_t* map, int64_t rows_dst, int32_t cols,
                          int32_t cols_dst, const float* colscale, float* dst, int64_t ld_dst, void* stream);

@@ -177,3 +177,23 @@ def test_adam_writes_split_shadow(K):
     assert torch.equal(lo[1:], (p[1:] - hi[1:].float()).bfloat16())
 
 
+
+
+@pytest.mark.parametrize('M,N,K_', [(8, 512, 294912), (2, 512, 294912), (16, 128, 4096), (5, 64, 256 * 7)])
+def test_skinny_linear(K, M, N, K_):
+    """The HBM-streaming skinny GEMM of the image projection (to_visual_latent, ct_clip/ct_clip.py:
+    564,767; csrc/proj.hip) against an f64 matmul of the same bf16 operands, integer-exact data for
+    the layout (a row / column / k-permutation slip cannot pass), and deterministic repeats."""
+    torch.manual_seed(4)
+    x = torch.randn(M, K_, device='cuda').bfloat16()
+    w = (torch.randn(N, K_, device='cuda') * 0.01).bfloat16()
+    y = K.skinny_linear(x, w)
+    assert y is not None
+    ref = (x.double() @ w.double().t())
+    assert _rel(y, ref) < 1e-5
+    assert torch.equal(K.skinny_linear(x, w), y)
+    xi = (torch.arange(M * K_, device='cuda').reshape(M, K_) % 5 - 2).bfloat16()
+    wi = ((torch.arange(N * K_, device='cuda').reshape(N, K_) * 7) % 3 - 1).bfloat16()
+    if K_ <= 4096:      # sums stay exact in f32
+        assert torch.equal(K.skinny_linear(xi, wi), (xi.double() @ wi.double().t()).float())
+    assert K.skinny_linear(torch.zeros(17, K_, device='cuda').bfloat16(), w) is None

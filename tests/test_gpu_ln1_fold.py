@@ -198,3 +198,35 @@ def test_l2norm_qk_bwd_fold_matches_two_passes(K):
     assert torch.equal(out1, out0)
     assert torch.equal(c11, c10) and torch.equal(be1, be0)
     assert _rel(u1, u0) < 1e-5 and _rel(dsq1, dsq0) < 1e-5 and _rel(dsk1, dsk0) < 1e-5
+
+
+def test_layer_heads16_runs_unfolded(K):
+    """heads * dim_head = 512 (heads = 16): the fold's merged q | k l2norm backward is built for 256
+    q columns only, so the layer must take the unfolded path even with the fold switched on --
+    forward + backward run (no assertion inside the backward) and match the unfolded layer exactly."""
+    from ctclip_mi355x import attention as A, functional as Fn
+    torch.manual_seed(1)
+    tr = A.Transformer(512, depth=1, dim_head=32, heads=16).cuda()
+    geo = Fn.Geo(B=1, T=8, Hg=8, Wg=8, heads=16, dim_head=32, mode=0)
+    xf0 = torch.randn(geo.M, 512, device='cuda') + 0.3
+    xb0 = xf0.bfloat16()
+    dy = torch.randn(geo.M, 512, device='cuda') * 1e-2
+
+    def run(fold):
+        Fn._LN1_FOLD = fold
+        for p in tr.parameters():
+            p.grad = None
+        xf = xf0.clone().requires_grad_(True)
+        yf, _ = tr.run(xf, xb0, geo)
+        yf.backward(dy)
+        torch.cuda.synchronize()
+        return yf.detach(), xf.grad
+
+    prev = Fn._LN1_FOLD
+    try:
+        y0, dx0 = run(False)
+        y1, dx1 = run(True)
+    finally:
+        Fn._LN1_FOLD = prev
+    assert torch.isfinite(y1).all() and torch.isfinite(dx1).all()
+    assert torch.equal(y1, y0) and torch.equal(dx1, dx0)

@@ -348,6 +348,28 @@ def test_deferred_text_adam_matches(setup):
     assert torch.equal(p0, p1), (p0 - p1).abs().max().item()
 
 
+def test_state_dict_after_deferred_adam_is_current(setup):
+    """CTCLIP.state_dict right after a step whose text Adam was deferred: copies of the
+    returned tensors queued on the caller's stream -- what torch.save does -- hold the updated
+    weights, not pre-update or torn ones (state_dict joins the text and auxiliary streams)."""
+    cfg, _, hu, ids, mask, text = setup
+    from ctclip_mi355x.trainer import CTClipTrainer
+    torch.manual_seed(0)
+    model = build(cfg)
+    tr = CTClipTrainer(model, lr=1e-3, defer_text_adam=True)
+    before = {k: v.detach().clone() for k, v in model.state_dict().items() if k.startswith('text_transformer.')}
+    tr.train_step(text, hu.cuda())
+    sd = model.state_dict()                       # no synchronize in between
+    snap = {k: sd[k].detach().clone() for k in before}      # queued on the current stream
+    torch.cuda.synchronize()
+    final = model.state_dict()
+    moved = 0
+    for k in before:
+        assert torch.equal(snap[k], final[k]), k
+        moved += int(not torch.equal(before[k], final[k]))
+    assert moved > 0
+
+
 def test_train_step_bit_reproducible():
     """Two runs of three training steps from the same seed give bit-identical losses, parameters,
     Adam moments, VQ codebook and cluster sizes, BERT dropout on, ragged reports (pad ids): no

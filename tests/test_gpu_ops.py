@@ -128,6 +128,29 @@ def test_peg(K, mode, shape, D):
     assert rel(db, br.grad) < 1e-5
 
 
+@pytest.mark.parametrize('mode', [0, 1])
+@pytest.mark.parametrize('shape,D', [((2, 6, 5, 7), 128), ((1, 24, 24, 24), 512), ((2, 24, 24, 24), 64),
+                                     ((1, 3, 4, 40), 64), ((2, 2, 3, 4), 24)])
+def test_peg_x32(K, mode, shape, D):
+    """The f32-tap PEG forward (ctclip_peg_fwd_x32): f32 x (not bf16-representable) against the torch
+    fp32 conv, its 16-bit copies the casts of its f32 output, and the LayerNorm statistics of the
+    output rows (32-channel groups merged) against torch."""
+    torch.manual_seed(12)
+    M = shape[0] * shape[1] * shape[2] * shape[3]
+    xf = torch.randn(M, D, device=dev) + 0.25
+    w = torch.randn(D, 1, 3, 3, 3, device=dev) * 0.2
+    b = torch.randn(D, device=dev) * 0.1
+    tiled = D % 32 == 0 and shape[3] <= 24
+    outf, outb, outh, mean, rstd = K.peg_fwd_x32(xf, *shape, w, b, mode, stats=tiled, want_f16=True)
+    ref = _peg_ref(xf, w, b, shape, mode)
+    assert rel(outf, ref) < 1e-5
+    assert torch.equal(outb, outf.bfloat16()) and torch.equal(outh, outf.half())
+    if tiled:
+        var, mu = torch.var_mean(outf.double(), dim=1, unbiased=False)
+        assert rel(mean, mu) < 1e-5
+        assert rel(rstd, torch.rsqrt(var + 1e-5)) < 1e-5
+
+
 # ----------------------------------------------------------------------------- attention
 def _gather_rows(n_inner, s_outer, s_inner, s_pos, nseq, L):
     s = torch.arange(nseq)[:, None]
@@ -160,7 +183,8 @@ def _cpb_table(H, gh, gw):
     return u, bins
 
 
-@pytest.mark.parametrize('case', ['spatial', 'spatial_small', 'spatial_8x8', 'temporal', 'temporal_l5_h3', 'temporal_l32', 'bert'])
+@pytest.mark.parametrize('case', ['spatial', 'spatial_small', 'spatial_8x8', 'temporal', 'temporal_l5_h3', 'temporal_l32', 'bert',
+                                  'bert_leftpad'])
 def test_attention(K, case):
     torch.manual_seed(3)
     if case.startswith('spatial'):
@@ -189,6 +213,10 @@ def test_attention(K, case):
         scale, u, bias, grid = 1 / 8, None, None, (0, 0)
         lens = torch.tensor([128, 77, 5])
         kmask = (torch.arange(L)[None, :] < lens[:, None]).int().to(dev)
+        if case == 'bert_leftpad':
+            # leading masked keys (left padding): whole first key chunks of -inf scores, which the
+            # lazy online-softmax rescale must still start from (exp2(-inf - -inf))
+            kmask = (torch.arange(L)[None, :] >= (L - lens)[:, None]).int().to(dev)
     rows = _gather_rows(*seq, nseq, L)
     q = (torch.randn(M, H * D, device=dev) * (0.3 if case == 'bert' else 0.18)).bfloat16()
     kv = (torch.randn(M, 2 * H * D, device=dev) * 0.18).bfloat16()
@@ -263,6 +291,26 @@ def test_vq_select_and_pool(K):
     _, _, ne, ncs = O.vq_forward(x.cpu(), cb.cpu()[None], torch.zeros(1, C), True, 0.8, force_ind=idx.cpu())
     assert rel(emb.cpu(), ne[0]) < 1e-5
     assert rel(cs.cpu(), ncs[0]) < 1e-6
+    # non-finite tokens: the row maps to code 0 and its normalised row is zero, so the
+    # EMA statistics stay finite and code 0's direction is untouched by it
+    xbad = x[:128].clone()
+    xbad[3] = float('nan')
+    xbad[7, 5] = float('inf')
+    cb_ = cb.bfloat16()
+    cand_b = torch.empty(128, nt, 2, device=dev)
+    cand2_b = torch.empty(128, nt, device=dev)
+    K.gemm_raw(128, C, D, F.normalize(xbad, dim=-1).bfloat16(), D, True, cb_, D, True, cand_b, nt, C2=cand2_b,
+               ldc2=nt, act=K.ACT_ARGMAX)
+    idb, xnb = K.vq_select(cand_b, xbad, cb, cand2=cand2_b)
+    assert idb[3].item() == 0 and idb[7].item() == 0
+    assert torch.isfinite(xnb).all() and xnb[3].abs().sum().item() == 0 and xnb[7].abs().sum().item() == 0
+    assert torch.equal(idb[:3], idx[:3])
+    bins_b = torch.zeros(C, device=dev)
+    esum_b = torch.zeros(C, D, device=dev, dtype=torch.int64)
+    K.vq_ema_accum(idb, xnb, bins_b, esum_b)
+    emb_b = cb.clone()
+    K.vq_ema_finalize(bins_b, esum_b, 0.8, emb_b, torch.zeros(C, device=dev))
+    assert torch.isfinite(emb_b).all()
 
 
 # ----------------------------------------------------------------------------- loss
