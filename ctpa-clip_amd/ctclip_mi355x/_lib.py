@@ -124,6 +124,7 @@ class ResampleArgs(ctypes.Structure):
 _SIGS = {
     'ctclip_version': [],
     'ctclip_device_arch': [ctypes.c_char_p, c_i32],
+    'ctclip_debug_hold_cus': [c_i32, c_i64, c_i32, c_vp],
     'ctclip_gemm': [ctypes.POINTER(GemmArgs), c_vp],
     'ctclip_gemm_ln': [ctypes.POINTER(GemmArgs), ctypes.POINTER(LnEpilogueArgs), c_vp],
     'ctclip_gemm_qkv_lnfold': [ctypes.POINTER(GemmArgs), c_vp, c_vp, c_vp, c_i32, c_vp],

@@ -144,9 +144,18 @@ class BucketedGradSync:
     each launched as soon as its ``mark_ready`` node has run; ``finish`` launches whatever no
     hook launched (a tower without gradients, world 1) and waits for all of them."""
 
-    def __init__(self, flat_grad: torch.Tensor, buckets, before_launch=None, force=False):
+    def __init__(self, flat_grad: torch.Tensor, buckets, before_launch=None, force=False, status=None):
         self.grad = flat_grad
         self.buckets = list(buckets)
+        # status = (slot, source): slot is the 1-element f32 view right after the last bucket in the
+        # arena; just before the last bucket's all-reduce it receives source() (this rank's int32
+        # status word, None = 0) and the all-reduce covers it too, so it ends up holding the SUM of
+        # every rank's status -- one extra float on an existing collective, no extra launch
+        self.status = status
+        if status is not None and self.buckets:
+            t, off, n = self.buckets[-1]
+            slot = status[0]
+            assert slot.data_ptr() == self.grad[off + n:off + n + 1].data_ptr(), 'status slot must follow the last bucket'
         self.before_launch = before_launch   # fold stray (non-arena) grads of a bucket
         self.force = force                   # arm the hooks even at world 1 (tests)
         self.launched = []
@@ -182,6 +191,18 @@ class BucketedGradSync:
             self.launched.append(t)
             self.log.append(t)
             world, _ = world_rank()
+            last = self.status is not None and t == self.buckets[-1][0]
+            if last:
+                slot, source = self.status
+                if self.grad.is_cuda and self.stream is not None:
+                    # the status words are written by the forward's kernels on the step's stream
+                    torch.cuda.current_stream().wait_stream(self.stream)
+                src = source()
+                if src is None:
+                    slot.zero_()
+                else:
+                    slot.copy_(src)
+                n += 1
             if world > 1:
                 self.works.append(dist.all_reduce(self.grad[off:off + n], async_op=True))
             if t == tag:

@@ -35,7 +35,11 @@ class FlatParams:
         n = sum(p.numel() for p in self.params)
         self.numel = n
         self.data = torch.empty(n, device=device, dtype=torch.float32)
-        self.grad = torch.zeros(n, device=device, dtype=torch.float32)
+        # one element past the gradients: the step's status slot.  It rides the last gradient bucket's
+        # SUM all-reduce (dist_sync.BucketedGradSync), so every rank sees the sum of the ranks'
+        # LayerNorm-exchange status words and all skip (or apply) the step together.
+        self.grad = torch.zeros(n + 1, device=device, dtype=torch.float32)
+        self.status = self.grad[n:]
         # (shadows only on the GPU: the CPU arenas serve the gloo rehearsal tests of the sync logic)
         gpu = torch.device(device).type == 'cuda' and os.environ.get('CTCLIP_BF16_SHADOW', '1') != '0'
         self.bf16 = torch.empty(n, device=device, dtype=torch.bfloat16) if gpu else None
@@ -142,12 +146,16 @@ class CTClipTrainer:
                 segs.append((tag, off, n))
                 self.bucket_params[tag] = [p for p in ps if p.requires_grad]
             off += n
-        self.grad_sync = dist_sync.BucketedGradSync(self.flat.grad, segs, before_launch=self._fold_bucket)
+        self.grad_sync = dist_sync.BucketedGradSync(self.flat.grad, segs, before_launch=self._fold_bucket,
+                                                    status=(self.flat.status, self._local_status))
         self.m = torch.zeros_like(self.flat.data)
         self.v = torch.zeros_like(self.flat.data)
         self.lr, self.wd, self.max_grad_norm, self.betas, self.eps = lr, wd, max_grad_norm, betas, eps
         self.steps = 0
         self.norm = torch.zeros(2, device=dev, dtype=torch.float32)
+        # the Adam kernels' skip guard of step s: skip_ring[s % 4] = (summed status slot != 0), written
+        # after the all-reduce; a ring so a deferred text-bucket Adam still reads its own step's word
+        self.skip_ring = torch.zeros(4, device=dev, dtype=torch.int32)
         self.world = dist_sync.world_rank()[0]
         # per-step host check of the LayerNorm-fused GEMMs' status word (kernels.ln_guard): an async
         # copy into pinned memory after each step, read once its event completed -- never more than
@@ -156,6 +164,10 @@ class CTClipTrainer:
         self._ln_pending = collections.deque()       # (step, event, pinned int32[1])
         self._ln_host = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(4)] if self._guard else []
         self.ln_steps_checked = 0
+
+    def _local_status(self):
+        """This rank's sticky LayerNorm-exchange status word (int32[1] on the device), or None (CPU)."""
+        return K.ln_status_tensor(self.device) if self._guard else None
 
     def _fold_bucket(self, tag):
         self.flat.rebind_grads(self.bucket_params.get(tag, ()))
@@ -202,8 +214,10 @@ class CTClipTrainer:
         streams.join_text(self.device)
         streams.join_aux(self.device)     # the VQ EMA update (already done by now; keeps state coherent)
         self.grad_sync.finish()
-        K.grad_norm(self.flat.grad, self.max_grad_norm if self.max_grad_norm else 0.0, self.norm)
         self.steps += 1
+        skip_word = self.skip_ring[self.steps % 4:self.steps % 4 + 1]
+        skip_word.copy_(self.flat.status != 0.0)          # any rank's exchange timed out -> all skip
+        K.grad_norm(self.flat.grad[:self.flat.numel], self.max_grad_norm if self.max_grad_norm else 0.0, self.norm)
         # the text bucket's Adam (and grad reset) goes on the text stream: the next step's image
         # tower does not wait for it, the next step's BERT (same stream) does.  It is queued
         # behind the 3D-ViT's Adam (main stream), not beside it: both are HBM-bound, and run side
@@ -262,7 +276,8 @@ class CTClipTrainer:
         if not self._guard:
             return
         host = self._ln_host[self.steps % len(self._ln_host)]
-        host.copy_(K.ln_status_tensor(self.device), non_blocking=True)
+        # the step's skip word (the ranks' summed status): every rank raises for the same step
+        host.copy_(self.skip_ring[self.steps % 4:self.steps % 4 + 1], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         self._ln_pending.append((self.steps, ev, host))
@@ -280,19 +295,21 @@ class CTClipTrainer:
             if int(host[0]) != 0:
                 self._ln_pending.clear()
                 raise LayerNormExchangeError(
-                    f'LayerNorm-fused GEMM exchange timed out (status word set by step {step} or earlier): '
-                    'its LayerNorm outputs were wrong and the Adam update of that step was skipped on the '
-                    'device; kernels.reset_ln_status() clears the word (CTCLIP_LN_FUSED=0 runs the unfused '
-                    'GEMM + LayerNorm pair instead)')
+                    f'LayerNorm-fused GEMM exchange timed out (status word set by step {step} or earlier, on '
+                    'this rank or another: the ranks\' words are summed with the gradients): its LayerNorm '
+                    'outputs were wrong and the Adam update of that step was skipped on every rank; '
+                    'kernels.reset_ln_status() clears the word (CTCLIP_LN_FUSED=0 runs the unfused GEMM + '
+                    'LayerNorm pair instead)')
             self.ln_steps_checked = step
 
     def _adam(self, off, n, step=None):
         sl = slice(off, off + n)
+        st = self.steps if step is None else step
         K.adam(self.flat.data[sl], self.flat.grad[sl], self.m[sl], self.v[sl], lr=self.lr, b1=self.betas[0],
                b2=self.betas[1], eps=self.eps, wd=self.wd, step=self.steps if step is None else step, coef=self.norm,
                p_bf16=self.flat.bf16[sl] if self.flat.bf16 is not None else None,
                p_bf16_lo=self.flat.bf16_lo[sl] if self.flat.bf16_lo is not None else None, zero_grad=True,
-               skip=K.ln_status_tensor(self.device) if self._guard else None)
+               skip=self.skip_ring[st % 4:st % 4 + 1] if self._guard else None)
         self.flat.sync_shadows(off, off + n)
 
     def train_step(self, text, video):

@@ -26,6 +26,9 @@ extern "C" {
 /* ---------------------------------------------------------------- version / probe */
 int ctclip_version(void);          /* ABI version */
 int ctclip_device_arch(char* buf, int n); /* writes gcnArchName of the current device */
+/* test knob: nwg workgroups, each holding lds_bytes of a CU's LDS, spin for `cycles` shader clocks on
+ * `stream` (a stand-in for resident RCCL kernels occupying CUs beside a persistent GEMM) */
+int ctclip_debug_hold_cus(int32_t nwg, int64_t cycles, int32_t lds_bytes, void* stream);
 
 /* ---------------------------------------------------------------- dense GEMM (MFMA)
  * C[m, n] = epilogue( alpha * sum_k A[m, k] * B[k, n] )   bf16 x bf16 -> f32 accumulate.

@@ -346,3 +346,68 @@ def _eval_worker(rank, port, out_dir):
 def test_two_rank_eval_call_issues_no_collective(tmp_path):
     mp.spawn(_eval_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
     assert all((tmp_path / f'ok{r}').exists() for r in range(WORLD))
+
+
+# ------------------------------------------------------------------ rank-consistent step skip
+def _adam_ref(p, g, m, v, lr, step, skip, b1=0.9, b2=0.99, eps=1e-8):
+    """torch restatement of the Adam kernel's update under its skip guard (optim.hip): a skipped
+    step leaves p, m, v untouched and clears the gradient."""
+    if not skip:
+        m.mul_(b1).add_(g, alpha=1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        mh = m / (1 - b1 ** step)
+        vh = v / (1 - b2 ** step)
+        p.sub_(lr * mh / (vh.sqrt() + eps))
+    g.zero_()
+
+
+def _status_worker(rank, port, out_dir, bad_rank):
+    """A LayerNorm-exchange timeout on ONE rank (its status word set) must stop the step on EVERY
+    rank: the word rides the last gradient bucket's SUM all-reduce (dist_sync.BucketedGradSync
+    status slot, trainer.FlatParams.status), every rank reads the same summed slot as its Adam skip
+    guard and raises for the same step, and the parameter arenas stay bit-identical across ranks."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=WORLD)
+    try:
+        from ctclip_mi355x import dist_sync
+        from ctclip_mi355x.trainer import FlatParams
+        g = torch.Generator().manual_seed(3)
+        ps = [torch.nn.Parameter(torch.randn(5, 4, generator=g)), torch.nn.Parameter(torch.randn(7, generator=g))]
+        flat = FlatParams(ps, torch.device('cpu'))
+        segs = [('a', 0, 20), ('b', 20, 7)]
+        word = torch.zeros(1, dtype=torch.int32)
+        gs = dist_sync.BucketedGradSync(flat.grad, segs, status=(flat.status, lambda: word))
+        m, v = torch.zeros(flat.numel), torch.zeros(flat.numel)
+        decisions = []
+        for step in (1, 2, 3):
+            # rank-local gradients (different on each rank), then the step's exchange
+            torch.manual_seed(100 * step + rank)
+            flat.grad[:flat.numel].copy_(torch.randn(flat.numel))
+            if rank == bad_rank and step == 2:
+                word.fill_(1)                  # this rank's fused LayerNorm exchange timed out
+            gs.arm()
+            gs.finish()
+            skip = bool(flat.status.item() != 0)
+            decisions.append(skip)
+            _adam_ref(flat.data, flat.grad[:flat.numel], m, v, 1e-2, step, skip)
+        # the word is sticky: steps 2 and 3 are skipped on both ranks, step 1 applied on both
+        assert decisions == ([False, False, False] if bad_rank < 0 else [False, True, True]), decisions
+        assert float(flat.status) == (0.0 if bad_rank < 0 else 1.0)
+        both = [torch.empty_like(flat.data) for _ in range(WORLD)]
+        dist.all_gather(both, flat.data)
+        assert torch.equal(both[0], both[1])
+        open(os.path.join(out_dir, f'ok{rank}'), 'w').close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_status_word_skips_every_rank(tmp_path):
+    """Rank 1's LayerNorm exchange times out at step 2: both ranks skip steps 2 and 3 together."""
+    mp.spawn(_status_worker, args=(_free_port(), str(tmp_path), 1), nprocs=WORLD, join=True)
+    assert all((tmp_path / f'ok{r}').exists() for r in range(WORLD))
+
+
+def test_two_rank_status_word_clean(tmp_path):
+    """No timeout anywhere: the summed status slot stays 0 and every step is applied on both ranks."""
+    mp.spawn(_status_worker, args=(_free_port(), str(tmp_path), -1), nprocs=WORLD, join=True)
+    assert all((tmp_path / f'ok{r}').exists() for r in range(WORLD))

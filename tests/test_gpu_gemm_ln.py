@@ -221,7 +221,34 @@ def test_train_step_raises_on_exchange_timeout(K):
         assert K.ln_fused_status() == 1
         assert torch.equal(tr.flat.data, before) and torch.equal(tr.m, m_before), \
             'a step with a timed-out LayerNorm exchange was applied'
-        assert float(tr.flat.grad.abs().max()) == 0.0      # the dropped step's gradients were cleared
+        assert float(tr.flat.grad[:tr.flat.numel].abs().max()) == 0.0   # the dropped step's gradients were cleared
+        assert float(tr.flat.status) == 1.0               # this rank's status word, summed (world 1)
     finally:
         K.linear_residual_ln = orig
         K.reset_ln_status()
+
+
+@pytest.mark.parametrize('nwg,lds_kb', [(16, 80), (64, 80), (200, 100)])
+def test_fused_ln_beside_cu_holding_kernels(K, nwg, lds_kb):
+    """The LayerNorm-fused GEMM pairs tiles 2k, 2k + 1 on workgroups w, w ^ 8 of one persistent round.
+    With other kernels holding CUs (here nwg spinning workgroups, each with enough LDS that no GEMM
+    workgroup fits beside it -- as RCCL's resident kernels at N > 1), some GEMM workgroups start only
+    when CUs free up; their partners wait (bounded) instead of timing out, and the outputs equal the
+    undisturbed launch bit for bit with the status word still 0."""
+    from ctclip_mi355x import _lib
+    o, W, res, gamma, beta = _fwd_case(110592, 256, 9)
+    K.reset_ln_status()
+    with K.ln_guard():
+        ref = K.linear_residual_ln(o, W, res, gamma, beta, 1e-5)
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    # ~1 ms of spinning at ~2.1 GHz, started first so it holds its CUs when the GEMM dispatches
+    with torch.cuda.stream(side):
+        _lib.call('ctclip_debug_hold_cus', nwg, 2_000_000, lds_kb * 1024, side.cuda_stream)
+    with K.ln_guard():
+        out = K.linear_residual_ln(o, W, res, gamma, beta, 1e-5)
+    torch.cuda.synchronize()
+    assert out is not None
+    for a, b in zip(out, ref):
+        assert torch.equal(a, b)
+    assert K.ln_fused_status() == 0
