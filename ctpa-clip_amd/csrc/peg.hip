@@ -589,8 +589,11 @@ __global__ __launch_bounds__(XNT, CTCLIP_PEGX_WAVES) void peg_fwd32_kernel(const
         }
       }
     }
-    // slot (p + 1) & 1 was last read in step p - 1, before the barrier that ended it: one barrier
-    // per step (after the store) orders the new plane before its reads
+    // slot (p + 1) & 1 holds plane p - 1.  lead 0: last read in step p - 1, before the barrier that
+    // ended it, so one barrier per step (after the store) orders the new plane before its reads.
+    // lead 1 (the temporal map's canonical walk): this step's finalize just read plane p - 1's centre
+    // row (the residual of output p - 1), so the store waits for every thread's finalize first
+    if constexpr (lead > 0) __syncthreads();
     if (p + 1 < g.T) xplane_store(smem + ((p + 1) & 1) * pb, g.W, reg, nvalid);
     __syncthreads();
   };

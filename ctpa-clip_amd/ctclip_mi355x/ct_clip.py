@@ -21,6 +21,10 @@ from . import streams
 
 # queue BERT's forward before the image tower's (A/B switch, default: image tower first)
 TEXT_FWD_FIRST = os.environ.get('CTCLIP_TEXT_FWD_FIRST', '0') != '0'
+# BERT's forward (text stream) starts after the image tower's patch embedding instead of with it: the
+# patch LayerNorm is HBM-bound (0.43 ms alone, ~1.1 ms beside BERT's first kernels in round 4) and BERT
+# is hidden behind the 3D-ViT either way.  CTCLIP_TEXT_GATE=0: start together (A/B).
+TEXT_GATE = os.environ.get('CTCLIP_TEXT_GATE', '1') != '0'
 
 
 class _nullctx:
@@ -134,6 +138,9 @@ class CTCLIP(nn.Module):
             pooled, pooled_b = self.visual_transformer.encode_pooled(image)
         else:
             pooled, pooled_b = self.visual_transformer.encode_pooled(image)
+            gate = getattr(self.visual_transformer, '_patch_done', None)
+            if TEXT_GATE and ready is not None and gate is not None:
+                ready = gate
             enc_text = self.text_transformer(text.input_ids, attention_mask=text.attention_mask, join=False,
                                              ready=ready)[0]
         ts = streams.text_stream(dev)

@@ -130,7 +130,7 @@ def test_peg(K, mode, shape, D):
 
 @pytest.mark.parametrize('mode', [0, 1])
 @pytest.mark.parametrize('shape,D', [((2, 6, 5, 7), 128), ((1, 24, 24, 24), 512), ((2, 24, 24, 24), 64),
-                                     ((1, 3, 4, 40), 64), ((2, 2, 3, 4), 24)])
+                                     ((8, 24, 24, 24), 512), ((1, 3, 4, 40), 64), ((2, 2, 3, 4), 24)])
 def test_peg_x32(K, mode, shape, D):
     """The f32-tap PEG forward (ctclip_peg_fwd_x32): f32 x (not bf16-representable) against the torch
     fp32 conv, its 16-bit copies the casts of its f32 output, and the LayerNorm statistics of the
@@ -144,6 +144,10 @@ def test_peg_x32(K, mode, shape, D):
     outf, outb, outh, mean, rstd = K.peg_fwd_x32(xf, *shape, w, b, mode, stats=tiled, want_f16=True)
     ref = _peg_ref(xf, w, b, shape, mode)
     assert rel(outf, ref) < 1e-5
+    # repeat: bit-identical (the plane ring has no read / overwrite race; the temporal map's walk
+    # reads the previous plane's centre row in the step that overwrites its slot)
+    for _ in range(3):
+        assert torch.equal(K.peg_fwd_x32(xf, *shape, w, b, mode)[0], outf)
     assert torch.equal(outb, outf.bfloat16()) and torch.equal(outh, outf.half())
     if tiled:
         var, mu = torch.var_mean(outf.double(), dim=1, unbiased=False)
