@@ -163,7 +163,10 @@ def test_vq_free_running_contract(base):
           f'pre-VQ |dxn| median {tok_err.median().item():.3e} max {tok_err.max().item():.3e}')
     unexplained = (gap > bound + 1e-6).sum().item()
     assert unexplained == 0, unexplained
-    assert diff.numel() < 0.05 * n
+    # round 5 (fp16 forward GEMMs + f32-tap PEG): 250 of 27,648 above the 1e-6 margin
+    # (667 with the all-bf16 tower of round 4); pre-VQ |dxn| median 4.6e-3 (1.07e-2)
+    assert (gap >= 1e-6).sum().item() < 400
+    assert diff.numel() < 0.02 * n
 
 
 def test_latents_and_loss_full_size(base):
@@ -191,13 +194,12 @@ def test_latents_and_loss_full_size(base):
     # codebook row, so they meet 1e-3 once the indices agree (forced, below) or in the f32 image
     # mode (test_f32_image_mode_vq_contract)
     assert dt < 1e-3
-    # free-running loss of the bf16 image tower: ~2.3 % of the VQ indices flip on near-ties (1e-2
-    # pre-VQ error) and every flip swaps a codebook row into the pooled latent, so |dloss| is a
-    # chaotic function of the kernels' rounding: 4.1e-4 and 1.4e-3 measured for two bit-different
-    # attention kernels of equal accuracy (profiles/r03c, r03d).  The north-star 1e-3 holds on the
-    # same indices (below) and free-running in the f32 image tower (test_f32_image_mode_vq_contract)
-    assert dl < 3e-3
-    assert di < 0.1 and dlog < 0.15
+    # free-running loss: every VQ index that flips on a near-tie swaps a codebook row into the pooled
+    # latent, so |dloss| scales with the flip count.  Round 5's fp16 forward GEMMs + f32-tap PEG cut
+    # the pre-VQ error 1.07e-2 -> 4.6e-3 and the flips 667 -> 250 (0.9 %): loss |d| 4.7e-4 measured
+    # (round 4's all-bf16 tower: 1.9e-3).  The north-star 1e-3, free-running:
+    assert dl < 1e-3
+    assert di < 0.04 and dlog < 0.04
     with torch.no_grad():
         forced = O.ctclip_forward(sd, base['ids'], base['mask'], O.normalize_hu(base['hu']), CFG,
                                   training=False, force_ind=idx)
