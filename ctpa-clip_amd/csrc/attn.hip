@@ -985,7 +985,16 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_bias_kernel(AP p, int nfc) {
 //    straight-line chunk code (254 VGPRs, no spills; 12 waves x 3 parts spill at the 168 cap);
 //  * the dQ exchange of the key parts reuses the finished frame's buffer; the bias bins reuse
 //    buffer 0 after the last frame.
+// KP = 3 (12 waves, 6 chunks per key part, 48 accumulator registers instead of 72): 168 VGPRs +
+// 140 B of scratch per lane whose per-frame reloads wait behind the LDS-DMA queue -- 887 vs 697 us
+// per spatial backward (profiles/r05e_attn_kp_ab.log), so 8 waves stay
 constexpr int DQD_W = 8, DQD_NT = DQD_W * 64, DQD_KP = 2;
+// key positions of the bias reads: 1 = kb_fast (VALU), 0 = the LDS table (A/B build switch).
+// Measured (profiles/r05d_attn_ab.log): the table, 699-705 us per spatial backward vs 718 for
+// kb_fast, whose per-chunk VALU spills 40 -> 56 B per lane at this kernel's 256-VGPR budget
+#ifndef CTCLIP_ATTN_DQ_KBFAST
+#define CTCLIP_ATTN_DQ_KBFAST 0
+#endif
 // bias-gradient binning of the dQ kernel: 1 = diagonal sums over an LDS image of the block's
 // frame-summed dS (no LDS float atomics); 0 = LDS atomics per (query, key) (A/B build switch).
 // Measured (profiles/r02ba_attn_bin_ab.log): spatial backward 837 -> 807 us per layer; without
@@ -993,13 +1002,13 @@ constexpr int DQD_W = 8, DQD_NT = DQD_W * 64, DQD_KP = 2;
 #ifndef CTCLIP_ATTN_DIAG_BIN
 #define CTCLIP_ATTN_DIAG_BIN 1
 #endif
-template <int LF>
-__global__ __launch_bounds__(DQD_NT) void attn_bwd_dq_bias_dma_kernel(AP p, int nfc) {
+template <int LF, int KP = DQD_KP>
+__global__ __launch_bounds__(4 * KP * 64) void attn_bwd_dq_bias_dma_kernel(AP p, int nfc) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int D = 32, DB = 2, L = LF, NC = L / 32, KP = DQD_KP, NCP = NC / KP, NTH = DQD_NT;
-  constexpr int IMG = L * 64, BUF = 2 * IMG, NG = BUF / 1024 / DQD_W;   // glds per wave per frame
-  static_assert(L % 64 == 0 && NC % KP == 0 && (BUF / 1024) % DQD_W == 0 && (IMG / 1024) % NG == 0,
-                "full-shape specialisation");
+  constexpr int D = 32, DB = 2, L = LF, NC = L / 32, NCP = NC / KP, NW = 4 * KP, NTH = NW * 64;
+  constexpr int IMG = L * 64, BUF = 2 * IMG, NG = BUF / 1024 / NW;   // glds per wave per frame
+  static_assert(L % 64 == 0 && NC % KP == 0 && (BUF / 1024) % NW == 0 && (IMG / 1024) % NG == 0 &&
+                (KP - 1) * 4 * 64 * 8 * 4 <= BUF, "full-shape specialisation");
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int h = blockIdx.x, qg = blockIdx.y, fc = blockIdx.z;
   const int qsub = w & 3, kpart = w >> 2;
@@ -1047,6 +1056,7 @@ __global__ __launch_bounds__(DQD_NT) void attn_bwd_dq_bias_dma_kernel(AP p, int 
   __builtin_amdgcn_s_barrier();   // tables (frame f0's DMA may still be in flight)
   __builtin_amdgcn_sched_barrier(0);
   const int cq = kb[q] + boff(p);
+  [[maybe_unused]] const KbFast kbf = kb_fast_init(p);
   for (int s = f0; s < f1; ++s) {
     const int b = (s - f0) & 1;
     const char* Kimg = smem + b * BUF;
@@ -1096,8 +1106,16 @@ __global__ __launch_bounds__(DQD_NT) void attn_bwd_dq_bias_dma_kernel(AP p, int 
       }
 #pragma unroll
       for (int bi = 0; bi < 2; ++bi) {
-        const int k0 = kc + 16 * bi + 4 * g;
+        int k0 = kc + 16 * bi + 4 * g;
+#if CTCLIP_ATTN_DQ_KBFAST
+        asm volatile("" : "+v"(k0));   // computed here, per chunk: hoisted out of the frame loop the
+                                       // 18 positions spill
+        // up[3 - r] = ub[bin(q, k0 + r)] (RUN); the key's position by VALU, not a table read the
+        // bias read's address would wait on (a two-deep LDS chain per chunk)
+        const float* up = ub + (cq - kb_fast(kbf, k0) - 3);
+#else
         const float* up = ub + (cq - kb[k0] - 3);   // up[3 - r] = ub[bin(q, k0 + r)] (RUN)
+#endif
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float x = sa[bi][r] * sc2 + up[3 - r];
@@ -1151,7 +1169,11 @@ __global__ __launch_bounds__(DQD_NT) void attn_bwd_dq_bias_dma_kernel(AP p, int 
   // free now: 64 x 576 x 4 B = 147,456 B = 2 BUF), then each thread sums whole bins along their
   // diagonals, bin (dh, dw) = sum over the 64 queries q of dS[q][q - (dh, dw)], in a fixed order
   {
-    static_assert(64 * L * 4 <= 2 * BUF, "dS block fits the two frame buffers");
+    // rows padded to LP = L + 3 floats: the 16 query rows of a half-wave's stores land in distinct
+    // banks (an L-float stride put all 16 in one); the image may run over the bias / position
+    // tables after the frame buffers, which nothing reads any more
+    constexpr int LP = L + 3;
+    static_assert(64 * LP * 4 <= 2 * BUF + 4 * (2209 + 3) + 4 * L, "dS block fits the buffers and tables");
     float* S = (float*)smem;
     const int ql = qsub * 16 + li;
 #pragma unroll
@@ -1159,17 +1181,23 @@ __global__ __launch_bounds__(DQD_NT) void attn_bwd_dq_bias_dma_kernel(AP p, int 
 #pragma unroll
       for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) S[ql * L + (c_begin + ci) * 32 + 16 * bi + 4 * g + r] = acc[ci][bi][r];
+        for (int r = 0; r < 4; ++r) S[ql * LP + (c_begin + ci) * 32 + 16 * bi + 4 * g + r] = acc[ci][bi][r];
     __syncthreads();
     const int Wg = p.Wg, Hg = p.Hg, W2 = 2 * Wg - 1, q0 = qg * 64;
+    const int r_lo = q0 / Wg, r_hi = (q0 + 63) / Wg;
     for (int b = tid; b < p.nbins; b += NTH) {
       const int dh = b / W2 - (Hg - 1), dw = b % W2 - (Wg - 1);
       float sum = 0.f;
-      int qh = q0 / Wg, qw = q0 - (q0 / Wg) * Wg;
-      for (int j = 0; j < 64; ++j) {
-        const int kh = qh - dh, kw = qw - dw;
-        if (kh >= 0 && kh < Hg && kw >= 0 && kw < Wg) sum += S[j * L + kh * Wg + kw];
-        if (++qw == Wg) { qw = 0; ++qh; }
+      // bin (dh, dw) = sum over the block's queries q = (qh, qw) of dS[q][(qh - dh, qw - dw)]: per
+      // grid row of the block, the queries with an in-grid key are one qw run, and their entries
+      // one diagonal of the image (stride LP + 1); q ascends as in the per-query walk it replaces
+      // (same sum, same order: only the 3 / 4 of (query, bin) pairs without a key are skipped)
+      for (int r = r_lo; r <= r_hi; ++r) {
+        const int kh = r - dh;
+        if (kh < 0 || kh >= Hg) continue;
+        const int lo = max(max(q0 - r * Wg, 0), dw), hi = min(min(q0 + 63 - r * Wg, Wg - 1), Wg - 1 + dw);
+        const float* sp = S + (r * Wg - q0) * LP + kh * Wg - dw;
+        for (int qw = lo; qw <= hi; ++qw) sum += sp[qw * (LP + 1)];
       }
       if (p.dbias_ws) p.dbias_ws[((int64_t)(qg * nfc + fc) * p.H + h) * p.nbins + b] = sum;
       else if (sum != 0.f) atomicAdd(&p.dbias_u[(int64_t)h * p.nbins + b], sum);
@@ -1335,6 +1363,145 @@ __global__ __launch_bounds__(DKP_NT) void attn_bwd_dkv_persist_kernel(AP p) {
 }
 #undef CT_DKV_LOAD
 
+// --------------------------- backward dK dV, biased, base spatial shape, LDS-DMA staged (round 5)
+// attn_bwd_dkv_persist_kernel with the next frame's Q / dO images landing in a second LDS buffer by
+// LDS-DMA (6 x 1 KB per wave, the dQ kernel's swizzled 64-B rows) instead of through 6 x 16 B of
+// staging registers per thread: at the 168-VGPR cap of 12 waves those registers went to scratch
+// right after their loads (112 B per lane), so every frame's staging latency was paid in full.
+// The frame's lse / delta still come through registers (2 floats per thread) into one LDS copy,
+// written between two barriers.  The K / V fragments of a wave's next key block -- the next
+// frame's first one during its last block -- are loaded one block ahead; their first use also
+// drains the DMA queue (hipcc cannot see it), which gives the next frame's images one key block
+// (of three) to land.  Same arithmetic and results as the persist kernel.
+// LDS: 2 x (Q + dO) 147,456 + lse / delta 4,608 + bias 8,848 + positions 2,304 = 163,216 B.
+constexpr int DKD_W = 12, DKD_NT = DKD_W * 64;
+template <int LF>
+__global__ __launch_bounds__(DKD_NT) void attn_bwd_dkv_dma_kernel(AP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int D = 32, DB = 2, W = DKD_W, NTH = DKD_NT, L = LF, NKB = L / 16;
+  constexpr int IMG = L * 64, BUF = 2 * IMG, NG = BUF / 1024 / W;   // 1-KB DMA rows per wave per frame
+  static_assert(L % 32 == 0 && BUF % (1024 * W) == 0 && IMG % (1024 * NG) == 0 && NKB >= W, "full shape");
+  const int tid = threadIdx.x, lane = tid & 63, wi = tid >> 6;
+  const int h = blockIdx.x % p.H, wg = blockIdx.x / p.H, nwg = gridDim.x / p.H;
+  float* ls = (float*)(smem + 2 * BUF);
+  float* dls = ls + L;
+  float* ub = dls + L;
+  const int nb4 = (p.nbins + 3) & ~3;
+  int* kb = (int*)(ub + nb4);
+  for (int i = tid; i < p.nbins; i += NTH) ub[i] = p.bias_u[(int64_t)h * p.nbins + i] * LOG2E;
+  for (int i = tid; i < L; i += NTH) kb[i] = kb_of(p, i);
+  const int g = lane >> 4, li = lane & 15;
+  const float sc2 = p.scale * LOG2E;
+  const KbFast kbf = kb_fast_init(p);
+  // DMA map: instruction j of wave wi fills bytes [(wi NG + j) KB, +1 KB) of a buffer (Q image below
+  // IMG, dO above: wave-uniform), lane l the 16 B at + 16 l: row, swizzled chunk
+  auto stage_frame = [&](int s, int b) {
+    const int64_t fb = (int64_t)s * p.s_outer;   // spatial: row(s, i) = s * s_outer + i (host-checked)
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+      const int pos = (wi * NG + j) * 1024 + lane * 16;
+      const bool isd = pos >= IMG;
+      const int pi = isd ? pos - IMG : pos, row = pi >> 6, ch = ((pi >> 4) & 3) ^ kv_swz(row);
+      const u16* src = isd ? p.dout + (fb + row) * p.lddo : p.q + (fb + row) * p.ldq;
+      glds16_asm(src + h * D + ch * 8, smem + b * BUF + (wi * NG + j) * 1024);
+    }
+  };
+  float lsv = 0.f, dlv = 0.f;   // this thread's lse / delta row of the next frame (tid < L)
+  bf16x8 kf = zero8(), vf = zero8();
+  auto load_kv = [&](int s, int kbk) {
+    const int64_t krow = (int64_t)s * p.s_outer + kbk * 16 + li;
+    kf = gload8(p.k + krow * p.ldk + h * D + 8 * g);
+    vf = gload8(p.v + krow * p.ldv + h * D + 8 * g);
+  };
+  int s = wg;
+  if (s < p.nseq) {
+    stage_frame(s, 0);
+    if (tid < L) {
+      lsv = p.lse[(int64_t)h * p.M + (int64_t)s * p.s_outer + tid];
+      dlv = p.delta[(int64_t)h * p.M + (int64_t)s * p.s_outer + tid];
+    }
+    load_kv(s, wi);
+  }
+  for (int it = 0; s < p.nseq; s += nwg, ++it) {
+    const int b = it & 1;
+    // this wave's DMA of frame s (and its lse / delta / first K V registers) landed; after the
+    // barrier every wave's has, and every wave is past frame s - nwg (lse / delta copy and the
+    // other buffer free)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid < L) {
+      ls[tid] = lsv * LOG2E;
+      dls[tid] = dlv;
+    }
+    __syncthreads();
+    const int sn = s + nwg;
+    if (sn < p.nseq) {
+      stage_frame(sn, b ^ 1);
+      if (tid < L) {
+        lsv = p.lse[(int64_t)h * p.M + (int64_t)sn * p.s_outer + tid];
+        dlv = p.delta[(int64_t)h * p.M + (int64_t)sn * p.s_outer + tid];
+      }
+    }
+    const char* Qimg = smem + b * BUF;
+    const char* Dimg = Qimg + IMG;
+    const int64_t fb = (int64_t)s * p.s_outer;
+    for (int kbk = wi; kbk < NKB; kbk += W) {
+      const bf16x8 kc = kf, vc = vf;
+      if (kbk + W < NKB) load_kv(s, kbk + W);
+      else if (sn < p.nseq) load_kv(sn, wi);
+      const int key = kbk * 16 + li;
+      const int ck = kb[key] - boff(p);   // bin(q, key) = kb[q] - ck
+      f32x4 dk[DB], dv[DB];
+#pragma unroll
+      for (int d = 0; d < DB; ++d) { dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[d] = f32x4{0.f, 0.f, 0.f, 0.f}; }
+      for (int qc = 0; qc < L; qc += 32) {
+        f32x4 sa[2], da[2];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi) {
+          sa[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Qimg, qc + 16 * bi, lane), kc,
+                                                           f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          da[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Dimg, qc + 16 * bi, lane), vc,
+                                                           f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        }
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi) {
+          const int q0 = qc + 16 * bi + 4 * g;
+          const f32x4 lv = *(const f32x4*)(ls + q0);
+          const f32x4 dlq = *(const f32x4*)(dls + q0);
+          const float* up = ub + (kb_fast(kbf, q0) - ck);   // up[r] = ub[bin(q0 + r, key)]
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float x = sa[bi][r] * sc2 + up[r];
+            const float pr = fexp2(x - lv[r]);
+            const float ds = pr * (da[bi][r] - dlq[r]);
+            sa[bi][r] = pr;
+            da[bi][r] = ds;   // the score scale is applied once per dK output below (exact for 8)
+          }
+        }
+        const bf16x8 pa = pack_perm(sa[0], sa[1]);
+        const bf16x8 dsa = pack_perm(da[0], da[1]);
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+          dv[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, trfrag_sw(Dimg, qc, d * 16, lane), dv[d], 0, 0, 0);
+          dk[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(dsa, trfrag_sw(Qimg, qc, d * 16, lane), dk[d], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < DB; ++d) dk[d] *= p.scale;
+      // C[key][d]: rows = keys kbk*16 + 4g + r, col = d*16 + li
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = fb + kbk * 16 + 4 * g + r;
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+          p.dk[row * p.lddk + h * D + d * 16 + li] = f2bf(dk[d][r]);
+          p.dv[row * p.lddv + h * D + d * 16 + li] = f2bf(dv[d][r]);
+        }
+      }
+    }
+  }
+}
+
 bool s_attr = false;
 
 template <int D, bool BIAS>
@@ -1359,6 +1526,8 @@ void set_attrs() {
   (void)hipFuncSetAttribute((const void*)attn_bwd_dq_bias_dma_kernel<576>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_persist_kernel<576>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_dma_kernel<576>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<32, true, 12, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -1465,9 +1634,17 @@ void launch_dkv(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
     if (persist < 0) { const char* e = getenv("CTCLIP_ATTN_DKV_PERSIST"); persist = e ? atoi(e) != 0 : 1; }
     if (persist && run_ok(p) && p.L == 576 && p.s_pos == 1 && p.n_inner == 1 && p.pp == 1 && !p.kmask &&
         p.nseq >= 2 && 256 % p.H == 0) {
+      const int per_head = std::min(p.nseq, 256 / p.H);
+      // LDS-DMA staged variant (CTCLIP_ATTN_DKV_DMA=0: the register-staged persist kernel; A/B)
+      static int dma = -1;
+      if (dma < 0) { const char* e = getenv("CTCLIP_ATTN_DKV_DMA"); dma = e ? atoi(e) != 0 : 1; }
+      const size_t lds_d = (size_t)4 * 576 * 64 + 2 * 576 * 4 + (size_t)((p.nbins + 3) & ~3) * 4 + 576 * 4;
+      if (dma && lds_d <= 160 * 1024) {
+        hipLaunchKernelGGL((attn_bwd_dkv_dma_kernel<576>), dim3(per_head * p.H), dim3(DKD_NT), lds_d, st, p);
+        return;
+      }
       const size_t lds_p = (size_t)2 * 576 * 64 + 2 * 576 * 4 + (size_t)((p.nbins + 3) & ~3) * 4 + 576 * 4;
       if (lds_p <= 160 * 1024) {
-        const int per_head = std::min(p.nseq, 256 / p.H);
         hipLaunchKernelGGL((attn_bwd_dkv_persist_kernel<576>), dim3(per_head * p.H), dim3(DKP_NT), lds_p, st, p);
         return;
       }
