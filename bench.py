@@ -171,7 +171,7 @@ def rocprof_avg_ms(key):
     return None, None, None
 
 
-PMC_TAG = 'r04t'   # tools/pmc_gemm.sh <shape> <tag> on the current tree -> profiles/pmc_<tag>_<shape>.json
+PMC_TAG = 'r05g'   # tools/pmc_gemm.sh <shape> <tag> on the current tree -> profiles/pmc_<tag>_<shape>.json
 
 
 def pmc_record(shape, kernel_key):
@@ -375,6 +375,13 @@ def main():
                           'devices_visible': torch.cuda.device_count()}
     if args.dist_backend != 'nccl':
         result['note'] = f'{args.dist_backend} rehearsal: {world} ranks on {torch.cuda.device_count()} GPU(s)'
+    # kernel names in the rocprof summary / counter records: the 8-phase kernel's fourth template
+    # argument is its fp16-operand flag (the default 3D-ViT forward, functional.vit_f16, round 5)
+    from ctclip_mi355x import functional as Fn
+    h16 = (Fn.vit_f16() and Fn._LN1_FOLD and Fn._PEG_X32 and not args.fp8 and not args.f32_tower)
+    ff1_key = f'gemm8p_kernel<true, true, 2, {"true" if h16 else "false"}>'
+    ff1_shape = 'ff1h16' if h16 else 'ff1'
+    dw_key = 'gemm8p_kernel<false, false, -5, false>'
     if ff1:
         tflops = ff1['flops'] / (ff1['avg_ms'] * 1e-3) / 1e12
         M = args.batch * 24 * 24 * 24
@@ -382,14 +389,15 @@ def main():
         # counter record of the SAME kernel (tools/pmc_gemm.sh ff1 -> tools/pmc_gemm_json.py): used only
         # when its kernel name matches the one reported here
         traffic, traffic_src, mfma_busy = None, None, None
-        rec = pmc_record('ff1', 'gemm8p_kernel<true, true, 2>') if args.batch == 8 else None
+        rec = pmc_record(ff1_shape, ff1_key) if args.batch == 8 else None
         if rec:
             traffic = round(rec['traffic_bytes_per_launch'] / 1e9, 4)
             mfma_busy = round(rec['mfma_busy'], 4)
             traffic_src = (f'{rec["_src"]} (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch; '
                            'mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / SIMD-cycles)')
         result['roofline'] = {
-            'kernel': 'g256::gemm8p_kernel<true,true,2> FF1 (LN-out x W1^T, GEGLU epilogue)',
+            'kernel': f'g256::{ff1_key} FF1 (LN-out x W1^T, GEGLU epilogue'
+                      f'{", fp16 operands and h" if h16 else ""})',
             'bound': 'mfma', 'achieved': round(tflops, 1), 'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
             'frac': round(tflops / PEAK_BF16_TFLOPS, 4), 'traffic': traffic, 'traffic_unit': 'GB',
             'traffic_source': traffic_src, 'mfma_busy': mfma_busy, 'algorithmic_bytes': algo_bytes,
@@ -398,7 +406,7 @@ def main():
             'launches': ff1['launches'], 'timing': 'HIP events around each launch on its stream, timed region'}
         # headline = the committed rocprofv3 summary's average for the same kernel (the judge's
         # reference clock); the live HIP-event figures stay beside it as live_*
-        rp_ms, rp_calls, rp_src = rocprof_avg_ms('gemm8p_kernel<true, true, 2>')
+        rp_ms, rp_calls, rp_src = rocprof_avg_ms(ff1_key)
         if rp_ms and args.batch == 8:
             rtf = ff1['flops'] / (rp_ms * 1e-3) / 1e12
             result['roofline'].update({
@@ -412,12 +420,12 @@ def main():
         # GEMM, 33 launches per step of five shapes (3D-ViT Q | K | V / attention-out / FF1 / FF2 dW per
         # layer + the patch-embed dW); achieved = their algorithmic flops / their summed durations
         tf = dw['total_flops'] / (dw['total_ms'] * 1e-3) / 1e12
-        rec = pmc_record('dwtn', 'gemm8p_kernel<false, false, -5>') if args.batch == 8 else None
+        rec = pmc_record('dwtn', dw_key) if args.batch == 8 else None
         # FF1-shape dW launch (2816 x 512 x 110592): algorithmic = dy + x bf16 reads + 11 f32 split-K
         # slabs (kernels.matmul_tn: 256 // 22 tiles)
         dw_algo = 2 * (args.batch * 13824 * (2816 + 512)) + 4 * 2816 * 512 * 11
         result['roofline_dominant'] = {
-            'kernel': 'g256::gemm8p_kernel<false,false,-5> split-K weight-gradient GEMMs (all launches of a step)',
+            'kernel': f'g256::{dw_key} split-K weight-gradient GEMMs (all launches of a step)',
             'bound': 'mfma', 'achieved': round(tf, 1), 'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
             'frac': round(tf / PEAK_BF16_TFLOPS, 4),
             'traffic': round(rec['traffic_bytes_per_launch'] / 1e9, 4) if rec else None, 'traffic_unit': 'GB',
@@ -428,7 +436,7 @@ def main():
             'avg_launch_ms': round(dw['total_ms'] / dw['launches'], 4),
             'launches_per_step': round(dw['launches'] / args.steps, 2),
             'flops_per_step': round(dw['total_flops'] / args.steps)}
-        rp_ms, rp_calls, rp_src = rocprof_avg_ms('gemm8p_kernel<false, false, -5>')
+        rp_ms, rp_calls, rp_src = rocprof_avg_ms(dw_key)
         # the rocprof average only prices this launch mix when the summary holds whole steps of it
         # (a summary of an older tree with another launch count per step would mis-state the frac)
         per_step = dw['launches'] // args.steps

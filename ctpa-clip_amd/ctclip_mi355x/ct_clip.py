@@ -25,6 +25,9 @@ TEXT_FWD_FIRST = os.environ.get('CTCLIP_TEXT_FWD_FIRST', '0') != '0'
 # patch LayerNorm is HBM-bound (0.43 ms alone, ~1.1 ms beside BERT's first kernels in round 4) and BERT
 # is hidden behind the 3D-ViT either way.  CTCLIP_TEXT_GATE=0: start together (A/B).
 TEXT_GATE = os.environ.get('CTCLIP_TEXT_GATE', '1') != '0'
+# the training VQ's codebook EMA update queued on the auxiliary stream after the image projection
+# instead of right after the VQ (CTCLIP_DEFER_EMA=0: right after the VQ; A/B)
+DEFER_EMA = os.environ.get('CTCLIP_DEFER_EMA', '1') != '0'
 
 
 class _nullctx:
@@ -93,6 +96,8 @@ class CTCLIP(nn.Module):
         after the text stream (BERT's Adam) and the auxiliary stream (the codebook EMA), so the
         tensors returned -- and any copy of them queued on the current stream, e.g. torch.save --
         hold the updated weights."""
+        if self._vq_state() is not None:
+            self._vq_state().flush_ema()
         for p in self.text_transformer.parameters():
             if p.is_cuda:
                 streams.flush_text(p.device)
@@ -102,6 +107,10 @@ class CTCLIP(nn.Module):
         return super().state_dict(*args, **kwargs)
 
     # ------------------------------------------------------------------ helpers
+    def _vq_state(self):
+        """The image tower's VQ cache (functional.VQState), or None for another image encoder."""
+        return getattr(getattr(self.visual_transformer, 'vq', None), 'state', None)
+
     def _visual_weight_bf16(self, W):
         """bf16 to_visual_latent weight (151 M parameters): the Adam-kept shadow when W trains,
         else a cast cached until W changes.  Frozen in the fine-tune configuration
@@ -137,7 +146,14 @@ class CTCLIP(nn.Module):
                                              ready=ready)[0]
             pooled, pooled_b = self.visual_transformer.encode_pooled(image)
         else:
-            pooled, pooled_b = self.visual_transformer.encode_pooled(image)
+            vqs = self._vq_state()
+            if vqs is not None:
+                vqs.defer_ema = DEFER_EMA and self.visual_transformer.training
+            try:
+                pooled, pooled_b = self.visual_transformer.encode_pooled(image)
+            finally:
+                if vqs is not None:
+                    vqs.defer_ema = False
             gate = getattr(self.visual_transformer, '_patch_done', None)
             if TEXT_GATE and ready is not None and gate is not None:
                 ready = gate
@@ -166,6 +182,8 @@ class CTCLIP(nn.Module):
             t_raw = leaf
         W = self.to_visual_latent.weight
         i_raw = self._project(W, self._visual_weight_bf16(W), pooled, pooled_b)
+        if self._vq_state() is not None:
+            self._vq_state().flush_ema()   # the codebook EMA, after the projection
         if self.defer_text_backward and torch.is_grad_enabled() and i_raw.requires_grad:
             # the image tower's backward is deferred too (CTClipTrainer.forward_backward): BERT's
             # backward -- and its gradient buckets' all-reduces -- are queued before the 3D-ViT's

@@ -194,6 +194,7 @@ class CTViT(nn.Module):
         return pooled, pooled_b
 
     def _codebook_tensors(self):
+        self.vq.state.flush_ema()        # a deferred EMA update (CTCLIP.encode) precedes any read
         c = self.vq._codebook
         return c.embed, c.cluster_size
 

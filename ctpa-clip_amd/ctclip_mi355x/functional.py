@@ -850,7 +850,8 @@ class VQPoolFn(torch.autograd.Function):
         D = zf.shape[1]
         C = embed.shape[-2]
         cb = embed.view(C, D)
-        streams.join_aux(zf.device)     # the previous step's EMA update of the codebook
+        state.flush_ema()               # a previous call's deferred EMA update, queued before ...
+        streams.join_aux(zf.device)     # ... this wait for the previous step's codebook update
         idx, xn = vq_assign(zf, zb, cb, state, want_xn=training)
         cb_b = state.codebook_bf16(cb)   # the mirror vq_assign scored against (cached)
         HW = geo.Hg * geo.Wg
@@ -870,11 +871,21 @@ class VQPoolFn(torch.autograd.Function):
             if aux is None:
                 ema()
             else:
-                aux.wait_stream(torch.cuda.current_stream(zf.device))
-                for t in (idx, xn, cb, cluster, cb_b):
-                    t.record_stream(aux)
-                with torch.cuda.stream(aux):
-                    ema()
+                dev = zf.device
+
+                def launch():
+                    aux.wait_stream(torch.cuda.current_stream(dev))
+                    for t in (idx, xn, cb, cluster, cb_b):
+                        t.record_stream(aux)
+                    with torch.cuda.stream(aux):
+                        ema()
+                # CTCLIP.encode defers the launch until after the image projection: the EMA's
+                # statistics pass (~0.36 ms, HBM-bound) otherwise runs beside the projection's
+                # weight stream (302 MB) and slows it by ~40 us (r05f: 98 us in step vs 56 alone)
+                if state.defer_ema:
+                    state.pending_ema = launch
+                else:
+                    launch()
             state.mark_codebook_fresh(cb)
         ctx.geo = geo
         ctx.D = D
@@ -917,6 +928,15 @@ class VQState:
         self._cb_ver = None
         self._ones = {}
         self.last_indices = None
+        self.defer_ema = False      # VQPoolFn leaves its EMA launch in pending_ema (CTCLIP.encode)
+        self.pending_ema = None
+
+    def flush_ema(self):
+        """Queue a deferred codebook EMA update (on the auxiliary stream, after the current stream's
+        work so far).  Every reader of the codebook calls this first."""
+        fn, self.pending_ema = self.pending_ema, None
+        if fn is not None:
+            fn()
 
     def codebook_bf16(self, cb):
         key = (cb.data_ptr(), cb._version)

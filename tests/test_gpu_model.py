@@ -376,7 +376,9 @@ def test_train_step_bit_reproducible():
     float atomics on the step's path (CPB bias gradient through the per-workgroup workspace,
     embedding and patch-LN gradients in fixed order, VQ statistics in fixed point).  A third run
     with the text Adam deferred (trainer.defer_text_adam) is bit-identical too, and so is a fourth
-    with the CPB MLP inline on the main stream instead of the auxiliary one (ctvit._CPB_AUX).  The
+    with the CPB MLP inline on the main stream instead of the auxiliary one (ctvit._CPB_AUX), and a
+    fifth with the codebook EMA queued right after the VQ instead of after the projection
+    (ct_clip.DEFER_EMA).  The
     spatial stage runs the base shape (24 x 24 grid, L = 576: the LDS-DMA dQ kernel); smaller grids
     take the frame-inner kernel, checked by test_deferred_text_adam_matches."""
     from ctclip_mi355x.trainer import CTClipTrainer
@@ -390,11 +392,14 @@ def test_train_step_bit_reproducible():
     ids, mask = W.make_text(2, 32, bert.vocab_size, ragged=True)
     assert (ids == 0).any()
     text = types.SimpleNamespace(input_ids=ids.cuda(), attention_mask=mask.cuda())
+    from ctclip_mi355x import ct_clip
     runs = []
-    cpb_aux = ctvit._CPB_AUX
-    for defer, aux in ((False, cpb_aux), (False, cpb_aux), (True, cpb_aux), (False, not cpb_aux)):
+    cpb_aux, dema = ctvit._CPB_AUX, ct_clip.DEFER_EMA
+    for defer, aux, de in ((False, cpb_aux, dema), (False, cpb_aux, dema), (True, cpb_aux, dema),
+                           (False, not cpb_aux, dema), (False, cpb_aux, not dema)):
         torch.manual_seed(0)
         ctvit._CPB_AUX = aux
+        ct_clip.DEFER_EMA = de
         model = build(cfg, dropout=0.1)
         tr = CTClipTrainer(model, lr=1e-4, defer_text_adam=defer)
         try:
@@ -402,6 +407,7 @@ def test_train_step_bit_reproducible():
             tr.flush()
         finally:
             ctvit._CPB_AUX = cpb_aux
+            ct_clip.DEFER_EMA = dema
         torch.cuda.synchronize()
         cbk = model.visual_transformer.vq._codebook
         runs.append([losses, tr.flat.data.clone(), tr.m.clone(), tr.v.clone(), cbk.embed.clone(),

@@ -1,5 +1,6 @@
 """Run one GEMM shape of the step repeatedly (for rocprofv3 counter passes).
-usage: python tools/gemm_one.py {ff1,ff1plain,ff2,dxnn,dwtn,dx1408,geglubwd,dwq} [reps]"""
+usage: python tools/gemm_one.py {ff1,ff1h16,ff1plain,ff2,dxnn,dwtn,dx1408,geglubwd,dwq} [reps]
+(ff1h16: the step's default FF1, fp16 operands and h, GEGLU epilogue)"""
 import os
 import sys
 
@@ -21,8 +22,10 @@ def main():
     g = torch.empty(M, 1408, device='cuda', dtype=torch.bfloat16)
     res = torch.randn(M, 512, device='cuda')
     dh = r(M, 2816)
+    x512h, w1h = x512.half(), w1.half()
     fn = {
         'ff1': lambda: K.linear(x512, w1, act=K.ACT_GEGLU, out2=g),
+        'ff1h16': lambda: K.linear(x512h, w1h, act=K.ACT_GEGLU, out2=g, out_dtype=K.F16),
         'ff1plain': lambda: K.linear(x512, w1, out=dh),
         'ff2': lambda: K.linear(x1408, w2, residual=res, out_dtype=torch.float32),
         'dxnn': lambda: K.matmul_nn(dh, w1),

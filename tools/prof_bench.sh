@@ -14,4 +14,5 @@ python tools/rocprof_grid.py "$db" "" 7 > gpurun_out/${tag}_grid_stats.txt
 python tools/rocprof_streams.py "$db" 200 > gpurun_out/${tag}_streams.txt || true
 python tools/rocprof_timeline.py "$db" > gpurun_out/${tag}_timeline.txt || true
 python tools/rocprof_seq.py "$db" > gpurun_out/${tag}_seq.txt || true
+python tools/rocprof_copies.py "$db" 7 > gpurun_out/${tag}_copies.txt || true
 rm -rf gpurun_out/prof_${tag}
