@@ -10,4 +10,4 @@ for ctrs in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" "SQ_WAIT_AN
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $ctrs --output-format csv -d $d/p$i -o p -- python tools/attn_bench.py > $d/log$i 2>&1
 done
-for k in "attn_fwd_kernel<32, true" attn_bwd_dq_bias_dma attn_bwd_dkv_persist attn_small_bwd attn_small_fwd; do echo "== $k"; python tools/pmc_table.py $d "$k"; done > gpurun_out/pmc_attn_$tag.txt
+for k in "attn_fwd_kernel<32, true" attn_bwd_dq_bias_dma attn_bwd_dkv_dma attn_small_bwd attn_small_fwd; do echo "== $k"; python tools/pmc_table.py $d "$k"; done > gpurun_out/pmc_attn_$tag.txt
