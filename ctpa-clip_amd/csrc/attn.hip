@@ -496,7 +496,10 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
         // chunks that rescale; the rescaled max is the same full max as before (bit-identical).
         // m[u] == -inf (every key so far masked, e.g. a left-padded BERT mask): rescale, so the
         // exp2 below never sees -inf - -inf
-        rescale[u] = p.lazy <= 0.f || __any(cmax > m[u] + p.lazy || m[u] == -INFINITY);
+        // (read back through an SGPR: the flag is wave-uniform, and as a VGPR condition hipcc
+        // if-converts the branches below into per-element selects)
+        rescale[u] = __builtin_amdgcn_readfirstlane(
+            (int)(p.lazy <= 0.f || __any(cmax > m[u] + p.lazy || m[u] == -INFINITY)));
         float msafe;
         if (rescale[u]) {
           cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
@@ -529,14 +532,22 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
         }
         pb[u] = pack_perm(sa[u][0], sa[u][1]);
       }
+      // rescale the running outputs only on chunks where some query block moved its max (wave-
+      // uniform; alpha = 1 for the others): the steady-state chunk skips the multiplies
+      int anyr = 0;
+#pragma unroll
+      for (int u = 0; u < QB; ++u) anyr |= (int)rescale[u];
+      if (__builtin_amdgcn_readfirstlane(anyr)) {
+#pragma unroll
+        for (int d = 0; d < DB; ++d)
+#pragma unroll
+          for (int u = 0; u < QB; ++u) o[u][d] *= alpha[u];
+      }
 #pragma unroll
       for (int d = 0; d < DB; ++d) {
         const bf16x8 vf = vfrag(Vimg, kc, d * 16);
 #pragma unroll
-        for (int u = 0; u < QB; ++u) {
-          if (rescale[u]) o[u][d] *= alpha[u];
-          o[u][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[u], o[u][d], 0, 0, 0);
-        }
+        for (int u = 0; u < QB; ++u) o[u][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[u], o[u][d], 0, 0, 0);
       }
     }
     }
@@ -989,6 +1000,17 @@ __global__ __launch_bounds__(NT) void attn_bwd_dq_bias_kernel(AP p, int nfc) {
 // 140 B of scratch per lane whose per-frame reloads wait behind the LDS-DMA queue -- 887 vs 697 us
 // per spatial backward (profiles/r05e_attn_kp_ab.log), so 8 waves stay
 constexpr int DQD_W = 8, DQD_NT = DQD_W * 64, DQD_KP = 2;
+// the spatial backward kernels fold each query's lse and delta into the score / dP MFMAs'
+// accumulator inputs (one VALU subtraction per score and per dP less; round 5), 0 = subtract them
+// per element (A/B build switch)
+#ifndef CTCLIP_ATTN_CFOLD
+#define CTCLIP_ATTN_CFOLD 1
+#endif
+// the same in the dQ kernel: its two constant accumulator inputs hold 8 more VGPRs across the frame
+// loop at a 256-VGPR budget (scratch 40 -> 128 B per lane), so off
+#ifndef CTCLIP_ATTN_CFOLD_DQ
+#define CTCLIP_ATTN_CFOLD_DQ 0
+#endif
 // key positions of the bias reads: 1 = kb_fast (VALU), 0 = the LDS table (A/B build switch).
 // Measured (profiles/r05d_attn_ab.log): the table, 699-705 us per spatial backward vs 718 for
 // kb_fast, whose per-chunk VALU spills 40 -> 56 B per lane at this kernel's 256-VGPR budget
@@ -1084,6 +1106,14 @@ __global__ __launch_bounds__(4 * KP * 64) void attn_bwd_dq_bias_dma_kernel(AP p,
     }
     const int64_t qrow = (int64_t)s * p.s_outer + q;
     if (g == 0 && kpart == 0) p.delta[(int64_t)h * p.M + qrow] = dl;
+#if CTCLIP_ATTN_CFOLD_DQ
+    // the query's lse and delta ride in the score / dP MFMAs' accumulator inputs (S^T layout: all 4
+    // registers of a lane are its query): x - l2 = sc2 (q.k - lse / scale) + bias, dP - delta
+    const float cl = -lse2 / p.scale;
+    const f32x4 cS = f32x4{cl, cl, cl, cl}, cD = f32x4{-dl, -dl, -dl, -dl};
+#else
+    const f32x4 cS = f32x4{0.f, 0.f, 0.f, 0.f}, cD = cS;
+#endif
     __builtin_amdgcn_sched_barrier(0);
     if (s + 1 < f1) {
       load_q(s + 1);
@@ -1099,10 +1129,8 @@ __global__ __launch_bounds__(4 * KP * 64) void attn_bwd_dq_bias_dma_kernel(AP p,
       f32x4 sa[2], da[2];
 #pragma unroll
       for (int bi = 0; bi < 2; ++bi) {
-        sa[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Kimg, kc + 16 * bi, lane), qc,
-                                                         f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        da[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Vimg, kc + 16 * bi, lane), dc,
-                                                         f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        sa[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Kimg, kc + 16 * bi, lane), qc, cS, 0, 0, 0);
+        da[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Vimg, kc + 16 * bi, lane), dc, cD, 0, 0, 0);
       }
 #pragma unroll
       for (int bi = 0; bi < 2; ++bi) {
@@ -1119,7 +1147,11 @@ __global__ __launch_bounds__(4 * KP * 64) void attn_bwd_dq_bias_dma_kernel(AP p,
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float x = sa[bi][r] * sc2 + up[3 - r];
+#if CTCLIP_ATTN_CFOLD_DQ
+          const float ds = fexp2(x) * da[bi][r];
+#else
           const float ds = fexp2(x - l2) * (da[bi][r] - dl);
+#endif
           acc[ci][bi][r] += ds;
           sa[bi][r] = ds;   // the score scale is applied once per dQ output below (exact for 8)
         }
@@ -1430,8 +1462,13 @@ __global__ __launch_bounds__(DKD_NT) void attn_bwd_dkv_dma_kernel(AP p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid < L) {
+#if CTCLIP_ATTN_CFOLD
+      ls[tid] = -lsv / p.scale;   // the score MFMA's accumulator input: sc2 (q.k - lse / scale) = x - lse
+      dls[tid] = -dlv;            // the dP MFMA's: dP - delta
+#else
       ls[tid] = lsv * LOG2E;
       dls[tid] = dlv;
+#endif
     }
     __syncthreads();
     const int sn = s + nwg;
@@ -1458,22 +1495,34 @@ __global__ __launch_bounds__(DKD_NT) void attn_bwd_dkv_dma_kernel(AP p) {
         f32x4 sa[2], da[2];
 #pragma unroll
         for (int bi = 0; bi < 2; ++bi) {
-          sa[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Qimg, qc + 16 * bi, lane), kc,
-                                                           f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          da[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Dimg, qc + 16 * bi, lane), vc,
-                                                           f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#if CTCLIP_ATTN_CFOLD
+          // C[q][key], register r = query q0 + r: its -lse / scale and -delta as the accumulator inputs
+          const int q0 = qc + 16 * bi + 4 * g;
+          const f32x4 cS = *(const f32x4*)(ls + q0), cD = *(const f32x4*)(dls + q0);
+#else
+          const f32x4 cS = f32x4{0.f, 0.f, 0.f, 0.f}, cD = cS;
+#endif
+          sa[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Qimg, qc + 16 * bi, lane), kc, cS, 0, 0, 0);
+          da[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Dimg, qc + 16 * bi, lane), vc, cD, 0, 0, 0);
         }
 #pragma unroll
         for (int bi = 0; bi < 2; ++bi) {
           const int q0 = qc + 16 * bi + 4 * g;
+#if !CTCLIP_ATTN_CFOLD
           const f32x4 lv = *(const f32x4*)(ls + q0);
           const f32x4 dlq = *(const f32x4*)(dls + q0);
+#endif
           const float* up = ub + (kb_fast(kbf, q0) - ck);   // up[r] = ub[bin(q0 + r, key)]
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float x = sa[bi][r] * sc2 + up[r];
+#if CTCLIP_ATTN_CFOLD
+            const float pr = fexp2(x);
+            const float ds = pr * da[bi][r];
+#else
             const float pr = fexp2(x - lv[r]);
             const float ds = pr * (da[bi][r] - dlq[r]);
+#endif
             sa[bi][r] = pr;
             da[bi][r] = ds;   // the score scale is applied once per dK output below (exact for 8)
           }
