@@ -217,21 +217,25 @@ __global__ __launch_bounds__(256) void vq_ema_accum_kernel(const int32_t* __rest
 
 // cluster_size = cs*decay + bins*(1-decay);  en = l2norm(esum / max(bins,1)); zero bins keep the
 // old code;  embed = embed*decay + en*(1-decay);  also refresh the bf16 working codebook.
-__global__ __launch_bounds__(64) void vq_ema_finalize_kernel(const float* __restrict__ bins,
-                                                             const long long* __restrict__ esum, int C, int D,
+// RESET: the statistics are zeroed behind their reads (bins / esum are then ready for the next
+// step's accumulation: persistent buffers instead of two fill launches per step)
+template <bool RESET = false>
+__global__ __launch_bounds__(64) void vq_ema_finalize_kernel(float* __restrict__ bins,
+                                                             long long* __restrict__ esum, int C, int D,
                                                              float decay, float* __restrict__ embed,
                                                              float* __restrict__ cluster, u16* __restrict__ embed_bf16) {
   const int c = blockIdx.x;
   const int lane = threadIdx.x;
   const float nb = bins[c];
   if (lane == 0) cluster[c] = cluster[c] * decay + nb * (1.f - decay);
+  if (RESET && lane == 0) bins[c] = 0.f;   // one wave: every lane read it above
   float* e = embed + (int64_t)c * D;
   if (nb == 0.f) {
     if (embed_bf16)
       for (int k = lane; k < D; k += 64) embed_bf16[(int64_t)c * D + k] = f2bf(e[k]);
     return;
   }
-  const long long* s = esum + (int64_t)c * D;
+  long long* s = esum + (int64_t)c * D;
   constexpr double FX_INV = 0x1p-40;
   float ss = 0.f;
   for (int k = lane; k < D; k += 64) { const float v = (float)((double)s[k] * FX_INV) / nb; ss += v * v; }
@@ -239,6 +243,7 @@ __global__ __launch_bounds__(64) void vq_ema_finalize_kernel(const float* __rest
   const float inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
   for (int k = lane; k < D; k += 64) {
     const float en = (float)((double)s[k] * FX_INV) / nb * inv;
+    if (RESET) s[k] = 0;                   // this lane's own element, read above
     const float v = e[k] * decay + en * (1.f - decay);
     e[k] = v;
     if (embed_bf16) embed_bf16[(int64_t)c * D + k] = f2bf(v);
@@ -313,9 +318,16 @@ extern "C" int ctclip_vq_ema_accum(const int32_t* idx, const float* xn, int64_t 
 
 extern "C" int ctclip_vq_ema_finalize(const float* bins, const int64_t* esum, int32_t C, int32_t D, float decay,
                                       float* embed, float* cluster_size, void* embed_bf16, void* stream) {
-  hipLaunchKernelGGL(vq_ema_finalize_kernel, dim3(C), dim3(64), 0, (hipStream_t)stream, bins, (const long long*)esum,
-                     C, D, decay,
-                     embed, cluster_size, (u16*)embed_bf16);
+  hipLaunchKernelGGL(vq_ema_finalize_kernel<false>, dim3(C), dim3(64), 0, (hipStream_t)stream, (float*)bins,
+                     (long long*)esum, C, D, decay, embed, cluster_size, (u16*)embed_bf16);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_vq_ema_finalize_reset(float* bins, int64_t* esum, int32_t C, int32_t D, float decay,
+                                            float* embed, float* cluster_size, void* embed_bf16, void* stream) {
+  hipLaunchKernelGGL(vq_ema_finalize_kernel<true>, dim3(C), dim3(64), 0, (hipStream_t)stream, bins,
+                     (long long*)esum, C, D, decay, embed, cluster_size, (u16*)embed_bf16);
   CT_CHECK_LAUNCH();
   return 0;
 }

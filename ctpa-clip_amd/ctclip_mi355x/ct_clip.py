@@ -25,9 +25,14 @@ TEXT_FWD_FIRST = os.environ.get('CTCLIP_TEXT_FWD_FIRST', '0') != '0'
 # patch LayerNorm is HBM-bound (0.43 ms alone, ~1.1 ms beside BERT's first kernels in round 4) and BERT
 # is hidden behind the 3D-ViT either way.  CTCLIP_TEXT_GATE=0: start together (A/B).
 TEXT_GATE = os.environ.get('CTCLIP_TEXT_GATE', '1') != '0'
-# the training VQ's codebook EMA update queued on the auxiliary stream after the image projection
-# instead of right after the VQ (CTCLIP_DEFER_EMA=0: right after the VQ; A/B)
-DEFER_EMA = os.environ.get('CTCLIP_DEFER_EMA', '1') != '0'
+# where the training VQ's codebook EMA update is queued on the auxiliary stream (A/B): '0' right
+# after the VQ (its ~0.34 ms of short workgroups then hold the CUs the projection's slab reduction
+# waits for: 5 -> 321 us in step, r05f_seq.txt), '1' after the image projection (the loss kernel and
+# the backward's first launches wait instead), '2' (default) after the optimizer step, beside the
+# next step's forward: CTClipTrainer.train_step calls flush_ema, and any codebook reader (the next
+# VQ, state_dict) queues a pending update first.  Measured (profiles/r05m_ema_site_ab.log):
+# '2' 204.30 vs '1' 203.70 pairs/s; '1' vs '0' within noise (r05g_ema_ab_env.log)
+DEFER_EMA = os.environ.get('CTCLIP_DEFER_EMA', '2')
 
 
 class _nullctx:
@@ -111,6 +116,12 @@ class CTCLIP(nn.Module):
         """The image tower's VQ cache (functional.VQState), or None for another image encoder."""
         return getattr(getattr(self.visual_transformer, 'vq', None), 'state', None)
 
+    def flush_ema(self):
+        """Queue a deferred codebook EMA update now (auxiliary stream; see DEFER_EMA)."""
+        vqs = self._vq_state()
+        if vqs is not None:
+            vqs.flush_ema()
+
     def _visual_weight_bf16(self, W):
         """bf16 to_visual_latent weight (151 M parameters): the Adam-kept shadow when W trains,
         else a cast cached until W changes.  Frozen in the fine-tune configuration
@@ -148,7 +159,7 @@ class CTCLIP(nn.Module):
         else:
             vqs = self._vq_state()
             if vqs is not None:
-                vqs.defer_ema = DEFER_EMA and self.visual_transformer.training
+                vqs.defer_ema = DEFER_EMA != '0' and self.visual_transformer.training
             try:
                 pooled, pooled_b = self.visual_transformer.encode_pooled(image)
             finally:
@@ -182,8 +193,8 @@ class CTCLIP(nn.Module):
             t_raw = leaf
         W = self.to_visual_latent.weight
         i_raw = self._project(W, self._visual_weight_bf16(W), pooled, pooled_b)
-        if self._vq_state() is not None:
-            self._vq_state().flush_ema()   # the codebook EMA, after the projection
+        if DEFER_EMA == '1':
+            self.flush_ema()               # the codebook EMA, after the projection
         if self.defer_text_backward and torch.is_grad_enabled() and i_raw.requires_grad:
             # the image tower's backward is deferred too (CTClipTrainer.forward_backward): BERT's
             # backward -- and its gradient buckets' all-reduces -- are queued before the 3D-ViT's

@@ -863,11 +863,12 @@ class VQPoolFn(torch.autograd.Function):
             aux = streams.aux_stream(zf.device)
 
             def ema():
-                bins = torch.zeros(C, device=zf.device, dtype=F32)
-                esum = torch.zeros(C, D, device=zf.device, dtype=torch.int64)   # 2^-40 fixed point
+                # persistent statistics (2^-40 fixed-point esum), zeroed once here and then by the
+                # finalize kernel behind its reads: no fill launches per step
+                bins, esum = state.ema_buffers(C, D, zf.device)
                 K.vq_ema_accum(idx, xn, bins, esum)
                 dist_sync.sum_codebook_stats(bins, esum)
-                K.vq_ema_finalize(bins, esum, decay, cb, cluster.view(-1), cb_b)
+                K.vq_ema_finalize(bins, esum, decay, cb, cluster.view(-1), cb_b, reset=True)
             if aux is None:
                 ema()
             else:
@@ -930,6 +931,15 @@ class VQState:
         self.last_indices = None
         self.defer_ema = False      # VQPoolFn leaves its EMA launch in pending_ema (CTCLIP.encode)
         self.pending_ema = None
+
+    def ema_buffers(self, C, D, device):
+        """(bins f32 [C], esum int64 [C, D]) of the EMA update, zero between updates (created on the
+        stream of the first update, which every later update also runs on)."""
+        b = getattr(self, '_ema_buf', None)
+        if b is None or b[1].shape != (C, D) or b[1].device != device:
+            b = (torch.zeros(C, device=device, dtype=F32), torch.zeros(C, D, device=device, dtype=torch.int64))
+            self._ema_buf = b
+        return b
 
     def flush_ema(self):
         """Queue a deferred codebook EMA update (on the auxiliary stream, after the current stream's

@@ -1085,11 +1085,12 @@ def vq_ema_accum(idx, xn, bins, esum):
     call('ctclip_vq_ema_accum', ptr(idx), ptr(xn), xn.shape[0], xn.shape[1], ptr(bins), ptr(esum), stream_ptr())
 
 
-def vq_ema_finalize(bins, esum, decay, embed, cluster, embed_bf16=None):
+def vq_ema_finalize(bins, esum, decay, embed, cluster, embed_bf16=None, reset=False):
+    """reset: zero bins / esum behind the reads (persistent statistics buffers)."""
     assert esum.dtype == torch.int64
     C, D = esum.shape
-    call('ctclip_vq_ema_finalize', ptr(bins), ptr(esum), C, D, decay, ptr(embed), ptr(cluster), ptr(embed_bf16),
-         stream_ptr())
+    call('ctclip_vq_ema_finalize_reset' if reset else 'ctclip_vq_ema_finalize', ptr(bins), ptr(esum), C, D, decay,
+         ptr(embed), ptr(cluster), ptr(embed_bf16), stream_ptr())
 
 
 # ----------------------------------------------------------------------------- loss

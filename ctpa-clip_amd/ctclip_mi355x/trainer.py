@@ -261,6 +261,9 @@ class CTClipTrainer:
         LayerNorm-exchange status (synchronises): call after the last ``train_step`` before reading
         the parameters."""
         streams.flush_text(self.device)
+        fe = getattr(self.model, 'flush_ema', None)
+        if fe is not None:
+            fe()
         # the text-bucket Adam runs on the text stream, the codebook EMA on the auxiliary one: order
         # the caller's stream after both, so parameters read (or saved) on it are the updated ones
         streams.join_text(self.device)
@@ -321,5 +324,8 @@ class CTClipTrainer:
         with K.ln_guard():
             loss = self.forward_backward(text, video)
         self.optimizer_step()
+        fe = getattr(self.model, 'flush_ema', None)
+        if fe is not None:
+            fe()          # a codebook EMA deferred past the optimizer (ct_clip.DEFER_EMA = '2')
         self._queue_ln_check()
         return loss.detach()

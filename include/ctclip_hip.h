@@ -495,6 +495,10 @@ int ctclip_vq_ema_accum(const int32_t* idx, const float* xn, int64_t rows, int32
                         void* stream);
 int ctclip_vq_ema_finalize(const float* bins, const int64_t* esum, int32_t C, int32_t D, float decay, float* embed,
                            float* cluster_size, void* embed_bf16, void* stream);
+/* ctclip_vq_ema_finalize that also zeroes bins / esum behind its reads, so persistent statistics
+ * buffers are ready for the next step's ctclip_vq_ema_accum (no fill launches). */
+int ctclip_vq_ema_finalize_reset(float* bins, int64_t* esum, int32_t C, int32_t D, float decay, float* embed,
+                                 float* cluster_size, void* embed_bf16, void* stream);
 
 /* ---------------------------------------------------------------- contrastive loss
  * symmetric InfoNCE over the (global) batch, ct_clip/ct_clip.py:771,796,845-901; one workgroup.
