@@ -143,12 +143,31 @@ __device__ __forceinline__ float erf_fast(float x) {
 // inside the GEGLU / GELU GEMM epilogues
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x; }
 __device__ __forceinline__ float gelu_erf_grad(float x) { return 0.5f + 0.1f * x; }
+__device__ __forceinline__ void gelu_erf_and_grad(float x, float& gelu, float& dgelu) {
+  gelu = gelu_erf(x);
+  dgelu = gelu_erf_grad(x);
+}
 #else
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_erf_grad(float x) {
-  const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+// GELU and its derivative together (the GEGLU backward needs both): one erf, and the pdf's
+// exp(-x^2 / 2) is the erf's own exp(-a^2), a = |x| / sqrt 2.  gelu bit-identical to gelu_erf.
+__device__ __forceinline__ void gelu_erf_and_grad(float x, float& gelu, float& dgelu) {
+  const float a = fabsf(x * 0.70710678118654752f);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.0f));
+  float y = fmaf(1.061405429f, t, -1.453152027f);
+  y = fmaf(y, t, 1.421413741f);
+  y = fmaf(y, t, -0.284496736f);
+  y = fmaf(y, t, 0.254829592f);
+  y *= t;
+  const float e = __expf(-a * a);
+  const float erf = copysignf(fmaf(-y, e, 1.0f), x);
+  gelu = 0.5f * x * (1.0f + erf);
+  dgelu = 0.5f * (1.0f + erf) + x * (0.39894228040143268f * e);
+}
+__device__ __forceinline__ float gelu_erf_grad(float x) {   // one exp (gelu_erf_and_grad)
+  float ge, dge;
+  gelu_erf_and_grad(x, ge, dge);
+  return dge;
 }
 #endif
 

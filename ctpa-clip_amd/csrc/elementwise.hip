@@ -23,8 +23,10 @@ __global__ __launch_bounds__(256) void geglu_bwd_kernel(const u16* __restrict__ 
     unpack8(*(const u32x4*)(h + r * ldh + t * 64 + 32 + c), gt);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      ox[j] = d[j] * gelu_erf(gt[j]);
-      og[j] = d[j] * x[j] * gelu_erf_grad(gt[j]);
+      float ge, dge;
+      gelu_erf_and_grad(gt[j], ge, dge);
+      ox[j] = d[j] * ge;
+      og[j] = d[j] * x[j] * dge;
     }
     *(u32x4*)(dh + r * lddh + t * 64 + c) = pack8(ox);
     *(u32x4*)(dh + r * lddh + t * 64 + 32 + c) = pack8(og);

@@ -235,8 +235,10 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float d = bf2f(f2bf(cs[row * CS_LD + cc + j] * p.alpha));
-        ox[j] = d * gelu_erf(gt[j]);
-        og[j] = d * x[j] * gelu_erf_grad(gt[j]);
+        float ge, dge;
+        gelu_erf_and_grad(gt[j], ge, dge);
+        ox[j] = d * ge;
+        og[j] = d * x[j] * dge;
       }
       *(u32x4*)dr = pack8(ox);
       *(u32x4*)(dr + 32) = pack8(og);

@@ -1039,8 +1039,10 @@ __device__ __forceinline__ void epilogue_geglu_bwd(const P& p, f32x4 (&acc)[8][4
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        ox[k] = d[k] * gelu_erf(gt[k]);
-        og[k] = d[k] * x[k] * gelu_erf_grad(gt[k]);
+        float ge, dge;
+        gelu_erf_and_grad(gt[k], ge, dge);
+        ox[k] = d[k] * ge;
+        og[k] = d[k] * x[k] * dge;
       }
       const int64_t t = t0 + jp;
       if (gm < p.M && t * 32 < p.N) {
