@@ -465,7 +465,14 @@ __device__ __forceinline__ void xplane_store(char* dst, int W, const u32x4 (&reg
   }
 }
 
-template <int GK = 0, int MD = 0>
+// TR = 1: the input gradient dx = dout + conv^T(dout) from the f32 dout (round 5; the bf16 tile kernel
+// reads the conv taps from dout's bf16 copy plus the f32 residual).  The transposed conv's offsets
+// are the forward's negated: with the view-space walk (MD 0 / 1) output t needs planes t .. t + 2,
+// so the walk runs BACKWARD in t (virtual time t' = T - 1 - t), where the offsets are the forward's
+// again and no plane is needed ahead; the canonical walk (MD 2: offsets -1 .. 1 on the walk axis)
+// keeps its direction and its one plane of lead.  Columns mirror (x[w + 1 - kw] instead of
+// x[w - 1 + kw]); rows use the transposed row offsets (Taps<MD, 1>).  No bias, no statistics.
+template <int GK = 0, int MD = 0, int TR = 0>
 __global__ __launch_bounds__(XNT, CTCLIP_PEGX_WAVES) void peg_fwd32_kernel(const float* __restrict__ xin, int D,
                                                         const float* __restrict__ w, const float* __restrict__ bias,
                                                         Geo g, float* __restrict__ out, u16* __restrict__ outb,
@@ -481,12 +488,15 @@ __global__ __launch_bounds__(XNT, CTCLIP_PEGX_WAVES) void peg_fwd32_kernel(const
     const int c = i / 27, tap = i - c * 27;
     ws[tap * XC + c] = w[(int64_t)(c0 + c) * 27 + tap];
   }
-  if (threadIdx.x < XC) bs[threadIdx.x] = bias ? bias[c0 + threadIdx.x] : 0.f;
-  using TP = Taps<MD, 0>;
-  constexpr int lead = TP::lead, hoff = TP::hoff;
+  if (threadIdx.x < XC) bs[threadIdx.x] = bias && !TR ? bias[c0 + threadIdx.x] : 0.f;
+  using TP = Taps<MD, TR>;
+  constexpr bool REV = TR && MD != 2;            // backward walk (see above)
+  using TW = Taps<MD, REV ? 0 : TR>;             // walk-axis offsets in walk time
+  constexpr int lead = TW::lead, hoff = TP::hoff;
+  auto real_t = [&](int p) { return REV ? g.T - 1 - p : p; };   // walk time -> t
   u32x4 reg[XNLD];
   {
-    const unsigned v = xplane_load(xin, g, D, b, h0, c0, 0, reg, hoff);
+    const unsigned v = xplane_load(xin, g, D, b, h0, c0, real_t(0), reg, hoff);
     xplane_store(smem, g.W, reg, v);
   }
   __syncthreads();
@@ -513,7 +523,7 @@ __global__ __launch_bounds__(XNT, CTCLIP_PEGX_WAVES) void peg_fwd32_kernel(const
     constexpr int P3 = decltype(p3c)::value;
     const bool have = p < g.T;
     // next plane into registers (always issued, clamped: no branch merges `reg`)
-    const unsigned nvalid = xplane_load(xin, g, D, b, h0, c0, min(p + 1, g.T - 1), reg, hoff);
+    const unsigned nvalid = xplane_load(xin, g, D, b, h0, c0, real_t(min(p + 1, g.T - 1)), reg, hoff);
     if (active && have) {
       const char* pl = smem + (p & 1) * pb;
 #pragma unroll 1
@@ -529,16 +539,18 @@ __global__ __launch_bounds__(XNT, CTCLIP_PEGX_WAVES) void peg_fwd32_kernel(const
         }
 #pragma unroll
         for (int kt = 0; kt < 3; ++kt) {
-          const int t = p + 2 - lead - kt;       // the output this tap of plane p feeds
+          const int t = p - TW::dt(kt);          // the output (walk time) this tap of plane p feeds
           if (t < 0 || t >= g.T) continue;
-          const int u = (P3 + 2 - lead - kt + 3) % 3;   // compile-time after the unroll
+          const int u = (P3 - TW::dt(kt) + 3) % 3;   // compile-time after the unroll
 #pragma unroll
           for (int kw = 0; kw < 3; ++kw) {
             const f32x4 wv = *(const f32x4*)(ws + TP::tap(kt, kh, kw) * XC + ch * 4);
 #pragma unroll
-            for (int j = 0; j < SEG; ++j)
+            for (int j = 0; j < SEG; ++j) {
+              const int q = TR ? j + 2 - kw : j + kw;
 #pragma unroll
-              for (int e = 0; e < 4; ++e) acc[u][j][e] += wv[e] * xv[j + kw][e];
+              for (int e = 0; e < 4; ++e) acc[u][j][e] += wv[e] * xv[q][e];
+            }
           }
         }
       }
@@ -558,13 +570,13 @@ __global__ __launch_bounds__(XNT, CTCLIP_PEGX_WAVES) void peg_fwd32_kernel(const
           acc[uf][j][e] = bs[ch * 4 + e];
         }
         if (wq < g.W) {
-          const int64_t orow = canon(g, b, (tf * g.H + h) * g.W + wq);
+          const int64_t orow = canon(g, b, (real_t(tf) * g.H + h) * g.W + wq);
           const int64_t co = orow * D + c0 + ch * 4;
           *(f32x4*)(out + co) = f32x4{v4[0], v4[1], v4[2], v4[3]};
           if (outb) *(uint2*)(outb + co) = pack4(v4);
           if (outh) *(uint2*)(outh + co) = make_uint2(pack2h(v4[0], v4[1]), pack2h(v4[2], v4[3]));
         }
-        if (stats) {
+        if (!TR && stats) {
           // the output row's (mean, M2) over this workgroup's 32 channels (two-pass over the 8 lanes
           // ch = 0..7 of the token), merged over the D / 32 groups by ctclip_ln_stats_merge
           float sm = v4[0] + v4[1] + v4[2] + v4[3];
@@ -583,7 +595,7 @@ __global__ __launch_bounds__(XNT, CTCLIP_PEGX_WAVES) void peg_fwd32_kernel(const
           m2 += __shfl_xor(m2, 4, 64);
           if (ch == 0 && wq < g.W) {
             const int64_t ntok = (int64_t)(gridDim.x / nht) * g.thw;
-            const int64_t orow = canon(g, b, (tf * g.H + h) * g.W + wq);
+            const int64_t orow = canon(g, b, (real_t(tf) * g.H + h) * g.W + wq);
             *(float2*)(stats + ((int64_t)blockIdx.y * ntok + orow) * 2) = make_float2(mu, m2);
           }
         }
@@ -913,6 +925,40 @@ extern "C" int ctclip_peg_fwd_x32(const float* x_f32, int64_t B, int32_t T, int3
     hipLaunchKernelGGL(peg_fwd32_naive_kernel, dim3(cdiv(ntok * (D / 4), 256)), dim3(256), 0, st, x_f32, ntok, D,
                        weight, bias, g, out_f32, (u16*)out_bf16, (u16*)out_f16);
   }
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+// dx = dout + conv^T(dout) from the f32 dout alone (the x32 kernel with TR = 1): the conv taps in
+// f32, no bf16 dout read.  Fixed 24^3 grids with the tiled shape only (CT_ESHAPE otherwise: the
+// caller runs ctclip_peg_bwd_data)
+extern "C" int ctclip_peg_bwd_data_x32(const float* dout_f32, int64_t B, int32_t T, int32_t H, int32_t W, int32_t D,
+                                       const float* weight, int32_t mode, float* dx_f32, void* dx_bf16, void* stream) {
+  CT_REQUIRE(D % 4 == 0 && dout_f32 && dx_f32 && aligned16(dout_f32) && aligned16(dx_f32), CT_EALIGN);
+  Geo g{T, H, W, T * H * W, mode};
+  if (B * g.thw == 0) return 0;
+  const bool tiled = D % XC == 0 && XHT * ((W + SEG - 1) / SEG) * 8 <= XNT && (XHT + 2) * (W + 2) * 8 <= XPCH;
+  if (!tiled || !fixed24(g)) return CT_ESHAPE;
+  const hipStream_t st = (hipStream_t)stream;
+  static bool attr = false;
+  const size_t smem = (size_t)2 * xplane_bytes(W) + (27 * XC + XC) * 4;
+  if (!attr) {
+    const void* ks[] = {(const void*)peg_fwd32_kernel<24, 0, 1>, (const void*)peg_fwd32_kernel<24, 1, 1>,
+                        (const void*)peg_fwd32_kernel<24, 2, 1>};
+    for (const void* k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    attr = true;
+  }
+  dim3 grid(B * ((H + XHT - 1) / XHT), D / XC);
+  const auto ob = (u16*)dx_bf16;
+  if (g.mode == 0)
+    hipLaunchKernelGGL((peg_fwd32_kernel<24, 0, 1>), grid, dim3(XNT), smem, st, dout_f32, D, weight,
+                       (const float*)nullptr, g, dx_f32, ob, (u16*)nullptr, (float*)nullptr);
+  else if (canon1())
+    hipLaunchKernelGGL((peg_fwd32_kernel<24, 2, 1>), grid, dim3(XNT), smem, st, dout_f32, D, weight,
+                       (const float*)nullptr, g, dx_f32, ob, (u16*)nullptr, (float*)nullptr);
+  else
+    hipLaunchKernelGGL((peg_fwd32_kernel<24, 1, 1>), grid, dim3(XNT), smem, st, dout_f32, D, weight,
+                       (const float*)nullptr, g, dx_f32, ob, (u16*)nullptr, (float*)nullptr);
   CT_CHECK_LAUNCH();
   return 0;
 }

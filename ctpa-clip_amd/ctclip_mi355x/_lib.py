@@ -188,6 +188,7 @@ _SIGS = {
     'ctclip_peg_fwd_stats': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp,
                              c_vp],
     'ctclip_peg_fwd_x32': [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
+    'ctclip_peg_bwd_data_x32': [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp],
     'ctclip_peg_bwd_data': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp],
     'ctclip_peg_bwd_weight': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp],
     'ctclip_peg_wgrad_reduce': [c_vp, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp],

@@ -183,6 +183,7 @@ LN_FUSED_BWD = os.environ.get('CTCLIP_LN_FUSED_BWD', '0') != '0'
 _XCHG = {}       # (device, stream) -> [int64 buffer, last epoch]
 _LN_STATUS = {}  # device -> int32[1], set by a launch whose partner statistics never arrived
 _CT_EINVAL, _CT_ESHAPE = 1001, 1003
+_PEG_BWD_X32 = os.environ.get('CTCLIP_PEG_BWD_X32', '1') != '0'
 # Fail loud: the exchange's partner wait is bounded, and a launch that gives up leaves
 # wrong LayerNorm outputs and sets the device status word.  The fused form is therefore only used
 # where something reads that word every step: inside ``ln_guard()`` (trainer.CTClipTrainer wraps
@@ -963,8 +964,17 @@ def peg_bwd(doutb, doutf, xb, B, T, H, W, weight, mode, dweight_out=None, dbias_
     D = xb.shape[1]
     dxf = torch.empty_like(doutf)
     dxb = torch.empty_like(doutb)
-    call('ctclip_peg_bwd_data', ptr(doutb), ptr(doutf), B, T, H, W, D, ptr(weight), mode, ptr(dxf), ptr(dxb),
-         stream_ptr())
+    # the input gradient from the f32 dout alone (conv taps in f32) where the x32 kernel takes the
+    # shape; else the bf16-tap tile kernel (CTCLIP_PEG_BWD_X32=0: always the latter, A/B)
+    rc = _CT_ESHAPE
+    if _PEG_BWD_X32 and doutf.is_contiguous():
+        rc = _lib.lib().ctclip_peg_bwd_data_x32(ptr(doutf), B, T, H, W, D, ptr(weight), mode, ptr(dxf), ptr(dxb),
+                                                stream_ptr())
+    if rc == _CT_ESHAPE:
+        call('ctclip_peg_bwd_data', ptr(doutb), ptr(doutf), B, T, H, W, D, ptr(weight), mode, ptr(dxf), ptr(dxb),
+             stream_ptr())
+    elif rc != 0:
+        raise _lib.KernelError(f'ctclip_peg_bwd_data_x32 failed with code {rc}')
     nblk = _lib.lib().ctclip_peg_wgrad_slabs(B, T, H, W, D)
     part = torch.empty(nblk, D * 28, device=xb.device, dtype=F32)
     call('ctclip_peg_bwd_weight', ptr(doutb), ptr(xb), B, T, H, W, D, mode, ptr(part), nblk, stream_ptr())

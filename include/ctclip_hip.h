@@ -364,6 +364,11 @@ int ctclip_peg_fwd_stats(const void* x_bf16, const float* x_f32, int64_t B, int3
 int ctclip_peg_fwd_x32(const float* x_f32, int64_t B, int32_t T, int32_t H, int32_t W, int32_t D,
                        const float* weight, const float* bias, int32_t mode, float* out_f32, void* out_bf16,
                        void* out_f16, float* stats, void* stream);
+/* dx = dout + conv^T(dout) from the f32 dout alone (the conv taps in f32; no bf16 dout read): the x32
+ * kernel's transposed form, fixed 24^3 grids (returns CT_ESHAPE otherwise: use ctclip_peg_bwd_data).
+ * ct_clip/attention.py:56-84 backward. */
+int ctclip_peg_bwd_data_x32(const float* dout_f32, int64_t B, int32_t T, int32_t H, int32_t W, int32_t D,
+                            const float* weight, int32_t mode, float* dx_f32, void* dx_bf16, void* stream);
 int ctclip_peg_bwd_data(const void* dout_bf16, const float* dout_f32, int64_t B, int32_t T, int32_t H,
                         int32_t W, int32_t D, const float* weight, int32_t mode, float* dx_f32,
                         void* dx_bf16, void* stream);

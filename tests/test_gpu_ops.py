@@ -79,6 +79,44 @@ def _peg_ref(x, w, b, shape, mode):
     return y.reshape(B, H, W, T, D).permute(0, 3, 1, 2, 4).reshape(-1, D)
 
 
+@pytest.mark.parametrize('mode', [0, 1])
+def test_peg_bwd_x32(K, mode):
+    """The input gradient from the f32 dout (ctclip_peg_bwd_data_x32: the transposed conv in f32, the
+    view-space walk run backward in t, the canonical temporal walk forward) against an f64 reference
+    with a dout that bf16 cannot hold: closer than the bf16-tap tile kernel, which reads the conv
+    taps from dout's bf16 copy; the weight / bias gradients are unchanged.  Both walks of mode 1."""
+    from ctclip_mi355x import _lib
+    torch.manual_seed(21 + mode)
+    shape, D = (2, 24, 24, 24), 128
+    M = 2 * 24 ** 3
+    xb = torch.randn(M, D, device=dev).bfloat16()
+    w = torch.randn(D, 1, 3, 3, 3, device=dev) * 0.2
+    b = torch.randn(D, device=dev) * 0.1
+    dyf = torch.randn(M, D, device=dev)
+    xr = xb.double().requires_grad_(True)
+    _peg_ref(xr, w.double(), b.double(), shape, mode).backward(dyf.double())
+    res = {}
+    for x32 in (True, False):
+        old = K._PEG_BWD_X32
+        K._PEG_BWD_X32 = x32
+        try:
+            res[x32] = K.peg_bwd(dyf.bfloat16(), dyf, xb, *shape, w, mode)
+        finally:
+            K._PEG_BWD_X32 = old
+    e32, e16 = rel(res[True][0], xr.grad), rel(res[False][0], xr.grad)
+    print(f'PEG input gradient mode {mode}: x32 rel {e32:.2e}, bf16-tap {e16:.2e}')
+    assert e32 < 1e-6 and e32 < 0.1 * e16
+    assert rel(res[True][1].float(), res[True][0]) < 4e-3       # the bf16 copy of dx
+    assert torch.equal(res[True][2], res[False][2]) and torch.equal(res[True][3], res[False][3])
+    if mode == 1:   # the view-order walk of the same gradient
+        prev = _lib.lib().ctclip_peg_set_canon1(0)
+        try:
+            alt = K.peg_bwd(dyf.bfloat16(), dyf, xb, *shape, w, mode)
+        finally:
+            _lib.lib().ctclip_peg_set_canon1(prev)
+        assert rel(alt[0], xr.grad) < 1e-6
+
+
 def test_peg_canonical_walk_matches_view_walk(K):
     """Mode 1 on the 24^3 cube: the canonical-order walk (default) against the view-order walk."""
     from ctclip_mi355x import _lib

@@ -1,4 +1,4 @@
-"""GPU micro-benchmark: the PEG forward kernels at the base shape (B = 8, 24^3 tokens, d = 512) --
+"""GPU micro-benchmark: the PEG forward and input-gradient kernels at the base shape (B = 8, 24^3 tokens, d = 512) --
 the bf16-tap kernel (ctclip_peg_fwd_stats) against the f32-tap kernel (ctclip_peg_fwd_x32) for
 both transformers' maps -- and the image projection (skinny streaming GEMM vs the split-K tile).
 HIP events around 20 launches each; prints us per launch.  CTCLIP_HIP_LIB selects a library."""
@@ -34,6 +34,12 @@ for mode in (0, 1):
     t_old = timeit(lambda: K.peg_fwd_stats(xb, xf, B, T, T, T, w, b, mode))
     t_new = timeit(lambda: K.peg_fwd_x32(xf, B, T, T, T, w, b, mode, stats=True))
     print(f'PEG fwd mode {mode}: bf16 taps {t_old:.1f} us, f32 taps {t_new:.1f} us', flush=True)
+    dxf, dxb = torch.empty_like(xf), torch.empty_like(xb)
+    t_bo = timeit(lambda: K.call('ctclip_peg_bwd_data', K.ptr(xb), K.ptr(xf), B, T, T, T, D, K.ptr(w), mode,
+                                 K.ptr(dxf), K.ptr(dxb), K.stream_ptr()))
+    t_bn = timeit(lambda: K.call('ctclip_peg_bwd_data_x32', K.ptr(xf), B, T, T, T, D, K.ptr(w), mode,
+                                 K.ptr(dxf), K.ptr(dxb), K.stream_ptr()))
+    print(f'PEG bwd data mode {mode}: bf16 taps {t_bo:.1f} us, f32 taps {t_bn:.1f} us', flush=True)
 Kd, N = 294912, 512
 pb = torch.randn(B, Kd, device='cuda').bfloat16()
 Wb = (torch.randn(N, Kd, device='cuda') * 0.002).bfloat16()
