@@ -29,8 +29,10 @@ TEXT_GATE = os.environ.get('CTCLIP_TEXT_GATE', '1') != '0'
 # after the VQ (its ~0.34 ms of short workgroups then hold the CUs the projection's slab reduction
 # waits for: 5 -> 321 us in step, r05f_seq.txt), '1' after the image projection (the loss kernel and
 # the backward's first launches wait instead), '2' (default) after the optimizer step, beside the
-# next step's forward: CTClipTrainer.train_step calls flush_ema, and any codebook reader (the next
-# VQ, state_dict) queues a pending update first.  Measured (profiles/r05m_ema_site_ab.log):
+# next step's forward -- only when CTClipTrainer owns the step (train_step sets ema_after_step,
+# optimizer_step calls flush_ema; any codebook reader, the next VQ or state_dict, queues a pending
+# update first); a plain model(...) call in train mode gets site '1', so the codebook read after it
+# is the updated one, as the reference updates it inside forward.  Measured (r05m_ema_site_ab.log):
 # '2' 204.30 vs '1' 203.70 pairs/s; '1' vs '0' within noise (r05g_ema_ab_env.log)
 DEFER_EMA = os.environ.get('CTCLIP_DEFER_EMA', '2')
 
@@ -86,6 +88,7 @@ class CTCLIP(nn.Module):
         self._deferred_text = None
         self._deferred_image = None
         self._t_gather = None
+        self.ema_after_step = False          # set by CTClipTrainer.train_step (DEFER_EMA '2')
 
     # ------------------------------------------------------------------ checkpoint
     def load(self, path):
@@ -193,7 +196,7 @@ class CTCLIP(nn.Module):
             t_raw = leaf
         W = self.to_visual_latent.weight
         i_raw = self._project(W, self._visual_weight_bf16(W), pooled, pooled_b)
-        if DEFER_EMA == '1':
+        if DEFER_EMA == '1' or (DEFER_EMA == '2' and not self.ema_after_step):
             self.flush_ema()               # the codebook EMA, after the projection
         if self.defer_text_backward and torch.is_grad_enabled() and i_raw.requires_grad:
             # the image tower's backward is deferred too (CTClipTrainer.forward_backward): BERT's

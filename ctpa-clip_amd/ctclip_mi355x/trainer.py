@@ -200,6 +200,14 @@ class CTClipTrainer:
         return loss
 
     def optimizer_step(self):
+        try:
+            self._optimizer_step()
+        finally:
+            fe = getattr(self.model, 'flush_ema', None)
+            if fe is not None:
+                fe()      # a codebook EMA train_step deferred past the optimizer (ct_clip.DEFER_EMA '2')
+
+    def _optimizer_step(self):
         if streams.pending_text(self.device):
             # the previous step's deferred text Adam was never queued (no text-tower forward ran
             # since): this step's text gradients were summed onto that step's and the shared clip
@@ -321,11 +329,15 @@ class CTClipTrainer:
         exchange (at the latest two steps later; ``check()`` / ``flush()`` wait for all)."""
         self._check_ln(block_upto=self.steps - 2)
         self.model.train()
-        with K.ln_guard():
-            loss = self.forward_backward(text, video)
+        own = hasattr(self.model, 'ema_after_step')
+        if own:
+            self.model.ema_after_step = True     # the codebook EMA goes after optimizer_step
+        try:
+            with K.ln_guard():
+                loss = self.forward_backward(text, video)
+        finally:
+            if own:
+                self.model.ema_after_step = False
         self.optimizer_step()
-        fe = getattr(self.model, 'flush_ema', None)
-        if fe is not None:
-            fe()          # a codebook EMA deferred past the optimizer (ct_clip.DEFER_EMA = '2')
         self._queue_ln_check()
         return loss.detach()
