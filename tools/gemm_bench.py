@@ -37,8 +37,11 @@ def main():
     cand = torch.empty(M, 128, 2, device='cuda')
     cand2 = torch.empty(M, 128, device='cuda')
     dh = r(M, 2816)
+    x512h, w1h = x512.half(), w1.half()
     cases = [
         ('FF1 NT+GEGLU  110592x2816x512', lambda: K.linear(x512, w1, act=K.ACT_GEGLU, out2=g), 2 * M * 2816 * 512),
+        ('FF1 f16 GEGLU 110592x2816x512', lambda: K.linear(x512h, w1h, act=K.ACT_GEGLU, out2=g,
+                                                           out_dtype=torch.float16), 2 * M * 2816 * 512),
         ('FF1 NT plain  110592x2816x512', lambda: K.linear(x512, w1, out=dh), 2 * M * 2816 * 512),
         ('FF2 NT+res32  110592x512x1408', lambda: K.linear(x1408, w2, residual=res, out_dtype=torch.float32),
          2 * M * 512 * 1408),
