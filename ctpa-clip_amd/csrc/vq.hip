@@ -215,6 +215,109 @@ __global__ __launch_bounds__(256) void vq_ema_accum_kernel(const int32_t* __rest
   if (cur >= 0) flush();
 }
 
+// Code-sorted EMA statistics (round 5; same sums as vq_ema_accum_kernel, bit for bit).  The
+// token-order kernel above flushes a run whenever the code changes; with a trained codebook
+// neighbouring tokens rarely share one, so it issues ~rows x D int64 atomics (56.6 M at B = 8:
+// ~1 ms on the auxiliary stream, beside the next step's HBM-bound patch LayerNorm).  Here the rows
+// are first bucketed by code (a counting sort: rank within the code by an int32 atomic, one
+// workgroup's exclusive scan, a scatter), then each wave walks VQ_EMA_CH consecutive positions of
+// the sorted order, where a code's rows are contiguous, so it flushes once per (code, chunk):
+// ~(C + rows / VQ_EMA_CH) x D atomics.  Integer addition is associative, so neither the rank order
+// nor the chunking changes any sum.  work (int32): cnt [C] (zero on entry, left zero), off [C],
+// rank [rows], perm [rows].
+constexpr int VQ_EMA_CH = 32;   // sorted positions per wave
+__global__ __launch_bounds__(256) void vq_rank_kernel(const int32_t* __restrict__ idx, int64_t rows, int C,
+                                                      int32_t* __restrict__ cnt, int32_t* __restrict__ rank) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < rows; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = min(max(idx[i], 0), C - 1);
+    rank[i] = atomicAdd(&cnt[c], 1);
+  }
+}
+
+// one workgroup of 1024 threads: off = exclusive prefix sum of cnt; bins += cnt (exact f32
+// integers, as the token-order kernel's f32 adds of run lengths); cnt zeroed for the next call
+__global__ __launch_bounds__(1024) void vq_code_scan_kernel(int32_t* __restrict__ cnt, int32_t* __restrict__ off, int C,
+                                                            float* __restrict__ bins) {
+  __shared__ int wsum[16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int per = (C + 1023) / 1024, c0 = min(C, t * per), c1 = min(C, c0 + per);
+  int s = 0;
+  for (int c = c0; c < c1; ++c) s += cnt[c];
+  int incl = s;   // inclusive scan over the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int base = 0;
+  for (int k = 0; k < w; ++k) base += wsum[k];
+  int run = base + incl - s;
+  for (int c = c0; c < c1; ++c) {
+    const int n = cnt[c];
+    off[c] = run;
+    run += n;
+    if (n) bins[c] += (float)n;
+    cnt[c] = 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void vq_scatter_kernel(const int32_t* __restrict__ idx, int64_t rows, int C,
+                                                         const int32_t* __restrict__ off,
+                                                         const int32_t* __restrict__ rank, int32_t* __restrict__ perm) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < rows; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = min(max(idx[i], 0), C - 1);
+    perm[off[c] + rank[i]] = (int32_t)i;
+  }
+}
+
+// lane owns columns lane + 64 j (D <= 1024); the next row's data is loaded before this row's adds
+__global__ __launch_bounds__(256) void vq_ema_sorted_kernel(const int32_t* __restrict__ idx,
+                                                            const int32_t* __restrict__ perm,
+                                                            const float* __restrict__ xn, int64_t rows, int D, int C,
+                                                            unsigned long long* __restrict__ esum) {
+  const int lane = threadIdx.x & 63;
+  const int64_t j0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * VQ_EMA_CH;
+  if (j0 >= rows) return;
+  const int64_t j1 = j0 + VQ_EMA_CH < rows ? j0 + VQ_EMA_CH : rows;
+  const int nj = (D + 63) >> 6;
+  long long acc[16];
+  float nx[16];
+  int cur = -1;
+  auto load = [&](int64_t j, float (&v)[16], int& code) {
+    const int r = perm[j];
+    code = min(max(idx[r], 0), C - 1);
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k < nj && lane + 64 * k < D) v[k] = xn[(int64_t)r * D + lane + 64 * k];
+  };
+  auto flush = [&]() {
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k < nj && lane + 64 * k < D) atomicAdd(&esum[(int64_t)cur * D + lane + 64 * k], (unsigned long long)acc[k]);
+  };
+  int code;
+  load(j0, nx, code);
+  for (int64_t j = j0; j < j1; ++j) {
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = nx[k];
+    const int c = code;
+    if (j + 1 < j1) load(j + 1, nx, code);
+    if (c != cur) {
+      if (cur >= 0) flush();
+      cur = c;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc[k] = 0;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+      if (k < nj && lane + 64 * k < D) acc[k] += (long long)rintf(v[k] * VQ_FX);
+  }
+  if (cur >= 0) flush();
+}
+
 // cluster_size = cs*decay + bins*(1-decay);  en = l2norm(esum / max(bins,1)); zero bins keep the
 // old code;  embed = embed*decay + en*(1-decay);  also refresh the bf16 working codebook.
 // RESET: the statistics are zeroed behind their reads (bins / esum are then ready for the next
@@ -312,6 +415,27 @@ extern "C" int ctclip_vq_ema_accum(const int32_t* idx, const float* xn, int64_t 
   const int blocks = cdiv(rows, 4 * VQ_EMA_RUN);
   hipLaunchKernelGGL(vq_ema_accum_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, idx, xn, rows, D, bins,
                      (unsigned long long*)esum);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+// the same statistics through the code-sorted kernels (work: int32 [2 C + 2 rows], the first C
+// entries zero on entry and left zero)
+extern "C" int ctclip_vq_ema_accum_sorted(const int32_t* idx, const float* xn, int64_t rows, int32_t D, int32_t C,
+                                          float* bins, int64_t* esum, int32_t* work, void* stream) {
+  if (rows == 0) return 0;
+  CT_REQUIRE(D <= 1024 && C > 0 && rows < (int64_t)1 << 31, CT_EINVAL);
+  hipStream_t st = (hipStream_t)stream;
+  int32_t *cnt = work, *off = work + C, *rank = work + 2 * (int64_t)C, *perm = rank + rows;
+  const int g = (int)std::min<int64_t>(cdiv(rows, 256), 2048);
+  hipLaunchKernelGGL(vq_rank_kernel, dim3(g), dim3(256), 0, st, idx, rows, C, cnt, rank);
+  CT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(vq_code_scan_kernel, dim3(1), dim3(1024), 0, st, cnt, off, C, bins);
+  CT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(vq_scatter_kernel, dim3(g), dim3(256), 0, st, idx, rows, C, off, rank, perm);
+  CT_CHECK_LAUNCH();
+  hipLaunchKernelGGL(vq_ema_sorted_kernel, dim3(cdiv(rows, 4 * VQ_EMA_CH)), dim3(256), 0, st, idx, perm, xn, rows, D,
+                     C, (unsigned long long*)esum);
   CT_CHECK_LAUNCH();
   return 0;
 }

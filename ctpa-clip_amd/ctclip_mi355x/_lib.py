@@ -210,6 +210,7 @@ _SIGS = {
     'ctclip_vq_pool_bwd': [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
     'ctclip_vq_gather': [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp],
     'ctclip_vq_ema_accum': [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp],
+    'ctclip_vq_ema_accum_sorted': [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp],
     'ctclip_vq_ema_finalize': [c_vp, c_vp, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp],
     'ctclip_vq_ema_finalize_reset': [c_vp, c_vp, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp],
     'ctclip_clip_loss': [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],

@@ -269,6 +269,10 @@ _L2N_FUSED = os.environ.get('CTCLIP_L2N_FUSED', '1') != '0'   # A/B switch of th
 # nor its output exists; the Q weight gradient uses the same fold (ctclip_lnfold_wgrad).
 # CTCLIP_LN1_FOLD=0: the LayerNorm kernel and the two projections (A/B switch).
 _LN1_FOLD = os.environ.get('CTCLIP_LN1_FOLD', '1') != '0'
+# the training VQ's EMA statistics accumulated in code-sorted order (kernels.vq_ema_accum with a work
+# buffer: ~10x fewer int64 atomics than the token-order kernel, same sums bit for bit);
+# CTCLIP_VQ_EMA_SORTED=0: token order (A/B)
+_EMA_SORTED = os.environ.get('CTCLIP_VQ_EMA_SORTED', '1') != '0'
 # fold backward: the q and k l2norm backwards as one pass (ctclip_l2norm_qk_bwd_fold); 0 = two (A/B)
 _QK_BWD_MERGED = os.environ.get('CTCLIP_QK_BWD_MERGED', '1') != '0'
 _QKV_WGRAD = os.environ.get('CTCLIP_QKV_WGRAD', '1') != '0'   # A/B switch of BERT's merged q/k/v wgrad
@@ -866,7 +870,8 @@ class VQPoolFn(torch.autograd.Function):
                 # persistent statistics (2^-40 fixed-point esum), zeroed once here and then by the
                 # finalize kernel behind its reads: no fill launches per step
                 bins, esum = state.ema_buffers(C, D, zf.device)
-                K.vq_ema_accum(idx, xn, bins, esum)
+                work = state.ema_work(C, xn.shape[0], zf.device) if _EMA_SORTED else None
+                K.vq_ema_accum(idx, xn, bins, esum, work=work)
                 dist_sync.sum_codebook_stats(bins, esum)
                 K.vq_ema_finalize(bins, esum, decay, cb, cluster.view(-1), cb_b, reset=True)
             if aux is None:
@@ -940,6 +945,16 @@ class VQState:
             b = (torch.zeros(C, device=device, dtype=F32), torch.zeros(C, D, device=device, dtype=torch.int64))
             self._ema_buf = b
         return b
+
+    def ema_work(self, C, rows, device):
+        """int32 scratch of the code-sorted EMA accumulation (kernels.vq_ema_accum): 2 C + 2 rows
+        entries, the first C zero between updates (the kernels leave them zero); grown as needed."""
+        w = getattr(self, '_ema_work', None)
+        n = 2 * C + 2 * rows
+        if w is None or w.numel() < n or w.device != device:
+            w = torch.zeros(n, device=device, dtype=torch.int32)
+            self._ema_work = w
+        return w
 
     def flush_ema(self):
         """Queue a deferred codebook EMA update (on the auxiliary stream, after the current stream's

@@ -1082,9 +1082,11 @@ def vq_gather(idx, codebook_f32):
     return out
 
 
-def vq_ema_accum(idx, xn, bins, esum):
+def vq_ema_accum(idx, xn, bins, esum, work=None):
     """bins (f32 counts) and esum (int64 [C][D], token sums in 2^-40 fixed point: bit-identical
-    whatever order the adds land in) accumulate the EMA statistics of rows xn (unit vectors)."""
+    whatever order the adds land in) accumulate the EMA statistics of rows xn (unit vectors).
+    work: int32 scratch of at least 2 C + 2 rows entries whose first C are zero (left zero): the
+    code-sorted kernels (ctclip_vq_ema_accum_sorted, ~10x fewer atomics); None: token order."""
     assert esum.dtype == torch.int64 and bins.dtype == F32
     # the 2^-40 fixed-point sums stay exact while every code's GLOBAL row count (summed over ranks
     # by dist_sync.sum_codebook_stats) is below 2^23; the f32 bins are exact below 2^24
@@ -1092,6 +1094,12 @@ def vq_ema_accum(idx, xn, bins, esum):
     if xn.shape[0] * dist_sync.world_rank()[0] >= (1 << 23):
         raise ValueError(f'vq_ema_accum: {xn.shape[0]} rows x {dist_sync.world_rank()[0]} ranks may exceed the 2^23 '
                          'rows per code that the int64 2^-40 fixed-point sums hold exactly')
+    if work is not None:
+        C = esum.shape[0]
+        assert work.dtype == torch.int32 and work.numel() >= 2 * C + 2 * xn.shape[0]
+        call('ctclip_vq_ema_accum_sorted', ptr(idx), ptr(xn), xn.shape[0], xn.shape[1], C, ptr(bins), ptr(esum),
+             ptr(work), stream_ptr())
+        return
     call('ctclip_vq_ema_accum', ptr(idx), ptr(xn), xn.shape[0], xn.shape[1], ptr(bins), ptr(esum), stream_ptr())
 
 

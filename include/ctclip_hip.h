@@ -498,6 +498,11 @@ int ctclip_vq_gather(const int32_t* idx, const float* codebook, int64_t rows, in
  * through a SUM all-reduce across ranks (bins: f32 counts, exact below 2^24). */
 int ctclip_vq_ema_accum(const int32_t* idx, const float* xn, int64_t rows, int32_t D, float* bins, int64_t* esum,
                         void* stream);
+/* the same statistics, bit for bit, with the rows first bucketed by code (counting sort), so the
+ * fixed-point adds go out once per (code, 32 sorted rows) instead of once per token-order run:
+ * work = int32 [2 C + 2 rows] scratch whose first C entries are zero on entry and left zero. */
+int ctclip_vq_ema_accum_sorted(const int32_t* idx, const float* xn, int64_t rows, int32_t D, int32_t C, float* bins,
+                               int64_t* esum, int32_t* work, void* stream);
 int ctclip_vq_ema_finalize(const float* bins, const int64_t* esum, int32_t C, int32_t D, float decay, float* embed,
                            float* cluster_size, void* embed_bf16, void* stream);
 /* ctclip_vq_ema_finalize that also zeroes bins / esum behind its reads, so persistent statistics

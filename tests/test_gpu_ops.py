@@ -327,6 +327,30 @@ def test_vq_select_and_pool(K):
                                                          torch.round(xno.cpu().double() * 2 ** 40).long())
     assert torch.equal(esum.cpu(), fx)
     assert torch.equal(bins.cpu(), torch.bincount(idx.long().cpu(), minlength=C).float())
+    # the code-sorted kernels: the same statistics bit for bit, on these rows and on a skewed index
+    # set (most rows on three codes, as from an untrained codebook) at the step's row count; the
+    # work buffer's count region is left zero, so a second call accumulates again
+    work = torch.zeros(2 * C + 2 * M, device=dev, dtype=torch.int32)
+    bins_s = torch.zeros(C, device=dev)
+    esum_s = torch.zeros(C, D, device=dev, dtype=torch.int64)
+    K.vq_ema_accum(idx, xno, bins_s, esum_s, work=work)
+    assert torch.equal(esum_s, esum) and torch.equal(bins_s, bins)
+    assert work[:C].abs().sum().item() == 0
+    Mb = 110592
+    gsk = torch.Generator(device=dev).manual_seed(12)
+    ids = torch.randint(0, C, (Mb,), device=dev, generator=gsk, dtype=torch.int32)
+    hotm = torch.rand(Mb, device=dev, generator=gsk) < 0.9
+    hot = torch.tensor([7, 4000, 8191], device=dev, dtype=torch.int32)
+    ids[hotm] = hot[torch.randint(0, 3, (int(hotm.sum().item()),), device=dev, generator=gsk)]
+    xs = F.normalize(torch.randn(Mb, D, device=dev, generator=gsk), dim=-1)
+    for ix in (ids, torch.randint(0, C, (Mb,), device=dev, generator=gsk, dtype=torch.int32)):
+        b0, e0 = torch.zeros(C, device=dev), torch.zeros(C, D, device=dev, dtype=torch.int64)
+        K.vq_ema_accum(ix, xs, b0, e0)
+        wk = torch.zeros(2 * C + 2 * Mb, device=dev, dtype=torch.int32)
+        b1, e1 = torch.zeros(C, device=dev), torch.zeros(C, D, device=dev, dtype=torch.int64)
+        K.vq_ema_accum(ix, xs, b1, e1, work=wk)
+        K.vq_ema_accum(ix, xs, b1, e1, work=wk)     # twice: statistics double exactly
+        assert torch.equal(b1, 2 * b0) and torch.equal(e1, 2 * e0)
     emb = cb.clone()
     cs = torch.zeros(C, device=dev)
     K.vq_ema_finalize(bins, esum, 0.8, emb, cs)
