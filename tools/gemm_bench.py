@@ -38,6 +38,8 @@ def main():
     cand2 = torch.empty(M, 128, device='cuda')
     dh = r(M, 2816)
     x512h, w1h = x512.half(), w1.half()
+    sqa, sqb = r(8192, 8192), r(8192, 8192)
+    sqo = torch.empty(8192, 8192, device='cuda', dtype=torch.bfloat16)
     cases = [
         ('FF1 NT+GEGLU  110592x2816x512', lambda: K.linear(x512, w1, act=K.ACT_GEGLU, out2=g), 2 * M * 2816 * 512),
         ('FF1 f16 GEGLU 110592x2816x512', lambda: K.linear(x512h, w1h, act=K.ACT_GEGLU, out2=g,
@@ -63,6 +65,9 @@ def main():
         ('dW  TN s4     2816x512x110592', lambda: K.matmul_tn(dh, x512, split_k=4), 2 * M * 512 * 2816),
         ('dW  TN s40    512x512x110592', lambda: K.matmul_tn(x512, x512, split_k=40), 2 * M * 512 * 512),
         ('dW  TN        512x512x110592', lambda: K.matmul_tn(x512, x512), 2 * M * 512 * 512),
+        ('sq  NT        8192x8192x8192', lambda: K.linear(sqa, sqb, out=sqo), 2 * 8192 ** 3),
+        ('sq  NN        8192x8192x8192', lambda: K.matmul_nn(sqa, sqb), 2 * 8192 ** 3),
+        ('sq  TN        8192x8192x8192', lambda: K.matmul_tn(sqa, sqb), 2 * 8192 ** 3),
     ]
     from ctclip_mi355x import _lib
     variants = [v for v in os.environ.get('GEMM_VARIANTS', '8,1').split(',')]
