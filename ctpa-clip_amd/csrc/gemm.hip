@@ -366,6 +366,34 @@ __global__ void reduce_slabs_kernel(const float* __restrict__ s, int64_t nslab, 
   }
 }
 
+// split-K slab reduction straight into a row-mapped, column-cropped f32 destination (the packed FF
+// weight gradients: dst[map[r]][c] (+)= sum_z s[z][r][c] for c < cols, rows with map[r] < 0 dropped):
+// the reduction and the unpack of the packed rows in one pass, summed in reduce_slabs_kernel's order
+// (0 + s0 + s1 + ...) and added to dst as the unpack did, so bit-identical to that pair
+template <bool V4>
+__global__ __launch_bounds__(256) void reduce_slabs_rows_kernel(const float* __restrict__ s, int64_t nslab, int64_t rows,
+                                                                int64_t cols, int64_t ld, const int32_t* __restrict__ map,
+                                                                float* __restrict__ dst, int64_t ldd, int accumulate) {
+  constexpr int W = V4 ? 4 : 1;
+  const int64_t nw = cols / W, total = rows * nw;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / nw, c = (i - r * nw) * W;
+    const int64_t dr = map ? (int64_t)map[r] : r;
+    if (dr < 0) continue;
+    if constexpr (V4) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int64_t z = 0; z < nslab; ++z) acc += *(const f32x4*)(s + (z * rows + r) * ld + c);
+      f32x4* o = (f32x4*)(dst + dr * ldd + c);
+      *o = accumulate ? *o + acc : acc;
+    } else {
+      float acc = 0.f;
+      for (int64_t z = 0; z < nslab; ++z) acc += s[(z * rows + r) * ld + c];
+      float* o = dst + dr * ldd + c;
+      *o = accumulate ? *o + acc : acc;
+    }
+  }
+}
+
 // skinny reduction (few output elements, many slabs): block = 64 float4 columns x 16 slab lanes
 __global__ __launch_bounds__(1024) void reduce_slabs_skinny_kernel(const float* __restrict__ s, int64_t nslab,
                                                                    int64_t rows, int64_t cols, int64_t ld,
@@ -644,6 +672,23 @@ extern "C" int ctclip_reduce_slabs_multi(const ctclip_slab_job* jobs, int32_t nj
                        (hipStream_t)stream, mj);
     CT_CHECK_LAUNCH();
   }
+  return 0;
+}
+
+extern "C" int ctclip_reduce_slabs_rows(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,
+                                        const int32_t* map, float* dst, int64_t ldd, int32_t accumulate, void* stream) {
+  if (rows == 0 || cols == 0) return 0;
+  CT_REQUIRE(cols <= ld, CT_EINVAL);
+  const bool v4 = cols % 4 == 0 && ld % 4 == 0 && ldd % 4 == 0 && aligned16(slabs) && aligned16(dst);
+  const int64_t total = rows * (v4 ? cols / 4 : cols);
+  const int blocks = (int)std::min<int64_t>(4096, (total + 255) / 256);
+  if (v4)
+    hipLaunchKernelGGL(reduce_slabs_rows_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slabs, nslab,
+                       rows, cols, ld, map, dst, ldd, accumulate);
+  else
+    hipLaunchKernelGGL(reduce_slabs_rows_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slabs, nslab,
+                       rows, cols, ld, map, dst, ldd, accumulate);
+  CT_CHECK_LAUNCH();
   return 0;
 }
 

@@ -175,6 +175,7 @@ _SIGS = {
     'ctclip_pack_rows_f32': [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp],
     'ctclip_sgemm_tn': [ctypes.POINTER(SgemmTnArgs), c_vp],
     'ctclip_unpack_rows': [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp],
+    'ctclip_reduce_slabs_rows': [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp],
     'ctclip_gelu_f32': [c_vp, c_vp, c_i64, c_vp],
     'ctclip_cast_f32_bf16': [c_vp, c_vp, c_i64, c_vp],
     'ctclip_cast_f32_bf16_split': [c_vp, c_vp, c_vp, c_i64, c_vp],

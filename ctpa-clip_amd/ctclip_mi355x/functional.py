@@ -269,6 +269,9 @@ _L2N_FUSED = os.environ.get('CTCLIP_L2N_FUSED', '1') != '0'   # A/B switch of th
 # nor its output exists; the Q weight gradient uses the same fold (ctclip_lnfold_wgrad).
 # CTCLIP_LN1_FOLD=0: the LayerNorm kernel and the two projections (A/B switch).
 _LN1_FOLD = os.environ.get('CTCLIP_LN1_FOLD', '1') != '0'
+# the FeedForward weight gradients' split-K slabs reduced straight into the unpacked .grad rows
+# (ctclip_reduce_slabs_rows); CTCLIP_DW_UNPACK_FUSED=0: slab reduction + unpack_rows (A/B)
+_DW_UNPACK_FUSED = os.environ.get('CTCLIP_DW_UNPACK_FUSED', '1') != '0'
 # the training VQ's EMA statistics accumulated in code-sorted order (kernels.vq_ema_accum with a work
 # buffer: ~10x fewer int64 atomics than the token-order kernel, same sums bit for bit);
 # CTCLIP_VQ_EMA_SORTED=0: token order (A/B)
@@ -665,7 +668,15 @@ class ViTLayerFn(torch.autograd.Function):
         # feed-forward (weight gradients accumulate straight into the parameters' .grad)
         dh_ = K.matmul_nn_geglu_bwd(dx3b, W2p, h)      # dg = dx3 . W2 and the GEGLU backward, fused
         M_ = dx3b.shape[0]
-        dW2p = K.matmul_tn(dx3b, g, tag='dw', flops=2.0 * M_ * W2.shape[0] * W2.shape[1])
+        # weight gradients reduced from their split-K slabs straight into the unpacked .grad rows
+        # (ctclip_reduce_slabs_rows: one pass instead of a slab reduction + unpack_rows)
+        if gsink(W2) is not None:
+            if _DW_UNPACK_FUSED:
+                K.matmul_tn(dx3b, g, tag='dw', flops=2.0 * M_ * W2.shape[0] * W2.shape[1],
+                            unpack=(gsink(W2), None, W2.shape[1]))
+            else:
+                K.unpack_rows(K.matmul_tn(dx3b, g, tag='dw', flops=2.0 * M_ * W2.shape[0] * W2.shape[1]), gsink(W2),
+                              cols=W2.shape[1], accumulate=True)
         # dx2 = LN'(dh . W1) + dx3 in one launch where the shape allows (gemm256.hip, EP -7)
         fused = K.matmul_nn_ln_bwd(dh_, W1p, x2b, m2, r2, ff_w, dx3f, dgamma_out=gsink(ff_w),
                                    dbeta_out=gsink(ff_b)) if K.ln_guarded() else None
@@ -674,14 +685,19 @@ class ViTLayerFn(torch.autograd.Function):
                 dxn2 = torch.matmul(dh_, W1p.t().contiguous().t())
             else:
                 dxn2 = K.matmul_nn(dh_, W1p)
-        dW1p = K.matmul_tn(dh_, xn2, tag='dw', flops=2.0 * M_ * W1.shape[0] * W1.shape[1])
+        if gsink(W1) is not None:
+            rmap = ff1_rowmap(W1.shape[0] // 2, dev)
+            if _DW_UNPACK_FUSED:
+                K.matmul_tn(dh_, xn2, tag='dw', flops=2.0 * M_ * W1.shape[0] * W1.shape[1],
+                            unpack=(gsink(W1), rmap, W1.shape[1]))
+            else:
+                K.unpack_rows(K.matmul_tn(dh_, xn2, tag='dw', flops=2.0 * M_ * W1.shape[0] * W1.shape[1]), gsink(W1),
+                              rowmap=rmap, accumulate=True)
         if fused is not None:
             dx2f, dx2b = fused
         else:
             dx2f, dx2b, _, _ = K.layernorm_bwd(dxn2, x2b, m2, r2, ff_w, dres=dx3f, dgamma_out=gsink(ff_w),
                                                dbeta_out=gsink(ff_b))
-        K.unpack_rows(dW1p, gsink(W1), rowmap=ff1_rowmap(W1.shape[0] // 2, dev), accumulate=True)
-        K.unpack_rows(dW2p, gsink(W2), cols=W2.shape[1], accumulate=True)
         # attention
         do = K.matmul_nn(dx2b, Wo_b)
         K.matmul_tn(dx2b, o, out=gsink(Wo), accumulate=True, tag='dw')

@@ -364,9 +364,12 @@ def split_for(m_rows, tiles):
     return max(1, s)
 
 
-def matmul_tn(dy, x, *, out=None, accumulate=False, split_k=None, alpha=1.0, tag=None, flops=None):
+def matmul_tn(dy, x, *, out=None, accumulate=False, split_k=None, alpha=1.0, tag=None, flops=None, unpack=None):
     """dW[N,K] (f32) = dy[M,N]^T @ x[M,K]; reduction over the M tokens (split-K slabs).
-    tag / flops: KernelTimer bracketing of the GEMM launch (not the slab reduction)."""
+    tag / flops: KernelTimer bracketing of the GEMM launch (not the slab reduction).
+    unpack=(dst, rowmap, cols): accumulate dW[r, :cols] into dst[rowmap[r]] (rowmap None = identity,
+    negative entries dropped) instead of returning dW -- with split-K slabs in one reduction pass
+    (ctclip_reduce_slabs_rows), bit-identical to dW followed by unpack_rows."""
     M, N = dy.shape
     K = x.shape[1]
     assert x.shape[0] == M
@@ -387,10 +390,20 @@ def matmul_tn(dy, x, *, out=None, accumulate=False, split_k=None, alpha=1.0, tag
     if s <= 1:
         gemm_raw(N, K, M, dy, dy.stride(0), False, x, x.stride(0), False, out, out.stride(0),
                  accumulate=accumulate, alpha=alpha, tag=tag, flops=flops)
+        if unpack is not None:
+            dst, rowmap, cols = unpack
+            return unpack_rows(out, dst, rowmap=rowmap, cols=cols, accumulate=True)
         return out
     slabs = torch.empty(s, N, K, device=dy.device, dtype=F32)
     gemm_raw(N, K, M, dy, dy.stride(0), False, x, x.stride(0), False, slabs, K, split_k=s, alpha=alpha, tag=tag,
              flops=flops)
+    if unpack is not None:
+        dst, rowmap, cols = unpack
+        assert dst.dtype == F32 and dst.stride(1) == 1 and cols <= K
+        assert rowmap is None or (rowmap.dtype == torch.int32 and rowmap.numel() == N)
+        call('ctclip_reduce_slabs_rows', ptr(slabs), s, N, cols, K, ptr(rowmap), ptr(dst), dst.stride(0), 1,
+             stream_ptr())
+        return dst
     reduce_slabs(slabs, out, accumulate=accumulate)
     return out
 

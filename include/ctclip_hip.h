@@ -202,6 +202,12 @@ int ctclip_lnfold_wgrad(const float* G, int64_t ldg, const float* u, const float
 int ctclip_skinny_gemm_slices(int64_t M, int64_t N, int64_t K);
 int ctclip_skinny_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
                        float* slabs, int32_t nslices, void* stream);
+/* split-K slab reduction into a row-mapped, column-cropped f32 destination: dst[map[r]][c] (+)=
+ * sum_z slabs[z][r][c] for c < cols <= ld (rows with map[r] < 0 dropped; map NULL = identity).
+ * Bit-identical to ctclip_reduce_slabs into a temporary followed by ctclip_unpack_rows (the packed
+ * GEGLU W1 / padded W2 weight gradients of attention.py:44-52). */
+int ctclip_reduce_slabs_rows(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,
+                             const int32_t* map, float* dst, int64_t ldd, int32_t accumulate, void* stream);
 /* sum f32 slabs [s][rows][ld] -> out (f32 or bf16), optional accumulate into f32 out */
 int ctclip_reduce_slabs(const float* slabs, int64_t nslab, int64_t rows, int64_t cols, int64_t ld,
                         void* out, int64_t ldo, int32_t out_f32, int32_t accumulate, void* stream);

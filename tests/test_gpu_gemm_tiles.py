@@ -132,6 +132,36 @@ def test_tn_split_slabs(K):
     assert torch.allclose(outs[8], outs[1], rtol=0, atol=1e-3)
 
 
+@pytest.mark.parametrize('N,Kd,cols,packed', [(2816, 512, 512, True), (512, 1408, 1365, False)])
+def test_tn_slabs_into_unpacked_rows(K, N, Kd, cols, packed):
+    """The FeedForward weight gradients at the step's token count: the split-K slabs reduced
+    straight into the unpacked, accumulated .grad rows (ctclip_reduce_slabs_rows; W1's GEGLU-packed
+    rows through ff1_rowmap, W2's padded columns cropped) equal dW followed by unpack_rows, bit for
+    bit."""
+    from ctclip_mi355x import functional as Fn
+    torch.manual_seed(3)
+    M = 110592
+    dy = (torch.randn(M, N, device='cuda') * 0.1).bfloat16()
+    x = (torch.randn(M, Kd, device='cuda') * 0.1).bfloat16()
+    rowmap = Fn.ff1_rowmap(1365, dy.device) if packed else None
+    rows = 2730 if packed else N
+    base = torch.randn(rows, cols, device='cuda')
+    fused, ref = base.clone(), base.clone()
+    K.matmul_tn(dy, x, unpack=(fused, rowmap, cols))
+    dw = K.matmul_tn(dy, x)
+    K.unpack_rows(dw, ref, rowmap=rowmap, cols=cols, accumulate=True)
+    torch.cuda.synchronize()
+    assert torch.equal(fused, ref)
+    full = dy.float().t() @ x.float()
+    want = base.clone()
+    if packed:
+        keep = rowmap >= 0
+        want.index_add_(0, rowmap[keep].long(), full[keep][:, :cols])
+    else:
+        want += full[:, :cols]
+    assert _rel(fused - base, want - base) < 1e-5
+
+
 def test_nn_accumulate_shadow(K):
     torch.manual_seed(3)
     M, N, Kd = 10000, 2816, 1024
