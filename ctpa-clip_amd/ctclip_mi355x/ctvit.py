@@ -136,7 +136,8 @@ class CTViT(nn.Module):
             with torch.cuda.stream(aux):
                 bias_u = self.spatial_rel_pos_bias(hg, wg)
                 # the layers' packed FeedForward weights too (16 small launches off the main stream)
-                packs = Fn.prepack_ff(self._ff_weights(), self._out_weights()) if _PREPACK_AUX else []
+                packs = Fn.prepack_ff(self._ff_weights(), self._out_weights(), self._qkv_weights()) \
+                    if _PREPACK_AUX else []
                 cpb_ev = aux.record_event()
             bias_u.record_stream(main)
             for t in packs:
@@ -178,6 +179,16 @@ class CTViT(nn.Module):
 
     def _out_weights(self):
         return [attn.to_out.weight for tr in (self.enc_spatial_transformer, self.enc_temporal_transformer)
+                for (_, attn, _, _) in tr.layers]
+
+    def _qkv_weights(self):
+        """(Wq, LayerNorm gamma, Wkv, q_scale, k_scale) of every layer whose Q | K | V projection
+        folds its LayerNorm (functional.ViTLayerFn; the fold's own gate decides per layer, an
+        unused prepack is dropped at the next one)"""
+        if not Fn._LN1_FOLD or self.dim_head != 32 or self.heads * self.dim_head != 256:
+            return []
+        return [(attn.to_q.weight, attn.norm.gamma, attn.to_kv.weight, attn.q_scale, attn.k_scale)
+                for tr in (self.enc_spatial_transformer, self.enc_temporal_transformer)
                 for (_, attn, _, _) in tr.layers]
 
     def _ff_weights(self):

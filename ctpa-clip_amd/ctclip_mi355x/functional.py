@@ -169,12 +169,43 @@ def h16(W):
     return K.pack_rows_h16(W, W.shape[0], W.shape[1])
 
 
-def prepack_ff(pairs, wo=()):
+def _fold_key(kind, Wq, gamma, Wkv, qs, ks):
+    return (kind,) + tuple((t.data_ptr(), t._version) for t in (Wq, gamma, Wkv, qs, ks)) + (K.weights_epoch(),)
+
+
+def qkv_fold_pack(Wq, gamma, Wkv, Wkv_b, q_scale, k_scale):
+    """K.pack_qkv_fold of a layer (bf16 [Wq o gamma ; Wkv], fold sums, scales), prepacked by
+    prepack_ff when the weights have not changed since."""
+    hit = _PREPACKED.get(_fold_key('qkvf', Wq, gamma, Wkv, q_scale, k_scale))
+    if hit is not None:
+        return hit
+    return K.pack_qkv_fold(Wq.detach(), gamma, Wkv_b, q_scale.detach(), k_scale.detach())
+
+
+def qkv_fold_pack_h16(Wq, gamma, Wkv, q_scale, k_scale):
+    """K.pack_qkv_fold_h16 of a layer (the fp16 forward's folded B operand and fold sums)."""
+    hit = _PREPACKED.get(_fold_key('qkvh', Wq, gamma, Wkv, q_scale, k_scale))
+    if hit is not None:
+        return hit
+    return K.pack_qkv_fold_h16(Wq.detach(), gamma, Wkv.detach())
+
+
+def prepack_ff(pairs, wo=(), qkv=()):
     """Pack every layer's FeedForward weights now (on the caller's current stream) for the layers
     that run later (pack_ff1 / pack_ff2 then return these) -- with the fp16 forward also the fp16 W1
-    images and the attention output weights `wo`; returns the packed tensors."""
+    images and the attention output weights `wo` -- and, for the LayerNorm-folded Q | K | V
+    projection, each layer's folded B operand (`qkv`: (Wq, gamma, Wkv, q_scale, k_scale) per
+    layer); returns the packed tensors."""
     _PREPACKED.clear()
     out = []
+    for Wq, gamma, Wkv, qs, ks in qkv:
+        f = K.pack_qkv_fold(Wq.detach(), gamma, bf(Wkv), qs.detach(), ks.detach())
+        _PREPACKED[_fold_key('qkvf', Wq, gamma, Wkv, qs, ks)] = f
+        out += list(f)
+        if vit_f16():
+            h = K.pack_qkv_fold_h16(Wq.detach(), gamma, Wkv.detach())
+            _PREPACKED[_fold_key('qkvh', Wq, gamma, Wkv, qs, ks)] = h
+            out += list(h)
     for W1, W2 in pairs:
         a, b = pack_ff1(W1), pack_ff2(W2)
         _PREPACKED[_pack_key('ff1', W1)] = a
@@ -569,9 +600,9 @@ class ViTLayerFn(torch.autograd.Function):
         else:
             xn, _, m1, r1 = K.layernorm_fwd(x1f, norm_g, None, 1e-5)
         if fold:
-            Wp, cs, scales = K.pack_qkv_fold(Wq.detach(), norm_g, Wkv_b, q_scale.detach(), k_scale.detach())
+            Wp, cs, scales = qkv_fold_pack(Wq, norm_g, Wkv, Wkv_b, q_scale, k_scale)
             if f16:
-                Wp16, cs16 = K.pack_qkv_fold_h16(Wq.detach(), norm_g, Wkv.detach())
+                Wp16, cs16 = qkv_fold_pack_h16(Wq, norm_g, Wkv, q_scale, k_scale)
                 qkv, qkn = K.linear_qkv_lnfold(x1h, Wp16, cs16, m1, r1, scales, inner, 2 * inner)
                 del x1h, Wp16
             else:
