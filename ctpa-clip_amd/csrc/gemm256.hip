@@ -1750,6 +1750,7 @@ int launch8_any(const P& p, bool bk, int batch, hipStream_t st) {
 int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream) {
   using namespace g256;
   P p;
+  memset(&p, 0, sizeof(p));
   p.M = a->M; p.N = a->N; p.K = a->K;
   p.A = (const u16*)a->A; p.lda = a->lda;
   p.B = (const u16*)a->B; p.ldb = a->ldb;
