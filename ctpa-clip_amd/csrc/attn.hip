@@ -1727,36 +1727,76 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// row fragments of rows 16u + (lane & 15), d chunk lane >> 4 (zero past L): exactly the MFMA
-// operand layout of rowfrag(), read straight from HBM (16 B per lane per block)
-__device__ __forceinline__ void load_rows(bf16x8 (&f)[2], const u16* x, int64_t ld, const AP& p, int s, int h,
-                                          int lane) {
+// A lane's two token rows 16u + (lane & 15) of sequence s: every load and store of the pair (Q, K,
+// V, dO, O, lse; O, dQ, dK, dV) touches only these.  The sequence base is wave-uniform (s derives
+// from a readfirstlane'd wave index, so its division and products run on the scalar unit); the
+// per-tensor offsets are 32 x 32 -> 64-bit products (small_ok: M and every ld < 2^31).  Written
+// per call, seq_row's division by n_inner and its int64 products had made both kernels VALU-issue
+// bound (895 / 1,564 VALU instructions per wave, 13 / 21 of them integer divisions).
+struct SmallRows {
+  unsigned row[2];
+  bool ok[2];
+};
+__device__ __forceinline__ SmallRows small_rows(const AP& p, int s, int lane) {
+  const unsigned base = (unsigned)seq_row(p, s, 0);
+  const unsigned sp = (unsigned)p.s_pos;
+  SmallRows R;
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int r = 16 * u + (lane & 15);
-    f[u] = r < p.L ? gload8(x + seq_row(p, s, r) * ld + h * 32 + 8 * (lane >> 4)) : zero8();
+    R.ok[u] = r < p.L;
+    R.row[u] = base + (unsigned)r * sp;
   }
+  return R;
+}
+__device__ __forceinline__ uint64_t roff(unsigned row, int64_t ld) { return (uint64_t)row * (unsigned)ld; }
+
+// row fragments of rows 16u + (lane & 15), d chunk lane >> 4 (zero past L): exactly the MFMA
+// operand layout of rowfrag(), read straight from HBM (16 B per lane per block)
+__device__ __forceinline__ void load_rows(bf16x8 (&f)[2], const u16* x, int64_t ld, const SmallRows& R, int h,
+                                          int lane) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) f[u] = R.ok[u] ? gload8(x + roff(R.row[u], ld) + h * 32 + 8 * (lane >> 4)) : zero8();
 }
 
-// the same fragments into a wave-private image (for the trfrag column reads)
+// the same fragments into a wave-private image for the trfrag column reads, its d columns
+// interleaved in 4-element chunks: image columns 0-15 hold d = 8c + 0..3 and columns 16-31
+// d = 8c + 4..7 (c = 0..3).  An MFMA pair over the two column blocks (rows 4g + r of each) then
+// leaves lane group g holding d = 8g .. 8g + 7 of its token row, stored as ONE 16-B piece per lane:
+// 64 contiguous bytes per row per instruction instead of two 32-B halves in two instructions (the
+// partial-line stores had bound the kernels: the forward's fp16 copy of O alone cost 44 -> 87 us).
 __device__ __forceinline__ void put_rows(char* img, const bf16x8 (&f)[2], int lane) {
+  const int g = lane >> 4;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) *(bf16x8*)(img + (16 * u + (lane & 15)) * Img<32>::RS + (lane >> 4) * 16) = f[u];
+  for (int u = 0; u < 2; ++u) {
+    char* row = img + (16 * u + (lane & 15)) * Img<32>::RS;
+    const u32x4 v = __builtin_bit_cast(u32x4, f[u]);
+    *(uint2*)(row + 8 * g) = make_uint2(v.x, v.y);           // d 8g .. 8g + 3   -> column 4g
+    *(uint2*)(row + 32 + 8 * g) = make_uint2(v.z, v.w);      // d 8g + 4 .. + 7 -> column 16 + 4g
+  }
+}
+__device__ __forceinline__ void cat8(float (&o)[8], const f32x4& a, const f32x4& b, float sc) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    o[r] = a[r] * sc;
+    o[4 + r] = b[r] * sc;
+  }
 }
 
 __global__ __launch_bounds__(SW * 64) void attn_small_fwd_kernel(AP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pair = blockIdx.x * SW + w;
   if (pair >= p.nseq * p.H) return;            // wave-uniform; no workgroup barriers below
   const int s = pair / p.H, h = pair - s * p.H;
   char* Vi = smem + w * SIMG;
+  const SmallRows R = small_rows(p, s, lane);
   bf16x8 qr[2], kr[2], vr[2];
-  load_rows(qr, p.q, p.ldq, p, s, h, lane);
-  load_rows(kr, p.k, p.ldk, p, s, h, lane);
-  load_rows(vr, p.v, p.ldv, p, s, h, lane);
+  load_rows(qr, p.q, p.ldq, R, h, lane);
+  load_rows(kr, p.k, p.ldk, R, h, lane);
+  load_rows(vr, p.v, p.ldv, R, h, lane);
   put_rows(Vi, vr, lane);
-  const int i = lane & 15, g = lane >> 4;
+  const int g = lane >> 4;                      // (query 16qb + (lane & 15): the lane's row qb)
   const float c2 = p.scale * LOG2E;
   const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
   // S^T blocks (key block kb, query block qb): lane column = query 16qb + i, rows = keys 16kb + 4g + r
@@ -1766,7 +1806,8 @@ __global__ __launch_bounds__(SW * 64) void attn_small_fwd_kernel(AP p) {
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) st[kb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kr[kb], qr[qb], z4, 0, 0, 0);
   wave_lds_sync();
-  // V^T column fragments (d block db): lane row d = 16db + i, keys 4g + 0..3 and 16 + 4g + 0..3
+  // V^T column fragments (image column block db: d = 8 (i / 4) + 4 db + i % 4), keys 4g + 0..3 and
+  // 16 + 4g + 0..3
   const bf16x8 vt[2] = {trfrag<32>(Vi, 0, 0, lane), trfrag<32>(Vi, 0, 16, lane)};
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
@@ -1793,29 +1834,28 @@ __global__ __launch_bounds__(SW * 64) void attn_small_fwd_kernel(AP p) {
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
     const bf16x8 pf = pack_perm(st[0][qb], st[1][qb]);       // P^T: keys in the trfrag order
-    const int q = 16 * qb + i;
     const float inv = 1.f / l;
-#pragma unroll
-    for (int db = 0; db < 2; ++db) {
-      // O^T block: lane column = query q, rows d = 16db + 4g + r
-      const f32x4 ot = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt[db], pf, z4, 0, 0, 0);
-      if (q < p.L) {
-        const float o4[4] = {ot[0] * inv, ot[1] * inv, ot[2] * inv, ot[3] * inv};
-        const int64_t off = seq_row(p, s, q) * p.ldout + h * 32 + 16 * db + 4 * g;
-        *(uint2*)(p.out + off) = pack4(o4);
-        if (p.out16) *(uint2*)(p.out16 + off) = pack4h(o4);
-      }
+    // O^T blocks: lane column = query 16 qb + i (the lane's row qb), rows d = 8g + 4db + r
+    const f32x4 o0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt[0], pf, z4, 0, 0, 0);
+    const f32x4 o1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt[1], pf, z4, 0, 0, 0);
+    if (R.ok[qb]) {
+      float o8[8];
+      cat8(o8, o0, o1, inv);
+      const uint64_t off = roff(R.row[qb], p.ldout) + h * 32 + 8 * g;
+      *(u32x4*)(p.out + off) = pack8(o8);
+      if (p.out16) *(u32x4*)(p.out16 + off) = pack8h(o8);
     }
-    if (g == 0 && q < p.L && p.lse) p.lse[(int64_t)h * p.M + seq_row(p, s, q)] = (m + __log2f(l)) * LN2;
+    if (g == 0 && R.ok[qb] && p.lse) p.lse[(int64_t)h * p.M + R.row[qb]] = (m + __log2f(l)) * LN2;
   }
 }
 
 __global__ __launch_bounds__(SW * 64) void attn_small_bwd_kernel(AP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pair = blockIdx.x * SW + w;
   if (pair >= p.nseq * p.H) return;
   const int s = pair / p.H, h = pair - s * p.H;
+  const SmallRows R = small_rows(p, s, lane);
   char* Qi = smem + w * (3 * SIMG + 256);
   char* Ki = Qi + SIMG;
   char* Di = Ki + SIMG;                         // dO
@@ -1823,17 +1863,14 @@ __global__ __launch_bounds__(SW * 64) void attn_small_bwd_kernel(AP p) {
   float* dlt = lse2 + 32;                       // [32] delta = rowsum(dO * O)
   const int i = lane & 15, g = lane >> 4;
   bf16x8 qr[2], kr[2], vr[2], dr[2], orr[2];
-  load_rows(qr, p.q, p.ldq, p, s, h, lane);
-  load_rows(kr, p.k, p.ldk, p, s, h, lane);
-  load_rows(vr, p.v, p.ldv, p, s, h, lane);
-  load_rows(dr, p.dout, p.lddo, p, s, h, lane);
-  load_rows(orr, p.o, p.ldo, p, s, h, lane);
+  load_rows(qr, p.q, p.ldq, R, h, lane);
+  load_rows(kr, p.k, p.ldk, R, h, lane);
+  load_rows(vr, p.v, p.ldv, R, h, lane);
+  load_rows(dr, p.dout, p.lddo, R, h, lane);
+  load_rows(orr, p.o, p.ldo, R, h, lane);
   float lq[2];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int q = 16 * u + i;
-    lq[u] = q < p.L ? p.lse[(int64_t)h * p.M + seq_row(p, s, q)] * LOG2E : INFINITY;
-  }
+  for (int u = 0; u < 2; ++u) lq[u] = R.ok[u] ? p.lse[(int64_t)h * p.M + R.row[u]] * LOG2E : INFINITY;
   put_rows(Qi, qr, lane);
   put_rows(Ki, kr, lane);
   put_rows(Di, dr, lane);
@@ -1873,23 +1910,22 @@ __global__ __launch_bounds__(SW * 64) void attn_small_bwd_kernel(AP p) {
     dsf[qb] = pack_perm(ds[0], ds[1]);
   }
   wave_lds_sync();
+  const bf16x8 kt0 = trfrag<32>(Ki, 0, 0, lane), kt1 = trfrag<32>(Ki, 0, 16, lane);
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
-    const int q = 16 * qb + i;
-#pragma unroll
-    for (int db = 0; db < 2; ++db) {
-      const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag<32>(Ki, 0, 16 * db, lane), dsf[qb], z4, 0, 0, 0);
-      if (q < p.L) {
-        const float d4[4] = {acc[0] * p.scale, acc[1] * p.scale, acc[2] * p.scale, acc[3] * p.scale};
-        *(uint2*)(p.dq + seq_row(p, s, q) * p.lddq + h * 32 + 16 * db + 4 * g) = pack4(d4);
-      }
+    // dQ^T blocks, rows d = 8g + 4db + r (interleaved images), column = query 16 qb + i
+    const f32x4 a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt0, dsf[qb], z4, 0, 0, 0);
+    const f32x4 a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt1, dsf[qb], z4, 0, 0, 0);
+    if (R.ok[qb]) {
+      float d8[8];
+      cat8(d8, a0, a1, p.scale);
+      *(u32x4*)(p.dq + roff(R.row[qb], p.lddq) + h * 32 + 8 * g) = pack8(d8);
     }
   }
   // ---- S layout (lane = key): dV^T = dO^T P, dK^T = scale * Q^T dS
 #pragma unroll
   for (int kb = 0; kb < 2; ++kb) {
-    const int k = 16 * kb + i;
-    const bool kv = k < p.L;
+    const bool kv = R.ok[kb];                   // key 16 kb + i: the lane's row kb
     f32x4 pm[2], ds[2];
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
@@ -1905,22 +1941,34 @@ __global__ __launch_bounds__(SW * 64) void attn_small_bwd_kernel(AP p) {
       }
     }
     const bf16x8 pf = pack_perm(pm[0], pm[1]), dsk = pack_perm(ds[0], ds[1]);
+    f32x4 dv[2], dk[2];
 #pragma unroll
     for (int db = 0; db < 2; ++db) {
-      const f32x4 dv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag<32>(Di, 0, 16 * db, lane), pf, z4, 0, 0, 0);
-      const f32x4 dk = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag<32>(Qi, 0, 16 * db, lane), dsk, z4, 0, 0, 0);
-      if (kv) {
-        const int64_t row = seq_row(p, s, k);
-        const float v4[4] = {dv[0], dv[1], dv[2], dv[3]};
-        const float k4[4] = {dk[0] * p.scale, dk[1] * p.scale, dk[2] * p.scale, dk[3] * p.scale};
-        *(uint2*)(p.dv + row * p.lddv + h * 32 + 16 * db + 4 * g) = pack4(v4);
-        *(uint2*)(p.dk + row * p.lddk + h * 32 + 16 * db + 4 * g) = pack4(k4);
-      }
+      dv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag<32>(Di, 0, 16 * db, lane), pf, z4, 0, 0, 0);
+      dk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag<32>(Qi, 0, 16 * db, lane), dsk, z4, 0, 0, 0);
+    }
+    if (kv) {   // rows d = 8g + 4db + r (interleaved images)
+      float v8[8], k8[8];
+      cat8(v8, dv[0], dv[1], 1.f);
+      cat8(k8, dk[0], dk[1], p.scale);
+      *(u32x4*)(p.dv + roff(R.row[kb], p.lddv) + h * 32 + 8 * g) = pack8(v8);
+      *(u32x4*)(p.dk + roff(R.row[kb], p.lddk) + h * 32 + 8 * g) = pack8(k8);
     }
   }
 }
 
-bool small_ok(const AP& p, int D) { return D == 32 && p.L <= 32 && !p.bias_u && !p.kmask && p.drop_p == 0.f; }
+// (32-bit token rows and 32 x 32-bit offset products in the small kernels: SmallRows / roff)
+bool small_ok(const AP& p, int D) {
+  const int64_t lim = (int64_t)1 << 31;
+  const bool fits = p.M < lim && p.ldq < lim && p.ldk < lim && p.ldv < lim && p.ldo < lim && p.ldout < lim &&
+                    p.lddo < lim && p.lddq < lim && p.lddk < lim && p.lddv < lim;
+  // 16-B loads and stores of each lane's 8 d (head offsets are multiples of 32 elements)
+  auto a16 = [](const void* x, int64_t ld) { return ((uintptr_t)x & 15) == 0 && ld % 8 == 0; };
+  const bool al = a16(p.q, p.ldq) && a16(p.k, p.ldk) && a16(p.v, p.ldv) && a16(p.o, p.ldo) &&
+                  a16(p.out, p.ldout) && a16(p.out16, p.ldout) && a16(p.dout, p.lddo) && a16(p.dq, p.lddq) &&
+                  a16(p.dk, p.lddk) && a16(p.dv, p.lddv);
+  return D == 32 && p.L <= 32 && !p.bias_u && !p.kmask && p.drop_p == 0.f && fits && al;
+}
 
 }  // namespace
 

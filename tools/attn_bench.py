@@ -18,8 +18,11 @@ def main():
     q, k, v, do = r(M, H * D), r(M, H * D), r(M, H * D), r(M, H * D)
     nb = (2 * Hg - 1) * (2 * Wg - 1)
     bias = torch.randn(H, nb, device='cuda') * 0.5
+    only = os.environ.get('ATTN_ONLY', '')   # 'spatial' | 'temporal' | '' (both)
     for name, L, nseq, seq, bu, grid in [('spatial', hw, B * T, (1, hw, 0, 1), bias, (Hg, Wg)),
                                         ('temporal', T, B * hw, (hw, T * hw, 1, hw), None, (0, 0))]:
+        if only and name != only:
+            continue
         o, lse = K.attn_fwd(q, k, v, L=L, H=H, D=D, nseq=nseq, scale=8.0, seq=seq, bias_u=bu, grid=grid)
         fl = 4.0 * nseq * H * L * L * D
         ms = timeit(lambda: K.attn_fwd(q, k, v, L=L, H=H, D=D, nseq=nseq, scale=8.0, seq=seq, bias_u=bu, grid=grid))

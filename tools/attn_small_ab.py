@@ -1,0 +1,61 @@
+"""Temporal (short-sequence) attention kernels at the base config, for library A/Bs:
+  python tools/attn_small_ab.py dump <out.pt>     -- forward (O, fp16 O, lse) and backward (dQ, dK, dV)
+                                                    of the library CTCLIP_HIP_LIB names, seeded inputs
+  python tools/attn_small_ab.py cmp <a.pt> <b.pt> -- bit-for-bit comparison of two dumps
+  python tools/attn_small_ab.py time              -- forward / backward microseconds
+Q | K | V live in one [M, 768] buffer (the layers' packed projection), as in the step."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'ctpa-clip_amd'))
+import torch  # noqa: E402
+
+
+def setup():
+    from ctclip_mi355x import kernels as K
+    torch.manual_seed(0)
+    B, T, Hg, Wg, H, D = 8, 24, 24, 24, 8, 32
+    hw = Hg * Wg
+    M = B * T * hw
+    do = (torch.randn(M, H * D, device='cuda') * 0.3).bfloat16()
+    kw = dict(L=T, H=H, D=D, nseq=B * hw, scale=8.0, seq=(hw, T * hw, 1, hw))
+    if os.environ.get('LAYOUT', 'packed') == 'packed':
+        qkv = (torch.randn(M, 3 * H * D, device='cuda') * 0.3).bfloat16()
+        q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    else:   # three [M, 256] tensors
+        q, k, v = [(torch.randn(M, H * D, device='cuda') * 0.3).bfloat16() for _ in range(3)]
+    return K, q, k, v, do, kw
+
+
+def run(K, q, k, v, do, kw):
+    o, lse, o16 = K.attn_fwd(q, k, v, want_o16=True, **kw)
+    dq, dk, dv = torch.empty_like(do), torch.empty_like(do), torch.empty_like(do)
+    K.attn_bwd(q, k, v, o, lse, do, dq, dk, dv, **kw)
+    return dict(o=o, o16=o16, lse=lse, dq=dq, dk=dk, dv=dv)
+
+
+def main():
+    mode = sys.argv[1]
+    if mode == 'cmp':
+        a, b = torch.load(sys.argv[2], weights_only=True), torch.load(sys.argv[3], weights_only=True)
+        bad = [n for n in a if not torch.equal(a[n], b[n])]
+        print('bit-identical' if not bad else f'DIFFER: {bad}', flush=True)
+        sys.exit(1 if bad else 0)
+    K, q, k, v, do, kw = setup()
+    if mode == 'dump':
+        out = run(K, q, k, v, do, kw)
+        torch.save({n: t.cpu() for n, t in out.items()}, sys.argv[2])
+        print('dumped', sys.argv[2], flush=True)
+        return
+    from gemm_bench import timeit
+    o16 = os.environ.get('O16', '1') != '0'
+    o, lse = K.attn_fwd(q, k, v, **kw)
+    dq, dk, dv = torch.empty_like(do), torch.empty_like(do), torch.empty_like(do)
+    f = timeit(lambda: K.attn_fwd(q, k, v, want_o16=o16, **kw), n=50)
+    b = timeit(lambda: K.attn_bwd(q, k, v, o, lse, do, dq, dk, dv, **kw), n=50)
+    print(f'temporal fwd {f * 1e3:7.1f} us  bwd {b * 1e3:7.1f} us  (layout {os.environ.get("LAYOUT", "packed")}, '
+          f'fp16 copy {int(o16)})', flush=True)
+
+
+if __name__ == '__main__':
+    main()
