@@ -397,7 +397,8 @@ int ctclip_peg_set_canon1(int32_t on);
  * softmax(scale * q.k^T + bias + mask) v per (sequence, head); q/k already l2-normalised and
  * scaled for CTViT.  Sequence rows: row(s,i) = (s/n_inner)*s_outer + (s%n_inner)*s_inner + i*s_pos.
  * bias_u: deduplicated continuous-position-bias table [H][(2gh-1)(2gw-1)] (attention.py:229-276).
- * bwd: writes dq, dk, dv (bf16), delta [H][M], accumulates dbias_u with atomics. */
+ * bwd: writes dq, dk, dv (bf16), delta [H][M], accumulates dbias_u with atomics.
+ * q, k, v, o, o16, dout, dq, dk, dv (those given): 16-B aligned, ld % 8 == 0, else CT_EALIGN. */
 typedef struct {
   const void* q; int64_t ldq;
   const void* k; int64_t ldk;

@@ -282,6 +282,20 @@ def test_attention(K, case):
         assert rel(du, ur.grad) < 2e-2, rel(du, ur.grad)
 
 
+def test_attention_rejects_unaligned_rows(K):
+    """Rows 16-B aligned (ld % 8 == 0) are part of the attention C-ABI contract (ctclip_hip.h: the
+    kernels load and store 8 head-dim elements per lane): anything else fails loudly (CT_EALIGN)."""
+    from ctclip_mi355x import _lib
+    M, H, D, L = 48, 8, 32, 24
+    q = torch.zeros(M, 260, device=dev, dtype=torch.bfloat16)[:, :H * D]      # ld 260
+    kv = torch.zeros(M, 2 * H * D, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(_lib.KernelError):
+        K.attn_fwd(q, kv[:, :H * D], kv[:, H * D:], L=L, H=H, D=D, nseq=M // L, scale=8.0, seq=(1, L, 0, 1))
+    o, _ = K.attn_fwd(q.contiguous(), kv[:, :H * D], kv[:, H * D:], L=L, H=H, D=D, nseq=M // L, scale=8.0,
+                      seq=(1, L, 0, 1))
+    assert torch.isfinite(o.float()).all()
+
+
 # ----------------------------------------------------------------------------- VQ
 def test_vq_select_and_pool(K):
     torch.manual_seed(4)

@@ -25,8 +25,10 @@ def main():
             continue
         o, lse = K.attn_fwd(q, k, v, L=L, H=H, D=D, nseq=nseq, scale=8.0, seq=seq, bias_u=bu, grid=grid)
         fl = 4.0 * nseq * H * L * L * D
-        ms = timeit(lambda: K.attn_fwd(q, k, v, L=L, H=H, D=D, nseq=nseq, scale=8.0, seq=seq, bias_u=bu, grid=grid))
-        print(f'{name:8s} fwd {ms * 1e3:8.1f} us {fl / ms / 1e9:7.1f} TF/s', flush=True)
+        o16 = os.environ.get('O16', '0') != '0'    # also write O's fp16 copy (the fp16 to_out GEMM's A)
+        ms = timeit(lambda: K.attn_fwd(q, k, v, L=L, H=H, D=D, nseq=nseq, scale=8.0, seq=seq, bias_u=bu, grid=grid,
+                                       want_o16=o16))
+        print(f'{name:8s} fwd {ms * 1e3:8.1f} us {fl / ms / 1e9:7.1f} TF/s (fp16 copy {int(o16)})', flush=True)
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         du = torch.zeros_like(bias) if bu is not None else None
 
