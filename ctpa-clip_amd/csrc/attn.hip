@@ -1788,11 +1788,29 @@ __device__ __forceinline__ void cat8(float (&o)[8], const f32x4& a, const f32x4&
   }
 }
 
+// COOP (H % SW == 0: a workgroup's four waves are four adjacent heads of ONE sequence): O and its
+// fp16 copy are staged in LDS tiles [32 rows][4 heads x 64 B] (over the V images) and stored by the
+// whole workgroup, 256 contiguous bytes of a token row per 16 lanes (two full 128-B lines), instead
+// of each wave storing 64-B halves of 16 rows per instruction.
+constexpr int SRS = 4 * 64 + 16;               // staging row stride (four heads + 16-B pad)
+constexpr size_t small_fwd_lds(bool coop) { return coop ? 2 * 32 * SRS : SW * SIMG; }
+
+__device__ __forceinline__ void coop_store_rows(u16* dst, int64_t ld, const char* tile, const AP& p, int s, int h0) {
+  const unsigned base = (unsigned)seq_row(p, s, 0), sp = (unsigned)p.s_pos;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int idx = pass * SW * 64 + threadIdx.x, row = idx >> 4, c = idx & 15;
+    if (row < p.L)
+      *(u32x4*)(dst + roff(base + (unsigned)row * sp, ld) + h0 * 32 + c * 8) = *(const u32x4*)(tile + row * SRS + c * 16);
+  }
+}
+
+template <bool COOP>
 __global__ __launch_bounds__(SW * 64) void attn_small_fwd_kernel(AP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pair = blockIdx.x * SW + w;
-  if (pair >= p.nseq * p.H) return;            // wave-uniform; no workgroup barriers below
+  if (pair >= p.nseq * p.H) return;            // wave-uniform (never taken when COOP: no partial workgroups)
   const int s = pair / p.H, h = pair - s * p.H;
   char* Vi = smem + w * SIMG;
   const SmallRows R = small_rows(p, s, lane);
@@ -1814,6 +1832,7 @@ __global__ __launch_bounds__(SW * 64) void attn_small_fwd_kernel(AP p) {
   // V^T column fragments (image column block db: d = 8 (i / 4) + 4 db + i % 4), keys 4g + 0..3 and
   // 16 + 4g + 0..3
   const bf16x8 vt[2] = {trfrag<32>(Vi, 0, 0, lane), trfrag<32>(Vi, 0, 16, lane)};
+  u32x4 ob[2], hb[2];
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     float m = -INFINITY;
@@ -1843,18 +1862,52 @@ __global__ __launch_bounds__(SW * 64) void attn_small_fwd_kernel(AP p) {
     // O^T blocks: lane column = query 16 qb + i (the lane's row qb), rows d = 8g + 4db + r
     const f32x4 o0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt[0], pf, z4, 0, 0, 0);
     const f32x4 o1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vt[1], pf, z4, 0, 0, 0);
-    if (R.ok[qb]) {
-      float o8[8];
-      cat8(o8, o0, o1, inv);
+    float o8[8];
+    cat8(o8, o0, o1, inv);
+    if constexpr (COOP) {
+      ob[qb] = pack8(o8);
+      if (p.out16) hb[qb] = pack8h(o8);
+    } else if (R.ok[qb]) {
       const uint64_t off = roff(R.row[qb], p.ldout) + h * 32 + 8 * g;
       *(u32x4*)(p.out + off) = pack8(o8);
       if (p.out16) *(u32x4*)(p.out16 + off) = pack8h(o8);
     }
     if (g == 0 && R.ok[qb] && p.lse) p.lse[(int64_t)h * p.M + R.row[qb]] = (m + __log2f(l)) * LN2;
   }
+  if constexpr (COOP) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();                            // every wave is past its V^T reads (the tiles overlay them)
+    char* t0 = smem;
+    char* t1 = smem + 32 * SRS;
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int row = 16 * qb + (lane & 15);
+      *(u32x4*)(t0 + row * SRS + w * 64 + g * 16) = ob[qb];
+      if (p.out16) *(u32x4*)(t1 + row * SRS + w * 64 + g * 16) = hb[qb];
+    }
+    __syncthreads();
+    coop_store_rows(p.out, p.ldout, t0, p, s, h - w);
+    if (p.out16) coop_store_rows(p.out16, p.ldout, t1, p, s, h - w);
+  }
 }
 
-__global__ __launch_bounds__(SW * 64) void attn_small_bwd_kernel(AP p) {
+// per-wave staging areas -> workgroup stores: 16 threads per token row, head c / 4 from wave c / 4's
+// area at byte offset off0 (rows of Img<32>::RS bytes, 16-B chunk c % 4)
+__device__ __forceinline__ void coop_store_areas(u16* dst, int64_t ld, const char* smem, int wstride, int off0,
+                                                 const AP& p, int s, int h0) {
+  const unsigned base = (unsigned)seq_row(p, s, 0), sp = (unsigned)p.s_pos;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int idx = pass * SW * 64 + threadIdx.x, row = idx >> 4, c = idx & 15;
+    if (row < p.L)
+      *(u32x4*)(dst + roff(base + (unsigned)row * sp, ld) + h0 * 32 + c * 8) =
+          *(const u32x4*)(smem + (c >> 2) * wstride + off0 + row * Img<32>::RS + (c & 3) * 16);
+  }
+}
+
+template <bool COOP>   // as attn_small_fwd_kernel: each wave stages dQ / dK / dV in its own K / Q / dO
+                       // image once it has read it, and the workgroup stores whole token rows
+__global__ __launch_bounds__(SW * 64) __attribute__((amdgpu_waves_per_eu(5, 8))) void attn_small_bwd_kernel(AP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int pair = blockIdx.x * SW + w;
@@ -1916,16 +1969,23 @@ __global__ __launch_bounds__(SW * 64) void attn_small_bwd_kernel(AP p) {
   }
   wave_lds_sync();
   const bf16x8 kt0 = trfrag<32>(Ki, 0, 0, lane), kt1 = trfrag<32>(Ki, 0, 16, lane);
+  // COOP: the dO^T and Q^T column fragments (the same for both key blocks) read up front, so all
+  // three images are free for staging
+  bf16x8 dt[2], qt[2];
+  if constexpr (COOP) {
+    dt[0] = trfrag<32>(Di, 0, 0, lane); dt[1] = trfrag<32>(Di, 0, 16, lane);
+    qt[0] = trfrag<32>(Qi, 0, 0, lane); qt[1] = trfrag<32>(Qi, 0, 16, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     // dQ^T blocks, rows d = 8g + 4db + r (interleaved images), column = query 16 qb + i
     const f32x4 a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt0, dsf[qb], z4, 0, 0, 0);
     const f32x4 a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt1, dsf[qb], z4, 0, 0, 0);
-    if (R.ok[qb]) {
-      float d8[8];
-      cat8(d8, a0, a1, p.scale);
-      *(u32x4*)(p.dq + roff(R.row[qb], p.lddq) + h * 32 + 8 * g) = pack8(d8);
-    }
+    float d8[8];
+    cat8(d8, a0, a1, p.scale);
+    if constexpr (COOP) *(u32x4*)(Ki + (16 * qb + (lane & 15)) * Img<32>::RS + g * 16) = pack8(d8);
+    else if (R.ok[qb]) *(u32x4*)(p.dq + roff(R.row[qb], p.lddq) + h * 32 + 8 * g) = pack8(d8);
   }
   // ---- S layout (lane = key): dV^T = dO^T P, dK^T = scale * Q^T dS
 #pragma unroll
@@ -1949,16 +2009,29 @@ __global__ __launch_bounds__(SW * 64) void attn_small_bwd_kernel(AP p) {
     f32x4 dv[2], dk[2];
 #pragma unroll
     for (int db = 0; db < 2; ++db) {
-      dv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag<32>(Di, 0, 16 * db, lane), pf, z4, 0, 0, 0);
-      dk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(trfrag<32>(Qi, 0, 16 * db, lane), dsk, z4, 0, 0, 0);
+      const bf16x8 a_dv = COOP ? dt[db] : trfrag<32>(Di, 0, 16 * db, lane);
+      const bf16x8 a_dk = COOP ? qt[db] : trfrag<32>(Qi, 0, 16 * db, lane);
+      dv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_dv, pf, z4, 0, 0, 0);
+      dk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_dk, dsk, z4, 0, 0, 0);
     }
-    if (kv) {   // rows d = 8g + 4db + r (interleaved images)
-      float v8[8], k8[8];
-      cat8(v8, dv[0], dv[1], 1.f);
-      cat8(k8, dk[0], dk[1], p.scale);
+    float v8[8], k8[8];   // rows d = 8g + 4db + r (interleaved images)
+    cat8(v8, dv[0], dv[1], 1.f);
+    cat8(k8, dk[0], dk[1], p.scale);
+    if constexpr (COOP) {
+      const int o = (16 * kb + (lane & 15)) * Img<32>::RS + g * 16;
+      *(u32x4*)(Di + o) = pack8(v8);
+      *(u32x4*)(Qi + o) = pack8(k8);
+    } else if (kv) {
       *(u32x4*)(p.dv + roff(R.row[kb], p.lddv) + h * 32 + 8 * g) = pack8(v8);
       *(u32x4*)(p.dk + roff(R.row[kb], p.lddk) + h * 32 + 8 * g) = pack8(k8);
     }
+  }
+  if constexpr (COOP) {
+    __syncthreads();                            // every wave's staging written
+    constexpr int WS = 3 * SIMG + 256;
+    coop_store_areas(p.dq, p.lddq, smem, WS, SIMG, p, s, h - w);        // K image: dQ
+    coop_store_areas(p.dk, p.lddk, smem, WS, 0, p, s, h - w);           // Q image: dK
+    coop_store_areas(p.dv, p.lddv, smem, WS, 2 * SIMG, p, s, h - w);    // dO image: dV
   }
 }
 
@@ -1980,8 +2053,13 @@ extern "C" int ctclip_attn_fwd(const ctclip_attn_args* a, void* stream) {
   const int Lp = (p.L + 31) & ~31;
   const int pairs = p.nseq * p.H;
   if (small_ok(p, a->D)) {
-    hipLaunchKernelGGL(attn_small_fwd_kernel, dim3(cdiv(pairs, SW)), dim3(SW * 64), (size_t)SW * SIMG,
-                       (hipStream_t)stream, p);
+    static const int coop_env = [] { const char* e = getenv("CTCLIP_ATTN_SMALL_COOP"); return e ? atoi(e) : 1; }();
+    if (coop_env && p.H % SW == 0)   // CTCLIP_ATTN_SMALL_COOP=0: per-wave stores (A/B)
+      hipLaunchKernelGGL(attn_small_fwd_kernel<true>, dim3(cdiv(pairs, SW)), dim3(SW * 64), small_fwd_lds(true),
+                         (hipStream_t)stream, p);
+    else
+      hipLaunchKernelGGL(attn_small_fwd_kernel<false>, dim3(cdiv(pairs, SW)), dim3(SW * 64), small_fwd_lds(false),
+                         (hipStream_t)stream, p);
     CT_CHECK_LAUNCH();
     return 0;
   }
@@ -2051,8 +2129,12 @@ extern "C" int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream) {
   dim3 grid(cdiv(pairs, p.pp));
   hipStream_t st = (hipStream_t)stream;
   if (small_ok(p, a->D)) {
-    hipLaunchKernelGGL(attn_small_bwd_kernel, dim3(cdiv(pairs, SW)), dim3(SW * 64), (size_t)SW * (3 * SIMG + 256), st,
-                       p);
+    static const int coop_env = [] { const char* e = getenv("CTCLIP_ATTN_SMALL_COOP"); return e ? atoi(e) : 1; }();
+    const size_t lds = (size_t)SW * (3 * SIMG + 256);
+    if (coop_env && p.H % SW == 0)
+      hipLaunchKernelGGL(attn_small_bwd_kernel<true>, dim3(cdiv(pairs, SW)), dim3(SW * 64), lds, st, p);
+    else
+      hipLaunchKernelGGL(attn_small_bwd_kernel<false>, dim3(cdiv(pairs, SW)), dim3(SW * 64), lds, st, p);
     CT_CHECK_LAUNCH();
     return 0;
   }
