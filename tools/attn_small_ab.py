@@ -5,6 +5,8 @@
   python tools/attn_small_ab.py time              -- forward / backward microseconds
   python tools/attn_small_ab.py dumpfwd <out.pt>  -- spatial (CPB bias) and BERT-shape forwards (O, fp16 O, lse)
   python tools/attn_small_ab.py timefwd           -- spatial forward microseconds (with the fp16 copy)
+  python tools/attn_small_ab.py dumpbwd <out.pt>  -- spatial (CPB bias) backward: dQ, dK, dV, bias gradient
+  python tools/attn_small_ab.py timebwd           -- spatial backward microseconds
 Q | K | V live in one [M, 768] buffer (the layers' packed projection), as in the step."""
 import os
 import sys
@@ -43,7 +45,7 @@ def main():
         bad = [n for n in a if not torch.equal(a[n], b[n])]
         print('bit-identical' if not bad else f'DIFFER: {bad}', flush=True)
         sys.exit(1 if bad else 0)
-    if mode in ('dumpfwd', 'timefwd'):
+    if mode in ('dumpfwd', 'timefwd', 'dumpbwd', 'timebwd'):
         return fwd_modes(mode)
     K, q, k, v, do, kw = setup()
     if mode == 'dump':
@@ -71,6 +73,24 @@ def fwd_modes(mode):
     q, kv = r(M, H * D), r(M, 2 * H * D)
     bias = torch.randn(H, (2 * G - 1) ** 2, device='cuda') * 0.5
     sp = dict(L=L, H=H, D=D, nseq=B * T, scale=8.0, seq=(1, L, 0, 1), bias_u=bias, grid=(G, G))
+    if mode in ('dumpbwd', 'timebwd'):
+        o, lse = K.attn_fwd(q, kv[:, :H * D], kv[:, H * D:], **sp)
+        do = r(M, H * D)
+        dq, dkv = torch.empty_like(q), torch.empty_like(kv)
+        du = torch.zeros_like(bias)
+
+        def bwd():
+            du.zero_()
+            K.attn_bwd(q, kv[:, :H * D], kv[:, H * D:], o, lse, do, dq, dkv[:, :H * D], dkv[:, H * D:],
+                       dbias_u=du, **sp)
+        if mode == 'timebwd':
+            from gemm_bench import timeit
+            print(f'spatial bwd {timeit(bwd, n=20) * 1e3:7.1f} us', flush=True)
+            return
+        bwd()
+        torch.save({n: t.cpu() for n, t in dict(dq=dq, dkv=dkv, du=du).items()}, sys.argv[2])
+        print('dumped', sys.argv[2], flush=True)
+        return
     if mode == 'timefwd':
         from gemm_bench import timeit
         f = timeit(lambda: K.attn_fwd(q, kv[:, :H * D], kv[:, H * D:], want_o16=True, **sp), n=30)
