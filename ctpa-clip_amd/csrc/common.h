@@ -194,6 +194,17 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return s;
 }
 
+// Step status word (include/ctclip_hip.h CT_STATUS_*): a kernel that detects a condition ORs its
+// bit in with ONE vector atomic per wave (the lowest lane that saw it); the word is sticky and the
+// trainer turns it into the Adam kernel's skip guard and a host-side exception.
+__device__ __forceinline__ void status_or(int* status, int bits, bool bad) {
+  const unsigned long long b = __ballot(bad);
+  if (status && b && (int)(threadIdx.x & 63) == __ffsll((long long)b) - 1)
+    __hip_atomic_fetch_or(status, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// fp16 range check of a value about to be stored as fp16 (false for NaN / inf / |v| > 65504)
+__device__ __forceinline__ bool f16_ok(float v) { return fabsf(v) <= 65504.f; }
+
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 static inline bool aligned16(const void* p) { return (((uintptr_t)p) & 15) == 0; }
 

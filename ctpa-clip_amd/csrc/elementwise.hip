@@ -117,7 +117,91 @@ __global__ __launch_bounds__(256) void add_f32_kernel(const float* __restrict__ 
 
 inline int grid_for(int64_t n) { return (int)std::min<int64_t>(8192, std::max<int64_t>(1, (n + 255) / 256)); }
 
+// Split-fp16 image pair of f32 values (the x3 GEMM's operands, ctclip_gemm_args.A_lo / B_lo):
+// hi = fp16(v s), lo = fp16(v s - hi), 8 values per thread (16-B hi / lo stores).  A value whose
+// scaled magnitude leaves fp16's range (or is NaN / inf) sets CT_STATUS_F16_RANGE.
+__device__ __forceinline__ void split8(const float* v, float s, u32x4& h, u32x4& l, bool& bad) {
+  float a[8], b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = v[j] * s;
+    bad |= !f16_ok(x);
+    a[j] = rh(x);
+    b[j] = x - a[j];
+  }
+  h = pack8h(a);
+  l = pack8h(b);
+}
+
+__global__ __launch_bounds__(256) void split_f16_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows,
+                                                        int cols, float s, u16* __restrict__ hi,
+                                                        u16* __restrict__ lo, int64_t ldo, int* status) {
+  const int nch = cols / 8;
+  const int64_t total = rows * nch;
+  bool bad = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / nch;
+    const int c = (int)(i - r * nch) * 8;
+    const float* xp = x + r * ldx + c;
+    const f32x4 a = *(const f32x4*)xp, b = *(const f32x4*)(xp + 4);
+    const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+    u32x4 h, l;
+    split8(v, s, h, l, bad);
+    *(u32x4*)(hi + r * ldo + c) = h;
+    *(u32x4*)(lo + r * ldo + c) = l;
+  }
+  status_or(status, CT_STATUS_F16_RANGE, bad);
+}
+
+// pack_rows (row map, column scale, zero padding) into a split-fp16 pair, values scaled by s
+__global__ __launch_bounds__(256) void pack_rows_x3_kernel(const float* __restrict__ src, int64_t ld_src,
+                                                           const int32_t* __restrict__ map, int64_t rows_dst, int cols,
+                                                           int cols_dst, const float* __restrict__ colscale, float s,
+                                                           u16* __restrict__ hi, u16* __restrict__ lo, int64_t ld_dst,
+                                                           int* status) {
+  const int64_t total = rows_dst * cols_dst;
+  bool bad = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / cols_dst;
+    const int c = (int)(i - r * cols_dst);
+    const int64_t sr = map ? (int64_t)map[r] : r;
+    float v = 0.f;
+    if (sr >= 0 && c < cols) {
+      v = src[sr * ld_src + c];
+      if (colscale) v *= colscale[c];
+    }
+    const float x = v * s;
+    bad |= !f16_ok(x);
+    const float h = rh(x);
+    hi[r * ld_dst + c] = f2h(h);
+    lo[r * ld_dst + c] = f2h(x - h);
+  }
+  status_or(status, CT_STATUS_F16_RANGE, bad);
+}
+
 }  // namespace
+
+extern "C" int ctclip_split_f16(const float* x, int64_t ldx, int64_t rows, int32_t cols, float scale, void* hi,
+                                void* lo, int64_t ldo, int32_t* status, void* stream) {
+  if (rows == 0) return 0;
+  CT_REQUIRE(x && hi && lo && rows > 0 && cols > 0 && cols % 8 == 0 && ldx % 4 == 0 && ldo % 8 == 0, CT_EINVAL);
+  CT_REQUIRE(aligned16(x) && aligned16(hi) && aligned16(lo), CT_EALIGN);
+  hipLaunchKernelGGL(split_f16_kernel, dim3(grid_for(rows * cols / 8)), dim3(256), 0, (hipStream_t)stream, x, ldx, rows,
+                     cols, scale, (u16*)hi, (u16*)lo, ldo, (int*)status);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int ctclip_pack_rows_x3(const float* src, int64_t ld_src, const int32_t* map, int64_t rows_dst,
+                                   int32_t cols, int32_t cols_dst, const float* colscale, float scale, void* hi,
+                                   void* lo, int64_t ld_dst, int32_t* status, void* stream) {
+  if (rows_dst == 0) return 0;
+  CT_REQUIRE(src && hi && lo && cols <= cols_dst, CT_EINVAL);
+  hipLaunchKernelGGL(pack_rows_x3_kernel, dim3(grid_for(rows_dst * cols_dst)), dim3(256), 0, (hipStream_t)stream, src,
+                     ld_src, map, rows_dst, cols, cols_dst, colscale, scale, (u16*)hi, (u16*)lo, ld_dst, (int*)status);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int ctclip_geglu_bwd(const void* dg, int64_t lddg, const void* h, int64_t ldh, int64_t rows, int32_t gcols,
                                 void* dh, int64_t lddh, void* stream) {

@@ -525,6 +525,21 @@ extern "C" int ctclip_gemm(const ctclip_gemm_args* a, void* stream) {
                    (a->batch <= 1) && a->N % 64 == 0 && a->n2 > 0 && a->n2 % 64 == 0 && a->n2 <= a->N,
                CT_EINVAL);
   if (a->B2) CT_REQUIRE(aligned16(a->B2) && a->act != 3, CT_EINVAL);
+  if (a->A_lo || a->B_lo) {
+    // split-fp16 x3 operands: the 8-phase kernel only (any M / N; rows past the matrix are clamped
+    // loads whose results are dropped), f32 rows or the x3 GEGLU pair
+    CT_REQUIRE(a->A_lo && a->B_lo && a->ab_f16 && aligned16(a->A_lo) && aligned16(a->B_lo) && a->K % 64 == 0,
+               CT_EINVAL);
+    CT_REQUIRE(a->a_kcontig && a->b_kcontig && !a->B2 && split == 1 && !a->accumulate && a->batch <= 1, CT_EINVAL);
+    CT_REQUIRE(a->K < (int64_t)64 * 10000, CT_ESHAPE);   // K-step index 3 k + s stays < 2^15
+    if (a->act == 2)
+      CT_REQUIRE(!a->c_f32 && !a->R && !a->bias && a->C3 && aligned16(a->C3) && a->ldc3 % 8 == 0 &&
+                     (!a->C4 || (aligned16(a->C4) && a->ldc4 % 8 == 0)),
+                 CT_EINVAL);
+    else
+      CT_REQUIRE(a->act == 0 && a->c_f32 && (!a->R || a->r_f32), CT_EINVAL);
+    return ctclip_gemm256(a, 1, 1, stream);
+  }
   if (a->ab_f16)   // fp16 operands: the 3D-ViT forward GEMMs (K-contiguous A and B, no split-K / B2)
     CT_REQUIRE(a->a_kcontig && a->b_kcontig && !a->B2 && split == 1 && (a->act == 0 || a->act == 2) &&
                    !a->accumulate && (a->batch <= 1),

@@ -69,6 +69,17 @@ struct P {
   // H16), read by the GEGLU backward (EP 4); ln_y16 = optional fp16 copy of the -6 LayerNorm output
   int h16;
   u16* ln_y16;
+  // split-fp16 "x3" GEMM (round 6, ctclip_gemm_args.A_lo / B_lo): A = Ah + Al, B = Bh + Bl as fp16
+  // image pairs; every 64-deep K-step runs three products Ah Bh, Ah Bl, Al Bh into the one f32
+  // accumulator (Al Bl, ~2^-22 relative, is dropped), so the GEMM sees ~22-bit operands at 3x the
+  // fp16 MFMA work (x3 != 0: tile_at's K-step count triples).  The x3 GEGLU
+  // epilogue writes h (fp16, C), g = gelu(gate) x from the unrounded f32 h as an fp16 pair (C2 hi,
+  // C3 lo, the FF2 GEMM's A operand) and as bf16 (C4, the FF2 weight gradient's operand).
+  const u16* alo;
+  const u16* blo;
+  u16* C3; int64_t ldc3;
+  u16* C4; int64_t ldc4;
+  int x3;
 };
 
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
@@ -729,7 +740,7 @@ __device__ __forceinline__ void store_blk_bf16_lds(char* scr, u16* C, int64_t ld
 // ds_bpermute on the VQ argmax GEMM (1.193 vs 1.171-1.176 ms, profiles/r02aw_*), so off
 constexpr bool GEMM_PERMLANE = CTCLIP_GEMM_PERMLANE;
 
-template <int MODE, bool LDS = false, bool H16 = false>
+template <int MODE, bool LDS = false, bool H16 = false, bool X3 = false>
 __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int wr, int wc, int lane, int64_t m0,
                                            int64_t n0, int split, int bidx, char* scr) {
   const int m = lane & 15, g = lane >> 4;
@@ -883,6 +894,30 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
         if (gm0 + r < p.M && wcol0 < p.N) {
           if (p.epi_lds == 2) st16_sc1(p.C2 + bidx * p.sC2 + (gm0 + r) * p.ldc2 + (wcol0 >> 1) + c, d);
           else st16(p.C2 + bidx * p.sC2 + (gm0 + r) * p.ldc2 + (wcol0 >> 1) + c, d);
+        }
+        continue;
+      }
+      if constexpr (X3) {
+        // split-fp16 kernel: h stored as fp16 (the GEGLU backward's operand), g from the unrounded
+        // f32 h (the x3 forward carries ~22-bit values end to end), stored as its fp16 pair
+        // (hi, lo = fp16(g - hi): FF2's A operand) and as bf16 (FF2's weight-gradient operand)
+        store_row_f16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N);
+        float gg[2][4], gh[2][4], gl[2][4];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            gg[j][r] = gelu_erf(v[j + 2][r]) * v[j][r];
+            gh[j][r] = rh(gg[j][r]);
+            gl[j][r] = gg[j][r] - gh[j][r];
+          }
+        // (cross-lane swaps outside the store guard: every lane takes part)
+        const u32x4 dh = pair_swap_h(gh[0], gh[1]), dl = pair_swap_h(gl[0], gl[1]), db = pair_swap(gg[0], gg[1]);
+        if (rok && wcol0 < p.N) {
+          const int64_t gc = (wcol0 >> 1) + pair_coff(g);
+          st16(p.C2 + bidx * p.sC2 + gm * p.ldc2 + gc, dh);
+          st16(p.C3 + gm * p.ldc3 + gc, dl);
+          if (p.C4) st16(p.C4 + gm * p.ldc4 + gc, db);
         }
         continue;
       }
@@ -1401,7 +1436,7 @@ __device__ __forceinline__ Tile tile_at(const P& p, int lin, int gx, int gy, int
   t.n0 = (int64_t)tx * p8::BNN;
   t.kbeg = t.split * p.kper;
   const int64_t kend = min(p.K, t.kbeg + p.kper);
-  t.nk = (kend > t.kbeg && !(p.debug & 2)) ? (int)((kend - t.kbeg) / p8::BKK) : 0;
+  t.nk = (kend > t.kbeg && !(p.debug & 2)) ? (int)((kend - t.kbeg) / p8::BKK) * (p.x3 ? 3 : 1) : 0;
   return t;
 }
 
@@ -1419,7 +1454,7 @@ __device__ unsigned long long g_stamps[256][32][6];
 #define STAMP(k, v) do { } while (0)
 #endif
 
-template <bool AK, bool BKC, int EP, bool H16 = false>
+template <bool AK, bool BKC, int EP, bool H16 = false, bool X3 = false>
 __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
   using namespace p8;
   constexpr bool TR = EP >= 0;
@@ -1453,9 +1488,20 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
   auto stage_of = [&](const Tile& tl, int which, int t) {
     if (t >= tl.nk) return;
     char* dst = smem + (t & 1) * TILEB + which * HALF;
-    const int64_t k0 = tl.kbeg + (int64_t)t * BKK;
-    if (which < 2) stage_half<AK, true>(dst, p.A + tl.bidx * p.sA, p.lda, p.M, tl.m0, k0, which, w, lane);
-    else stage_half<BKC, false>(dst, p.B + tl.bidx * p.sB, p.ldb, p.N, tl.n0, k0, which - 2, w, lane);
+    int tk = t;
+    const u16* Ab = p.A;
+    const u16* Bb = p.B;
+    if constexpr (X3) {
+      // step t = 3 k + s (k-step major, so the second read of Ah_k hits the L2 line the first
+      // brought in): s = 0 Ah Bh, 1 Ah Bl, 2 Al Bh (t / 3 as a multiply-shift, exact for t < 2^15)
+      tk = (t * 21846) >> 16;
+      const int sub = t - 3 * tk;
+      if (sub == 2) Ab = p.alo;
+      if (sub == 1) Bb = p.blo;
+    }
+    const int64_t k0 = tl.kbeg + (int64_t)tk * BKK;
+    if (which < 2) stage_half<AK, true>(dst, Ab + tl.bidx * p.sA, p.lda, p.M, tl.m0, k0, which, w, lane);
+    else stage_half<BKC, false>(dst, Bb + tl.bidx * p.sB, p.ldb, p.N, tl.n0, k0, which - 2, w, lane);
   };
   auto stage = [&](int which, int t) { stage_of(T, which, t); };
 
@@ -1589,7 +1635,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
     } else if constexpr (EP == 2 || EP == 12) {
-      epilogue_t<2, EP == 12, H16>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx, scr);
+      epilogue_t<2, EP == 12, H16, X3>(p, acc, wr, wc, lane, T.m0, T.n0, T.split, T.bidx, scr);
     } else if constexpr (EP == 4) {
       epilogue_geglu_bwd(p, acc, wr, wc, lane, T.m0, T.n0, T.bidx);
     } else if constexpr (EP == 0 || EP == 10) {
@@ -1628,13 +1674,13 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
 // the chip (ctclip_gemm_set_grid_cap)
 static int g_grid_cap = 0;
 
-template <bool AK, bool BKC, int EP, bool H16 = false>
+template <bool AK, bool BKC, int EP, bool H16 = false, bool X3 = false>
 int launch8(const P& p, int batch, hipStream_t st) {
   constexpr int smem = EP == -6 || EP == -7 ? SMEM_LN : p8::SMEM_P;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<AK, BKC, EP, H16>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              smem);
+    (void)hipFuncSetAttribute((const void*)gemm8p_kernel<AK, BKC, EP, H16, X3>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
   const int64_t ntiles = cdiv(p.N, p8::BNN) * cdiv(p.M, p8::BM) * (int64_t)p.gz;
@@ -1651,10 +1697,10 @@ int launch8(const P& p, int batch, hipStream_t st) {
     dim3 grid((unsigned)(ntiles < cap ? ntiles : cap));
     P q = p;
     q.pre1 = pre1;
-    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP, H16>), grid, dim3(p8::NTH), smem, st, q);
+    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP, H16, X3>), grid, dim3(p8::NTH), smem, st, q);
   } else {
     dim3 grid(cdiv(p.N, p8::BNN), cdiv(p.M, p8::BM), batch * p.split_k);
-    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP, H16>), grid, dim3(p8::NTH), smem, st, p);
+    hipLaunchKernelGGL((gemm8p_kernel<AK, BKC, EP, H16, X3>), grid, dim3(p8::NTH), smem, st, p);
   }
   CT_CHECK_LAUNCH();
   return 0;
@@ -1732,6 +1778,14 @@ int launch8_ep(const P& p, int batch, hipStream_t st) {
 // fp16), plain 16-bit / l2norm-free outputs, the LDS-staged f32 / bias / residual rows
 int launch8_h16(const P& p, int batch, hipStream_t st) {
   if (p.split_k > 1 || p.act == 3 || p.act == 4 || p.act == 5 || p.act == 6) return CT_EINVAL;
+  if (p.x3) {
+    // split-fp16 operands: the GEGLU pair epilogue, f32 rows (bias / f32 residual / bf16 copy)
+    if (p.act == 2) return launch8<true, true, 2, true, true>(p, batch, st);
+    if (!p.c_f32 || p.act != 0) return CT_EINVAL;
+    if (p.R && p.r_f32 && !p.accumulate) return launch8<true, true, -2, true, true>(p, batch, st);
+    if (p.R) return CT_EINVAL;
+    return launch8<true, true, -1, true, true>(p, batch, st);
+  }
   const bool tr = !p.c_f32 && !p.R;
   if (p.act == 2) return launch8<true, true, 2, true>(p, batch, st);
   if (tr) return launch8<true, true, 0, true>(p, batch, st);
@@ -1765,6 +1819,11 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   p.nfold = 0;
   p.h16 = a->ab_f16 || a->r_f16;
   p.ln_y16 = nullptr;
+  p.x3 = a->A_lo != nullptr;
+  p.alo = (const u16*)a->A_lo;
+  p.blo = (const u16*)a->B_lo;
+  p.C3 = (u16*)a->C3; p.ldc3 = a->ldc3;
+  p.C4 = (u16*)a->C4; p.ldc4 = a->ldc4;
   const int kstep = (variant() == 8 || a->act == 4 || a->act == 5) ? p8::BKK : BK;
   p.kper = (a->K / kstep + split - 1) / split * kstep;
   static int dbg = -1, stag = 0;

@@ -3,7 +3,7 @@
 #include "common.h"
 #include "../../include/ctclip_hip.h"
 
-extern "C" int ctclip_version(void) { return 1; }
+extern "C" int ctclip_version(void) { return CTCLIP_ABI_VERSION; }
 
 extern "C" int ctclip_device_arch(char* buf, int n) {
   int dev = 0;

@@ -82,8 +82,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
                                                      float eps, u16* __restrict__ yb, int64_t ldyb,
                                                      float* __restrict__ yf, int64_t ldyf,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                     u16* __restrict__ yh) {
+                                                     u16* __restrict__ yh, u16* __restrict__ yl, int* status) {
   const int lane = threadIdx.x & 63;
+  bool bad = false;
   const int64_t row0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
   float gv[CPL][8], bv[CPL][8];
   load_param<CPL>(gamma, D, lane, 1.f, gv);
@@ -122,7 +123,17 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = (v[r][c][j] - mean) * rstd * gv[c][j] + bv[c][j];
       if (yb) *(u32x4*)(yb + row * ldyb + col) = pack8(o);
-      if (yh) *(u32x4*)(yh + row * ldyb + col) = pack8h(o);   // optional fp16 copy (ldyb)
+      if (yh) {   // optional fp16 copy (ldyb) and its lo residual (the x3 GEMM's pair)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bad |= !f16_ok(o[j]);
+        *(u32x4*)(yh + row * ldyb + col) = pack8h(o);
+        if (yl) {
+          float l[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) l[j] = o[j] - rh(o[j]);
+          *(u32x4*)(yl + row * ldyb + col) = pack8h(l);
+        }
+      }
       if (yf) {
         float* p = yf + row * ldyf + col;
         *(f32x4*)p = f32x4{o[0], o[1], o[2], o[3]};
@@ -130,6 +141,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const void* __restrict__ x,
       }
     }
   }
+  status_or(status, CT_STATUS_F16_RANGE, bad);
 }
 
 // dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat)) [+ dres];  dgamma/dbeta partials.
@@ -422,13 +434,13 @@ int ln_cpl(int D) { return (D + 511) / 512; }
 template <int C, int R>
 void launch_ln_fwd(bool xf, dim3 grid, hipStream_t st, const void* x, int64_t ldx, int64_t rows, int D,
                    const float* gamma, const float* beta, float eps, u16* yb, int64_t ldyb, float* yf, int64_t ldyf,
-                   float* mean, float* rstd, u16* yh) {
+                   float* mean, float* rstd, u16* yh, u16* yl, int* status) {
   if (xf)
     hipLaunchKernelGGL((ln_fwd_kernel<C, R, true>), grid, dim3(256), 0, st, x, ldx, rows, D, gamma, beta, eps, yb,
-                       ldyb, yf, ldyf, mean, rstd, yh);
+                       ldyb, yf, ldyf, mean, rstd, yh, yl, status);
   else
     hipLaunchKernelGGL((ln_fwd_kernel<C, R, false>), grid, dim3(256), 0, st, x, ldx, rows, D, gamma, beta, eps, yb,
-                       ldyb, yf, ldyf, mean, rstd, yh);
+                       ldyb, yf, ldyf, mean, rstd, yh, yl, status);
 }
 
 template <int C>
@@ -458,19 +470,28 @@ extern "C" int ctclip_layernorm_fwd_x2(const void* x, int32_t x_f32, int64_t ldx
                                        const float* gamma, const float* beta, float eps, void* y_bf16, void* y_f16,
                                        int64_t ldyb, float* y_f32, int64_t ldyf, float* mean, float* rstd,
                                        void* stream) {
+  return ctclip_layernorm_fwd_x3(x, x_f32, ldx, rows, D, gamma, beta, eps, y_bf16, y_f16, nullptr, ldyb, y_f32, ldyf,
+                                 mean, rstd, nullptr, stream);
+}
+
+extern "C" int ctclip_layernorm_fwd_x3(const void* x, int32_t x_f32, int64_t ldx, int64_t rows, int32_t D,
+                                       const float* gamma, const float* beta, float eps, void* y_bf16, void* y_f16,
+                                       void* y_f16lo, int64_t ldyb, float* y_f32, int64_t ldyf, float* mean,
+                                       float* rstd, int32_t* status, void* stream) {
   if (rows == 0) return 0;
+  if (y_f16lo && !y_f16) return CT_EINVAL;
   CT_REQUIRE(D % 8 == 0 && ldx % 8 == 0, CT_EALIGN);
   const int cpl = ln_cpl(D);
   hipStream_t st = (hipStream_t)stream;
   if (cpl == 1)
     launch_ln_fwd<1, 4>(x_f32, dim3(cdiv(rows, 16)), st, x, ldx, rows, D, gamma, beta, eps, (u16*)y_bf16, ldyb,
-                        y_f32, ldyf, mean, rstd, (u16*)y_f16);
+                        y_f32, ldyf, mean, rstd, (u16*)y_f16, (u16*)y_f16lo, (int*)status);
   else if (cpl == 2)
     launch_ln_fwd<2, 2>(x_f32, dim3(cdiv(rows, 8)), st, x, ldx, rows, D, gamma, beta, eps, (u16*)y_bf16, ldyb,
-                        y_f32, ldyf, mean, rstd, (u16*)y_f16);
+                        y_f32, ldyf, mean, rstd, (u16*)y_f16, (u16*)y_f16lo, (int*)status);
   else if (cpl <= 8)
     launch_ln_fwd<8, 1>(x_f32, dim3(cdiv(rows, 4)), st, x, ldx, rows, D, gamma, beta, eps, (u16*)y_bf16, ldyb,
-                        y_f32, ldyf, mean, rstd, (u16*)y_f16);
+                        y_f32, ldyf, mean, rstd, (u16*)y_f16, (u16*)y_f16lo, (int*)status);
   else
     return CT_ESHAPE;
   CT_CHECK_LAUNCH();

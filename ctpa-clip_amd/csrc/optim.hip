@@ -22,7 +22,7 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ x,
 }
 
 __global__ __launch_bounds__(256) void clip_coef_kernel(const float* __restrict__ part, int nblk, float max_norm,
-                                                        float* __restrict__ out) {
+                                                        float* __restrict__ out, int* skip) {
   __shared__ float red[8];
   float s = 0.f;
   for (int i = threadIdx.x; i < nblk; i += 256) s += part[i];
@@ -31,6 +31,11 @@ __global__ __launch_bounds__(256) void clip_coef_kernel(const float* __restrict_
     const float norm = sqrtf(s);
     out[0] = norm;
     out[1] = max_norm > 0.f ? fminf(1.f, max_norm / (norm + 1e-6f)) : 1.f;
+    // a NaN / inf gradient would reach every parameter through Adam (torch's clip_grad_norm_ would
+    // scale by a NaN coefficient): flag the step in the Adam kernels' skip word instead.  The norm is
+    // taken after the SUM all-reduce, so every rank sees the same value and skips together.
+    if (skip && !(norm <= 3.4e38f))
+      __hip_atomic_fetch_or(skip, CT_STATUS_NONFINITE_GRAD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -118,8 +123,14 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
 
 extern "C" int ctclip_grad_norm(const float* g, int64_t n, float max_norm, float* part, int32_t nblk, float* out,
                                 void* stream) {
+  return ctclip_grad_norm_s(g, n, max_norm, part, nblk, out, nullptr, stream);
+}
+
+extern "C" int ctclip_grad_norm_s(const float* g, int64_t n, float max_norm, float* part, int32_t nblk, float* out,
+                                  int32_t* skip, void* stream) {
   hipLaunchKernelGGL(sumsq_kernel, dim3(nblk), dim3(256), 0, (hipStream_t)stream, g, n, part);
-  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, part, nblk, max_norm, out);
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, part, nblk, max_norm, out,
+                     (int*)skip);
   CT_CHECK_LAUNCH();
   return 0;
 }

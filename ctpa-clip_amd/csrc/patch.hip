@@ -20,7 +20,8 @@ __global__ __launch_bounds__(256) void patch_ln_kernel(const void* __restrict__ 
                                                        int64_t ntok, int T, int Hg, int Wg, int64_t vol_stride,
                                                        int64_t frame_elems, int W, int PT, int P,
                                                        const int32_t* __restrict__ offs, int pd, float eps,
-                                                       u16* __restrict__ out, int64_t ldo, u16* __restrict__ out16) {
+                                                       u16* __restrict__ out, int64_t ldo, u16* __restrict__ out16,
+                                                       u16* __restrict__ out16lo) {
   const int lane = threadIdx.x & 63;
   const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (tok >= ntok) return;
@@ -58,17 +59,21 @@ __global__ __launch_bounds__(256) void patch_ln_kernel(const void* __restrict__ 
   const float rstd = rsqrtf(warp_sum(q) / pd + eps);
   u16* o = out + tok * ldo;
   u16* oh = out16 ? out16 + tok * ldo : nullptr;
+  u16* ol = out16lo ? out16lo + tok * ldo : nullptr;
 #pragma unroll
   for (int i = 0; i < MAXC; ++i) {
     const int e = lane + 64 * i;
     if (e < pd) {
-      o[e] = f2bf((v[i] - mean) * rstd);
-      if (oh) oh[e] = f2h((v[i] - mean) * rstd);
+      const float a = (v[i] - mean) * rstd;
+      o[e] = f2bf(a);
+      if (oh) oh[e] = f2h(a);
+      if (ol) ol[e] = f2h(a - rh(a));
     }
   }
   for (int e = pd + lane; e < ldo; e += 64) {   // K padding of the patch-embed GEMM
     o[e] = 0;
     if (oh) oh[e] = 0;
+    if (ol) ol[e] = 0;
   }
 }
 
@@ -86,7 +91,8 @@ template <bool F32>
 __global__ __launch_bounds__(256) void patch_ln_strip_kernel(const void* __restrict__ video, int is_hu, int T,
                                                              int Hg, int Wg, int64_t vol_stride, int H, int W,
                                                              int PT, int P, float eps, u16* __restrict__ out,
-                                                             int64_t ldo, u16* __restrict__ out16) {
+                                                             int64_t ldo, u16* __restrict__ out16,
+                                                             u16* __restrict__ out16lo) {
   using E = typename std::conditional<F32, float, short>::type;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   E* sx = (E*)smem_raw;   // [PW][pd]
@@ -166,6 +172,7 @@ __global__ __launch_bounds__(256) void patch_ln_strip_kernel(const void* __restr
   const int64_t tok = (((int64_t)b * T + t) * Hg + hg) * Wg + wg0 + w;
   uint32_t* o = (uint32_t*)(out + tok * ldo);
   uint32_t* oh = out16 ? (uint32_t*)(out16 + tok * ldo) : nullptr;   // optional fp16 copy
+  uint32_t* ol = out16lo ? (uint32_t*)(out16lo + tok * ldo) : nullptr;   // ... and its lo residual (x3)
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
     const int e = 2 * (lane + 64 * i);
@@ -173,11 +180,13 @@ __global__ __launch_bounds__(256) void patch_ln_strip_kernel(const void* __restr
       const float a = (v[i][0] - mean) * rstd, c = (v[i][1] - mean) * rstd;
       o[e >> 1] = (uint32_t)f2bf(a) | ((uint32_t)f2bf(c) << 16);
       if (oh) oh[e >> 1] = pack2h(a, c);
+      if (ol) ol[e >> 1] = pack2h(a - rh(a), c - rh(c));
     }
   }
   for (int e = pd + 2 * lane; e < ldo; e += 128) {   // K padding of the patch-embed GEMM
     o[e >> 1] = 0u;
     if (oh) oh[e >> 1] = 0u;
+    if (ol) ol[e >> 1] = 0u;
   }
 }
 
@@ -199,7 +208,8 @@ template <bool F32>
 __global__ __launch_bounds__(256) void patch_ln_strip20_kernel(const void* __restrict__ video, int is_hu, int T,
                                                                int Hg, int Wg, int64_t vol_stride, int H, int W,
                                                                int PT, float eps, u16* __restrict__ out,
-                                                               int64_t ldo, int g_remap, u16* __restrict__ out16) {
+                                                               int64_t ldo, int g_remap, u16* __restrict__ out16,
+                                                               u16* __restrict__ out16lo) {
   using E = typename std::conditional<F32, float, short>::type;
   constexpr int P = 20, VEC = F32 ? 4 : 8;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -288,6 +298,7 @@ __global__ __launch_bounds__(256) void patch_ln_strip20_kernel(const void* __res
   const int64_t tok = (((int64_t)b * T + t) * Hg + hg) * Wg + wg0 + w;
   uint32_t* o = (uint32_t*)(out + tok * ldo);
   uint32_t* oh = out16 ? (uint32_t*)(out16 + tok * ldo) : nullptr;   // optional fp16 copy
+  uint32_t* ol = out16lo ? (uint32_t*)(out16lo + tok * ldo) : nullptr;   // ... and its lo residual (x3)
 #pragma unroll
   for (int i = 0; i < NP; ++i) {
     const int e = 2 * (lane + 64 * i);
@@ -295,11 +306,13 @@ __global__ __launch_bounds__(256) void patch_ln_strip20_kernel(const void* __res
       const float a = (v[i][0] - mean) * rstd, c = (v[i][1] - mean) * rstd;
       o[e >> 1] = (uint32_t)f2bf(a) | ((uint32_t)f2bf(c) << 16);
       if (oh) oh[e >> 1] = pack2h(a, c);
+      if (ol) ol[e >> 1] = pack2h(a - rh(a), c - rh(c));
     }
   }
   for (int e = pd + 2 * lane; e < ldo; e += 128) {   // K padding of the patch-embed GEMM
     o[e >> 1] = 0u;
     if (oh) oh[e >> 1] = 0u;
+    if (ol) ol[e >> 1] = 0u;
   }
 }
 
@@ -432,6 +445,13 @@ extern "C" int ctclip_patch_ln(const void* video, int32_t is_f32, int32_t is_hu,
 extern "C" int ctclip_patch_ln_x2(const void* video, int32_t is_f32, int32_t is_hu, int64_t B, int32_t C, int32_t F,
                                   int32_t H, int32_t W, int32_t PT, int32_t P, const int32_t* offs, float eps,
                                   void* out, void* out16, int64_t ldo, void* stream) {
+  return ctclip_patch_ln_x3(video, is_f32, is_hu, B, C, F, H, W, PT, P, offs, eps, out, out16, nullptr, ldo, stream);
+}
+
+extern "C" int ctclip_patch_ln_x3(const void* video, int32_t is_f32, int32_t is_hu, int64_t B, int32_t C, int32_t F,
+                                  int32_t H, int32_t W, int32_t PT, int32_t P, const int32_t* offs, float eps,
+                                  void* out, void* out16, void* out16lo, int64_t ldo, void* stream) {
+  if (out16lo && !out16) return CT_EINVAL;
   const int pd = C * PT * P * P;
   CT_REQUIRE(pd <= 64 * MAXC, CT_ESHAPE);
   if (ldo <= 0) ldo = pd;
@@ -463,19 +483,20 @@ extern "C" int ctclip_patch_ln_x2(const void* video, int32_t is_f32, int32_t is_
       }
       if (is_f32)
         hipLaunchKernelGGL(patch_ln_strip20_kernel<true>, grid, dim3(256), sm, (hipStream_t)stream, video, is_hu, T,
-                           Hg, Wg, vol, H, W, PT, eps, (u16*)out, ldo, s_patch_remap, (u16*)out16);
+                           Hg, Wg, vol, H, W, PT, eps, (u16*)out, ldo, s_patch_remap, (u16*)out16, (u16*)out16lo);
       else
         hipLaunchKernelGGL(patch_ln_strip20_kernel<false>, grid, dim3(256), sm, (hipStream_t)stream, video, is_hu, T,
-                           Hg, Wg, vol, H, W, PT, eps, (u16*)out, ldo, s_patch_remap, (u16*)out16);
+                           Hg, Wg, vol, H, W, PT, eps, (u16*)out, ldo, s_patch_remap, (u16*)out16, (u16*)out16lo);
     } else if (is_f32)
       hipLaunchKernelGGL(patch_ln_strip_kernel<true>, grid, dim3(256), sm, (hipStream_t)stream, video, is_hu, T, Hg,
-                         Wg, vol, H, W, PT, P, eps, (u16*)out, ldo, (u16*)out16);
+                         Wg, vol, H, W, PT, P, eps, (u16*)out, ldo, (u16*)out16, (u16*)out16lo);
     else
       hipLaunchKernelGGL(patch_ln_strip_kernel<false>, grid, dim3(256), sm, (hipStream_t)stream, video, is_hu, T,
-                         Hg, Wg, vol, H, W, PT, P, eps, (u16*)out, ldo, (u16*)out16);
+                         Hg, Wg, vol, H, W, PT, P, eps, (u16*)out, ldo, (u16*)out16, (u16*)out16lo);
   } else {
     hipLaunchKernelGGL(patch_ln_kernel, dim3(cdiv(ntok, 4)), dim3(256), 0, (hipStream_t)stream, video, is_f32,
-                       is_hu, ntok, T, Hg, Wg, vol, frame, W, PT, P, offs, pd, eps, (u16*)out, ldo, (u16*)out16);
+                       is_hu, ntok, T, Hg, Wg, vol, frame, W, PT, P, offs, pd, eps, (u16*)out, ldo, (u16*)out16,
+                       (u16*)out16lo);
   }
   CT_CHECK_LAUNCH();
   return 0;

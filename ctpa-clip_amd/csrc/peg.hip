@@ -476,9 +476,11 @@ template <int GK = 0, int MD = 0, int TR = 0>
 __global__ __launch_bounds__(XNT, CTCLIP_PEGX_WAVES) void peg_fwd32_kernel(const float* __restrict__ xin, int D,
                                                         const float* __restrict__ w, const float* __restrict__ bias,
                                                         Geo g, float* __restrict__ out, u16* __restrict__ outb,
-                                                        u16* __restrict__ outh, float* __restrict__ stats) {
+                                                        u16* __restrict__ outh, float* __restrict__ stats,
+                                                        u16* __restrict__ outl, int* status) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   fix_geo<GK, MD>(g);
+  bool bad = false;   // an fp16 output out of range (CT_STATUS_F16_RANGE)
   const int nht = (g.H + XHT - 1) / XHT;
   const int b = blockIdx.x / nht, h0 = (blockIdx.x - b * nht) * XHT, c0 = blockIdx.y * XC;
   const int pb = xplane_bytes(g.W);
@@ -574,7 +576,13 @@ __global__ __launch_bounds__(XNT, CTCLIP_PEGX_WAVES) void peg_fwd32_kernel(const
           const int64_t co = orow * D + c0 + ch * 4;
           *(f32x4*)(out + co) = f32x4{v4[0], v4[1], v4[2], v4[3]};
           if (outb) *(uint2*)(outb + co) = pack4(v4);
-          if (outh) *(uint2*)(outh + co) = make_uint2(pack2h(v4[0], v4[1]), pack2h(v4[2], v4[3]));
+          if (outh) {
+            *(uint2*)(outh + co) = make_uint2(pack2h(v4[0], v4[1]), pack2h(v4[2], v4[3]));
+            bad |= !(f16_ok(v4[0]) && f16_ok(v4[1]) && f16_ok(v4[2]) && f16_ok(v4[3]));
+            if (outl)   // the split-fp16 pair's lo residual (x3 GEMM operand)
+              *(uint2*)(outl + co) = make_uint2(pack2h(v4[0] - rh(v4[0]), v4[1] - rh(v4[1])),
+                                                pack2h(v4[2] - rh(v4[2]), v4[3] - rh(v4[3])));
+          }
         }
         if (!TR && stats) {
           // the output row's (mean, M2) over this workgroup's 32 channels (two-pass over the 8 lanes
@@ -614,6 +622,7 @@ __global__ __launch_bounds__(XNT, CTCLIP_PEGX_WAVES) void peg_fwd32_kernel(const
     if (p + 1 < nsteps) step(std::integral_constant<int, 1>{}, p + 1);
     if (p + 2 < nsteps) step(std::integral_constant<int, 2>{}, p + 2);
   }
+  if (!TR) status_or(status, CT_STATUS_F16_RANGE, bad);
 }
 
 // any geometry / width (D % 4 == 0): one thread per (token, 4 channels), taps from global memory
@@ -621,7 +630,8 @@ __global__ __launch_bounds__(256) void peg_fwd32_naive_kernel(const float* __res
                                                               const float* __restrict__ w,
                                                               const float* __restrict__ bias, Geo g,
                                                               float* __restrict__ out, u16* __restrict__ outb,
-                                                              u16* __restrict__ outh) {
+                                                              u16* __restrict__ outh, u16* __restrict__ outl,
+                                                              int* status) {
   const int nc = D / 4;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= ntok * nc) return;
@@ -653,7 +663,14 @@ __global__ __launch_bounds__(256) void peg_fwd32_naive_kernel(const float* __res
   for (int e = 0; e < 4; ++e) acc[e] += rx[e];
   *(f32x4*)(out + co) = f32x4{acc[0], acc[1], acc[2], acc[3]};
   if (outb) *(uint2*)(outb + co) = pack4(acc);
-  if (outh) *(uint2*)(outh + co) = make_uint2(pack2h(acc[0], acc[1]), pack2h(acc[2], acc[3]));
+  if (outh) {
+    *(uint2*)(outh + co) = make_uint2(pack2h(acc[0], acc[1]), pack2h(acc[2], acc[3]));
+    if (outl)
+      *(uint2*)(outl + co) = make_uint2(pack2h(acc[0] - rh(acc[0]), acc[1] - rh(acc[1])),
+                                        pack2h(acc[2] - rh(acc[2]), acc[3] - rh(acc[3])));
+  }
+  status_or(status, CT_STATUS_F16_RANGE,
+            outh && !(f16_ok(acc[0]) && f16_ok(acc[1]) && f16_ok(acc[2]) && f16_ok(acc[3])));
 }
 
 // weight/bias gradient: grid (B * ceil(H/HT), D/64), WNTH threads; thread = (row, w-segment of
@@ -890,6 +907,14 @@ extern "C" int ctclip_peg_fwd_stats(const void* x_bf16, const float* x_f32, int6
 extern "C" int ctclip_peg_fwd_x32(const float* x_f32, int64_t B, int32_t T, int32_t H, int32_t W, int32_t D,
                                   const float* weight, const float* bias, int32_t mode, float* out_f32, void* out_bf16,
                                   void* out_f16, float* stats, void* stream) {
+  return ctclip_peg_fwd_x32s(x_f32, B, T, H, W, D, weight, bias, mode, out_f32, out_bf16, out_f16, nullptr, stats,
+                             nullptr, stream);
+}
+
+extern "C" int ctclip_peg_fwd_x32s(const float* x_f32, int64_t B, int32_t T, int32_t H, int32_t W, int32_t D,
+                                   const float* weight, const float* bias, int32_t mode, float* out_f32, void* out_bf16,
+                                   void* out_f16, void* out_f16lo, float* stats, int32_t* status, void* stream) {
+  if (out_f16lo && !out_f16) return CT_EINVAL;
   CT_REQUIRE(D % 4 == 0 && x_f32 && out_f32 && aligned16(x_f32) && aligned16(out_f32), CT_EALIGN);
   Geo g{T, H, W, T * H * W, mode};
   const int64_t ntok = B * g.thw;
@@ -909,21 +934,23 @@ extern "C" int ctclip_peg_fwd_x32(const float* x_f32, int64_t B, int32_t T, int3
     dim3 grid(B * ((H + XHT - 1) / XHT), D / XC);
     const auto ob = (u16*)out_bf16;
     const auto oh = (u16*)out_f16;
+    const auto ol = (u16*)out_f16lo;
+    int* sw = (int*)status;
     if (fixed24(g) && g.mode == 0)
       hipLaunchKernelGGL((peg_fwd32_kernel<24, 0>), grid, dim3(XNT), smem, st, x_f32, D, weight, bias, g, out_f32, ob,
-                         oh, stats);
+                         oh, stats, ol, sw);
     else if (fixed24(g) && canon1())
       hipLaunchKernelGGL((peg_fwd32_kernel<24, 2>), grid, dim3(XNT), smem, st, x_f32, D, weight, bias, g, out_f32, ob,
-                         oh, stats);
+                         oh, stats, ol, sw);
     else if (fixed24(g))
       hipLaunchKernelGGL((peg_fwd32_kernel<24, 1>), grid, dim3(XNT), smem, st, x_f32, D, weight, bias, g, out_f32, ob,
-                         oh, stats);
+                         oh, stats, ol, sw);
     else
       hipLaunchKernelGGL((peg_fwd32_kernel<>), grid, dim3(XNT), smem, st, x_f32, D, weight, bias, g, out_f32, ob, oh,
-                         stats);
+                         stats, ol, sw);
   } else {
     hipLaunchKernelGGL(peg_fwd32_naive_kernel, dim3(cdiv(ntok * (D / 4), 256)), dim3(256), 0, st, x_f32, ntok, D,
-                       weight, bias, g, out_f32, (u16*)out_bf16, (u16*)out_f16);
+                       weight, bias, g, out_f32, (u16*)out_bf16, (u16*)out_f16, (u16*)out_f16lo, (int*)status);
   }
   CT_CHECK_LAUNCH();
   return 0;
@@ -952,13 +979,16 @@ extern "C" int ctclip_peg_bwd_data_x32(const float* dout_f32, int64_t B, int32_t
   const auto ob = (u16*)dx_bf16;
   if (g.mode == 0)
     hipLaunchKernelGGL((peg_fwd32_kernel<24, 0, 1>), grid, dim3(XNT), smem, st, dout_f32, D, weight,
-                       (const float*)nullptr, g, dx_f32, ob, (u16*)nullptr, (float*)nullptr);
+                       (const float*)nullptr, g, dx_f32, ob, (u16*)nullptr, (float*)nullptr, (u16*)nullptr,
+                       (int*)nullptr);
   else if (canon1())
     hipLaunchKernelGGL((peg_fwd32_kernel<24, 2, 1>), grid, dim3(XNT), smem, st, dout_f32, D, weight,
-                       (const float*)nullptr, g, dx_f32, ob, (u16*)nullptr, (float*)nullptr);
+                       (const float*)nullptr, g, dx_f32, ob, (u16*)nullptr, (float*)nullptr, (u16*)nullptr,
+                       (int*)nullptr);
   else
     hipLaunchKernelGGL((peg_fwd32_kernel<24, 1, 1>), grid, dim3(XNT), smem, st, dout_f32, D, weight,
-                       (const float*)nullptr, g, dx_f32, ob, (u16*)nullptr, (float*)nullptr);
+                       (const float*)nullptr, g, dx_f32, ob, (u16*)nullptr, (float*)nullptr, (u16*)nullptr,
+                       (int*)nullptr);
   CT_CHECK_LAUNCH();
   return 0;
 }

@@ -28,7 +28,8 @@ __global__ __launch_bounds__(256) void vq_select_kernel(const float2* __restrict
                                                         const float* __restrict__ cand2, int ntiles,
                                                         const float* __restrict__ x, int64_t rows, int D,
                                                         const float* __restrict__ cb, int C, float margin,
-                                                        int32_t* __restrict__ idx_out, float* __restrict__ xn_out) {
+                                                        int32_t* __restrict__ idx_out, float* __restrict__ xn_out,
+                                                        int* status) {
   extern __shared__ float xs_all[];
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -133,6 +134,9 @@ __global__ __launch_bounds__(256) void vq_select_kernel(const float2* __restrict
   if (lane == 0) idx_out[row] = bad ? 0 : bi;
   if (bad && xn_out)
     for (int c = lane; c < D; c += 64) xn_out[row * D + c] = 0.f;
+  // ... and it flags the step (CT_STATUS_VQ_NONFINITE): the trainer skips the step's Adam on every
+  // rank and raises, and the guarded EMA finalize drops the step's codebook update
+  status_or(status, CT_STATUS_VQ_NONFINITE, bad);
 }
 
 // pooled[b][hw][d] = (1/T) sum_t cb[idx[b][t*HW + hw]][d]
@@ -326,10 +330,21 @@ template <bool RESET = false>
 __global__ __launch_bounds__(64) void vq_ema_finalize_kernel(float* __restrict__ bins,
                                                              long long* __restrict__ esum, int C, int D,
                                                              float decay, float* __restrict__ embed,
-                                                             float* __restrict__ cluster, u16* __restrict__ embed_bf16) {
+                                                             float* __restrict__ cluster, u16* __restrict__ embed_bf16,
+                                                             const float* __restrict__ guard) {
   const int c = blockIdx.x;
   const int lane = threadIdx.x;
   const float nb = bins[c];
+  if (guard && *guard != 0.f) {
+    // a flagged step (the summed step status words ride the statistics' all-reduce in the slot
+    // after the bins, so every rank takes this branch together): its codebook update is dropped --
+    // embed / cluster_size untouched -- and only the statistics are cleared for the next step
+    if (RESET) {
+      if (lane == 0) bins[c] = 0.f;
+      for (int k = lane; k < D; k += 64) esum[(int64_t)c * D + k] = 0;
+    }
+    return;
+  }
   if (lane == 0) cluster[c] = cluster[c] * decay + nb * (1.f - decay);
   if (RESET && lane == 0) bins[c] = 0.f;   // one wave: every lane read it above
   float* e = embed + (int64_t)c * D;
@@ -384,8 +399,16 @@ extern "C" int ctclip_vq_select(const float* cand, const float* cand2, int32_t n
                                 float* xn_out, void* stream) {
   if (rows == 0) return 0;
   CT_REQUIRE(D % 4 == 0 && D <= 4096 && aligned16(codebook) && ntiles == (C + 63) / 64, CT_EINVAL);
+  return ctclip_vq_select_s(cand, cand2, ntiles, x, rows, D, codebook, C, margin, idx, xn_out, nullptr, stream);
+}
+
+extern "C" int ctclip_vq_select_s(const float* cand, const float* cand2, int32_t ntiles, const float* x, int64_t rows,
+                                  int32_t D, const float* codebook, int32_t C, float margin, int32_t* idx,
+                                  float* xn_out, int32_t* status, void* stream) {
+  if (rows == 0) return 0;
+  CT_REQUIRE(D % 4 == 0 && D <= 4096 && aligned16(codebook) && ntiles == (C + 63) / 64, CT_EINVAL);
   hipLaunchKernelGGL(vq_select_kernel, dim3(cdiv(rows, 4)), dim3(256), 4 * D * sizeof(float), (hipStream_t)stream,
-                     (const float2*)cand, cand2, ntiles, x, rows, D, codebook, C, margin, idx, xn_out);
+                     (const float2*)cand, cand2, ntiles, x, rows, D, codebook, C, margin, idx, xn_out, (int*)status);
   CT_CHECK_LAUNCH();
   return 0;
 }
@@ -443,15 +466,21 @@ extern "C" int ctclip_vq_ema_accum_sorted(const int32_t* idx, const float* xn, i
 extern "C" int ctclip_vq_ema_finalize(const float* bins, const int64_t* esum, int32_t C, int32_t D, float decay,
                                       float* embed, float* cluster_size, void* embed_bf16, void* stream) {
   hipLaunchKernelGGL(vq_ema_finalize_kernel<false>, dim3(C), dim3(64), 0, (hipStream_t)stream, (float*)bins,
-                     (long long*)esum, C, D, decay, embed, cluster_size, (u16*)embed_bf16);
+                     (long long*)esum, C, D, decay, embed, cluster_size, (u16*)embed_bf16, (const float*)nullptr);
   CT_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int ctclip_vq_ema_finalize_reset(float* bins, int64_t* esum, int32_t C, int32_t D, float decay,
                                             float* embed, float* cluster_size, void* embed_bf16, void* stream) {
+  return ctclip_vq_ema_finalize_guard(bins, esum, C, D, decay, embed, cluster_size, embed_bf16, nullptr, stream);
+}
+
+extern "C" int ctclip_vq_ema_finalize_guard(float* bins, int64_t* esum, int32_t C, int32_t D, float decay,
+                                            float* embed, float* cluster_size, void* embed_bf16, const float* guard,
+                                            void* stream) {
   hipLaunchKernelGGL(vq_ema_finalize_kernel<true>, dim3(C), dim3(64), 0, (hipStream_t)stream, bins,
-                     (long long*)esum, C, D, decay, embed, cluster_size, (u16*)embed_bf16);
+                     (long long*)esum, C, D, decay, embed, cluster_size, (u16*)embed_bf16, guard);
   CT_CHECK_LAUNCH();
   return 0;
 }

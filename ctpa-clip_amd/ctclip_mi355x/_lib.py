@@ -27,6 +27,9 @@ class SlabJob(ctypes.Structure):
                 ('pad', c_i32)]
 
 
+ABI_VERSION = 2     # CTCLIP_ABI_VERSION of include/ctclip_hip.h that the structs below mirror
+
+
 class GemmArgs(ctypes.Structure):
     _fields_ = [
         ('M', c_i64), ('N', c_i64), ('K', c_i64),
@@ -46,6 +49,9 @@ class GemmArgs(ctypes.Structure):
         ('B2', c_vp),
         ('ab_f16', c_i32),
         ('r_f16', c_i32),
+        ('A_lo', c_vp), ('B_lo', c_vp),
+        ('C3', c_vp), ('ldc3', c_i64),
+        ('C4', c_vp), ('ldc4', c_i64),
     ]
 
 
@@ -152,8 +158,12 @@ _SIGS = {
                                   c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_f32, ctypes.c_uint64, c_vp],
     'ctclip_patch_ln_x2': [c_vp, c_i32, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp,
                            c_vp, c_i64, c_vp],
+    'ctclip_patch_ln_x3': [c_vp, c_i32, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp,
+                           c_vp, c_vp, c_i64, c_vp],
     'ctclip_layernorm_fwd_x2': [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_i64, c_vp, c_i64,
                                 c_vp, c_vp, c_vp],
+    'ctclip_layernorm_fwd_x3': [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_f32, c_vp, c_vp, c_vp, c_i64, c_vp,
+                                c_i64, c_vp, c_vp, c_vp, c_vp],
     'ctclip_pack_rows_h16': [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp],
     'ctclip_pack_qkv_fold_h16': [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp],
     'ctclip_skinny_gemm_slices': [c_i64, c_i64, c_i64],
@@ -173,6 +183,8 @@ _SIGS = {
     'ctclip_gelu_bwd': [c_vp, c_vp, c_vp, c_i64, c_vp],
     'ctclip_pack_rows': [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp],
     'ctclip_pack_rows_f32': [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp],
+    'ctclip_split_f16': [c_vp, c_i64, c_i64, c_i32, c_f32, c_vp, c_vp, c_i64, c_vp, c_vp],
+    'ctclip_pack_rows_x3': [c_vp, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp, c_f32, c_vp, c_vp, c_i64, c_vp, c_vp],
     'ctclip_sgemm_tn': [ctypes.POINTER(SgemmTnArgs), c_vp],
     'ctclip_unpack_rows': [c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_vp],
     'ctclip_reduce_slabs_rows': [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp],
@@ -189,6 +201,8 @@ _SIGS = {
     'ctclip_peg_fwd_stats': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp,
                              c_vp],
     'ctclip_peg_fwd_x32': [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
+    'ctclip_peg_fwd_x32s': [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp,
+                            c_vp, c_vp],
     'ctclip_peg_bwd_data_x32': [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp],
     'ctclip_peg_bwd_data': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp],
     'ctclip_peg_bwd_weight': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_i32, c_vp],
@@ -207,6 +221,7 @@ _SIGS = {
     'ctclip_l2norm_scale_fwd_f32': [c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp],
     'ctclip_geglu_f32': [c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
     'ctclip_vq_select': [c_vp, c_vp, c_i32, c_vp, c_i64, c_i32, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp],
+    'ctclip_vq_select_s': [c_vp, c_vp, c_i32, c_vp, c_i64, c_i32, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp],
     'ctclip_vq_pool': [c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
     'ctclip_vq_pool_bwd': [c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp],
     'ctclip_vq_gather': [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp],
@@ -214,6 +229,7 @@ _SIGS = {
     'ctclip_vq_ema_accum_sorted': [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp],
     'ctclip_vq_ema_finalize': [c_vp, c_vp, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp],
     'ctclip_vq_ema_finalize_reset': [c_vp, c_vp, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp],
+    'ctclip_vq_ema_finalize_guard': [c_vp, c_vp, c_i32, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp, c_vp],
     'ctclip_clip_loss': [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     'ctclip_clip_scores': [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp],
     'ctclip_zero_shot': [c_vp, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp],
@@ -223,6 +239,7 @@ _SIGS = {
     'ctclip_embed_fwd': [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
     'ctclip_embed_bwd': [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp],
     'ctclip_grad_norm': [c_vp, c_i64, c_f32, c_vp, c_i32, c_vp, c_vp],
+    'ctclip_grad_norm_s': [c_vp, c_i64, c_f32, c_vp, c_i32, c_vp, c_vp, c_vp],
     'ctclip_adam': [c_vp, c_vp, c_vp, c_vp, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_i32, c_vp, c_vp, c_vp, c_i32,
                     c_vp, c_vp],
 }
@@ -243,6 +260,14 @@ def lib():
             raise RuntimeError(f'ctclip_mi355x: HIP library not built ({LIB_PATH}); run '
                                '`python -c "import __graft_entry__ as g; g.build()"` from the repo root')
         _LIB = ctypes.CDLL(LIB_PATH)
+        # the structs below mirror include/ctclip_hip.h of ABI version ABI_VERSION: a library of
+        # another version reads (or misses) trailing struct fields, so it is refused outright
+        _LIB.ctclip_version.restype = c_i32
+        v = _LIB.ctclip_version()
+        if v != ABI_VERSION and 'CTCLIP_HIP_LIB' not in os.environ:
+            _LIB = None
+            raise RuntimeError(f'ctclip_mi355x: {LIB_PATH} has ABI version {v}, this binding needs '
+                               f'{ABI_VERSION} (rebuild: `make -C ctpa-clip_amd/csrc`)')
         # an A/B library named by CTCLIP_HIP_LIB may predate entry points added since; those are
         # skipped (calling one fails).  The in-tree library must export every one.
         ab = 'CTCLIP_HIP_LIB' in os.environ

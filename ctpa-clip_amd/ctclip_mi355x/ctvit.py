@@ -52,6 +52,27 @@ class VectorQuantize(nn.Module):
     def codebook(self):
         return self._codebook.embed[0]
 
+    # The training step's codebook EMA runs on the auxiliary stream, possibly deferred past the
+    # optimizer step (ct_clip.DEFER_EMA): every torch-API reader / writer of the codebook buffers is
+    # ordered after it here, so a state_dict (checkpoint) holds the updated codebook and a load is not
+    # overwritten by an EMA still in flight.  A pending (not yet queued) update is applied before a
+    # save, and dropped by a load -- the loaded codebook replaces the state it would have updated.
+    def _join_ema(self):
+        dev = self._codebook.embed.device
+        if dev.type == 'cuda':
+            from . import streams
+            streams.join_aux(dev)
+
+    def state_dict(self, *args, **kwargs):
+        self.state.flush_ema()
+        self._join_ema()
+        return super().state_dict(*args, **kwargs)
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self.state.pending_ema = None
+        self._join_ema()
+        return super()._load_from_state_dict(*args, **kwargs)
+
 
 class _Slot(nn.Module):
     """Parameter-free placeholder keeping Sequential indices identical to the reference (Rearrange)."""

@@ -76,6 +76,28 @@ def precise_f32():
     return precise.vit_precision() == 'f32'
 
 
+def precise_split():
+    """True in the split-fp16 image-tower mode (precise.set_vit_precision('split'), round 6): the
+    forward's Linears on the x3 GEMM (~22-bit operands, f32 accumulation), everything else in f32 --
+    the f32 mode's numerics at a fraction of its cost; the backward as in the other modes."""
+    from . import precise
+    return precise.vit_precision() == 'split'
+
+
+def x3_weight(W, rows=None, cols=None, rowmap=None, colscale=None, tag='w'):
+    """Split-fp16 pair of f32 weight W for the x3 GEMM (kernels.pack_rows_x3, scaled by X3_WSCALE),
+    cached on the parameter until the master changes (optimizer epoch, version, storage)."""
+    key = (K.weights_epoch(), W._version, W.data_ptr(),
+           None if colscale is None else (colscale.data_ptr(), colscale._version))
+    cache = W.__dict__.setdefault('_ctclip_x3', {})
+    e = cache.get(tag)
+    if e is None or e[0] != key:
+        e = (key, K.pack_rows_x3(W.detach(), rows or W.shape[0], cols or W.shape[1], rowmap=rowmap,
+                                 colscale=None if colscale is None else colscale.detach()))
+        cache[tag] = e
+    return e[1]
+
+
 # ----------------------------------------------------------------------------- geometry
 @dataclass(frozen=True)
 class Geo:
@@ -402,12 +424,19 @@ class PatchEmbedFn(torch.autograd.Function):
     def forward(ctx, video, ln1_w, ln1_b, W, b, ln2_w, ln2_b, PT, P, is_hu, offs):
         pd = W.shape[1]
         kp = (pd + 63) // 64 * 64                                      # K padded to the 64-deep GEMM step
-        f16 = vit_f16() and not precise_f32() and not vit_fp8()
-        xhat_p = K.patch_ln(video, is_hu, PT, P, offs, ld=kp, want_f16=f16)   # [M, kp], zero pad columns
-        if f16:
-            xhat_p, xhat16 = xhat_p      # bf16 (the weight gradient's operand) and fp16 (the GEMM's)
+        split = precise_split()
+        f16 = vit_f16() and not precise_f32() and not vit_fp8() and not split
+        xhat_p = K.patch_ln(video, is_hu, PT, P, offs, ld=kp, want_f16=f16, want_x3=split)   # [M, kp], 0 pads
+        if f16 or split:
+            xhat_p, xhat16 = xhat_p      # bf16 (the weight gradient's operand) and fp16 (pair) (the GEMM's)
         xhat = xhat_p[:, :pd]
-        if precise_f32():
+        if split:
+            # split-fp16 tower: the LayerNorm(4000) affine folded into the Linear in f32 (W diag(g),
+            # b + W beta), then the x3 GEMM on the LayerNorm'd patches' fp16 pair
+            bp = K.slinear(ln1_b.view(1, -1), W, bias=b).view(-1)
+            y1, _ = K.linear_x3(xhat16, x3_weight(W, cols=kp, colscale=ln1_w, tag='patch'), bias=bp)
+            del xhat16
+        elif precise_f32():
             # f32 tower: LayerNorm(4000) with its affine, then the Linear, both exact f32
             # (ct_clip/ctvit.py:170-172); xhat (bf16) above is what the backward reads
             xn0 = K.patch_ln_f32(video, is_hu, PT, P, offs, ln1_w.detach(), ln1_b.detach())
@@ -573,9 +602,9 @@ class ViTLayerFn(torch.autograd.Function):
             acc = bias_u.__dict__.setdefault('_ctclip_bias_acc', {'n': 0, 'du': None})
             ctx.bias_acc, ctx.bias_first = acc, acc['n'] == 0
             acc['n'] += 1
-        if precise_f32():
+        if precise_f32() or precise_split():
             return _vit_layer_forward_f32(ctx, xf, xb, bias_u, geo, peg_w, peg_b, norm_g, q_scale, k_scale, Wq,
-                                          Wkv, Wo, ff_w, ff_b, W1, W2)
+                                          Wkv, Wo, ff_w, ff_b, W1, W2, split=precise_split())
         H, dh = geo.heads, geo.dim_head
         inner = H * dh
         Wq_b, Wkv_b, Wo_b = bf(Wq), bf(Wkv), bf(Wo)
@@ -815,22 +844,46 @@ class ViTLayerFn(torch.autograd.Function):
 
 
 def _vit_layer_forward_f32(ctx, xf, xb, bias_u, geo, peg_w, peg_b, norm_g, q_scale, k_scale, Wq, Wkv, Wo, ff_w,
-                           ff_b, W1, W2):
+                           ff_b, W1, W2, split=False):
     """ViTLayerFn.forward of the f32 image tower: the layer (ct_clip/attention.py:322-331) with f32
     activations and exact-f32 products (every Linear on the f32 MFMA GEMM, PEG / LayerNorm / l2norm /
     cosine attention with the CPB bias / GEGLU in f32 with libm transcendentals), saving exactly the
     tensors ViTLayerFn.backward reads, as the bf16 forward saves them (bf16 copies of the f32
     activations; the attention's o / lse from the bf16 attention kernel on the bf16 q / k / v, so the
-    backward's recomputed probabilities are those of its own operands)."""
+    backward's recomputed probabilities are those of its own operands).
+    split (precise 'split' mode, round 6): the Linears on the x3 GEMM instead -- each operand an fp16
+    (hi, lo) pair written by its producer (the f32-tap PEG, the LayerNorms, the x3 GEGLU epilogue; the
+    attention output through ctclip_split_f16), ~22-bit operands with f32 accumulation -- and the PEG
+    on the f32-tap x32 kernel; FF1's h is saved in fp16 (the GEGLU backward reads it as in the fp16
+    default), g in bf16."""
     H, dh = geo.heads, geo.dim_head
     inner = H * dh
     d = lambda t: t.detach()    # noqa: E731
+    if split:
+        x1f, x1b, x1s, _, _ = K.peg_fwd_x32(xf.detach().contiguous(), geo.B, geo.T, geo.Hg, geo.Wg, d(peg_w),
+                                            d(peg_b), geo.mode, want_x3=True)
+        xn, _, m1, r1, xns = K.layernorm_fwd(x1f, norm_g, None, 1e-5, out_bf16=True, out_x3=True)   # q side only
+        q32, q = K.linear_x3(xns, x3_weight(Wq), want_bf16=True)
+        kv32, kv = K.linear_x3(x1s, x3_weight(Wkv), want_bf16=True)   # K / V from the un-normalised x
+        del xns, x1s
+        return _vit_layer_tail_f32(ctx, x1f, x1b, xn, m1, r1, q32, q, kv32, kv, xb, bias_u, geo, peg_w, peg_b, norm_g,
+                                   q_scale, k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1, W2, split=True)
     x1f = K.peg_fwd_f32(xf.detach().contiguous(), geo.B, geo.T, geo.Hg, geo.Wg, d(peg_w), d(peg_b), geo.mode)
     x1b = K.cast_bf16(x1f)
     xn, xnf, m1, r1 = K.layernorm_fwd(x1f, norm_g, None, 1e-5, out_bf16=True, out_f32=True)   # q side only
     q32, q = K.linear_f32(xnf, d(Wq), want_bf16=True)
     kv32, kv = K.linear_f32(x1f, d(Wkv), want_bf16=True)          # K / V from the un-normalised x
     del xnf
+    return _vit_layer_tail_f32(ctx, x1f, x1b, xn, m1, r1, q32, q, kv32, kv, xb, bias_u, geo, peg_w, peg_b, norm_g,
+                               q_scale, k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1, W2, split=False)
+
+
+def _vit_layer_tail_f32(ctx, x1f, x1b, xn, m1, r1, q32, q, kv32, kv, xb, bias_u, geo, peg_w, peg_b, norm_g, q_scale,
+                        k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1, W2, split):
+    """_vit_layer_forward_f32 from the f32 q / kv on: l2norm, attention, to_out, FeedForward."""
+    H, dh = geo.heads, geo.dim_head
+    inner = H * dh
+    d = lambda t: t.detach()    # noqa: E731
     qn32 = K.l2norm_scale_fwd_f32(q32, H, dh, d(q_scale))
     kn32 = K.l2norm_scale_fwd_f32(kv32[:, :inner], H, dh, d(k_scale))
     L, nseq, seq = geo.seq()
@@ -842,16 +895,26 @@ def _vit_layer_forward_f32(ctx, xf, xb, bias_u, geo, peg_w, peg_b, norm_g, q_sca
     del q32, qn32, kn32
     o, lse = K.attn_fwd(qn, kn, kv[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
                         bias_u=bias_u if use_bias else None, grid=grid)
-    x2f, x2b = K.linear_f32(o32, d(Wo), residual=x1f, want_bf16=True)
-    del o32, kv32, x1f
-    xn2, xn2f, m2, r2 = K.layernorm_fwd(x2f, ff_w, ff_b, 1e-5, out_bf16=True, out_f32=True)
     inner_ff = W1.shape[0] // 2
-    W1p32 = K.pack_rows_f32(d(W1), 2 * ff_pad(inner_ff), W1.shape[1], rowmap=ff1_rowmap(inner_ff, W1.device))
-    h, g32, g = K.linear_f32_geglu(xn2f, W1p32)
-    del xn2f
-    W2p32 = K.pack_rows_f32(d(W2), W2.shape[0], ff_pad(W2.shape[1]))
-    x3f, x3b = K.linear_f32(g32, W2p32, residual=x2f, want_bf16=True)
-    del g32
+    if split:
+        x2f, x2b = K.linear_x3(K.split_f16(o32), x3_weight(Wo), residual=x1f, want_bf16=True)
+        del o32, kv32, x1f
+        xn2, _, m2, r2, xn2s = K.layernorm_fwd(x2f, ff_w, ff_b, 1e-5, out_bf16=True, out_x3=True)
+        W1s = x3_weight(W1, rows=2 * ff_pad(inner_ff), rowmap=ff1_rowmap(inner_ff, W1.device), tag='ff1')
+        h, gs, g = K.linear_x3_geglu(xn2s, W1s, tag='ff1', flops=2.0 * x2f.shape[0] * W1.shape[0] * W1.shape[1])
+        del xn2s
+        x3f, x3b = K.linear_x3(gs, x3_weight(W2, cols=ff_pad(W2.shape[1]), tag='ff2'), residual=x2f, want_bf16=True)
+        del gs
+    else:
+        x2f, x2b = K.linear_f32(o32, d(Wo), residual=x1f, want_bf16=True)
+        del o32, kv32, x1f
+        xn2, xn2f, m2, r2 = K.layernorm_fwd(x2f, ff_w, ff_b, 1e-5, out_bf16=True, out_f32=True)
+        W1p32 = K.pack_rows_f32(d(W1), 2 * ff_pad(inner_ff), W1.shape[1], rowmap=ff1_rowmap(inner_ff, W1.device))
+        h, g32, g = K.linear_f32_geglu(xn2f, W1p32)
+        del xn2f
+        W2p32 = K.pack_rows_f32(d(W2), W2.shape[0], ff_pad(W2.shape[1]))
+        x3f, x3b = K.linear_f32(g32, W2p32, residual=x2f, want_bf16=True)
+        del g32
     ctx.geo = geo
     ctx.use_bias = use_bias
     ctx.params = (peg_w, peg_b, norm_g, q_scale, k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1, W2)
@@ -915,12 +978,19 @@ class VQPoolFn(torch.autograd.Function):
 
             def ema():
                 # persistent statistics (2^-40 fixed-point esum), zeroed once here and then by the
-                # finalize kernel behind its reads: no fill launches per step
-                bins, esum = state.ema_buffers(C, D, zf.device)
+                # finalize kernel behind its reads: no fill launches per step.  bins has one slot past
+                # the C counts: this rank's step status word (a flagged forward: fp16 range, a
+                # non-finite token, a LayerNorm exchange timeout), summed over the ranks with the
+                # statistics, so every rank drops a flagged step's codebook update together
+                bins_g, esum = state.ema_buffers(C, D, zf.device)
+                bins = bins_g[:C]
+                if zf.is_cuda:
+                    bins_g[C:].copy_(K.status_word(zf.device))
                 work = state.ema_work(C, xn.shape[0], zf.device) if _EMA_SORTED else None
                 K.vq_ema_accum(idx, xn, bins, esum, work=work)
-                dist_sync.sum_codebook_stats(bins, esum)
-                K.vq_ema_finalize(bins, esum, decay, cb, cluster.view(-1), cb_b, reset=True)
+                dist_sync.sum_codebook_stats(bins_g, esum)
+                K.vq_ema_finalize(bins, esum, decay, cb, cluster.view(-1), cb_b, reset=True,
+                                  guard=bins_g[C:] if zf.is_cuda else None)
             if aux is None:
                 ema()
             else:
@@ -985,11 +1055,12 @@ class VQState:
         self.pending_ema = None
 
     def ema_buffers(self, C, D, device):
-        """(bins f32 [C], esum int64 [C, D]) of the EMA update, zero between updates (created on the
-        stream of the first update, which every later update also runs on)."""
+        """(bins f32 [C + 1], esum int64 [C, D]) of the EMA update, zero between updates (created on the
+        stream of the first update, which every later update also runs on); bins[C] is the guard slot
+        (the step status word, VQPoolFn.forward)."""
         b = getattr(self, '_ema_buf', None)
         if b is None or b[1].shape != (C, D) or b[1].device != device:
-            b = (torch.zeros(C, device=device, dtype=F32), torch.zeros(C, D, device=device, dtype=torch.int64))
+            b = (torch.zeros(C + 1, device=device, dtype=F32), torch.zeros(C, D, device=device, dtype=torch.int64))
             self._ema_buf = b
         return b
 
@@ -1036,7 +1107,7 @@ class ImageProjFn(torch.autograd.Function):
     def forward(ctx, pooled, pooled_b, W, Wb):
         ctx.save_for_backward(pooled_b, Wb)
         ctx.W = W
-        if precise_f32():      # the f32 image tower's projection: exact f32 (split-K f32 MFMA)
+        if precise_f32() or precise_split():   # the precise towers' projection: exact f32 (split-K f32 MFMA)
             return K.slinear(pooled.detach().contiguous(), W.detach())
         # the HBM-streaming skinny GEMM (csrc/proj.hip): the 302 MB weight read once at ~HBM speed
         # (the generic split-K 128-row MFMA tile ran at 0.85 TB/s at M = 8, round 4)

@@ -534,16 +534,21 @@ def colsum(x, out=None, accumulate=False):
 
 
 # ----------------------------------------------------------------------------- LayerNorm
-def layernorm_fwd(x, gamma, beta, eps, *, out_bf16=True, out_f32=False, out_f16=False):
-    """Returns (y bf16, y f32, mean, rstd), plus y's fp16 copy when out_f16 (requires out_bf16)."""
+def layernorm_fwd(x, gamma, beta, eps, *, out_bf16=True, out_f32=False, out_f16=False, out_x3=False):
+    """Returns (y bf16, y f32, mean, rstd), plus y's fp16 copy when out_f16 (requires out_bf16), or
+    its split-fp16 pair (hi, lo) when out_x3 (the x3 GEMM's A operand)."""
     rows, D = x.shape
     yb = torch.empty(rows, D, device=x.device, dtype=BF16) if out_bf16 else None
     yf = torch.empty(rows, D, device=x.device, dtype=F32) if out_f32 else None
-    yh = torch.empty(rows, D, device=x.device, dtype=F16) if out_f16 else None
+    yh = torch.empty(rows, D, device=x.device, dtype=F16) if out_f16 or out_x3 else None
+    yl = torch.empty(rows, D, device=x.device, dtype=F16) if out_x3 else None
     mean = torch.empty(rows, device=x.device, dtype=F32)
     rstd = torch.empty(rows, device=x.device, dtype=F32)
-    call('ctclip_layernorm_fwd_x2', ptr(x), int(x.dtype == F32), x.stride(0), rows, D, ptr(gamma), ptr(beta), eps,
-         ptr(yb), ptr(yh), D, ptr(yf), D, ptr(mean), ptr(rstd), stream_ptr())
+    call('ctclip_layernorm_fwd_x3', ptr(x), int(x.dtype == F32), x.stride(0), rows, D, ptr(gamma), ptr(beta), eps,
+         ptr(yb), ptr(yh), ptr(yl), D, ptr(yf), D, ptr(mean), ptr(rstd),
+         ptr(status_word(x.device)) if yh is not None else None, stream_ptr())
+    if out_x3:
+        return yb, yf, mean, rstd, (yh, yl)
     if out_f16:
         return yb, yf, mean, rstd, yh
     return yb, yf, mean, rstd
@@ -714,17 +719,21 @@ def add_f32(a, b, out=None, out_bf16=None):
 
 
 # ----------------------------------------------------------------------------- patch embed
-def patch_ln(video, is_hu, PT, P, offs, eps=1e-5, ld=None, want_f16=False):
+def patch_ln(video, is_hu, PT, P, offs, eps=1e-5, ld=None, want_f16=False, want_x3=False):
     """LayerNorm'd patch rows [tokens, ld] bf16 (columns pd..ld-1 zero: K padding for the GEMM);
-    with want_f16 also their fp16 copy (returns (bf16, f16))."""
+    with want_f16 also their fp16 copy (returns (bf16, f16)); with want_x3 their split-fp16 pair
+    (returns (bf16, (hi, lo)))."""
     B, C, Fr, H, W = video.shape
     T, Hg, Wg = Fr // PT, H // P, W // P
     pd = C * PT * P * P
     ld = pd if ld is None else ld
     out = torch.empty(B * T * Hg * Wg, ld, device=video.device, dtype=BF16)
-    out16 = torch.empty(B * T * Hg * Wg, ld, device=video.device, dtype=F16) if want_f16 else None
-    call('ctclip_patch_ln_x2', ptr(video), int(video.dtype == F32), int(is_hu), B, C, Fr, H, W, PT, P, ptr(offs), eps,
-         ptr(out), ptr(out16), ld, stream_ptr())
+    out16 = torch.empty(B * T * Hg * Wg, ld, device=video.device, dtype=F16) if want_f16 or want_x3 else None
+    out16lo = torch.empty(B * T * Hg * Wg, ld, device=video.device, dtype=F16) if want_x3 else None
+    call('ctclip_patch_ln_x3', ptr(video), int(video.dtype == F32), int(is_hu), B, C, Fr, H, W, PT, P, ptr(offs), eps,
+         ptr(out), ptr(out16), ptr(out16lo), ld, stream_ptr())
+    if want_x3:
+        return out, (out16, out16lo)
     return (out, out16) if want_f16 else out
 
 
@@ -793,19 +802,24 @@ def skinny_linear(x, w):
     return out
 
 
-def peg_fwd_x32(xf, B, T, H, W, weight, bias, mode, stats=False, want_f16=False, eps=1e-5):
+def peg_fwd_x32(xf, B, T, H, W, weight, bias, mode, stats=False, want_f16=False, eps=1e-5, want_x3=False):
     """PEG forward with the taps read from the f32 residual stream (ctclip_peg_fwd_x32; the bf16
     shadow's rounding never enters the conv).  Returns (out_f32, out_bf16, out_f16 or None, mean,
     rstd) -- mean / rstd the LayerNorm statistics of the output rows when stats (merged from the
-    kernel's 32-channel groups), else None."""
+    kernel's 32-channel groups), else None; with want_x3 the third entry is the output's split-fp16
+    pair (hi, lo) (the x3 Q | K | V GEMM's A operand).  The fp16 outputs are range-checked into the
+    step status word (CT_STATUS_F16_RANGE)."""
     M, D = xf.shape
     assert xf.dtype == F32 and xf.is_contiguous()
     outf = torch.empty_like(xf)
     outb = torch.empty(M, D, device=xf.device, dtype=BF16)
-    outh = torch.empty(M, D, device=xf.device, dtype=torch.float16) if want_f16 else None
+    outh = torch.empty(M, D, device=xf.device, dtype=torch.float16) if want_f16 or want_x3 else None
+    outl = torch.empty(M, D, device=xf.device, dtype=torch.float16) if want_x3 else None
     part = torch.empty(D // 32, M, 2, device=xf.device, dtype=F32) if stats else None
-    call('ctclip_peg_fwd_x32', ptr(xf), B, T, H, W, D, ptr(weight), ptr(bias), mode, ptr(outf), ptr(outb), ptr(outh),
-         ptr(part), stream_ptr())
+    call('ctclip_peg_fwd_x32s', ptr(xf), B, T, H, W, D, ptr(weight), ptr(bias), mode, ptr(outf), ptr(outb), ptr(outh),
+         ptr(outl), ptr(part), ptr(status_word(xf.device)) if outh is not None else None, stream_ptr())
+    if want_x3:
+        outh = (outh, outl)
     if not stats:
         return outf, outb, outh, None, None
     mean = torch.empty(M, device=xf.device, dtype=F32)
@@ -1068,8 +1082,9 @@ def vq_select(cand, x, codebook_f32, margin=2e-2, want_xn=True, cand2=None):
     rows, D = x.shape
     idx = torch.empty(rows, device=x.device, dtype=torch.int32)
     xn = torch.empty(rows, D, device=x.device, dtype=F32) if want_xn else None
-    call('ctclip_vq_select', ptr(cand), ptr(cand2), cand.shape[1], ptr(x), rows, D, ptr(codebook_f32),
-         codebook_f32.shape[0], margin, ptr(idx), ptr(xn), stream_ptr())
+    # a token without a finite score sets CT_STATUS_VQ_NONFINITE in the step status word
+    call('ctclip_vq_select_s', ptr(cand), ptr(cand2), cand.shape[1], ptr(x), rows, D, ptr(codebook_f32),
+         codebook_f32.shape[0], margin, ptr(idx), ptr(xn), ptr(status_word(x.device)), stream_ptr())
     return idx, xn
 
 
@@ -1116,10 +1131,16 @@ def vq_ema_accum(idx, xn, bins, esum, work=None):
     call('ctclip_vq_ema_accum', ptr(idx), ptr(xn), xn.shape[0], xn.shape[1], ptr(bins), ptr(esum), stream_ptr())
 
 
-def vq_ema_finalize(bins, esum, decay, embed, cluster, embed_bf16=None, reset=False):
-    """reset: zero bins / esum behind the reads (persistent statistics buffers)."""
+def vq_ema_finalize(bins, esum, decay, embed, cluster, embed_bf16=None, reset=False, guard=None):
+    """reset: zero bins / esum behind the reads (persistent statistics buffers).  guard (f32 [1], with
+    reset): a nonzero value drops this update (embed / cluster untouched, statistics zeroed)."""
     assert esum.dtype == torch.int64
     C, D = esum.shape
+    if guard is not None:
+        assert reset and guard.dtype == F32
+        call('ctclip_vq_ema_finalize_guard', ptr(bins), ptr(esum), C, D, decay, ptr(embed), ptr(cluster),
+             ptr(embed_bf16), ptr(guard), stream_ptr())
+        return
     call('ctclip_vq_ema_finalize_reset' if reset else 'ctclip_vq_ema_finalize', ptr(bins), ptr(esum), C, D, decay,
          ptr(embed), ptr(cluster), ptr(embed_bf16), stream_ptr())
 
@@ -1221,10 +1242,12 @@ def embed_bwd(ids, dx, dword, dpos, dtype0, pad_id=-1):
 
 
 # ----------------------------------------------------------------------------- optimizer
-def grad_norm(g, max_norm, out):
+def grad_norm(g, max_norm, out, skip=None):
+    """out[0] = ||g||, out[1] = the clip coefficient; skip (device int32[1]): a non-finite norm ORs
+    CT_STATUS_NONFINITE_GRAD (4) into it (the Adam kernels' guard word)."""
     nblk = 1024
     part = torch.empty(nblk, device=g.device, dtype=F32)
-    call('ctclip_grad_norm', ptr(g), g.numel(), max_norm, ptr(part), nblk, ptr(out), stream_ptr())
+    call('ctclip_grad_norm_s', ptr(g), g.numel(), max_norm, ptr(part), nblk, ptr(out), ptr(skip), stream_ptr())
     return out
 
 
@@ -1385,3 +1408,98 @@ def attn_fwd_f32(q, k, v, *, L, H, D, nseq, scale, seq, bias_u=None, grid=(0, 0)
     a = _attn_args(q, k, v, o, L=L, H=H, D=D, nseq=nseq, M=M, scale=scale, seq=seq, bias_u=bias_u, grid=grid)
     call('ctclip_attn_fwd_f32', _lib.ctypes.byref(a), stream_ptr())
     return o
+
+
+# ---------------------------------------------------------------- split-fp16 x3 image tower (round 6)
+# precise.set_vit_precision('split'): every forward Linear of the 3D-ViT on the x3 GEMM (gemm256.hip,
+# ctclip_gemm_args.A_lo / B_lo): operands as fp16 (hi, lo) image pairs, three fp16 MFMA products per
+# K-step into one f32 accumulator -- ~22-bit operands at 3x the fp16 MFMA work instead of f32 MFMA
+# at 1/16 of the rate (tools/vit_precision.py 's:' / 'S:' sites: pre-VQ 1.2e-6, 0 flips).
+X3_WSCALE = 256.0   # weights are packed x256 (their ~1e-2 entries keep a normal fp16 lo part); alpha = 1/256
+
+
+def status_word(device):
+    """The device's sticky int32[1] step status word (include/ctclip_hip.h CT_STATUS_*): the
+    LayerNorm exchange timeouts, fp16 range / non-finite flags of the producers that take it."""
+    return ln_status_tensor(device)
+
+
+def split_f16(x, scale=1.0, out=None):
+    """(hi, lo) fp16 images of f32 x [rows, cols]: hi = fp16(x s), lo = fp16(x s - hi)."""
+    rows, cols = x.shape
+    assert x.dtype == F32 and x.stride(1) == 1
+    hi, lo = out if out is not None else (torch.empty(rows, cols, device=x.device, dtype=F16),
+                                          torch.empty(rows, cols, device=x.device, dtype=F16))
+    call('ctclip_split_f16', ptr(x), x.stride(0), rows, cols, float(scale), ptr(hi), ptr(lo), hi.stride(0),
+         ptr(status_word(x.device)), stream_ptr())
+    return hi, lo
+
+
+def pack_rows_x3(src, rows_dst, cols_dst, rowmap=None, colscale=None, scale=X3_WSCALE):
+    """pack_rows of an f32 weight into its split-fp16 pair, scaled by `scale` (see X3_WSCALE)."""
+    rows, cols = src.shape
+    assert src.dtype == F32 and src.stride(1) == 1
+    hi = torch.empty(rows_dst, cols_dst, device=src.device, dtype=F16)
+    lo = torch.empty(rows_dst, cols_dst, device=src.device, dtype=F16)
+    call('ctclip_pack_rows_x3', ptr(src), src.stride(0), ptr(rowmap), rows_dst, cols, cols_dst, ptr(colscale),
+         float(scale), ptr(hi), ptr(lo), hi.stride(0), ptr(status_word(src.device)), stream_ptr())
+    return hi, lo
+
+
+def _x3_args(xs, ws, C, alpha):
+    (xh, xl), (wh, wl) = xs, ws
+    M, Kd = xh.shape
+    N = wh.shape[0]
+    assert xh.dtype == F16 and xl.dtype == F16 and wh.dtype == F16 and wl.dtype == F16
+    assert xl.shape == xh.shape and xl.stride() == xh.stride() and wl.shape == wh.shape and wl.stride() == wh.stride()
+    assert wh.shape[1] == Kd and xh.stride(1) == 1 and wh.stride(1) == 1 and Kd % 64 == 0
+    a = GemmArgs()
+    a.M, a.N, a.K = M, N, Kd
+    a.A, a.lda, a.a_kcontig = ptr(xh), xh.stride(0), 1
+    a.B, a.ldb, a.b_kcontig = ptr(wh), wh.stride(0), 1
+    a.A_lo, a.B_lo = ptr(xl), ptr(wl)
+    a.C, a.ldc = ptr(C), C.stride(0)
+    a.alpha, a.split_k, a.batch, a.ab_f16 = float(alpha), 1, 1, 1
+    return a
+
+
+def linear_x3(xs, ws, *, bias=None, residual=None, want_bf16=False, alpha=1.0 / X3_WSCALE, tag=None, flops=None):
+    """y [M, N] f32 = alpha xs . ws^T (+ bias) (+ f32 residual) on the x3 GEMM, xs / ws split-fp16
+    pairs ([M, K] activations, [N, K] weights packed by pack_rows_x3); returns (y, bf16 copy or None)."""
+    M, N = xs[0].shape[0], ws[0].shape[0]
+    y = torch.empty(M, N, device=xs[0].device, dtype=F32)
+    yb = torch.empty(M, N, device=y.device, dtype=BF16) if want_bf16 else None
+    a = _x3_args(xs, ws, y, alpha)
+    a.c_f32 = 1
+    a.C2, a.ldc2 = ptr(yb), N if yb is not None else 0
+    a.bias = ptr(bias)
+    if residual is not None:
+        assert residual.dtype == F32 and residual.shape == (M, N) and residual.stride(1) == 1
+        a.R, a.ldr, a.r_f32 = ptr(residual), residual.stride(0), 1
+    end = TIMER(tag, flops if flops is not None else 2.0 * M * N * xs[0].shape[1]) if tag else None
+    call('ctclip_gemm', _lib.ctypes.byref(a), stream_ptr())
+    if end is not None:
+        end.record()
+    return y, yb
+
+
+def linear_x3_geglu(xs, w1s, *, alpha=1.0 / X3_WSCALE, want_bf16=True, tag=None, flops=None):
+    """FF1 + GEGLU on the x3 GEMM over the packed [32 x | 32 gate] weight pair (functional.pack_ff1
+    order): returns (h fp16 [M, N], (g hi, g lo) fp16 [M, N/2] -- FF2's A operand --, g bf16 or None)."""
+    M, N = xs[0].shape[0], w1s[0].shape[0]
+    assert N % 64 == 0
+    dev = xs[0].device
+    h = torch.empty(M, N, device=dev, dtype=F16)
+    gh = torch.empty(M, N // 2, device=dev, dtype=F16)
+    gl = torch.empty(M, N // 2, device=dev, dtype=F16)
+    gb = torch.empty(M, N // 2, device=dev, dtype=BF16) if want_bf16 else None
+    a = _x3_args(xs, w1s, h, alpha)
+    a.act = ACT_GEGLU
+    a.C2, a.ldc2 = ptr(gh), N // 2
+    a.C3, a.ldc3 = ptr(gl), N // 2
+    a.C4, a.ldc4 = ptr(gb), N // 2 if gb is not None else 0
+    end = TIMER(tag, flops if flops is not None else 2.0 * M * N * xs[0].shape[1]) if tag else None
+    call('ctclip_gemm', _lib.ctypes.byref(a), stream_ptr())
+    if end is not None:
+        end.record()
+    return h, (gh, gl), gb

@@ -21,16 +21,29 @@ of the tower's autograd Functions (functional.PatchEmbedFn / ViTLayerFn / ImageP
 Each Function saves the bf16 copies its backward kernels read, so ``CTClipTrainer.train_step``
 runs in this mode too: exact-f32 forward (the SURVEY 8(c) contract on the loss the step
 differentiates), bf16 backward (gradients are not in the tolerance, as for BERT's hi / lo split
-weights).  Cost: DESIGN.md §5.1 and bench.py's ``precise_f32_tower`` entry."""
+weights).  Cost: DESIGN.md §5.1 and bench.py's ``precise_f32_tower`` entry.
+
+``set_vit_precision('split')`` (round 6) keeps that structure but runs every Linear on the split-fp16
+x3 GEMM instead of the f32 MFMA one (gemm256.hip, ctclip_gemm_args.A_lo / B_lo): each operand is an
+fp16 (hi, lo) pair -- hi = fp16(x), lo = fp16(x - hi), ~22 mantissa bits -- written by its producer
+(patch LayerNorm, f32-tap PEG, the LayerNorms, the x3 GEGLU epilogue), and every K-step runs
+Ah Bh + Ah Bl + Al Bh into one f32 accumulator: 3x the fp16 MFMA work instead of f32 MFMA at 1/16 of
+the rate.  tools/vit_precision.py prices it on the CPU restatement (sites 's:' / 'S:'): pre-VQ token error
+1.2e-6 and 0 flips at base size, against 2.8e-6 for the f32 mode.  Cost: bench.py's
+``precise_split_tower`` entry."""
 from __future__ import annotations
 
 _MODE = {'vit': 'bf16'}
 
 
+MODES = ('bf16', 'f32', 'split')
+
+
 def set_vit_precision(mode):
-    """'bf16' (default: bf16 MFMA kernels, forward + backward) or 'f32' (exact-f32 image-tower
-    forward, bf16 backward).  Returns the previous mode."""
-    if mode not in ('bf16', 'f32'):
+    """'bf16' (default: 16-bit MFMA kernels, forward + backward), 'f32' (exact-f32 image-tower
+    forward, bf16 backward) or 'split' (the f32 mode on split-fp16 x3 GEMMs).  Returns the previous
+    mode."""
+    if mode not in MODES:
         raise ValueError(mode)
     old = _MODE['vit']
     _MODE['vit'] = mode

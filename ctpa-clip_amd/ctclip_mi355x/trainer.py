@@ -87,11 +87,40 @@ class FlatParams:
                 p.grad = g
 
 
-class LayerNormExchangeError(RuntimeError):
+class StepGuardError(RuntimeError):
+    """A training step was flagged on the device and NOT applied: the summed step status words
+    (include/ctclip_hip.h CT_STATUS_*) are the Adam kernels' skip guard, so no rank changed its
+    parameters or moments (the gradients were cleared), and the codebook EMA of that step was dropped.
+    ``bits`` holds the (rank-summed) status value.  The status word is sticky: later steps are skipped
+    too until ``kernels.reset_ln_status()``."""
+
+    def __init__(self, msg, bits=0):
+        super().__init__(msg)
+        self.bits = bits
+
+
+class LayerNormExchangeError(StepGuardError):
     """A LayerNorm-fused GEMM (kernels.linear_residual_ln, gemm256.hip EP -6 / -7) gave up waiting for
     its partner tile's row statistics: that step's LayerNorm outputs were wrong.  The step's Adam
     update was not applied (the status word is the Adam kernel's skip guard); later steps are not
     applied either until ``kernels.reset_ln_status()``."""
+
+
+class NonFiniteStepError(StepGuardError):
+    """The step's forward or gradients left the representable range: an fp16 operand copy saturated or
+    was non-finite (CT_STATUS_F16_RANGE, the 16-bit image-tower forward), a token reached the vector
+    quantiser without a finite score (CT_STATUS_VQ_NONFINITE), or the gradient norm was NaN / inf
+    (CT_STATUS_NONFINITE_GRAD).  The reference's fp32 step would have propagated the NaN into every
+    parameter; here no rank applied the step."""
+
+
+_STATUS_NAMES = ((1, 'LayerNorm exchange timeout'), (2, 'fp16 range (saturated / non-finite fp16 operand)'),
+                 (4, 'non-finite gradient norm'), (8, 'non-finite VQ token'))
+
+
+def describe_status(v):
+    """Names of the status bits of a (single-rank) status value."""
+    return ', '.join(n for b, n in _STATUS_NAMES if v & b) or 'none'
 
 
 # queue BERT's backward before the 3D-ViT's (CTCLIP_TEXT_FIRST=0: after it, the r02 order; A/B)
@@ -224,8 +253,11 @@ class CTClipTrainer:
         self.grad_sync.finish()
         self.steps += 1
         skip_word = self.skip_ring[self.steps % 4:self.steps % 4 + 1]
-        skip_word.copy_(self.flat.status != 0.0)          # any rank's exchange timed out -> all skip
-        K.grad_norm(self.flat.grad[:self.flat.numel], self.max_grad_norm if self.max_grad_norm else 0.0, self.norm)
+        # the ranks' summed status words (any rank flagged -> all skip); the norm kernel ORs in a
+        # non-finite gradient (the norm of the all-reduced gradient: the same on every rank)
+        skip_word.copy_(self.flat.status)
+        K.grad_norm(self.flat.grad[:self.flat.numel], self.max_grad_norm if self.max_grad_norm else 0.0, self.norm,
+                    skip=skip_word if self._guard else None)
         # the text bucket's Adam (and grad reset) goes on the text stream: the next step's image
         # tower does not wait for it, the next step's BERT (same stream) does.  It is queued
         # behind the 3D-ViT's Adam (main stream), not beside it: both are HBM-bound, and run side
@@ -303,14 +335,20 @@ class CTClipTrainer:
             elif not ev.query():
                 break
             self._ln_pending.popleft()
-            if int(host[0]) != 0:
+            v = int(host[0])
+            if v != 0:
                 self._ln_pending.clear()
-                raise LayerNormExchangeError(
-                    f'LayerNorm-fused GEMM exchange timed out (status word set by step {step} or earlier, on '
-                    'this rank or another: the ranks\' words are summed with the gradients): its LayerNorm '
-                    'outputs were wrong and the Adam update of that step was skipped on every rank; '
-                    'kernels.reset_ln_status() clears the word (CTCLIP_LN_FUSED=0 runs the unfused GEMM + '
-                    'LayerNorm pair instead)')
+                if v == 1:
+                    raise LayerNormExchangeError(
+                        f'LayerNorm-fused GEMM exchange timed out (status word set by step {step} or earlier, on '
+                        'this rank or another: the ranks\' words are summed with the gradients): its LayerNorm '
+                        'outputs were wrong and the Adam update of that step was skipped on every rank; '
+                        'kernels.reset_ln_status() clears the word (CTCLIP_LN_FUSED=0 runs the unfused GEMM + '
+                        'LayerNorm pair instead)', bits=v)
+                raise NonFiniteStepError(
+                    f'step {step} (or earlier) was flagged on the device, status {v} ({describe_status(v)}; summed '
+                    'over the ranks): its Adam update and codebook EMA were skipped on every rank, parameters and '
+                    'moments unchanged; kernels.reset_ln_status() clears the sticky word', bits=v)
             self.ln_steps_checked = step
 
     def _adam(self, off, n, step=None):

@@ -24,7 +24,21 @@ extern "C" {
 #endif
 
 /* ---------------------------------------------------------------- version / probe */
-int ctclip_version(void);          /* ABI version */
+/* ABI version: bumped whenever a public struct changes layout (round 6: 2 -- ctclip_gemm_args gained
+ * A_lo / B_lo / C3 / C4, and the round-5 trailing fields ab_f16 / r_f16, ctclip_ln_epilogue.Y16,
+ * ctclip_attn_args.o16 now count as part of version 2).  A binding must check ctclip_version() ==
+ * CTCLIP_ABI_VERSION before passing any struct: a binding built against an older header passes a
+ * shorter struct, and the library would read its missing trailing fields from the caller's stack. */
+#define CTCLIP_ABI_VERSION 2
+/* Bits of the step status word (an int32 the caller owns; sticky, never cleared by the library):
+ * the kernels that take a `status` pointer OR their bit in when they see the condition.  The
+ * trainer sums the ranks' words with the last gradient bucket and passes the result to ctclip_adam
+ * as its skip guard, so a step with any bit set is applied by no rank, then raises on the host. */
+#define CT_STATUS_LN_TIMEOUT 1       /* a LayerNorm-fused GEMM's partner statistics never arrived */
+#define CT_STATUS_F16_RANGE 2        /* a value stored as fp16 was non-finite or beyond +-65504 */
+#define CT_STATUS_NONFINITE_GRAD 4   /* the gradient norm (ctclip_grad_norm) is not finite */
+#define CT_STATUS_VQ_NONFINITE 8     /* a VQ token had no finite codebook score */
+int ctclip_version(void);          /* returns CTCLIP_ABI_VERSION */
 int ctclip_device_arch(char* buf, int n); /* writes gcnArchName of the current device */
 /* test knob: nwg workgroups, each holding lds_bytes of a CU's LDS, spin for `cycles` shader clocks on
  * `stream` (a stand-in for resident RCCL kernels occupying CUs beside a persistent GEMM) */
@@ -75,6 +89,18 @@ typedef struct {
                                      * than bf16 at the same MFMA rate).  With act 2 the h output
                                      * C is fp16 too and g is computed from the fp16-rounded h */
   int32_t r_f16;                    /* act 4: R (h) is fp16 (written by an ab_f16 act-2 GEMM) */
+  /* split-fp16 "x3" operands (round 6, ab_f16 required; K % 64 == 0, both K-contiguous, no bias-free
+   * restrictions beyond act 0 / 2): A_lo / B_lo are the fp16 residual images of A / B (same ld), e.g.
+   * A = fp16(x), A_lo = fp16(x - A), so the GEMM reads x to ~22 mantissa bits; every K-step runs
+   * A.B + A.B_lo + A_lo.B into one f32 accumulator (3x the fp16 MFMA work) -- the f32-equivalent
+   * image-tower forward of precise.set_vit_precision('split').  act 0: C f32 (c_f32 = 1) with
+   * optional bias, f32 residual R and bf16 copy C2.  act 2 (GEGLU): C = h (fp16), g = gelu(gate) x
+   * from the unrounded f32 h written as the fp16 pair C2 (hi, ldc2) / C3 (lo, ldc3) and, when C4 is
+   * given, as bf16 C4 (ldc4).  Both NULL: an ordinary GEMM. */
+  const void* A_lo;
+  const void* B_lo;
+  void* C3; int64_t ldc3;
+  void* C4; int64_t ldc4;
 } ctclip_gemm_args;
 int ctclip_gemm(const ctclip_gemm_args* a, void* stream);
 /* diagnostic: large-tile kernel variant (8 = 8-phase 256x256x64 default, 1 = 128x256x32,
@@ -264,6 +290,12 @@ int ctclip_gemm_mxfp8_set_tile(int bm);
 int ctclip_layernorm_fwd_x2(const void* x, int32_t x_f32, int64_t ldx, int64_t rows, int32_t D, const float* gamma,
                             const float* beta, float eps, void* y_bf16, void* y_f16, int64_t ldyb, float* y_f32,
                             int64_t ldyf, float* mean, float* rstd, void* stream);
+/* ... with, beside y_f16, its lo residual y_f16lo = fp16(y - y_f16) (the split-fp16 x3 GEMM's A pair,
+ * round 6; y_f16 required) and the fp16 range check: an fp16 output beyond +-65504 or non-finite
+ * sets CT_STATUS_F16_RANGE in *status (optional) */
+int ctclip_layernorm_fwd_x3(const void* x, int32_t x_f32, int64_t ldx, int64_t rows, int32_t D, const float* gamma,
+                            const float* beta, float eps, void* y_bf16, void* y_f16, void* y_f16lo, int64_t ldyb,
+                            float* y_f32, int64_t ldyf, float* mean, float* rstd, int32_t* status, void* stream);
 int ctclip_layernorm_fwd(const void* x, int32_t x_f32, int64_t ldx, int64_t rows, int32_t D,
                          const float* gamma, const float* beta, float eps,
                          void* y_bf16, int64_t ldyb, float* y_f32, int64_t ldyf,
@@ -338,6 +370,11 @@ int ctclip_patch_ln(const void* video, int32_t is_f32, int32_t is_hu, int64_t B,
 int ctclip_patch_ln_x2(const void* video, int32_t is_f32, int32_t is_hu, int64_t B, int32_t C, int32_t F,
                        int32_t H, int32_t W, int32_t PT, int32_t P, const int32_t* offs, float eps,
                        void* xhat, void* xhat16, int64_t ldo, void* stream);
+/* ... and, with xhat16, its lo residual xhat16lo = fp16(xhat - xhat16) (same ldo): the split-fp16
+ * patch-embed GEMM's A pair (round 6, precise 'split' mode) */
+int ctclip_patch_ln_x3(const void* video, int32_t is_f32, int32_t is_hu, int64_t B, int32_t C, int32_t F,
+                       int32_t H, int32_t W, int32_t PT, int32_t P, const int32_t* offs, float eps,
+                       void* xhat, void* xhat16, void* xhat16lo, int64_t ldo, void* stream);
 int ctclip_patch_wgrad(const float* G, const float* colsum_dy, const float* W, const float* gamma,
                        const float* beta, int32_t N, int32_t K, float* dW, float* dgamma, float* dbeta,
                        int32_t accumulate, void* stream);
@@ -370,6 +407,12 @@ int ctclip_peg_fwd_stats(const void* x_bf16, const float* x_f32, int64_t B, int3
 int ctclip_peg_fwd_x32(const float* x_f32, int64_t B, int32_t T, int32_t H, int32_t W, int32_t D,
                        const float* weight, const float* bias, int32_t mode, float* out_f32, void* out_bf16,
                        void* out_f16, float* stats, void* stream);
+/* ... with, beside out_f16, its lo residual out_f16lo = fp16(out - out_f16) (the split-fp16 x3 Q | K | V
+ * GEMM's A pair, round 6; out_f16 required) and the fp16 range check: an fp16 output beyond +-65504
+ * or non-finite sets CT_STATUS_F16_RANGE in *status (optional) */
+int ctclip_peg_fwd_x32s(const float* x_f32, int64_t B, int32_t T, int32_t H, int32_t W, int32_t D,
+                        const float* weight, const float* bias, int32_t mode, float* out_f32, void* out_bf16,
+                        void* out_f16, void* out_f16lo, float* stats, int32_t* status, void* stream);
 /* dx = dout + conv^T(dout) from the f32 dout alone (the conv taps in f32; no bf16 dout read): the x32
  * kernel's transposed form, fixed 24^3 grids (returns CT_ESHAPE otherwise: use ctclip_peg_bwd_data).
  * ct_clip/attention.py:56-84 backward. */
@@ -478,6 +521,19 @@ int ctclip_sgemm_tn(const ctclip_sgemm_tn_args* a, void* stream);
 /* fp16 working weights of the fp16 forward GEMMs, as ctclip_pack_rows (round 5) */
 int ctclip_pack_rows_h16(const float* src, int64_t ld_src, const int32_t* map, int64_t rows_dst, int32_t cols,
                          int32_t cols_dst, const float* colscale, void* dst, int64_t ld_dst, void* stream);
+/* split-fp16 operands of the x3 GEMM (ctclip_gemm_args.A_lo / B_lo; precise.set_vit_precision('split'),
+ * round 6): hi = fp16(v scale), lo = fp16(v scale - hi) of every f32 value v, so hi + lo carries v
+ * to ~22 mantissa bits (the dropped remainder is < 2^-22 |v| for |v scale| in [2^-3, 65504]; smaller
+ * values keep an absolute 2^-25 / scale).  A value outside fp16's range after scaling sets
+ * CT_STATUS_F16_RANGE in *status (optional).  The weights are scaled by 256 (the GEMM's alpha undoes
+ * it, exactly: a power of two) so their ~1e-2 entries keep a normal lo part.
+ *   split_f16: x [rows][cols] (ldx, f32, cols % 8 == 0) -> hi / lo [rows][cols] (ldo);
+ *   pack_rows_x3: ctclip_pack_rows (row map, column scale, zero padding) into the pair. */
+int ctclip_split_f16(const float* x, int64_t ldx, int64_t rows, int32_t cols, float scale, void* hi, void* lo,
+                     int64_t ldo, int32_t* status, void* stream);
+int ctclip_pack_rows_x3(const float* src, int64_t ld_src, const int32_t* map, int64_t rows_dst, int32_t cols,
+                        int32_t cols_dst, const float* colscale, float scale, void* hi, void* lo, int64_t ld_dst,
+                        int32_t* status, void* stream);
 /* f32 working weights: dst[r][c] = src[map[r]][c] * colscale[c] (zero pads), as ctclip_pack_rows */
 int ctclip_pack_rows_f32(const float* src, int64_t ld_src, const int32_t* map, int64_t rows_dst, int32_t cols,
                          int32_t cols_dst, const float* colscale, float* dst, int64_t ld_dst, void* stream);
@@ -492,6 +548,11 @@ int ctclip_pack_rows_f32(const float* src, int64_t ld_src, const int32_t* map, i
  * bound, see vq.hip).  cand2 = NULL re-scores group winners only.  D % 4 == 0, D <= 4096. */
 int ctclip_vq_select(const float* cand, const float* cand2, int32_t ntiles, const float* x, int64_t rows, int32_t D,
                      const float* codebook, int32_t C, float margin, int32_t* idx, float* xn_out, void* stream);
+/* ... with the step status word: a row without any finite score (NaN / inf token) gets idx 0 and a
+ * zero xn row as above AND sets CT_STATUS_VQ_NONFINITE in *status (round 6) */
+int ctclip_vq_select_s(const float* cand, const float* cand2, int32_t ntiles, const float* x, int64_t rows, int32_t D,
+                       const float* codebook, int32_t C, float margin, int32_t* idx, float* xn_out, int32_t* status,
+                       void* stream);
 /* pooled[b][hw][:] = mean_t codebook[idx[b][t*HW+hw]]   (ct_clip/ct_clip.py:724,740) */
 int ctclip_vq_pool(const int32_t* idx, const float* codebook, int64_t B, int32_t T, int32_t HW, int32_t D,
                    float* out, void* out_bf16, void* stream);
@@ -516,6 +577,11 @@ int ctclip_vq_ema_finalize(const float* bins, const int64_t* esum, int32_t C, in
  * buffers are ready for the next step's ctclip_vq_ema_accum (no fill launches). */
 int ctclip_vq_ema_finalize_reset(float* bins, int64_t* esum, int32_t C, int32_t D, float decay, float* embed,
                                  float* cluster_size, void* embed_bf16, void* stream);
+/* ... guarded (round 6): when *guard != 0 (the summed step status words, carried through the
+ * statistics' all-reduce in the slot after the bins) the step's update is dropped on every rank --
+ * embed / cluster_size untouched -- and only the statistics are zeroed.  guard NULL: unguarded. */
+int ctclip_vq_ema_finalize_guard(float* bins, int64_t* esum, int32_t C, int32_t D, float decay, float* embed,
+                                 float* cluster_size, void* embed_bf16, const float* guard, void* stream);
 
 /* ---------------------------------------------------------------- contrastive loss
  * symmetric InfoNCE over the (global) batch, ct_clip/ct_clip.py:771,796,845-901; one workgroup.
@@ -560,6 +626,10 @@ int ctclip_embed_bwd(const int64_t* ids, int64_t B, int32_t L, int32_t Hd, const
  * the LayerNorm-fused GEMM status of ctclip_gemm_ln).
  * p, g, m, v must share one alignment modulo 16 B (slices of arenas with one layout): CT_EALIGN. */
 int ctclip_grad_norm(const float* g, int64_t n, float max_norm, float* part, int32_t nblk, float* out, void* stream);
+/* ... and a non-finite norm ORs CT_STATUS_NONFINITE_GRAD into *skip (the Adam kernels' guard word of
+ * the step, round 6): a NaN / inf gradient never reaches the parameters or the moments */
+int ctclip_grad_norm_s(const float* g, int64_t n, float max_norm, float* part, int32_t nblk, float* out, int32_t* skip,
+                       void* stream);
 int ctclip_adam(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
                 float wd, int32_t step, const float* coef, void* p_bf16, void* p_bf16_lo, int32_t zero_grad,
                 const int32_t* skip, void* stream);   /* p_bf16_lo (needs p_bf16): bf16(p - bf16(p)), the

@@ -370,6 +370,33 @@ def test_state_dict_after_deferred_adam_is_current(setup):
     assert moved > 0
 
 
+def test_load_after_train_step_keeps_checkpoint_codebook(setup, tmp_path):
+    """the codebook EMA of a train_step runs on the auxiliary stream after the optimizer
+    step (ct_clip.DEFER_EMA '2').  A checkpoint loaded right after the step -- no synchronize -- must
+    end with exactly the checkpoint's codebook (the load joins the EMA first and drops a pending
+    one), and a state_dict taken right after a step holds the updated codebook."""
+    cfg, _, hu, ids, mask, text = setup
+    from ctclip_mi355x.trainer import CTClipTrainer
+    torch.manual_seed(0)
+    model = build(cfg)
+    ck = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    path = tmp_path / 'ck.pt'
+    torch.save(ck, str(path))
+    tr = CTClipTrainer(model, lr=1e-4)
+    cbk = model.visual_transformer.vq._codebook
+    for _ in range(2):
+        tr.train_step(text, hu.cuda())
+        model.load(str(path))                     # no synchronize in between
+        torch.cuda.synchronize()
+        assert torch.equal(cbk.embed.cpu(), ck['visual_transformer.vq._codebook.embed'])
+        assert torch.equal(cbk.cluster_size.cpu(), ck['visual_transformer.vq._codebook.cluster_size'])
+    tr.train_step(text, hu.cuda())
+    snap = model.state_dict()['visual_transformer.vq._codebook.embed'].clone()   # queued, no sync
+    torch.cuda.synchronize()
+    assert torch.equal(snap, cbk.embed)
+    assert not torch.equal(snap.cpu(), ck['visual_transformer.vq._codebook.embed'])
+
+
 def test_train_step_bit_reproducible():
     """Two runs of three training steps from the same seed give bit-identical losses, parameters,
     Adam moments, VQ codebook and cluster sizes, BERT dropout on, ragged reports (pad ids): no

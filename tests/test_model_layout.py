@@ -65,7 +65,7 @@ def test_cabi_exports_every_declared_symbol():
     assert not missing, missing
     # every declared symbol has a ctypes signature on the Python side
     assert not [n for n in names if n not in _lib._SIGS]
-    assert lib.ctclip_version() == 1
+    assert lib.ctclip_version() == 2
 
 
 def test_product_has_no_cpu_fallback():

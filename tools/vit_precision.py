@@ -42,15 +42,27 @@ def h(t):
     return t.half().float()
 
 
+def sp(t, scale=1.0):
+    """split-fp16 image: hi + lo, hi = fp16(t s), lo = fp16(t s - hi) (the x3 GEMM operands)"""
+    ts = t * scale
+    hi = ts.half().float()
+    return (hi + (ts - hi).half().float()) / scale
+
+
 def rs(t, S, site):
-    """site rounded as bf16 ('site'), as fp16 ('h:site') or not at all"""
+    """site rounded as bf16 ('site'), as fp16 ('h:site'), as a split-fp16 pair ('s:site'; 'S:site'
+    with the operand scaled by 2^8 first, as the x3 GEMM's weight images) or not at all"""
     if 'h:' + site in S:
         return h(t)
+    if 's:' + site in S:
+        return sp(t)
+    if 'S:' + site in S:
+        return sp(t, 256.0)
     return r(t) if site in S else t
 
 
 def lin(x, w, S, site='w', name=None):
-    if name is not None and ('w:' + name in S or 'h:w:' + name in S):
+    if name is not None and any(m + 'w:' + name in S for m in ('', 'h:', 's:', 'S:')):
         return F.linear(x, rs(w, S, 'w:' + name))
     return F.linear(x, rs(w, S, site))
 
@@ -76,7 +88,7 @@ def attn(p, x1, S, bias, heads=8, dh=32):
     xa = R(x1, 'x1b')
     if 'fold' in S:
         Wp = g * Wq
-        Wp = rs(Wp, S, 'w:q' if ('w:q' in S or 'h:w:q' in S) else 'w')
+        Wp = rs(Wp, S, 'w:q' if any(m + 'w:q' in S for m in ('', 'h:', 's:', 'S:')) else 'w')
         mean = x1.mean(-1, keepdim=True)
         rstd = torch.rsqrt(x1.var(-1, unbiased=False, keepdim=True) + 1e-5)
         q = rstd * (xa @ Wp.t() - mean * Wp.sum(1))
