@@ -562,7 +562,7 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
         for (int d = 0; d < DB; ++d) {
           const float o4[4] = {o[u][d][0] * inv, o[u][d][1] * inv, o[u][d][2] * inv, o[u][d][3] * inv};
           const int64_t off = qrow[u] * p.ldout + h * D + d * 16 + 4 * g;
-          *(uint2*)(p.out + off) = pack4(o4);
+          if (p.out) *(uint2*)(p.out + off) = pack4(o4);   // (bf16 O optional: eval forward, round 6)
           if (p.out16) *(uint2*)(p.out16 + off) = pack4h(o4);
         }
         // natural-log LSE: ln(sum exp(x)) = (m2 + log2(lsum)) * ln 2
@@ -1869,7 +1869,7 @@ __global__ __launch_bounds__(SW * 64) void attn_small_fwd_kernel(AP p) {
       if (p.out16) hb[qb] = pack8h(o8);
     } else if (R.ok[qb]) {
       const uint64_t off = roff(R.row[qb], p.ldout) + h * 32 + 8 * g;
-      *(u32x4*)(p.out + off) = pack8(o8);
+      if (p.out) *(u32x4*)(p.out + off) = pack8(o8);
       if (p.out16) *(u32x4*)(p.out16 + off) = pack8h(o8);
     }
     if (g == 0 && R.ok[qb] && p.lse) p.lse[(int64_t)h * p.M + R.row[qb]] = (m + __log2f(l)) * LN2;
@@ -1886,7 +1886,7 @@ __global__ __launch_bounds__(SW * 64) void attn_small_fwd_kernel(AP p) {
       if (p.out16) *(u32x4*)(t1 + row * SRS + w * 64 + g * 16) = hb[qb];
     }
     __syncthreads();
-    coop_store_rows(p.out, p.ldout, t0, p, s, h - w);
+    if (p.out) coop_store_rows(p.out, p.ldout, t0, p, s, h - w);
     if (p.out16) coop_store_rows(p.out16, p.ldout, t1, p, s, h - w);
   }
 }

@@ -80,6 +80,7 @@ struct P {
   u16* C3; int64_t ldc3;
   u16* C4; int64_t ldc4;
   int x3;
+  int c_col0;    // EP 6 / 8: first C column stored (ctclip_gemm_qkv_lnfold2; 0 = all)
 };
 
 __device__ __forceinline__ int mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
@@ -835,7 +836,8 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) qb[j][r] = bf2f(f2bf(v[j][r]));
-      store_row_bf16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N);
+      // (EP 8: columns below c_col0 -- q, k in the eval forward, round 6 -- only feed the l2norm)
+      store_row_bf16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok && wcol0 >= p.c_col0, wcol0, p.N);
       if (wcol0 < p.n2) {
         const int d0 = pair_coff(g);
         const float* sp = p.bias + d0 + (MODE == 8 && !fold ? 32 : 0);   // EP 8: the second scale set
@@ -923,7 +925,8 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
       }
       // fp16 kernel: h stored as fp16, g from the fp16-rounded h (the backward recomputes g' from
       // the stored h); bf16 kernel: both in bf16
-      if constexpr (H16) store_row_f16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N);
+      // (h may be discarded, C = NULL: the eval forward needs only g, round 6)
+      if constexpr (H16) store_row_f16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok && p.C, wcol0, p.N);
       else store_row_bf16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N, p.epi_lds == 3);
       float gg[2][4];
 #pragma unroll
@@ -1328,7 +1331,7 @@ __device__ __forceinline__ void epilogue_ln(const P& p, f32x4 (&acc)[8][4], char
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = (keep[quarter][it][j] - f.x) * f.y * gam[j] + bet[j];
-        *(u32x4*)(p.ln_y + (rbase + it * 8 + rl) * p.ln_ldy + gn) = pack8(o);
+        if (p.ln_y) *(u32x4*)(p.ln_y + (rbase + it * 8 + rl) * p.ln_ldy + gn) = pack8(o);
         if (p.ln_y16) *(u32x4*)(p.ln_y16 + (rbase + it * 8 + rl) * p.ln_ldy + gn) = pack8h(o);
       }
     } else {
@@ -1889,7 +1892,8 @@ extern "C" int ctclip_gemm_ln(const ctclip_gemm_args* a, const ctclip_ln_epilogu
     CT_REQUIRE(a->M * ldmax < ((int64_t)1 << 31), CT_ESHAPE);   // 32-bit element offsets (mode 2)
   }
   if (ln->mode == 1) {
-    CT_REQUIRE(a->R && ln->Y && aligned16(ln->Y) && ln->ldy % 8 == 0, CT_EINVAL);
+    // Y (bf16) may be NULL when the fp16 copy Y16 is given: the eval forward (round 6)
+    CT_REQUIRE(a->R && (ln->Y || ln->Y16) && aligned16(ln->Y) && aligned16(ln->Y16) && ln->ldy % 8 == 0, CT_EINVAL);
     if (ln->beta) CT_REQUIRE(aligned16(ln->beta), CT_EALIGN);
   } else {
     CT_REQUIRE(ln->X && aligned16(ln->X) && ln->ldx % 8 == 0 && ln->part_gamma && !ln->beta && a->C2 && a->R,
@@ -1939,7 +1943,13 @@ extern "C" int ctclip_gemm_ln(const ctclip_gemm_args* a, const ctclip_ln_epilogu
 // output never exists; both l2norms ride in the epilogue as in act 5.
 extern "C" int ctclip_gemm_qkv_lnfold(const ctclip_gemm_args* a, const float* mean, const float* rstd,
                                       const float* fold_cs, int32_t nfold, void* stream) {
+  return ctclip_gemm_qkv_lnfold2(a, mean, rstd, fold_cs, nfold, 0, stream);
+}
+
+extern "C" int ctclip_gemm_qkv_lnfold2(const ctclip_gemm_args* a, const float* mean, const float* rstd,
+                                       const float* fold_cs, int32_t nfold, int32_t c_col0, void* stream) {
   using namespace g256;
+  if (c_col0 < 0 || c_col0 % 64) return CT_EINVAL;
   if (!a || !mean || !rstd || !fold_cs) return CT_EINVAL;
   if (a->M == 0) return 0;
   CT_REQUIRE(a->M > 0 && a->N % 256 == 0 && a->K > 0 && a->K % 64 == 0, CT_ESHAPE);
@@ -1974,6 +1984,7 @@ extern "C" int ctclip_gemm_qkv_lnfold(const ctclip_gemm_args* a, const float* me
   p.ln_rstd = (float*)rstd;
   p.fold_cs = fold_cs;
   p.nfold = nfold;
+  p.c_col0 = c_col0;
   if (a->ab_f16) return launch8<true, true, 8, true>(p, 1, (hipStream_t)stream);
   return launch8<true, true, 8>(p, 1, (hipStream_t)stream);
 }

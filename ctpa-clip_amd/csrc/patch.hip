@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void patch_ln_kernel(const void* __restrict__ 
     if (e < pd) { const float d = v[i] - mean; q += d * d; }
   }
   const float rstd = rsqrtf(warp_sum(q) / pd + eps);
-  u16* o = out + tok * ldo;
+  u16* o = out ? out + tok * ldo : nullptr;   // (bf16 xhat optional with out16: the eval forward)
   u16* oh = out16 ? out16 + tok * ldo : nullptr;
   u16* ol = out16lo ? out16lo + tok * ldo : nullptr;
 #pragma unroll
@@ -65,13 +65,13 @@ __global__ __launch_bounds__(256) void patch_ln_kernel(const void* __restrict__ 
     const int e = lane + 64 * i;
     if (e < pd) {
       const float a = (v[i] - mean) * rstd;
-      o[e] = f2bf(a);
+      if (o) o[e] = f2bf(a);
       if (oh) oh[e] = f2h(a);
       if (ol) ol[e] = f2h(a - rh(a));
     }
   }
   for (int e = pd + lane; e < ldo; e += 64) {   // K padding of the patch-embed GEMM
-    o[e] = 0;
+    if (o) o[e] = 0;
     if (oh) oh[e] = 0;
     if (ol) ol[e] = 0;
   }
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(256) void patch_ln_strip_kernel(const void* __restr
   }
   const float rstd = rsqrtf(warp_sum(q) / pd + eps);
   const int64_t tok = (((int64_t)b * T + t) * Hg + hg) * Wg + wg0 + w;
-  uint32_t* o = (uint32_t*)(out + tok * ldo);
+  uint32_t* o = out ? (uint32_t*)(out + tok * ldo) : nullptr;       // (optional with out16: eval forward)
   uint32_t* oh = out16 ? (uint32_t*)(out16 + tok * ldo) : nullptr;   // optional fp16 copy
   uint32_t* ol = out16lo ? (uint32_t*)(out16lo + tok * ldo) : nullptr;   // ... and its lo residual (x3)
 #pragma unroll
@@ -178,13 +178,13 @@ __global__ __launch_bounds__(256) void patch_ln_strip_kernel(const void* __restr
     const int e = 2 * (lane + 64 * i);
     if (e < pd) {
       const float a = (v[i][0] - mean) * rstd, c = (v[i][1] - mean) * rstd;
-      o[e >> 1] = (uint32_t)f2bf(a) | ((uint32_t)f2bf(c) << 16);
+      if (o) o[e >> 1] = (uint32_t)f2bf(a) | ((uint32_t)f2bf(c) << 16);
       if (oh) oh[e >> 1] = pack2h(a, c);
       if (ol) ol[e >> 1] = pack2h(a - rh(a), c - rh(c));
     }
   }
   for (int e = pd + 2 * lane; e < ldo; e += 128) {   // K padding of the patch-embed GEMM
-    o[e >> 1] = 0u;
+    if (o) o[e >> 1] = 0u;
     if (oh) oh[e >> 1] = 0u;
     if (ol) ol[e >> 1] = 0u;
   }
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(256) void patch_ln_strip20_kernel(const void* __res
   }
   const float rstd = rsqrtf(warp_sum(q) / pd + eps);
   const int64_t tok = (((int64_t)b * T + t) * Hg + hg) * Wg + wg0 + w;
-  uint32_t* o = (uint32_t*)(out + tok * ldo);
+  uint32_t* o = out ? (uint32_t*)(out + tok * ldo) : nullptr;       // (optional with out16: eval forward)
   uint32_t* oh = out16 ? (uint32_t*)(out16 + tok * ldo) : nullptr;   // optional fp16 copy
   uint32_t* ol = out16lo ? (uint32_t*)(out16lo + tok * ldo) : nullptr;   // ... and its lo residual (x3)
 #pragma unroll
@@ -304,13 +304,13 @@ __global__ __launch_bounds__(256) void patch_ln_strip20_kernel(const void* __res
     const int e = 2 * (lane + 64 * i);
     if (e < pd) {
       const float a = (v[i][0] - mean) * rstd, c = (v[i][1] - mean) * rstd;
-      o[e >> 1] = (uint32_t)f2bf(a) | ((uint32_t)f2bf(c) << 16);
+      if (o) o[e >> 1] = (uint32_t)f2bf(a) | ((uint32_t)f2bf(c) << 16);
       if (oh) oh[e >> 1] = pack2h(a, c);
       if (ol) ol[e >> 1] = pack2h(a - rh(a), c - rh(c));
     }
   }
   for (int e = pd + 2 * lane; e < ldo; e += 128) {   // K padding of the patch-embed GEMM
-    o[e >> 1] = 0u;
+    if (o) o[e >> 1] = 0u;
     if (oh) oh[e >> 1] = 0u;
     if (ol) ol[e >> 1] = 0u;
   }
@@ -451,7 +451,7 @@ extern "C" int ctclip_patch_ln_x2(const void* video, int32_t is_f32, int32_t is_
 extern "C" int ctclip_patch_ln_x3(const void* video, int32_t is_f32, int32_t is_hu, int64_t B, int32_t C, int32_t F,
                                   int32_t H, int32_t W, int32_t PT, int32_t P, const int32_t* offs, float eps,
                                   void* out, void* out16, void* out16lo, int64_t ldo, void* stream) {
-  if (out16lo && !out16) return CT_EINVAL;
+  if ((out16lo || !out) && !out16) return CT_EINVAL;
   const int pd = C * PT * P * P;
   CT_REQUIRE(pd <= 64 * MAXC, CT_ESHAPE);
   if (ldo <= 0) ldo = pd;

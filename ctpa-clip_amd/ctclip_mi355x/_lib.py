@@ -134,6 +134,7 @@ _SIGS = {
     'ctclip_gemm': [ctypes.POINTER(GemmArgs), c_vp],
     'ctclip_gemm_ln': [ctypes.POINTER(GemmArgs), ctypes.POINTER(LnEpilogueArgs), c_vp],
     'ctclip_gemm_qkv_lnfold': [ctypes.POINTER(GemmArgs), c_vp, c_vp, c_vp, c_i32, c_vp],
+    'ctclip_gemm_qkv_lnfold2': [ctypes.POINTER(GemmArgs), c_vp, c_vp, c_vp, c_i32, c_i32, c_vp],
     'ctclip_pack_qkv_fold': [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp,
                              c_i32, c_vp, c_vp],
     'ctclip_ln_stats_merge': [c_vp, c_i32, c_i64, c_i32, c_f32, c_vp, c_vp, c_vp],

@@ -426,10 +426,12 @@ class PatchEmbedFn(torch.autograd.Function):
         kp = (pd + 63) // 64 * 64                                      # K padded to the 64-deep GEMM step
         split = precise_split()
         f16 = vit_f16() and not precise_f32() and not vit_fp8() and not split
-        xhat_p = K.patch_ln(video, is_hu, PT, P, offs, ld=kp, want_f16=f16, want_x3=split)   # [M, kp], 0 pads
+        lean = f16 and not any(ctx.needs_input_grad)      # eval forward: no bf16 xhat (backward only)
+        xhat_p = K.patch_ln(video, is_hu, PT, P, offs, ld=kp, want_f16=f16, want_x3=split,
+                            want_bf16=not lean)                                             # [M, kp], 0 pads
         if f16 or split:
             xhat_p, xhat16 = xhat_p      # bf16 (the weight gradient's operand) and fp16 (pair) (the GEMM's)
-        xhat = xhat_p[:, :pd]
+        xhat = xhat_p[:, :pd] if xhat_p is not None else None
         if split:
             # split-fp16 tower: the LayerNorm(4000) affine folded into the Linear in f32 (W diag(g),
             # b + W beta), then the x3 GEMM on the LayerNorm'd patches' fp16 pair
@@ -452,6 +454,9 @@ class PatchEmbedFn(torch.autograd.Function):
                 Wp = K.pack_rows(W, W.shape[0], kp, colscale=ln1_w)    # bf16 [D, kp], zero pad columns
                 y1 = K.linear(xhat_p, Wp, bias=bp, out_dtype=F32)       # [M, D]
         yb, yf, mean, rstd = K.layernorm_fwd(y1, ln2_w, ln2_b, 1e-5, out_bf16=True, out_f32=True)
+        if lean:
+            ctx.mark_non_differentiable(yb)
+            return yf, yb
         ctx.save_for_backward(xhat, y1, mean, rstd, ln1_w, ln1_b, W, ln2_w)
         ctx.b, ctx.ln2_w, ctx.ln2_b = b, ln2_w, ln2_b
         ctx.mark_non_differentiable(yb)
@@ -617,9 +622,14 @@ class ViTLayerFn(torch.autograd.Function):
                 and dim <= 1024 and geo.Wg <= 24 and Wkv.shape[0] == 2 * inner)
         # fp16 forward GEMMs (vit_f16): the folded Q | K | V projection, to_out, FF1
         f16 = vit_f16() and fold and _PEG_X32
+        # eval forward (round 6; no input needs a gradient, e.g. zero-shot inference under no_grad, the
+        # VisionFeatureExtractor): none of the tensors only the backward reads is written -- the bf16
+        # copies of x1, x2, LN(x2), O, the raw q / k, the attention LSE and FF1's h (~1.3 GB per layer
+        # at B = 8)
+        lean = f16 and not fp8 and not any(ctx.needs_input_grad)
         if _PEG_X32:
             x1f, x1b, x1h, m1, r1 = K.peg_fwd_x32(xf.detach().contiguous(), geo.B, geo.T, geo.Hg, geo.Wg, peg_w,
-                                                  peg_b, geo.mode, stats=fold, want_f16=f16)
+                                                  peg_b, geo.mode, stats=fold, want_f16=f16, want_bf16=not lean)
         elif fold:
             x1f, x1b, m1, r1 = K.peg_fwd_stats(xb, xf, geo.B, geo.T, geo.Hg, geo.Wg, peg_w, peg_b, geo.mode)
         else:
@@ -632,7 +642,8 @@ class ViTLayerFn(torch.autograd.Function):
             Wp, cs, scales = qkv_fold_pack(Wq, norm_g, Wkv, Wkv_b, q_scale, k_scale)
             if f16:
                 Wp16, cs16 = qkv_fold_pack_h16(Wq, norm_g, Wkv, q_scale, k_scale)
-                qkv, qkn = K.linear_qkv_lnfold(x1h, Wp16, cs16, m1, r1, scales, inner, 2 * inner)
+                qkv, qkn = K.linear_qkv_lnfold(x1h, Wp16, cs16, m1, r1, scales, inner, 2 * inner,
+                                               c_col0=2 * inner if lean else 0)
                 del x1h, Wp16
             else:
                 qkv, qkn = K.linear_qkv_lnfold(x1b, Wp, cs, m1, r1, scales, inner, 2 * inner)
@@ -659,25 +670,25 @@ class ViTLayerFn(torch.autograd.Function):
         streams.mark_image_head(xf.device, 'attn')   # deferred text-stream work may start (streams.py)
         att = K.attn_fwd(qn, kn, kv[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
                          bias_u=bias_u if use_bias else None, grid=(geo.Hg, geo.Wg) if use_bias else (0, 0),
-                         want_o16=f16)
+                         want_o16=f16, eval_only=lean)
         o, lse = att[0], att[1]
         o_in, Wo_in = (att[2], h16(Wo)) if f16 else (o, Wo_b)   # to_out's operands
         # to_out + residual + the FeedForward's LayerNorm in one launch (gemm256.hip, EP -6) -- only
         # where a caller checks the launch's status word every step (kernels.ln_guard: the trainer)
         fused = None if fp8 or not K.ln_guarded() else K.linear_residual_ln(o_in, Wo_in, x1f, ff_w, ff_b, 1e-5,
-                                                                            y16=f16)
+                                                                            y16=f16, eval_only=lean)
         xn2h = None
         if fused is not None:
             x2f, x2b, xn2, m2, r2 = fused[:5]
             if f16:
                 xn2h = fused[5]
         else:
-            x2b = torch.empty_like(xb)
+            x2b = None if lean else torch.empty_like(xb)
             if fp8:
                 x2f = fp8_linear(o, Wo, 'o', Wo_b, residual=x1f, out_f32=True, out2=x2b)
             else:
                 x2f = K.linear(o_in, Wo_in, residual=x1f, out_dtype=F32, out2=x2b)
-            lnr = K.layernorm_fwd(x2f, ff_w, ff_b, 1e-5, out_f16=f16)
+            lnr = K.layernorm_fwd(x2f, ff_w, ff_b, 1e-5, out_f16=f16, out_bf16=not lean)
             xn2, _, m2, r2 = lnr[:4]
             if f16:
                 xn2h = lnr[4]
@@ -691,7 +702,7 @@ class ViTLayerFn(torch.autograd.Function):
         elif f16:
             # fp16 FF1: h stored in fp16 (read by the GEGLU backward), g (bf16) from the fp16 h
             h = K.linear(xn2h, pack_ff1_h16(W1), act=K.ACT_GEGLU, out2=g, out_dtype=K.F16, tag='ff1',
-                         flops=2.0 * xf.shape[0] * W1.shape[0] * W1.shape[1])
+                         flops=2.0 * xf.shape[0] * W1.shape[0] * W1.shape[1], discard_out=lean)
             del xn2h
             x3f = K.linear(g, W2p, residual=x2f, out_dtype=F32, out2=x3b)
         else:
@@ -699,6 +710,9 @@ class ViTLayerFn(torch.autograd.Function):
             h = K.linear(xn2, W1p, act=K.ACT_GEGLU, out2=g, tag='ff1',
                          flops=2.0 * xf.shape[0] * W1.shape[0] * W1.shape[1])
             x3f = K.linear(g, W2p, residual=x2f, out_dtype=F32, out2=x3b)
+        if lean:
+            ctx.mark_non_differentiable(x3b)
+            return x3f, x3b
         ctx.geo = geo
         ctx.use_bias = use_bias
         ctx.fold = fold

@@ -137,13 +137,29 @@ def _auto_split(M, N, K, act, split_k, batch, accumulate, C):
 
 
 def linear(x, w, *, bias=None, residual=None, out=None, out_dtype=BF16, act=ACT_NONE, out2=None, alpha=1.0,
-           accumulate=False, tag=None, flops=None, l2n_scale=None, l2n_cols=0, w_lo=None, dropout=None):
+           accumulate=False, tag=None, flops=None, l2n_scale=None, l2n_cols=0, w_lo=None, dropout=None,
+           discard_out=False):
     """y[M,N] = x[M,K] @ w[N,K]^T (+bias) (+residual); x, w bf16 row-major.  l2n_scale (the [32]
     head-dim scale): out2[:, :l2n_cols] = per 32-column head l2norm(y) * scale, fused (act 5).
-    w_lo: the bf16 lo image of a split f32 weight (cast_bf16_split): y = x @ (w + w_lo)^T."""
+    w_lo: the bf16 lo image of a split f32 weight (cast_bf16_split): y = x @ (w + w_lo)^T.
+    discard_out (fp16 GEGLU only): h is not stored, only out2 = g (the eval forward); returns None."""
     M, K = x.shape
     N = w.shape[0]
     assert w.shape[1] == K and x.stride(1) == 1 and w.stride(1) == 1
+    if discard_out:
+        assert act == ACT_GEGLU and x.dtype == F16 and out2 is not None and out is None
+        a = GemmArgs()
+        a.M, a.N, a.K = M, N, K
+        a.A, a.lda, a.a_kcontig = ptr(x), x.stride(0), 1
+        a.B, a.ldb, a.b_kcontig = ptr(w), w.stride(0), 1
+        a.C, a.ldc = None, N
+        a.C2, a.ldc2 = ptr(out2), out2.stride(0)
+        a.alpha, a.act, a.split_k, a.batch, a.ab_f16 = alpha, ACT_GEGLU, 1, 1, 1
+        end = TIMER(tag, flops if flops is not None else 2.0 * M * N * K) if tag else None
+        call('ctclip_gemm', _lib.ctypes.byref(a), stream_ptr())
+        if end is not None:
+            end.record()
+        return None
     if out is None:
         out = torch.empty(M, N, device=x.device, dtype=out_dtype)
     if l2n_scale is not None:
@@ -292,18 +308,20 @@ def _gemm_ln(M, K, A, B, b_kcontig, C, C2, R, ln, tag=None, flops=None):
     return True
 
 
-def linear_residual_ln(x, w, residual, gamma, beta, eps, *, tag=None, y16=False):
+def linear_residual_ln(x, w, residual, gamma, beta, eps, *, tag=None, y16=False, eval_only=False):
     """x1 = residual + x @ w^T (w [512, K] nn.Linear weight) and y = LayerNorm(x1) (gamma, beta;
     bf16) in ONE launch (ctclip_gemm_ln mode 1).  Returns (x1 f32, x1 bf16, y bf16, mean, rstd) --
     plus y's fp16 copy when y16 -- or None when the shape / configuration does not allow the fused
-    form.  x, w fp16: the fp16 GEMM."""
+    form.  x, w fp16: the fp16 GEMM.  eval_only (with y16): the backward-only bf16 x1 and y are not
+    written (None)."""
     M, K = x.shape
     if not ln_fusable(M, w.shape[0]) or K % 64 or residual.dtype != F32:
         return None
+    assert y16 or not eval_only
     dev = x.device
     x1f = torch.empty(M, 512, device=dev, dtype=F32)
-    x1b = torch.empty(M, 512, device=dev, dtype=BF16)
-    y = torch.empty(M, 512, device=dev, dtype=BF16)
+    x1b = None if eval_only else torch.empty(M, 512, device=dev, dtype=BF16)
+    y = None if eval_only else torch.empty(M, 512, device=dev, dtype=BF16)
     mean = torch.empty(M, device=dev, dtype=F32)
     rstd = torch.empty(M, device=dev, dtype=F32)
     ln = LnEpilogueArgs()
@@ -719,15 +737,16 @@ def add_f32(a, b, out=None, out_bf16=None):
 
 
 # ----------------------------------------------------------------------------- patch embed
-def patch_ln(video, is_hu, PT, P, offs, eps=1e-5, ld=None, want_f16=False, want_x3=False):
+def patch_ln(video, is_hu, PT, P, offs, eps=1e-5, ld=None, want_f16=False, want_x3=False, want_bf16=True):
     """LayerNorm'd patch rows [tokens, ld] bf16 (columns pd..ld-1 zero: K padding for the GEMM);
     with want_f16 also their fp16 copy (returns (bf16, f16)); with want_x3 their split-fp16 pair
-    (returns (bf16, (hi, lo)))."""
+    (returns (bf16, (hi, lo))).  want_bf16=False (with want_f16): the bf16 rows -- the weight
+    gradient's operand -- are not written (None; the eval forward)."""
     B, C, Fr, H, W = video.shape
     T, Hg, Wg = Fr // PT, H // P, W // P
     pd = C * PT * P * P
     ld = pd if ld is None else ld
-    out = torch.empty(B * T * Hg * Wg, ld, device=video.device, dtype=BF16)
+    out = torch.empty(B * T * Hg * Wg, ld, device=video.device, dtype=BF16) if want_bf16 else None
     out16 = torch.empty(B * T * Hg * Wg, ld, device=video.device, dtype=F16) if want_f16 or want_x3 else None
     out16lo = torch.empty(B * T * Hg * Wg, ld, device=video.device, dtype=F16) if want_x3 else None
     call('ctclip_patch_ln_x3', ptr(video), int(video.dtype == F32), int(is_hu), B, C, Fr, H, W, PT, P, ptr(offs), eps,
@@ -802,7 +821,8 @@ def skinny_linear(x, w):
     return out
 
 
-def peg_fwd_x32(xf, B, T, H, W, weight, bias, mode, stats=False, want_f16=False, eps=1e-5, want_x3=False):
+def peg_fwd_x32(xf, B, T, H, W, weight, bias, mode, stats=False, want_f16=False, eps=1e-5, want_x3=False,
+                want_bf16=True):
     """PEG forward with the taps read from the f32 residual stream (ctclip_peg_fwd_x32; the bf16
     shadow's rounding never enters the conv).  Returns (out_f32, out_bf16, out_f16 or None, mean,
     rstd) -- mean / rstd the LayerNorm statistics of the output rows when stats (merged from the
@@ -812,7 +832,7 @@ def peg_fwd_x32(xf, B, T, H, W, weight, bias, mode, stats=False, want_f16=False,
     M, D = xf.shape
     assert xf.dtype == F32 and xf.is_contiguous()
     outf = torch.empty_like(xf)
-    outb = torch.empty(M, D, device=xf.device, dtype=BF16)
+    outb = torch.empty(M, D, device=xf.device, dtype=BF16) if want_bf16 else None
     outh = torch.empty(M, D, device=xf.device, dtype=torch.float16) if want_f16 or want_x3 else None
     outl = torch.empty(M, D, device=xf.device, dtype=torch.float16) if want_x3 else None
     part = torch.empty(D // 32, M, 2, device=xf.device, dtype=F32) if stats else None
@@ -859,10 +879,11 @@ def pack_qkv_fold_h16(wq, gamma, wkv):
     return out, cs
 
 
-def linear_qkv_lnfold(x, wp, cs, mean, rstd, scales, nfold, n2, out=None, out2=None):
+def linear_qkv_lnfold(x, wp, cs, mean, rstd, scales, nfold, n2, out=None, out2=None, c_col0=0):
     """C = x @ wp^T with the LayerNorm folded into columns < nfold and the per-head l2norm * scale
     of columns < n2 in C2 (ctclip_gemm_qkv_lnfold); scales = [64] f32 (folded columns' 32, then
-    the rest's).  Returns (C [M, N] bf16, C2 [M, n2] bf16)."""
+    the rest's).  Returns (C [M, N] bf16, C2 [M, n2] bf16); c_col0 > 0: C's columns below it are not
+    written (the eval forward keeps only V, ctclip_gemm_qkv_lnfold2)."""
     M, K = x.shape
     N = wp.shape[0]
     assert wp.shape[1] == K and x.stride(1) == 1 and wp.stride(1) == 1 and scales.numel() == 64
@@ -881,7 +902,8 @@ def linear_qkv_lnfold(x, wp, cs, mean, rstd, scales, nfold, n2, out=None, out2=N
     a.n2 = n2
     assert wp.dtype == x.dtype
     a.ab_f16 = int(x.dtype == F16)     # fp16 x and packed weight (pack_qkv_fold_h16)
-    call('ctclip_gemm_qkv_lnfold', _lib.ctypes.byref(a), ptr(mean), ptr(rstd), ptr(cs), nfold, stream_ptr())
+    call('ctclip_gemm_qkv_lnfold2', _lib.ctypes.byref(a), ptr(mean), ptr(rstd), ptr(cs), nfold, int(c_col0),
+         stream_ptr())
     return out, out2
 
 
@@ -1038,15 +1060,19 @@ def _attn_args(q, k, v, o, *, L, H, D, nseq, M, scale, seq, bias_u=None, grid=(0
 
 
 def attn_fwd(q, k, v, *, L, H, D, nseq, scale, seq, bias_u=None, grid=(0, 0), kmask=None, dropout=(0.0, 0),
-             want_o16=False):
+             want_o16=False, eval_only=False):
     """q/k/v: 2D views [M, ...] whose head h occupies columns h*D:(h+1)*D.  Returns (o [M, H*D], lse [H, M]),
-    plus o's fp16 copy when want_o16."""
+    plus o's fp16 copy when want_o16.  eval_only (with want_o16): neither the bf16 o nor the lse -- the
+    backward's operands -- is written (returned as None)."""
     M = q.shape[0]
-    o = torch.empty(M, H * D, device=q.device, dtype=BF16)
+    assert want_o16 or not eval_only
+    o = None if eval_only else torch.empty(M, H * D, device=q.device, dtype=BF16)
     o16 = torch.empty(M, H * D, device=q.device, dtype=F16) if want_o16 else None
-    lse = torch.empty(H, M, device=q.device, dtype=F32)
-    a = _attn_args(q, k, v, o, L=L, H=H, D=D, nseq=nseq, M=M, scale=scale, seq=seq, bias_u=bias_u, grid=grid,
-                   kmask=kmask, lse=lse, dropout=dropout)
+    lse = None if eval_only else torch.empty(H, M, device=q.device, dtype=F32)
+    a = _attn_args(q, k, v, o if o is not None else o16, L=L, H=H, D=D, nseq=nseq, M=M, scale=scale, seq=seq,
+                   bias_u=bias_u, grid=grid, kmask=kmask, lse=lse, dropout=dropout)
+    if o is None:
+        a.o = None
     a.o16 = ptr(o16)
     call('ctclip_attn_fwd', _lib.ctypes.byref(a), stream_ptr())
     return (o, lse, o16) if want_o16 else (o, lse)

@@ -123,6 +123,25 @@ def describe_status(v):
     return ', '.join(n for b, n in _STATUS_NAMES if v & b) or 'none'
 
 
+def raise_for_status(v, step):
+    """Raise the StepGuardError of a step's skip word ``v`` (the ranks' summed status words, with the
+    gradient-norm bit ORed in), if it is nonzero.  Every rank holds the same value, so every rank
+    raises for the same step."""
+    if v == 0:
+        return
+    if v == 1:
+        raise LayerNormExchangeError(
+            f'LayerNorm-fused GEMM exchange timed out (status word set by step {step} or earlier, on '
+            'this rank or another: the ranks\' words are summed with the gradients): its LayerNorm '
+            'outputs were wrong and the Adam update of that step was skipped on every rank; '
+            'kernels.reset_ln_status() clears the word (CTCLIP_LN_FUSED=0 runs the unfused GEMM + '
+            'LayerNorm pair instead)', bits=v)
+    raise NonFiniteStepError(
+        f'step {step} (or earlier) was flagged on the device, status {v} ({describe_status(v)}; summed '
+        'over the ranks): its Adam update and codebook EMA were skipped on every rank, parameters and '
+        'moments unchanged; kernels.reset_ln_status() clears the sticky word', bits=v)
+
+
 # queue BERT's backward before the 3D-ViT's (CTCLIP_TEXT_FIRST=0: after it, the r02 order; A/B)
 TEXT_FIRST = os.environ.get('CTCLIP_TEXT_FIRST', '1') != '0'
 
@@ -338,17 +357,7 @@ class CTClipTrainer:
             v = int(host[0])
             if v != 0:
                 self._ln_pending.clear()
-                if v == 1:
-                    raise LayerNormExchangeError(
-                        f'LayerNorm-fused GEMM exchange timed out (status word set by step {step} or earlier, on '
-                        'this rank or another: the ranks\' words are summed with the gradients): its LayerNorm '
-                        'outputs were wrong and the Adam update of that step was skipped on every rank; '
-                        'kernels.reset_ln_status() clears the word (CTCLIP_LN_FUSED=0 runs the unfused GEMM + '
-                        'LayerNorm pair instead)', bits=v)
-                raise NonFiniteStepError(
-                    f'step {step} (or earlier) was flagged on the device, status {v} ({describe_status(v)}; summed '
-                    'over the ranks): its Adam update and codebook EMA were skipped on every rank, parameters and '
-                    'moments unchanged; kernels.reset_ln_status() clears the sticky word', bits=v)
+                raise_for_status(v, step)
             self.ln_steps_checked = step
 
     def _adam(self, off, n, step=None):

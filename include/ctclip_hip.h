@@ -188,6 +188,10 @@ int ctclip_gemm_ln(const ctclip_gemm_args* a, const ctclip_ln_epilogue* ln, void
  * + two act-5 GEMMs. */
 int ctclip_gemm_qkv_lnfold(const ctclip_gemm_args* a, const float* mean, const float* rstd, const float* fold_cs,
                            int32_t nfold, void* stream);
+/* ... storing only the C columns >= c_col0 (a multiple of 64; the l2norm'd C2 is written in full): the
+ * eval forward keeps V and drops the raw q / k, which only the backward reads (round 6) */
+int ctclip_gemm_qkv_lnfold2(const ctclip_gemm_args* a, const float* mean, const float* rstd, const float* fold_cs,
+                            int32_t nfold, int32_t c_col0, void* stream);
 /* B operand of ctclip_gemm_qkv_lnfold: out rows [0, nq) = bf16(Wq o gamma) (Wq f32 [nq][K]), rows
  * [nq, nq + nrest) = the bf16 rows of Wrest; cs [nq] = row sums of the bf16 folded rows (f32);
  * s_out (optional) [2 ns] = s_fold ++ s_rest (the epilogue's two l2norm scales). */
@@ -470,7 +474,8 @@ typedef struct {
    * atomics.  Its size in floats is ctclip_attn_bwd_ws_floats(a) (0: this shape does not use it). */
   float* dbias_ws;
   int64_t dbias_ws_floats;
-  void* o16;   /* fwd, optional: an fp16 copy of O (ldo) -- the fp16 to_out GEMM's A operand */
+  void* o16;   /* fwd, optional: an fp16 copy of O (ldo) -- the fp16 to_out GEMM's A operand; the
+                * forward's o and lse may be NULL when o16 is given (the eval forward, round 6) */
 } ctclip_attn_args;
 int ctclip_attn_fwd(const ctclip_attn_args* a, void* stream);
 int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream);

@@ -411,3 +411,56 @@ def test_two_rank_status_word_clean(tmp_path):
     """No timeout anywhere: the summed status slot stays 0 and every step is applied on both ranks."""
     mp.spawn(_status_worker, args=(_free_port(), str(tmp_path), -1), nprocs=WORLD, join=True)
     assert all((tmp_path / f'ok{r}').exists() for r in range(WORLD))
+
+
+def _nan_worker(rank, port, out_dir):
+    """A NaN on ONE rank (round 6 guards): at step 2 rank 1's forward flags CT_STATUS_F16_RANGE (an fp16
+    copy went non-finite) and its local gradient holds a NaN.  The flag reaches every rank through the
+    summed status slot; the NaN reaches every rank through the gradient SUM, so the norm the
+    gradient-norm kernel takes after the all-reduce is NaN on every rank (CT_STATUS_NONFINITE_GRAD).
+    Every rank skips step 2 (and, the word being sticky, step 3), raises the same NonFiniteStepError
+    (trainer.raise_for_status) and keeps a parameter arena bit-identical to the other rank's."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=WORLD)
+    try:
+        from ctclip_mi355x import dist_sync
+        from ctclip_mi355x.trainer import FlatParams, NonFiniteStepError, raise_for_status
+        g = torch.Generator().manual_seed(5)
+        ps = [torch.nn.Parameter(torch.randn(6, 3, generator=g)), torch.nn.Parameter(torch.randn(5, generator=g))]
+        flat = FlatParams(ps, torch.device('cpu'))
+        segs = [('a', 0, 18), ('b', 18, 5)]
+        word = torch.zeros(1, dtype=torch.int32)
+        gs = dist_sync.BucketedGradSync(flat.grad, segs, status=(flat.status, lambda: word))
+        m, v = torch.zeros(flat.numel), torch.zeros(flat.numel)
+        raised = []
+        for step in (1, 2, 3):
+            torch.manual_seed(100 * step + rank)
+            flat.grad[:flat.numel].copy_(torch.randn(flat.numel))
+            if rank == 1 and step == 2:
+                word.fill_(2)                            # CT_STATUS_F16_RANGE on this rank only
+                flat.grad[7] = float('nan')
+            gs.arm()
+            gs.finish()
+            skip_word = int(flat.status.item())          # trainer: skip_word.copy_(flat.status)
+            norm = flat.grad[:flat.numel].norm()
+            if not torch.isfinite(norm):                 # the gradient-norm kernel's OR (optim.hip)
+                skip_word |= 4
+            _adam_ref(flat.data, flat.grad[:flat.numel], m, v, 1e-2, step, skip_word != 0)
+            try:
+                raise_for_status(skip_word, step)
+                raised.append(None)
+            except NonFiniteStepError as e:
+                raised.append(e.bits)
+        assert raised == [None, 6, 2], raised          # step 3: the sticky range bit alone
+        assert torch.isfinite(flat.data).all()
+        both = [torch.empty_like(flat.data) for _ in range(WORLD)]
+        dist.all_gather(both, flat.data)
+        assert torch.equal(both[0], both[1])
+        open(os.path.join(out_dir, f'ok{rank}'), 'w').close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_nan_on_one_rank_skips_every_rank(tmp_path):
+    mp.spawn(_nan_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    assert all((tmp_path / f'ok{r}').exists() for r in range(WORLD))
