@@ -44,7 +44,9 @@ def parse():
     ap.add_argument('--text-len', type=int, default=128)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--f32-tower', action='store_true',
-                    help="run the whole bench in the f32 image-tower mode (precise.set_vit_precision('f32'))")
+                    help="run the whole bench in the f32 image-tower mode (= --vit-precision f32)")
+    ap.add_argument('--vit-precision', default=None, choices=['bf16', 'f32', 'split'],
+                    help='run the whole bench in this image-tower mode (precise.set_vit_precision; profiling)')
     ap.add_argument('--no-precise', action='store_true',
                     help='skip the precise image-tower measurements (precise_split_tower / precise_f32_tower)')
     ap.add_argument('--cpu-batch', type=int, default=2)
@@ -237,9 +239,12 @@ def main():
         from ctclip_mi355x import functional as Fn
         Fn.set_vit_fp8(True)
     if args.f32_tower:
+        args.vit_precision = 'f32'
+    if args.vit_precision and args.vit_precision != 'bf16':
         from ctclip_mi355x import precise
-        precise.set_vit_precision('f32')
+        precise.set_vit_precision(args.vit_precision)
         args.no_precise = True
+        args.f32_tower = True   # (labels: the image-tower forward is the precise one)
     torch.manual_seed(0)   # identical random-init weights on every rank
     model = set_finetune_trainable(build_ctclip()).to(dev)
     model.train()
@@ -373,7 +378,7 @@ def main():
         'scaling': 'weak',
         'vs_baseline': None,
         'dtype': 'mx-fp8 e4m3 (3D-ViT forward linears) + bf16' if args.fp8 else
-                 ('f32 image-tower forward + bf16 backward' if args.f32_tower else 'bf16'),
+                 (f'{args.vit_precision} image-tower forward + bf16 backward' if args.f32_tower else 'bf16'),
         'data': 'synthetic: int16 HU volumes 1x240x480x480 (randint -1200..1200) + 128-token reports; '
                 'random-init CT-CLIP base weights',
         'config': {'workload': 'CT-CLIP base contrastive train step: BERT-base(128 tok, train-mode dropout '

@@ -72,7 +72,7 @@ struct P {
   // split-fp16 "x3" GEMM (round 6, ctclip_gemm_args.A_lo / B_lo): A = Ah + Al, B = Bh + Bl as fp16
   // image pairs; every 64-deep K-step runs three products Ah Bh, Ah Bl, Al Bh into the one f32
   // accumulator (Al Bl, ~2^-22 relative, is dropped), so the GEMM sees ~22-bit operands at 3x the
-  // fp16 MFMA work (x3 != 0: tile_at's K-step count triples).  The x3 GEGLU
+  // fp16 MFMA work (the X3 kernels: tile_at's K-step count triples).  The x3 GEGLU
   // epilogue writes h (fp16, C), g = gelu(gate) x from the unrounded f32 h as an fp16 pair (C2 hi,
   // C3 lo, the FF2 GEMM's A operand) and as bf16 (C4, the FF2 weight gradient's operand).
   const u16* alo;
@@ -1410,6 +1410,7 @@ struct Tile {
   int nk, split, bidx;
 };
 
+template <bool X3 = false>
 __device__ __forceinline__ Tile tile_at(const P& p, int lin, int gx, int gy, int ntiles) {
   // XCD-aware remap of the linear tile index (round-robin dispatch: lin & 7 = XCD), so each
   // XCD walks a contiguous range of tiles (x fastest, then y, then batch / split)
@@ -1439,7 +1440,7 @@ __device__ __forceinline__ Tile tile_at(const P& p, int lin, int gx, int gy, int
   t.n0 = (int64_t)tx * p8::BNN;
   t.kbeg = t.split * p.kper;
   const int64_t kend = min(p.K, t.kbeg + p.kper);
-  t.nk = (kend > t.kbeg && !(p.debug & 2)) ? (int)((kend - t.kbeg) / p8::BKK) * (p.x3 ? 3 : 1) : 0;
+  t.nk = (kend > t.kbeg && !(p.debug & 2)) ? (int)((kend - t.kbeg) / p8::BKK) * (X3 ? 3 : 1) : 0;
   return t;
 }
 
@@ -1468,7 +1469,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
   int lin = p.persist ? (int)blockIdx.x : (int)((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x);
   const int lstride = p.persist ? (int)gridDim.x : ntiles;
   if (lin >= ntiles) return;
-  Tile T = tile_at(p, lin, gx, gy, ntiles);
+  Tile T = tile_at<X3>(p, lin, gx, gy, ntiles);
   // desynchronise the CUs: half of the first dispatch round (every other workgroup within each
   // XCD) starts p.stagger x ~2k cycles late, so later rounds' store-heavy epilogues on those CUs
   // fall under the other half's MFMA main loops instead of all CUs storing at once
@@ -1624,7 +1625,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
     lin += lstride;
     const bool more = lin < ntiles;
     if (more) {
-      const Tile nx = tile_at(p, lin, gx, gy, ntiles);
+      const Tile nx = tile_at<X3>(p, lin, gx, gy, ntiles);
       stage_of(nx, A0, 0); stage_of(nx, A1, 0); stage_of(nx, B0, 0); stage_of(nx, B1, 0);
       if constexpr (TR) { stage_of(nx, A0, 1); stage_of(nx, B0, 1); }
       if constexpr (PRE_OK) {
@@ -1660,7 +1661,7 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(P p) {
     STAMP(4, __builtin_amdgcn_s_memtime());
     ++tcount;
     if (!more) break;
-    T = tile_at(p, lin, gx, gy, ntiles);
+    T = tile_at<X3>(p, lin, gx, gy, ntiles);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
