@@ -436,6 +436,167 @@ __global__ __launch_bounds__(256) void attn_f32_mfma_kernel(ctclip_attn_args a) 
     *(f32x4*)(O + db * 16 + 4 * g) = f32x4{o[db][0] / l, o[db][1] / l, o[db][2] / l, o[db][3] / l};
 }
 
+// The same attention on the 16-bit matrix pipe with split-fp16 operands (precise 'split' mode,
+// round 6): q, k, v (f32) become fp16 (hi, lo) pairs, the probabilities too, and every product is the
+// x3 sum hi.hi + hi.lo + lo.hi of v_mfma_f32_16x16x32_f16 (~22-bit operands, f32 accumulation) --
+// 6 MFMAs of 16 cycles per 16 queries x 32 keys against 16 of 32 cycles on the f32 pipe.  Layouts
+// follow the f32 kernel: S^T = K Q^T (a lane holds keys 16 j + 4 g + r of query lane & 15); for PV
+// the k-slots of lane group g in key pair P are keys 32 P + 16 (i >> 2) + 4 g + (i & 3), i = 0..7,
+// exactly the probabilities the lane holds, so V^T is staged in that key order.  Outputs: O as the
+// fp16 pair of the x3 to_out GEMM (oh, ol), O in bf16 and the natural-log LSE (the bf16 backward's
+// operands: it recomputes P from its bf16 q / k against this LSE).
+constexpr int X3_KLD = 40;            // K image row: 32 d + 8 pad (fp16)
+constexpr int X3_VLD = 72;            // V^T image row: 64 keys + 8 pad (fp16)
+
+__device__ __forceinline__ void split2h(float x, _Float16& h, _Float16& l) {
+  h = (_Float16)x;
+  l = (_Float16)(x - (float)h);
+}
+
+__global__ __launch_bounds__(256) void attn_x3_fwd_kernel(ctclip_attn_args a, u16* __restrict__ oh,
+                                                          u16* __restrict__ ol, u16* __restrict__ ob,
+                                                          float* __restrict__ lse) {
+  __shared__ __attribute__((aligned(16))) _Float16 Kh[64 * X3_KLD], Kl[64 * X3_KLD];
+  __shared__ __attribute__((aligned(16))) _Float16 Vh[32 * X3_VLD], Vl[32 * X3_VLD];
+  __shared__ float Bs[FA_MAXNB];
+  __shared__ __attribute__((aligned(16))) int Kx[FA_MAXL + 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
+  const int h = blockIdx.y;
+  const int64_t sq = blockIdx.z;
+  const int L = a.L;
+  const int64_t rbase = (sq / a.n_inner) * a.s_outer + (sq % a.n_inner) * a.s_inner;
+  const float* Q = (const float*)a.q;
+  const float* Kp = (const float*)a.k;
+  const float* Vp = (const float*)a.v;
+  const bool bias = a.bias_u != nullptr;
+  const int Wg = bias ? a.grid_w : 1;
+  const int nb = bias ? (2 * a.grid_h - 1) * (2 * Wg - 1) : 0;
+  if (bias) {
+    for (int i = tid; i < nb; i += 256) Bs[i] = a.bias_u[(int64_t)h * nb + i];
+    for (int i = tid; i < L + 64; i += 256) Kx[i] = i < L ? (i / Wg) * (2 * Wg - 1) + i % Wg : 0;
+  }
+  const int qi = blockIdx.x * 64 + w * 16 + r16;
+  const bool qv = qi < L;
+  const int64_t qrow = rbase + (int64_t)min(qi, L - 1) * a.s_pos;
+  // B operand of S^T: query lane & 15, head dims 8 g .. 8 g + 7 as an fp16 pair
+  f16x8 qh, ql;
+  {
+    const float* qp = Q + qrow * a.ldq + h * 32 + 8 * g;
+    const f32x4 q0 = *(const f32x4*)qp, q1 = *(const f32x4*)(qp + 4);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      _Float16 hh, ll;
+      split2h(qv ? (e < 4 ? q0[e] : q1[e - 4]) : 0.f, hh, ll);
+      qh[e] = hh;
+      ql[e] = ll;
+    }
+  }
+  int qbase = 0;
+  if (bias) qbase = (qi / Wg + a.grid_h - 1) * (2 * Wg - 1) + qi % Wg + Wg - 1;
+  float m = -INFINITY, l = 0.f;
+  f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const int kk = tid >> 2, c = tid & 3;   // staging: key kk of the chunk, head dims 8 c .. 8 c + 7
+  // the key's position in the V^T image: pair P = kk >> 5, lane group gk = (kk >> 2) & 3, slot
+  // i = 4 ((kk >> 4) & 1) + (kk & 3) (see above)
+  const int vpos = (kk >> 5) * 32 + ((kk >> 2) & 3) * 8 + 4 * ((kk >> 4) & 1) + (kk & 3);
+  for (int k0 = 0; k0 < L; k0 += 64) {
+    __syncthreads();
+    {
+      const int64_t krow = rbase + (int64_t)min(k0 + kk, L - 1) * a.s_pos;
+      const f32x4 k_lo = *(const f32x4*)(Kp + krow * a.ldk + h * 32 + 8 * c);
+      const f32x4 k_hi = *(const f32x4*)(Kp + krow * a.ldk + h * 32 + 8 * c + 4);
+      const f32x4 v_lo = *(const f32x4*)(Vp + krow * a.ldv + h * 32 + 8 * c);
+      const f32x4 v_hi = *(const f32x4*)(Vp + krow * a.ldv + h * 32 + 8 * c + 4);
+      f16x8 kh8, kl8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        _Float16 hh, ll;
+        split2h(j < 4 ? k_lo[j] : k_hi[j - 4], hh, ll);
+        kh8[j] = hh;
+        kl8[j] = ll;
+        split2h(j < 4 ? v_lo[j] : v_hi[j - 4], hh, ll);
+        Vh[(8 * c + j) * X3_VLD + vpos] = hh;
+        Vl[(8 * c + j) * X3_VLD + vpos] = ll;
+      }
+      *(f16x8*)(Kh + kk * X3_KLD + 8 * c) = kh8;
+      *(f16x8*)(Kl + kk * X3_KLD + 8 * c) = kl8;
+    }
+    __syncthreads();
+    float x[4][4];
+    float cm = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f16x8 kah = *(const f16x8*)(Kh + (16 * j + r16) * X3_KLD + 8 * g);
+      const f16x8 kal = *(const f16x8*)(Kl + (16 * j + r16) * X3_KLD + 8 * g);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(kah, qh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(kah, ql, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(kal, qh, acc, 0, 0, 0);
+      const int key0 = k0 + 16 * j + 4 * g;
+      int kx[4] = {0, 0, 0, 0};
+      if (bias) {
+        const int4 t4 = *(const int4*)(Kx + key0);
+        kx[0] = t4.x; kx[1] = t4.y; kx[2] = t4.z; kx[3] = t4.w;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = acc[r] * a.scale;
+        if (bias) v += qv ? Bs[qbase - kx[r]] : 0.f;
+        x[j][r] = key0 + r < L ? v : -INFINITY;
+        cm = fmaxf(cm, x[j][r]);
+      }
+    }
+    cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+    cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+    const float mn = fmaxf(m, cm);
+    const float corr = expf(m - mn);   // m = -inf on the first chunk -> 0
+    l *= corr;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { o[0][r] *= corr; o[1][r] *= corr; }
+    m = mn;
+#pragma unroll
+    for (int P = 0; P < 2; ++P) {
+      f16x8 ph, pl;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float pv = expf(x[2 * P + (i >> 2)][i & 3] - mn);
+        l += pv;
+        _Float16 hh, ll;
+        split2h(pv, hh, ll);
+        ph[i] = hh;
+        pl[i] = ll;
+      }
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const int vo = (db * 16 + r16) * X3_VLD + P * 32 + g * 8;
+        const f16x8 vh = *(const f16x8*)(Vh + vo), vl = *(const f16x8*)(Vl + vo);
+        o[db] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, ph, o[db], 0, 0, 0);
+        o[db] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, pl, o[db], 0, 0, 0);
+        o[db] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, ph, o[db], 0, 0, 0);
+      }
+    }
+  }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  if (!qv) return;
+  // lane: query qi, head dims 16 db + 4 g + [0, 4)
+  const int64_t ro = qrow * a.ldo + h * 32 + 4 * g;
+#pragma unroll
+  for (int db = 0; db < 2; ++db) {
+    float ov[4], hv[4], lv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      ov[r] = o[db][r] / l;
+      hv[r] = rh(ov[r]);
+      lv[r] = ov[r] - hv[r];
+    }
+    *(uint2*)(oh + ro + 16 * db) = pack4h(hv);
+    *(uint2*)(ol + ro + 16 * db) = pack4h(lv);
+    if (ob) *(uint2*)(ob + ro + 16 * db) = pack4(ov);
+  }
+  if (g == 0 && lse) lse[(int64_t)h * a.M + qrow] = m + logf(l);
+}
+
 inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
 
 }  // namespace
@@ -530,6 +691,28 @@ extern "C" int ctclip_attn_fwd_f32(const ctclip_attn_args* a, void* stream) {
     hipLaunchKernelGGL(attn_f32_kernel<64>, grid, dim3(64), 0, (hipStream_t)stream, *a);
   else
     return CT_ESHAPE;
+  CT_CHECK_LAUNCH();
+  return 0;
+}
+
+// split-fp16 x3 attention forward (precise 'split' mode, round 6): q, k, v f32 in `a` (D = 32, as
+// ctclip_attn_fwd_f32's MFMA kernel); O written as an fp16 pair (oh, ol; ldo) + optional bf16 copy ob,
+// optional natural-log lse [H][M].
+extern "C" int ctclip_attn_fwd_x3(const ctclip_attn_args* a, void* oh, void* ol, void* ob, float* lse, void* stream) {
+  CT_REQUIRE(a && a->q && a->k && a->v && oh && ol && a->L > 0 && a->nseq >= 0 && a->n_inner > 0, CT_EINVAL);
+  CT_REQUIRE(a->D == 32 && !a->kmask && a->dropout_p == 0.f, CT_EINVAL);
+  if (a->bias_u)
+    CT_REQUIRE(a->grid_h > 0 && a->grid_w > 0 && a->grid_h * a->grid_w == a->L &&
+                   (2 * a->grid_h - 1) * (2 * a->grid_w - 1) <= FA_MAXNB && a->L <= FA_MAXL,
+               CT_ESHAPE);
+  CT_REQUIRE(aligned16(a->q) && aligned16(a->k) && aligned16(a->v) && a->ldq % 4 == 0 && a->ldk % 4 == 0 &&
+                 a->ldv % 4 == 0 && ((uintptr_t)oh & 7) == 0 && ((uintptr_t)ol & 7) == 0 &&
+                 ((uintptr_t)ob & 7) == 0 && a->ldo % 4 == 0,
+             CT_EALIGN);
+  if (a->nseq == 0) return 0;
+  dim3 grid((unsigned)cdiv(a->L, 64), (unsigned)a->H, (unsigned)a->nseq);
+  hipLaunchKernelGGL(attn_x3_fwd_kernel, grid, dim3(256), 0, (hipStream_t)stream, *a, (u16*)oh, (u16*)ol, (u16*)ob,
+                     lse);
   CT_CHECK_LAUNCH();
   return 0;
 }

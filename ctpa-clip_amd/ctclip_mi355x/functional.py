@@ -903,16 +903,25 @@ def _vit_layer_tail_f32(ctx, x1f, x1b, xn, m1, r1, q32, q, kv32, kv, xb, bias_u,
     L, nseq, seq = geo.seq()
     use_bias = bias_u is not None
     grid = (geo.Hg, geo.Wg) if use_bias else (0, 0)
-    o32 = K.attn_fwd_f32(qn32, kn32, kv32[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
-                         bias_u=bias_u if use_bias else None, grid=grid)
-    qn, kn = K.cast_bf16(qn32), K.cast_bf16(kn32)
-    del q32, qn32, kn32
-    o, lse = K.attn_fwd(qn, kn, kv[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
-                        bias_u=bias_u if use_bias else None, grid=grid)
+    if split and dh == 32:
+        # x3 attention: O straight as to_out's fp16 pair, plus the bf16 O / LSE the backward reads
+        os_, o, lse = K.attn_fwd_x3(qn32, kn32, kv32[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
+                                    bias_u=bias_u if use_bias else None, grid=grid)
+        qn, kn = K.cast_bf16(qn32), K.cast_bf16(kn32)
+        del q32, qn32, kn32
+        o32 = None
+    else:
+        o32 = K.attn_fwd_f32(qn32, kn32, kv32[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
+                             bias_u=bias_u if use_bias else None, grid=grid)
+        qn, kn = K.cast_bf16(qn32), K.cast_bf16(kn32)
+        del q32, qn32, kn32
+        o, lse = K.attn_fwd(qn, kn, kv[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
+                            bias_u=bias_u if use_bias else None, grid=grid)
+        os_ = K.split_f16(o32) if split else None
     inner_ff = W1.shape[0] // 2
     if split:
-        x2f, x2b = K.linear_x3(K.split_f16(o32), x3_weight(Wo), residual=x1f, want_bf16=True)
-        del o32, kv32, x1f
+        x2f, x2b = K.linear_x3(os_, x3_weight(Wo), residual=x1f, want_bf16=True)
+        del o32, os_, kv32, x1f
         xn2, _, m2, r2, xn2s = K.layernorm_fwd(x2f, ff_w, ff_b, 1e-5, out_bf16=True, out_x3=True)
         W1s = x3_weight(W1, rows=2 * ff_pad(inner_ff), rowmap=ff1_rowmap(inner_ff, W1.device), tag='ff1')
         h, gs, g = K.linear_x3_geglu(xn2s, W1s, tag='ff1', flops=2.0 * x2f.shape[0] * W1.shape[0] * W1.shape[1])

@@ -1529,3 +1529,18 @@ def linear_x3_geglu(xs, w1s, *, alpha=1.0 / X3_WSCALE, want_bf16=True, tag=None,
     if end is not None:
         end.record()
     return h, (gh, gl), gb
+
+
+def attn_fwd_x3(q, k, v, *, L, H, D, nseq, scale, seq, bias_u=None, grid=(0, 0), want_bf16=True, want_lse=True):
+    """The cosine attention on split-fp16 x3 MFMAs (ctclip_attn_fwd_x3): q, k, v f32 (head h in columns
+    h D .. h D + D - 1).  Returns ((o hi, o lo) fp16 [M, H D], o bf16 or None, lse [H, M] or None)."""
+    M = q.shape[0]
+    dev = q.device
+    oh = torch.empty(M, H * D, device=dev, dtype=F16)
+    ol = torch.empty(M, H * D, device=dev, dtype=F16)
+    ob = torch.empty(M, H * D, device=dev, dtype=BF16) if want_bf16 else None
+    lse = torch.empty(H, M, device=dev, dtype=F32) if want_lse else None
+    a = _attn_args(q, k, v, oh, L=L, H=H, D=D, nseq=nseq, M=M, scale=scale, seq=seq, bias_u=bias_u, grid=grid)
+    a.o = None
+    call('ctclip_attn_fwd_x3', _lib.ctypes.byref(a), ptr(oh), ptr(ol), ptr(ob), ptr(lse), stream_ptr())
+    return (oh, ol), ob, lse

@@ -480,7 +480,13 @@ typedef struct {
 int ctclip_attn_fwd(const ctclip_attn_args* a, void* stream);
 int ctclip_attn_bwd(const ctclip_attn_args* a, void* stream);
 int ctclip_attn_bwd_ws_floats(const ctclip_attn_args* a);
-int ctclip_attn_fwd_f32(const ctclip_attn_args* a, void* stream);   /* f32 image tower, see below */
+int ctclip_attn_fwd_f32(const ctclip_attn_args* a, void* stream);
+/* split-fp16 x3 attention forward (precise 'split' mode, round 6; D = 32): q, k, v f32 as for
+ * ctclip_attn_fwd_f32, every product on v_mfma_f32_16x16x32_f16 as hi.hi + hi.lo + lo.hi of fp16
+ * (hi, lo) operand pairs (the probabilities included), f32 softmax.  O is written as the fp16 pair
+ * (oh, ol) that the x3 to_out GEMM reads (ldo = a->ldo), optionally as bf16 ob and with the natural-log
+ * lse [H][M] -- the operands of the bf16 backward (ctclip_attn_bwd) -- so no bf16 forward re-run. */
+int ctclip_attn_fwd_x3(const ctclip_attn_args* a, void* oh, void* ol, void* ob, float* lse, void* stream);   /* f32 image tower, see below */
 /* diagnostic: query blocks per wave processed together by the spatial (CPB-bias) forward kernel,
  * 1..3 (default 3); results are bit-identical.  Returns the previous setting. */
 int ctclip_attn_set_fwd_qb(int qb);

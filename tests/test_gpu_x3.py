@@ -218,3 +218,51 @@ def test_split_tower_matches_oracle_small(K):
         l2 = tr.train_step(text, hu.cuda())
         tr.flush()
     assert torch.isfinite(l1) and torch.isfinite(l2) and not torch.equal(before, p.detach())
+
+
+@pytest.mark.parametrize('case', ['spatial', 'spatial_5x7', 'temporal'])
+def test_attention_x3(K, case):
+    """The split-fp16 x3 attention forward (ctclip_attn_fwd_x3) against the f64 reference: O (hi + lo)
+    at the f32 level, its bf16 copy the rounding of it, and the natural-log LSE the bf16 backward
+    (ctclip_attn_bwd) reads."""
+    from test_gpu_ops import _attn_ref, _cpb_table, _gather_rows
+    torch.manual_seed(16)
+    if case.startswith('spatial'):
+        gh, gw = {'spatial': (24, 24), 'spatial_5x7': (5, 7)}[case]
+        L, H, D, nseq = gh * gw, 8, 32, 3
+        M, seq, grid = nseq * L, (1, L, 0, 1), (gh, gw)
+        u, bins = _cpb_table(H, gh, gw)
+        bias = u[:, bins].double()
+    else:
+        B, T, HW, H = 2, 24, 20, 8
+        L, D, nseq = T, 32, B * HW
+        M, seq, grid = B * T * HW, (HW, T * HW, 1, HW), (0, 0)
+        u, bias = None, None
+    rows = _gather_rows(*seq, nseq, L)
+    q = F.normalize(torch.randn(M, H, D, device=dev), dim=-1).reshape(M, H * D)
+    kv = torch.randn(M, 2 * H * D, device=dev)
+    kv[:, :H * D] = F.normalize(kv[:, :H * D].reshape(M, H, D), dim=-1).reshape(M, H * D)
+    k, v = kv[:, :H * D], kv[:, H * D:]
+    (oh, ol), ob, lse = K.attn_fwd_x3(q, k, v, L=L, H=H, D=D, nseq=nseq, scale=8.0, seq=seq, bias_u=u, grid=grid)
+    ref = _attn_ref(q.double(), k.double(), v.double(), rows, H, D, 8.0, bias)
+    o = _pair(oh, ol)
+    e = rel(o, ref)
+    e32 = rel(K.attn_fwd_f32(q, k, v, L=L, H=H, D=D, nseq=nseq, scale=8.0, seq=seq, bias_u=u, grid=grid), ref)
+    print(f'x3 attention {case}: O rel {e:.2e} (f32 kernel {e32:.2e})')
+    assert e < 1e-6
+    # the bf16 copy is the rounding of the kernel's f32 O: half an ulp (2^-8 relative just above a power
+    # of two) plus that O's own absolute error, bounded here by twice the pair's worst element error
+    eabs = (o - ref).abs().max().item()
+    slack = ((ob.double() - ref).abs() - ref.abs() * 2.0 ** -8).max().item()
+    print(f'  bf16 copy: max excess over half an ulp {slack:.2e} (pair max abs err {eabs:.2e})')
+    assert slack <= 2 * eabs + 1e-9
+    # LSE: ln sum_k exp(8 q.k + bias) per (head, query row)
+    qd, kd = q.double().view(M, H, D), k.double().view(M, H, D)
+    lref = torch.empty(H, M, dtype=torch.float64, device=dev)
+    for s_ in range(nseq):
+        r = rows[s_]
+        sc = 8.0 * torch.einsum('ihd,jhd->hij', qd[r], kd[r])
+        if bias is not None:
+            sc = sc + bias
+        lref[:, r] = torch.logsumexp(sc, dim=-1)
+    assert (lse.double() - lref).abs().max().item() < 1e-5
