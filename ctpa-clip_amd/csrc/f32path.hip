@@ -200,7 +200,8 @@ __global__ __launch_bounds__(256) void peg_f32_kernel(const float* __restrict__ 
 template <int G>
 __global__ __launch_bounds__(256) void l2norm_f32_vec_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows,
                                                              int H, const float* __restrict__ scale,
-                                                             float* __restrict__ y, int64_t ldy) {
+                                                             float* __restrict__ y, int64_t ldy,
+                                                             u16* __restrict__ yb, int64_t ldyb) {
   const int64_t i = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G;
   const int q = threadIdx.x % G;
   const bool ok = i < rows * H;
@@ -216,7 +217,11 @@ __global__ __launch_bounds__(256) void l2norm_f32_vec_kernel(const float* __rest
   if (!ok) return;
   const float n = fmaxf(sqrtf(s), 1e-12f);
   const f32x4 sc = *(const f32x4*)(scale + 4 * q);
-  *(f32x4*)(y + row * ldy + h * D + 4 * q) = f32x4{v[0] / n * sc[0], v[1] / n * sc[1], v[2] / n * sc[2], v[3] / n * sc[3]};
+  float out[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) out[e] = v[e] / n * sc[e];
+  *(f32x4*)(y + row * ldy + h * D + 4 * q) = f32x4{out[0], out[1], out[2], out[3]};
+  if (yb) *(uint2*)(yb + row * ldyb + h * D + 4 * q) = pack4(out);   // the bf16 copy (the backward's operand)
 }
 
 // one thread per (row, head): y = x / max(||x||, 1e-12) * scale  (F.normalize semantics)
@@ -642,18 +647,25 @@ extern "C" int ctclip_peg_fwd_f32(const float* x, int64_t B, int32_t T, int32_t 
 
 extern "C" int ctclip_l2norm_scale_fwd_f32(const float* x, int64_t ldx, int64_t rows, int32_t H, int32_t D,
                                            const float* scale, float* y, int64_t ldy, void* stream) {
+  return ctclip_l2norm_scale_fwd_f32b(x, ldx, rows, H, D, scale, y, ldy, nullptr, 0, stream);
+}
+
+extern "C" int ctclip_l2norm_scale_fwd_f32b(const float* x, int64_t ldx, int64_t rows, int32_t H, int32_t D,
+                                            const float* scale, float* y, int64_t ldy, void* y_bf16, int64_t ldyb,
+                                            void* stream) {
   if (rows == 0) return 0;
   const bool vec = (D == 32 || D == 64) && aligned16(x) && aligned16(y) && aligned16(scale) && ldx % 4 == 0 &&
                    ldy % 4 == 0;
+  if (y_bf16) CT_REQUIRE(vec && ((uintptr_t)y_bf16 & 7) == 0 && ldyb % 4 == 0, CT_EALIGN);
   if (vec) {
     const int G = D / 4;
     const unsigned nb = (unsigned)cdiv(rows * H, 256 / G);
     if (G == 8)
       hipLaunchKernelGGL(l2norm_f32_vec_kernel<8>, dim3(nb), dim3(256), 0, (hipStream_t)stream, x, ldx, rows, H, scale,
-                         y, ldy);
+                         y, ldy, (u16*)y_bf16, ldyb);
     else
       hipLaunchKernelGGL(l2norm_f32_vec_kernel<16>, dim3(nb), dim3(256), 0, (hipStream_t)stream, x, ldx, rows, H,
-                         scale, y, ldy);
+                         scale, y, ldy, (u16*)y_bf16, ldyb);
     CT_CHECK_LAUNCH();
     return 0;
   }

@@ -169,6 +169,8 @@ _SIGS = {
     'ctclip_pack_qkv_fold_h16': [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp],
     'ctclip_skinny_gemm_slices': [c_i64, c_i64, c_i64],
     'ctclip_skinny_gemm': [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp],
+    'ctclip_skinny_sgemm_slices': [c_i64, c_i64, c_i64],
+    'ctclip_skinny_sgemm': [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp],
     'ctclip_reduce_slabs': [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp],
     'ctclip_reduce_slabs_multi': [ctypes.POINTER(SlabJob), c_i32, c_vp],
     'ctclip_layernorm_fwd': [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_vp, c_f32, c_vp, c_i64, c_vp, c_i64,
@@ -221,6 +223,7 @@ _SIGS = {
                             c_vp, c_vp, c_i64, c_vp],
     'ctclip_peg_fwd_f32': [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp],
     'ctclip_l2norm_scale_fwd_f32': [c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp],
+    'ctclip_l2norm_scale_fwd_f32b': [c_vp, c_i64, c_i64, c_i32, c_i32, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp],
     'ctclip_geglu_f32': [c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
     'ctclip_vq_select': [c_vp, c_vp, c_i32, c_vp, c_i64, c_i32, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp],
     'ctclip_vq_select_s': [c_vp, c_vp, c_i32, c_vp, c_i64, c_i32, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp, c_vp],

@@ -618,8 +618,7 @@ class ViTLayerFn(torch.autograd.Function):
         # the merged q | k l2norm backward of the fold (kernels.l2norm_qk_bwd_fold) is built for
         # exactly 256 q columns, the statistics merge (ctclip_ln_stats_merge) for <= 16 64-channel
         # groups: other widths run the unfolded LayerNorm + projections
-        fold = (_LN1_FOLD and not fp8 and _L2N_FUSED and dh == 32 and inner == 256 and dim % 64 == 0
-                and dim <= 1024 and geo.Wg <= 24 and Wkv.shape[0] == 2 * inner)
+        fold = not fp8 and _fold_shape_ok(geo, dim, Wkv)
         # fp16 forward GEMMs (vit_f16): the folded Q | K | V projection, to_out, FF1
         f16 = vit_f16() and fold and _PEG_X32
         # eval forward (round 6; no input needs a gradient, e.g. zero-shot inference under no_grad, the
@@ -857,6 +856,15 @@ class ViTLayerFn(torch.autograd.Function):
                 None, None, None)
 
 
+def _fold_shape_ok(geo, dim, Wkv):
+    """The LN1-folded Q | K | V path's shape conditions: the merged q | k l2norm backward of the fold
+    (kernels.l2norm_qk_bwd_fold) is built for exactly 256 q columns, the statistics merge
+    (ctclip_ln_stats_merge) for <= 16 64-channel groups."""
+    inner = geo.heads * geo.dim_head
+    return (_LN1_FOLD and _L2N_FUSED and geo.dim_head == 32 and inner == 256 and dim % 64 == 0 and dim <= 1024
+            and geo.Wg <= 24 and Wkv.shape[0] == 2 * inner)
+
+
 def _vit_layer_forward_f32(ctx, xf, xb, bias_u, geo, peg_w, peg_b, norm_g, q_scale, k_scale, Wq, Wkv, Wo, ff_w,
                            ff_b, W1, W2, split=False):
     """ViTLayerFn.forward of the f32 image tower: the layer (ct_clip/attention.py:322-331) with f32
@@ -873,23 +881,32 @@ def _vit_layer_forward_f32(ctx, xf, xb, bias_u, geo, peg_w, peg_b, norm_g, q_sca
     H, dh = geo.heads, geo.dim_head
     inner = H * dh
     d = lambda t: t.detach()    # noqa: E731
+    # round 6: the backward is the default's LN1-folded one where the shape allows (ctx.fold; it reads
+    # the LayerNorm statistics, x1 and the raw q | k | v in one bf16 [M, 3 inner] buffer, not the
+    # LayerNorm output): the Q-side LayerNorm writes no bf16 copy and the backward runs no LayerNorm
+    # backward kernel -- the same backward kernels as the default tower
+    fold = _fold_shape_ok(geo, xf.shape[1], Wkv)
+    qkvb = torch.empty(xf.shape[0], 3 * inner, device=xf.device, dtype=BF16) if fold else None
+    qb_out = qkvb[:, :inner] if fold else None
+    kvb_out = qkvb[:, inner:] if fold else None
     if split:
         x1f, x1b, x1s, _, _ = K.peg_fwd_x32(xf.detach().contiguous(), geo.B, geo.T, geo.Hg, geo.Wg, d(peg_w),
                                             d(peg_b), geo.mode, want_x3=True)
-        xn, _, m1, r1, xns = K.layernorm_fwd(x1f, norm_g, None, 1e-5, out_bf16=True, out_x3=True)   # q side only
-        q32, q = K.linear_x3(xns, x3_weight(Wq), want_bf16=True)
-        kv32, kv = K.linear_x3(x1s, x3_weight(Wkv), want_bf16=True)   # K / V from the un-normalised x
+        xn, _, m1, r1, xns = K.layernorm_fwd(x1f, norm_g, None, 1e-5, out_bf16=not fold, out_x3=True)  # q side
+        q32, q = K.linear_x3(xns, x3_weight(Wq), want_bf16=True, out_bf16=qb_out)
+        kv32, kv = K.linear_x3(x1s, x3_weight(Wkv), want_bf16=True, out_bf16=kvb_out)   # K / V: un-normalised x
         del xns, x1s
-        return _vit_layer_tail_f32(ctx, x1f, x1b, xn, m1, r1, q32, q, kv32, kv, xb, bias_u, geo, peg_w, peg_b, norm_g,
-                                   q_scale, k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1, W2, split=True)
-    x1f = K.peg_fwd_f32(xf.detach().contiguous(), geo.B, geo.T, geo.Hg, geo.Wg, d(peg_w), d(peg_b), geo.mode)
-    x1b = K.cast_bf16(x1f)
-    xn, xnf, m1, r1 = K.layernorm_fwd(x1f, norm_g, None, 1e-5, out_bf16=True, out_f32=True)   # q side only
-    q32, q = K.linear_f32(xnf, d(Wq), want_bf16=True)
-    kv32, kv = K.linear_f32(x1f, d(Wkv), want_bf16=True)          # K / V from the un-normalised x
-    del xnf
+    else:
+        x1f = K.peg_fwd_f32(xf.detach().contiguous(), geo.B, geo.T, geo.Hg, geo.Wg, d(peg_w), d(peg_b), geo.mode)
+        x1b = K.cast_bf16(x1f)
+        xn, xnf, m1, r1 = K.layernorm_fwd(x1f, norm_g, None, 1e-5, out_bf16=not fold, out_f32=True)   # q side
+        q32, q = K.linear_f32(xnf, d(Wq), want_bf16=True, out_bf16=qb_out)
+        kv32, kv = K.linear_f32(x1f, d(Wkv), want_bf16=True, out_bf16=kvb_out)   # K / V from the un-normalised x
+        del xnf
+    ctx.fold = fold
+    ctx.fold_w = qkv_fold_pack(Wq, norm_g, Wkv, bf(Wkv), q_scale, k_scale)[:2] if fold else None
     return _vit_layer_tail_f32(ctx, x1f, x1b, xn, m1, r1, q32, q, kv32, kv, xb, bias_u, geo, peg_w, peg_b, norm_g,
-                               q_scale, k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1, W2, split=False)
+                               q_scale, k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1, W2, split=split)
 
 
 def _vit_layer_tail_f32(ctx, x1f, x1b, xn, m1, r1, q32, q, kv32, kv, xb, bias_u, geo, peg_w, peg_b, norm_g, q_scale,
@@ -898,8 +915,11 @@ def _vit_layer_tail_f32(ctx, x1f, x1b, xn, m1, r1, q32, q, kv32, kv, xb, bias_u,
     H, dh = geo.heads, geo.dim_head
     inner = H * dh
     d = lambda t: t.detach()    # noqa: E731
-    qn32 = K.l2norm_scale_fwd_f32(q32, H, dh, d(q_scale))
-    kn32 = K.l2norm_scale_fwd_f32(kv32[:, :inner], H, dh, d(k_scale))
+    # the l2norms write the bf16 copies the backward reads (and the bf16 attention below) themselves
+    qn = torch.empty(q32.shape[0], inner, device=q32.device, dtype=BF16)
+    kn = torch.empty(q32.shape[0], inner, device=q32.device, dtype=BF16)
+    qn32 = K.l2norm_scale_fwd_f32(q32, H, dh, d(q_scale), out_bf16=qn)
+    kn32 = K.l2norm_scale_fwd_f32(kv32[:, :inner], H, dh, d(k_scale), out_bf16=kn)
     L, nseq, seq = geo.seq()
     use_bias = bias_u is not None
     grid = (geo.Hg, geo.Wg) if use_bias else (0, 0)
@@ -907,13 +927,11 @@ def _vit_layer_tail_f32(ctx, x1f, x1b, xn, m1, r1, q32, q, kv32, kv, xb, bias_u,
         # x3 attention: O straight as to_out's fp16 pair, plus the bf16 O / LSE the backward reads
         os_, o, lse = K.attn_fwd_x3(qn32, kn32, kv32[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
                                     bias_u=bias_u if use_bias else None, grid=grid)
-        qn, kn = K.cast_bf16(qn32), K.cast_bf16(kn32)
         del q32, qn32, kn32
         o32 = None
     else:
         o32 = K.attn_fwd_f32(qn32, kn32, kv32[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
                              bias_u=bias_u if use_bias else None, grid=grid)
-        qn, kn = K.cast_bf16(qn32), K.cast_bf16(kn32)
         del q32, qn32, kn32
         o, lse = K.attn_fwd(qn, kn, kv[:, inner:], L=L, H=H, D=dh, nseq=nseq, scale=8.0, seq=seq,
                             bias_u=bias_u if use_bias else None, grid=grid)
@@ -941,6 +959,7 @@ def _vit_layer_tail_f32(ctx, x1f, x1b, xn, m1, r1, q32, q, kv32, kv, xb, bias_u,
     ctx.geo = geo
     ctx.use_bias = use_bias
     ctx.params = (peg_w, peg_b, norm_g, q_scale, k_scale, Wq, Wkv, Wo, ff_w, ff_b, W1, W2)
+    # (ctx.fold / fold_w set by _vit_layer_forward_f32; with the fold xn is None)
     ctx.save_for_backward(xb, x1b, m1, r1, xn, q, kv, qn, kn, o, lse, x2b, m2, r2, xn2, h, g,
                           bias_u if use_bias else torch.empty(0), bf(Wq), bf(Wkv), bf(Wo), pack_ff1(W1), pack_ff2(W2))
     ctx.mark_non_differentiable(x3b)
@@ -1130,8 +1149,11 @@ class ImageProjFn(torch.autograd.Function):
     def forward(ctx, pooled, pooled_b, W, Wb):
         ctx.save_for_backward(pooled_b, Wb)
         ctx.W = W
-        if precise_f32() or precise_split():   # the precise towers' projection: exact f32 (split-K f32 MFMA)
-            return K.slinear(pooled.detach().contiguous(), W.detach())
+        if precise_f32() or precise_split():
+            # the precise towers' projection in f32: the HBM-streaming skinny GEMM on the f32 weight
+            # (ctclip_skinny_sgemm, an f32 fma per product; 604 MB read once), else split-K f32 MFMA
+            out = K.skinny_linear(pooled.detach().contiguous(), W.detach()) if _SKINNY_PROJ else None
+            return out if out is not None else K.slinear(pooled.detach().contiguous(), W.detach())
         # the HBM-streaming skinny GEMM (csrc/proj.hip): the 302 MB weight read once at ~HBM speed
         # (the generic split-K 128-row MFMA tile ran at 0.85 TB/s at M = 8, round 4)
         if _SKINNY_PROJ:

@@ -804,18 +804,20 @@ def peg_fwd_stats(xb, xf, B, T, H, W, weight, bias, mode, eps=1e-5):
 
 
 def skinny_linear(x, w):
-    """y[M, N] f32 = x[M, K] @ w[N, K]^T for M <= 16 rows, both bf16 K-contiguous, through the
-    HBM-streaming skinny GEMM (ctclip_skinny_gemm: w read once, partial sums per k-slice reduced in
-    a fixed order).  Returns None when the shape does not qualify."""
+    """y[M, N] f32 = x[M, K] @ w[N, K]^T for M <= 16 rows, both bf16 (ctclip_skinny_gemm) or both f32
+    (ctclip_skinny_sgemm, an f32 fma per product) K-contiguous, through the HBM-streaming skinny GEMM
+    (w read once, partial sums per k-slice reduced in a fixed order).  Returns None when the shape
+    does not qualify."""
     M, Kd = x.shape
     N = w.shape[0]
-    if x.dtype != BF16 or w.dtype != BF16 or x.stride(1) != 1 or w.stride(1) != 1 or w.shape[1] != Kd:
+    if x.dtype != w.dtype or x.dtype not in (BF16, F32) or x.stride(1) != 1 or w.stride(1) != 1 or w.shape[1] != Kd:
         return None
-    ns = _lib.lib().ctclip_skinny_gemm_slices(M, N, Kd)
+    name = 'ctclip_skinny_gemm' if x.dtype == BF16 else 'ctclip_skinny_sgemm'
+    ns = getattr(_lib.lib(), name + '_slices')(M, N, Kd)
     if ns <= 0:
         return None
     slabs = torch.empty(ns, M, N, device=x.device, dtype=F32)
-    call('ctclip_skinny_gemm', ptr(x), x.stride(0), ptr(w), w.stride(0), M, N, Kd, ptr(slabs), ns, stream_ptr())
+    call(name, ptr(x), x.stride(0), ptr(w), w.stride(0), M, N, Kd, ptr(slabs), ns, stream_ptr())
     out = torch.empty(M, N, device=x.device, dtype=F32)
     reduce_slabs(slabs, out)
     return out
@@ -1382,23 +1384,30 @@ def peg_fwd_f32(x, B, T, H, W, weight, bias, mode):
     return out
 
 
-def l2norm_scale_fwd_f32(x, H, D, scale):
+def l2norm_scale_fwd_f32(x, H, D, scale, out_bf16=None):
+    """f32 l2norm * scale per head; out_bf16: also write its bf16 copy there ([rows, H D] view)."""
     out = torch.empty(x.shape[0], H * D, device=x.device, dtype=F32)
-    call('ctclip_l2norm_scale_fwd_f32', ptr(x), x.stride(0), x.shape[0], H, D, ptr(scale), ptr(out), out.stride(0),
-         stream_ptr())
+    call('ctclip_l2norm_scale_fwd_f32b', ptr(x), x.stride(0), x.shape[0], H, D, ptr(scale), ptr(out), out.stride(0),
+         ptr(out_bf16), out_bf16.stride(0) if out_bf16 is not None else 0, stream_ptr())
     return out
 
 
-def linear_f32(x, w, *, bias=None, residual=None, want_bf16=False, alpha=1.0):
+def linear_f32(x, w, *, bias=None, residual=None, want_bf16=False, alpha=1.0, out_bf16=None):
     """Exact-f32 y[M, N] = alpha x[M, K] @ w[N, K]^T (+ bias) (+ residual f32) on the f32 MFMA GEMM
-    (ctclip_sgemm_tn; one ascending-k fma chain per output).  Returns (y f32, bf16 copy or None)."""
+    (ctclip_sgemm_tn; one ascending-k fma chain per output).  Returns (y f32, bf16 copy or None);
+    out_bf16: the bf16 copy goes into this [M, N] view."""
     M, Kd = x.shape
     N = w.shape[0]
     assert w.shape[1] == Kd and x.dtype == F32 and w.dtype == F32 and x.stride(1) == 1 and w.stride(1) == 1
     y = torch.empty(M, N, device=x.device, dtype=F32)
-    yb = torch.empty(M, N, device=x.device, dtype=BF16) if want_bf16 else None
+    yb = out_bf16
+    if yb is not None:
+        assert yb.dtype == BF16 and yb.shape == (M, N) and yb.stride(1) == 1
+    elif want_bf16:
+        yb = torch.empty(M, N, device=x.device, dtype=BF16)
     a = _lib.SgemmTnArgs(M=M, N=N, K=Kd, A=ptr(x), lda=x.stride(0), B=ptr(w), ldb=w.stride(0), C=ptr(y), ldc=N,
-                         C2=ptr(yb), ldc2=N, C3=None, ldc3=0, bias=ptr(bias), R=ptr(residual),
+                         C2=ptr(yb), ldc2=yb.stride(0) if yb is not None else N, C3=None, ldc3=0, bias=ptr(bias),
+                         R=ptr(residual),
                          ldr=residual.stride(0) if residual is not None else 0, alpha=float(alpha), act=0)
     call('ctclip_sgemm_tn', _lib.ctypes.byref(a), stream_ptr())
     return y, yb
@@ -1489,15 +1498,21 @@ def _x3_args(xs, ws, C, alpha):
     return a
 
 
-def linear_x3(xs, ws, *, bias=None, residual=None, want_bf16=False, alpha=1.0 / X3_WSCALE, tag=None, flops=None):
+def linear_x3(xs, ws, *, bias=None, residual=None, want_bf16=False, alpha=1.0 / X3_WSCALE, tag=None, flops=None,
+              out_bf16=None):
     """y [M, N] f32 = alpha xs . ws^T (+ bias) (+ f32 residual) on the x3 GEMM, xs / ws split-fp16
-    pairs ([M, K] activations, [N, K] weights packed by pack_rows_x3); returns (y, bf16 copy or None)."""
+    pairs ([M, K] activations, [N, K] weights packed by pack_rows_x3); returns (y, bf16 copy or None).
+    out_bf16: write the bf16 copy into this [M, N] view (e.g. columns of a wider buffer)."""
     M, N = xs[0].shape[0], ws[0].shape[0]
     y = torch.empty(M, N, device=xs[0].device, dtype=F32)
-    yb = torch.empty(M, N, device=y.device, dtype=BF16) if want_bf16 else None
+    yb = out_bf16
+    if yb is not None:
+        assert yb.dtype == BF16 and yb.shape == (M, N) and yb.stride(1) == 1
+    elif want_bf16:
+        yb = torch.empty(M, N, device=y.device, dtype=BF16)
     a = _x3_args(xs, ws, y, alpha)
     a.c_f32 = 1
-    a.C2, a.ldc2 = ptr(yb), N if yb is not None else 0
+    a.C2, a.ldc2 = ptr(yb), yb.stride(0) if yb is not None else 0
     a.bias = ptr(bias)
     if residual is not None:
         assert residual.dtype == F32 and residual.shape == (M, N) and residual.stride(1) == 1

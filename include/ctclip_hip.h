@@ -232,6 +232,11 @@ int ctclip_lnfold_wgrad(const float* G, int64_t ldg, const float* u, const float
 int ctclip_skinny_gemm_slices(int64_t M, int64_t N, int64_t K);
 int ctclip_skinny_gemm(const void* A, int64_t lda, const void* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
                        float* slabs, int32_t nslices, void* stream);
+/* Round 6: the f32 twin (A, B f32, K % 128 == 0, lda / ldb % 4 == 0; v_mfma_f32_16x16x4_f32, an f32
+ * fma per product) for the precise image towers' projection: the 604 MB f32 weight streamed once. */
+int ctclip_skinny_sgemm_slices(int64_t M, int64_t N, int64_t K);
+int ctclip_skinny_sgemm(const float* A, int64_t lda, const float* B, int64_t ldb, int64_t M, int64_t N, int64_t K,
+                        float* slabs, int32_t nslices, void* stream);
 /* split-K slab reduction into a row-mapped, column-cropped f32 destination: dst[map[r]][c] (+)=
  * sum_z slabs[z][r][c] for c < cols <= ld (rows with map[r] < 0 dropped; map NULL = identity).
  * Bit-identical to ctclip_reduce_slabs into a temporary followed by ctclip_unpack_rows (the packed
@@ -509,6 +514,10 @@ int ctclip_peg_fwd_f32(const float* x, int64_t B, int32_t T, int32_t H, int32_t 
                        const float* weight, const float* bias, int32_t mode, float* out, void* stream);
 int ctclip_l2norm_scale_fwd_f32(const float* x, int64_t ldx, int64_t rows, int32_t H, int32_t D,
                                 const float* scale, float* y, int64_t ldy, void* stream);
+/* Round 6: the same with an optional bf16 copy y_bf16 (ldyb % 4 == 0, 8-B aligned; D = 32 or 64) --
+ * the precise 'split' tower's q / k for the bf16 backward, without a separate cast pass. */
+int ctclip_l2norm_scale_fwd_f32b(const float* x, int64_t ldx, int64_t rows, int32_t H, int32_t D,
+                                 const float* scale, float* y, int64_t ldy, void* y_bf16, int64_t ldyb, void* stream);
 int ctclip_geglu_f32(const float* h, int64_t ldh, int64_t rows, int32_t inner, float* g, int64_t ldg,
                      void* stream);
 /* Round 4: the f32 tower trains (its forward feeds the bf16 backward kernels) and its Linears run on

@@ -65,6 +65,11 @@ def test_l2norm_geglu_patch_f32(K):
     y = K.l2norm_scale_fwd_f32(x[:, :256], 8, 32, sc)
     ref = F.normalize(x[:, :256].double().reshape(-1, 8, 32), dim=-1) * sc.double()
     assert rel(y.reshape(-1, 8, 32), ref) < 2e-7
+    # with the bf16 copy written into columns of a wider buffer (the precise towers' q | k | v image)
+    yb = torch.zeros(999, 768, device=dev, dtype=torch.bfloat16)
+    y2 = K.l2norm_scale_fwd_f32(x[:, :256], 8, 32, sc, out_bf16=yb[:, 256:512])
+    assert torch.equal(y2, y) and torch.equal(yb[:, 256:512], y.bfloat16())
+    assert not yb[:, :256].any() and not yb[:, 512:].any()
     h = torch.randn(999, 2 * 1365, device=dev)
     g = K.geglu_f32(h)
     hd = h.double()

@@ -197,3 +197,20 @@ def test_skinny_linear(K, M, N, K_):
     if K_ <= 4096:      # sums stay exact in f32
         assert torch.equal(K.skinny_linear(xi, wi), (xi.double() @ wi.double().t()).float())
     assert K.skinny_linear(torch.zeros(17, K_, device='cuda').bfloat16(), w) is None
+
+
+@pytest.mark.parametrize('M,N,K_', [(8, 512, 294912), (3, 128, 128 * 5)])
+def test_skinny_linear_f32(K, M, N, K_):
+    """The f32 twin (ctclip_skinny_sgemm: the precise image towers' projection): f32 accuracy against
+    f64 (an f32 fma per product, f32 slabs), integer-exact data for the k layout, deterministic."""
+    torch.manual_seed(5)
+    x = torch.randn(M, K_, device='cuda')
+    w = torch.randn(N, K_, device='cuda') * 0.01
+    y = K.skinny_linear(x, w)
+    assert y is not None and y.dtype == torch.float32
+    assert _rel(y, x.double() @ w.double().t()) < 1e-6
+    assert torch.equal(K.skinny_linear(x, w), y)
+    xi = (torch.arange(M * K_, device='cuda').reshape(M, K_) % 5 - 2).float()
+    wi = ((torch.arange(N * K_, device='cuda').reshape(N, K_) * 7) % 3 - 1).float()
+    assert torch.equal(K.skinny_linear(xi, wi), (xi.double() @ wi.double().t()).float())
+    assert K.skinny_linear(x[:, :K_ - 4], w[:, :K_ - 4]) is None     # K % 128 != 0
