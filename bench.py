@@ -47,6 +47,8 @@ def parse():
                     help="run the whole bench in the f32 image-tower mode (= --vit-precision f32)")
     ap.add_argument('--vit-precision', default=None, choices=['bf16', 'f32', 'split'],
                     help='run the whole bench in this image-tower mode (precise.set_vit_precision; profiling)')
+    ap.add_argument('--no-eval-forward', action='store_true',
+                    help='skip the eval-mode forward measurement (vit_forward_eval; e.g. under a profiler)')
     ap.add_argument('--no-precise', action='store_true',
                     help='skip the precise image-tower measurements (precise_split_tower / precise_f32_tower)')
     ap.add_argument('--cpu-batch', type=int, default=2)
@@ -333,7 +335,7 @@ def main():
     # the eval-mode 3D-ViT forward (zero-shot inference / VisionFeatureExtractor): encode + VQ + pool +
     # projection under no_grad, no backward-only tensors written (functional.ViTLayerFn lean path)
     vit_eval_ms = None
-    if not args.fp8:
+    if not args.fp8 and not args.no_eval_forward:
         model.eval()
         W = model.to_visual_latent.weight
         with torch.no_grad():

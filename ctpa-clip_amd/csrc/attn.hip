@@ -236,7 +236,9 @@ __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(
 //   ub[nbins]  bias table * log2 e        (BIAS)
 //   kb[Lp]     position table             (BIAS)
 //   madd[pp][Lp] additive key validity     (0 / -inf: padding past L, key mask)
-template <bool BIAS, int NTH = NT>
+// REV (the C-init forward below): the table reversed and in units of the raw score, ub[i] =
+// bias[nbins - 1 - i] / scale, so 4 keys of one grid row read 4 ascending entries
+template <bool BIAS, int NTH = NT, bool REV = false>
 __device__ __forceinline__ void load_tables(const AP& p, char* tab, int Lp, int tid, int h, float*& ub, int*& kb,
                                             float*& madd) {
   char* t = tab;
@@ -245,7 +247,18 @@ __device__ __forceinline__ void load_tables(const AP& p, char* tab, int Lp, int 
     t += ((p.nbins + 3) & ~3) * 4;   // keep kb / madd 16-B aligned for the vector reads
     kb = (int*)t;
     t += Lp * 4;
-    for (int i = tid; i < p.nbins; i += NTH) ub[i] = p.bias_u[(int64_t)h * p.nbins + i] * LOG2E;
+    if constexpr (REV) {
+      // (the RUN shapes have no padded / masked keys: no validity table; the position table, read
+      // once per query block, from kb_fast instead of two integer divisions per entry)
+      const float isc = 1.f / p.scale;   // exact for the power-of-two scale 8
+      for (int i = tid; i < p.nbins; i += NTH) ub[i] = p.bias_u[(int64_t)h * p.nbins + p.nbins - 1 - i] * isc;
+      const KbFast f = kb_fast_init(p);
+      for (int i = tid; i < Lp; i += NTH) kb[i] = kb_fast(f, i);
+      madd = (float*)t;
+      return;
+    } else {
+      for (int i = tid; i < p.nbins; i += NTH) ub[i] = p.bias_u[(int64_t)h * p.nbins + i] * LOG2E;
+    }
     for (int i = tid; i < Lp; i += NTH) kb[i] = i < p.L ? kb_of(p, i) : 0;
   }
   madd = (float*)t;
@@ -284,8 +297,17 @@ __device__ __forceinline__ void load_tables(const AP& p, char* tab, int Lp, int 
 #ifndef CTCLIP_ATTN_FWD_SWZ
 #define CTCLIP_ATTN_FWD_SWZ 0
 #endif
-template <int D, bool BIAS, int W = (BIAS ? 12 : NW), bool RUN = false, int QB = 1, bool SMAX = false>
+// CINIT (RUN shapes, round 6): the score chain with the least vector work per score -- the bias
+// enters as the MFMA's C operand (read from the reversed, 1/scale table straight into the
+// accumulator), so score -> probability is one v_fma (scale log2 e, minus the running max) and one
+// v_exp; the row sums come from one more MFMA per key chunk (an all-ones A operand against the
+// bf16 probabilities, i.e. the sum of exactly the P the PV product uses) instead of a v_add per
+// score; the lazy-rescale logic is unchanged.  Per score: fma + exp + 1/4 max3 + 1/2 cvt_pk
+// against fma + max + sub + exp + add + 1/2 cvt_pk.
+template <int D, bool BIAS, int W = (BIAS ? 12 : NW), bool RUN = false, int QB = 1, bool SMAX = false,
+          bool CINIT = false>
 __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
+  static_assert(!CINIT || (RUN && !SMAX && BIAS), "CINIT: the RUN shapes' online-max forward");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // head dim 32: swizzled 64-B-row K / V images (kv_swz); 64: the padded rows
   constexpr bool SWZ = D == 32 && CTCLIP_ATTN_FWD_SWZ;
@@ -317,7 +339,8 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
   float* ub = nullptr;
   int* kb = nullptr;
   float* madd = nullptr;
-  load_tables<BIAS, NTH>(p, smem + p.pp * pair_bytes, Lp, tid, blockIdx.x % p.H, ub, kb, madd);  // pp == 1 with BIAS
+  load_tables<BIAS, NTH, CINIT>(p, smem + p.pp * pair_bytes, Lp, tid, blockIdx.x % p.H, ub, kb,
+                                madd);  // pp == 1 with BIAS
   __syncthreads();
   const int pair = blockIdx.x * p.pp + pair_local;
   if (pair >= p.nseq * p.H) return;
@@ -437,6 +460,96 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
           }
         }
       }
+    } else if constexpr (CINIT) {
+      const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
+      f32x4 osum[QB];
+      int cqr[QB];
+      // per block: nm = -m (log2 units) and the raw-score threshold (m + lazy) / sc2 of the lazy
+      // test, both refreshed only when the block rescales (-inf before the first chunk: rescale)
+      float nm[QB], mlz[QB];
+#pragma unroll
+      for (int u = 0; u < QB; ++u) {
+        m[u] = -INFINITY;
+        nm[u] = 0.f;
+        mlz[u] = -INFINITY;
+        osum[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        cqr[u] = p.nbins - 1 - cq[u];          // reversed-table index of key 0's bin offset
+      }
+      const float isc2 = 1.f / sc2;
+      for (int kc = 0; kc < Lp; kc += 32) {
+        bf16x8 kf[2][KK];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+          for (int kk = 0; kk < KK; ++kk) kf[bi][kk] = kfrag(Kimg, kc + 16 * bi, kk);
+        int kx[2];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi) kx[bi] = kb_fast(kbf, kc + 16 * bi + 4 * g);
+        f32x4 sa[QB][2];
+#pragma unroll
+        for (int u = 0; u < QB; ++u)
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi) {
+            const float* up = ub + (kx[bi] + cqr[u]);   // up[r] = bias(q, k0 + r) / scale
+            sa[u][bi] = f32x4{up[0], up[1], up[2], up[3]};
+#pragma unroll
+            for (int kk = 0; kk < KK; ++kk)
+              sa[u][bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[bi][kk], qf[u][kk], sa[u][bi], 0, 0, 0);
+          }
+        // chunk maxima (the raw MFMA outputs are not known canonical, so fmaxf would add a
+        // canonicalising v_max per value: v_max3 directly) and ONE wave-uniform test for all QB
+        // blocks -- after the first chunks no block moves its max by more than p.lazy
+        float cmax[QB];      // raw-score units (q.k + bias / scale)
+        bool need = p.lazy <= 0.f;
+#pragma unroll
+        for (int u = 0; u < QB; ++u) {
+          float t1, t2, t3, c;
+          asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(t1) : "v"(sa[u][0][0]), "v"(sa[u][0][1]), "v"(sa[u][0][2]));
+          asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(t2) : "v"(sa[u][0][3]), "v"(sa[u][1][0]), "v"(sa[u][1][1]));
+          asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(t3) : "v"(sa[u][1][2]), "v"(sa[u][1][3]), "v"(t1));
+          asm volatile("v_max_f32 %0, %1, %2" : "=v"(c) : "v"(t2), "v"(t3));
+          cmax[u] = c;
+          need = need || c > mlz[u];
+        }
+        const bool resc = __builtin_amdgcn_readfirstlane((int)__any(need)) != 0;
+        if (resc) {
+#pragma unroll
+          for (int u = 0; u < QB; ++u) {
+            float c = cmax[u] * sc2;                               // log2 units, as m
+            c = fmaxf(c, __shfl_xor(c, 16, 64));
+            c = fmaxf(c, __shfl_xor(c, 32, 64));
+            const float mnew = fmaxf(m[u], c);
+            const float ms = mnew == -INFINITY ? 0.f : mnew;
+            const float alpha = fexp2(m[u] - ms);
+            m[u] = mnew;
+            nm[u] = -ms;
+            mlz[u] = (mnew + p.lazy) * isc2;
+#pragma unroll
+            for (int d = 0; d < DB; ++d) o[u][d] *= alpha;
+            osum[u] *= alpha;
+          }
+        }
+        bf16x8 pb[QB];
+#pragma unroll
+        for (int u = 0; u < QB; ++u) {
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sa[u][bi][r] = fexp2(fmaf(sa[u][bi][r], sc2, nm[u]));
+          pb[u] = pack_perm(sa[u][0], sa[u][1]);
+        }
+#pragma unroll
+        for (int d = 0; d < DB; ++d) {
+          const bf16x8 vf = vfrag(Vimg, kc, d * 16);
+#pragma unroll
+          for (int u = 0; u < QB; ++u) o[u][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[u], o[u][d], 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < QB; ++u) osum[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, pb[u], osum[u], 0, 0, 0);
+      }
+      // every row of the all-ones product is the query's full sum: no cross-lane reduction below
+#pragma unroll
+      for (int u = 0; u < QB; ++u) lsum[u] = osum[u][0];
     } else {
 #pragma unroll
     for (int u = 0; u < QB; ++u) m[u] = -INFINITY;
@@ -554,8 +667,10 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
 #pragma unroll
     for (int u = 0; u < QB; ++u) {
       float ls = lsum[u];
-      ls += __shfl_xor(ls, 16, 64);
-      ls += __shfl_xor(ls, 32, 64);
+      if constexpr (!CINIT) {
+        ls += __shfl_xor(ls, 16, 64);
+        ls += __shfl_xor(ls, 32, 64);
+      }
       const float inv = ls > 0.f ? 1.f / ls : 0.f;
       if (qv[u]) {
 #pragma unroll
@@ -1024,6 +1139,11 @@ constexpr int DQD_W = 8, DQD_NT = DQD_W * 64, DQD_KP = 2;
 #ifndef CTCLIP_ATTN_DIAG_BIN
 #define CTCLIP_ATTN_DIAG_BIN 1
 #endif
+// round 6: the score MFMA's accumulator input is the CPB bias itself (the forward's C-init chain:
+// reversed 1/scale table, one fma with the query's -lse per score instead of fma + sub)
+#ifndef CTCLIP_ATTN_DQ_CINIT
+#define CTCLIP_ATTN_DQ_CINIT 1
+#endif
 template <int LF, int KP = DQD_KP>
 __global__ __launch_bounds__(4 * KP * 64) void attn_bwd_dq_bias_dma_kernel(AP p, int nfc) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1038,7 +1158,14 @@ __global__ __launch_bounds__(4 * KP * 64) void attn_bwd_dq_bias_dma_kernel(AP p,
   float* ub = (float*)(smem + 2 * BUF);
   const int nb4 = (p.nbins + 3) & ~3;
   int* kb = (int*)(ub + nb4);
+#if CTCLIP_ATTN_DQ_CINIT
+  {
+    const float isc = 1.f / p.scale;   // the forward's table (load_tables REV), bit for bit
+    for (int i = tid; i < p.nbins; i += NTH) ub[i] = p.bias_u[(int64_t)h * p.nbins + p.nbins - 1 - i] * isc;
+  }
+#else
   for (int i = tid; i < p.nbins; i += NTH) ub[i] = p.bias_u[(int64_t)h * p.nbins + i] * LOG2E;
+#endif
   for (int i = tid; i < L; i += NTH) kb[i] = kb_of(p, i);
   const int g = lane >> 4, li = lane & 15;
   const int q = qg * 64 + qsub * 16 + li;   // < L: L % 64 == 0
@@ -1078,6 +1205,7 @@ __global__ __launch_bounds__(4 * KP * 64) void attn_bwd_dq_bias_dma_kernel(AP p,
   __builtin_amdgcn_s_barrier();   // tables (frame f0's DMA may still be in flight)
   __builtin_amdgcn_sched_barrier(0);
   const int cq = kb[q] + boff(p);
+  [[maybe_unused]] const int cqr = p.nbins - 1 - cq;   // (C-init: reversed-table index of key 0)
   [[maybe_unused]] const KbFast kbf = kb_fast_init(p);
   for (int s = f0; s < f1; ++s) {
     const int b = (s - f0) & 1;
@@ -1127,6 +1255,29 @@ __global__ __launch_bounds__(4 * KP * 64) void attn_bwd_dq_bias_dma_kernel(AP p,
     for (int ci = 0; ci < NCP; ++ci) {
       const int kc = (c_begin + ci) * 32;
       f32x4 sa[2], da[2];
+#if CTCLIP_ATTN_DQ_CINIT
+      (void)cS;
+      const float nl2 = -l2;
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi) {
+        const float* up = ub + (kb[kc + 16 * bi + 4 * g] + cqr);   // up[r] = bias(q, k0 + r) / scale
+        sa[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Kimg, kc + 16 * bi, lane), qc,
+                                                         f32x4{up[0], up[1], up[2], up[3]}, 0, 0, 0);
+        da[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Vimg, kc + 16 * bi, lane), dc, cD, 0, 0, 0);
+      }
+#pragma unroll
+      for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#if CTCLIP_ATTN_CFOLD_DQ
+          const float ds = fexp2(fmaf(sa[bi][r], sc2, nl2)) * da[bi][r];
+#else
+          const float ds = fexp2(fmaf(sa[bi][r], sc2, nl2)) * (da[bi][r] - dl);
+#endif
+          acc[ci][bi][r] += ds;
+          sa[bi][r] = ds;
+        }
+#else
 #pragma unroll
       for (int bi = 0; bi < 2; ++bi) {
         sa[bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rowfrag_sw(Kimg, kc + 16 * bi, lane), qc, cS, 0, 0, 0);
@@ -1156,6 +1307,7 @@ __global__ __launch_bounds__(4 * KP * 64) void attn_bwd_dq_bias_dma_kernel(AP p,
           sa[bi][r] = ds;   // the score scale is applied once per dQ output below (exact for 8)
         }
       }
+#endif
       const bf16x8 dsb = pack_perm(sa[0], sa[1]);
 #pragma unroll
       for (int d = 0; d < DB; ++d)
@@ -1586,6 +1738,8 @@ void set_attrs() {
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<32, true, 12, true, 3, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)attn_fwd_kernel<32, true, 12, true, 3, false, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_kernel<32, true, 12, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
 }
@@ -1653,6 +1807,8 @@ int g_fwd_qb = -1;
 // key norms and bias-table range over 576 rows + 2,209 bins, a block reduction and a barrier for
 // each of 1,536 workgroups) costs more than the per-chunk max / rescale it removes -- so off
 int g_fwd_smax = -1;
+// the C-init score chain (attn_fwd_kernel CINIT; CTCLIP_ATTN_FWD_CINIT=0 restores the round-5 kernel)
+int g_fwd_cinit = -1;
 
 template <int D>
 void launch_fwd(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
@@ -1663,8 +1819,11 @@ void launch_fwd(const AP& p, dim3 grid, size_t lds, hipStream_t st) {
       if (g_fwd_qb < 0) { const char* e = getenv("CTCLIP_ATTN_FWD_QB"); g_fwd_qb = e ? atoi(e) : 3; }
       const int qb = g_fwd_qb;
       if (g_fwd_smax < 0) { const char* e = getenv("CTCLIP_ATTN_FWD_SMAX"); g_fwd_smax = e ? atoi(e) != 0 : 0; }
+      if (g_fwd_cinit < 0) { const char* e = getenv("CTCLIP_ATTN_FWD_CINIT"); g_fwd_cinit = e ? atoi(e) != 0 : 1; }
       if (qb == 3 && g_fwd_smax)
         hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true, 3, true>), grid, dim3(12 * 64), lds, st, p);
+      else if (qb == 3 && g_fwd_cinit)
+        hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true, 3, false, true>), grid, dim3(12 * 64), lds, st, p);
       else if (qb == 3) hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true, 3>), grid, dim3(12 * 64), lds, st, p);
       else if (qb == 2) hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true, 2>), grid, dim3(12 * 64), lds, st, p);
       else hipLaunchKernelGGL((attn_fwd_kernel<D, true, 12, true>), grid, dim3(12 * 64), lds, st, p);
@@ -2178,6 +2337,13 @@ extern "C" int ctclip_attn_set_fwd_smax(int on) {
   if (g_fwd_smax < 0) { const char* e = getenv("CTCLIP_ATTN_FWD_SMAX"); g_fwd_smax = e ? atoi(e) != 0 : 0; }
   const int old = g_fwd_smax;
   g_fwd_smax = on != 0;
+  return old;
+}
+
+extern "C" int ctclip_attn_set_fwd_cinit(int on) {
+  if (g_fwd_cinit < 0) { const char* e = getenv("CTCLIP_ATTN_FWD_CINIT"); g_fwd_cinit = e ? atoi(e) != 0 : 1; }
+  const int old = g_fwd_cinit;
+  g_fwd_cinit = on != 0;
   return old;
 }
 

@@ -219,6 +219,7 @@ _SIGS = {
     'ctclip_attn_fwd_x3': [ctypes.POINTER(AttnArgs), c_vp, c_vp, c_vp, c_vp, c_vp],
     'ctclip_attn_set_fwd_qb': [c_i32],
     'ctclip_attn_set_fwd_smax': [c_i32],
+    'ctclip_attn_set_fwd_cinit': [c_i32],
     'ctclip_patch_ln_f32': [c_vp, c_i32, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_f32, c_vp,
                             c_vp, c_vp, c_i64, c_vp],
     'ctclip_peg_fwd_f32': [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp],

@@ -498,6 +498,9 @@ int ctclip_attn_set_fwd_qb(int qb);
 /* diagnostic: static-bound softmax in the 3-block spatial forward (1) or the online max (0, default:
  * measured faster); see attn.hip.  Returns the previous setting. */
 int ctclip_attn_set_fwd_smax(int on);
+/* the C-init score chain of the 3-block spatial forward (1, default, round 6: the CPB bias as the
+ * MFMA's accumulator input, row sums on the MFMA) or the round-5 chain (0); returns the previous. */
+int ctclip_attn_set_fwd_cinit(int on);
 
 /* ---------------------------------------------------------------- f32 image tower (opt-in)
  * Exact-f32 forward stages of functional.set_vit_precision('f32') (csrc/f32path.hip); the linears

@@ -286,6 +286,10 @@ def test_f32_image_mode_vq_contract(base, mode):
     assert above == 0
     assert dl < 1e-3                  # free-running, the north-star loss tolerance
     assert dlog < 5e-3                # free-running logits: only f32 ties (margin < 1e-6) can flip
+    if mode == 'split':
+        # the split tower (round 6) also resolves the f32 tie as the reference does: the literal
+        # north-star logits bound free-running (4.5e-4 measured)
+        assert dlog < 1e-3 and di < 1e-3
     assert fi < 1e-4 and flog < 1e-3 and fl < 1e-3
     model.train()
 

@@ -650,6 +650,7 @@ def test_attention_fwd_query_blocks_bit_identical(K):
                           seq=(1, L, 0, 1), bias_u=u, grid=(gh, gw))
     outs = []
     old, old_s = lib.ctclip_attn_set_fwd_qb(1), lib.ctclip_attn_set_fwd_smax(0)
+    old_c = lib.ctclip_attn_set_fwd_cinit(0)     # the round-5 score chain: bit-identical across QB
     try:
         for qb in (1, 2, 3):
             lib.ctclip_attn_set_fwd_qb(qb)
@@ -671,3 +672,37 @@ def test_attention_fwd_query_blocks_bit_identical(K):
     finally:
         lib.ctclip_attn_set_fwd_qb(old)
         lib.ctclip_attn_set_fwd_smax(old_s)
+        lib.ctclip_attn_set_fwd_cinit(old_c)
+
+
+@pytest.mark.parametrize('gh', [24, 8])
+def test_attention_fwd_cinit(K, gh):
+    """The C-init spatial forward (round 6: bias as the MFMA accumulator input from the reversed
+    1/scale table, one fma + exp2 per score, row sums by an all-ones MFMA over the bf16 P) against the
+    round-5 chain and the f64 reference: O within bf16 rounding of the old kernel, closer or as close
+    to the reference; the LSE within 2e-3 (the sum of the bf16-rounded P the PV product uses)."""
+    from ctclip_mi355x import _lib
+    torch.manual_seed(6)
+    L, H, D, nseq = gh * gh, 8, 32, 4
+    M = nseq * L
+    u, bins = _cpb_table(H, gh, gh)
+    q = F.normalize(torch.randn(M, H, D, device=dev), dim=-1).reshape(M, H * D).bfloat16()
+    kv = torch.randn(M, 2 * H * D, device=dev)
+    kv[:, :H * D] = F.normalize(kv[:, :H * D].reshape(M, H, D), dim=-1).reshape(M, H * D)
+    kv = kv.bfloat16()
+    lib = _lib.lib()
+    args = dict(L=L, H=H, D=D, nseq=nseq, scale=8.0, seq=(1, L, 0, 1), bias_u=u, grid=(gh, gh))
+    old = lib.ctclip_attn_set_fwd_cinit(0)
+    try:
+        o0, lse0 = K.attn_fwd(q, kv[:, :H * D], kv[:, H * D:], **args)
+        lib.ctclip_attn_set_fwd_cinit(1)
+        o1, lse1 = K.attn_fwd(q, kv[:, :H * D], kv[:, H * D:], **args)
+    finally:
+        lib.ctclip_attn_set_fwd_cinit(old)
+    rows = _gather_rows(1, L, 0, 1, nseq, L)
+    ref = _attn_ref(q.double(), kv[:, :H * D].double(), kv[:, H * D:].double(), rows, H, D, 8.0,
+                    u[:, bins].double())
+    e0, e1 = rel(o0, ref), rel(o1, ref)
+    dl = (lse1 - lse0).abs().max().item()
+    print(f'cinit {gh}x{gh}: O rel vs f64 {e1:.3e} (round-5 chain {e0:.3e}), |dLSE| max {dl:.2e}')
+    assert rel(o1, o0) < 6e-3 and e1 < 1.1 * e0 + 1e-4 and dl < 2e-3

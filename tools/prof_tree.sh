@@ -5,10 +5,10 @@ set -e
 tag=${1:-run}
 export TMPDIR=/tmp
 for tree in new old; do
-  if [ $tree = new ]; then b=bench.py; else b=_ab_old/bench.py; fi
+  if [ $tree = new ]; then b=bench.py; x=--no-eval-forward; else b=_ab_old/bench.py; x=; fi
   rm -rf gpurun_out/prof_${tag}_${tree}
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${tag}_${tree} -o run --output-format rocpd -- \
-    python3 -u $b --steps 5 --warmup 2 --no-cpu-baseline --no-precise > gpurun_out/${tag}_${tree}_prof_bench.log 2>&1
+    python3 -u $b --steps 5 --warmup 2 --no-cpu-baseline --no-precise $x > gpurun_out/${tag}_${tree}_prof_bench.log 2>&1
   db=$(find gpurun_out/prof_${tag}_${tree} -name '*.db' | head -1)
   python tools/rocprof_summary.py "$db" 7 > gpurun_out/${tag}_${tree}_kernel_stats.txt
   rm -rf gpurun_out/prof_${tag}_${tree}
