@@ -464,18 +464,19 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
       const bf16x8 ones = __builtin_bit_cast(bf16x8, make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u));
       f32x4 osum[QB];
       int cqr[QB];
-      // per block: nm = -m (log2 units) and the raw-score threshold (m + lazy) / sc2 of the lazy
-      // test, both refreshed only when the block rescales (-inf before the first chunk: rescale)
-      float nm[QB], mlz[QB];
+      // per block: nm = -m (log2 units, 0 before the first rescale) -- the exponent argument
+      // x = sc2 * score + nm is formed FIRST (one fma per score), and the chunk max / lazy test run
+      // on x: x is an ordinary VALU result, so the max needs no canonicalising v_max per MFMA output
+      // (and no inline asm, whose MFMA read hazards the compiler does not see); the first chunk
+      // always rescales
+      float nm[QB];
 #pragma unroll
       for (int u = 0; u < QB; ++u) {
         m[u] = -INFINITY;
         nm[u] = 0.f;
-        mlz[u] = -INFINITY;
         osum[u] = f32x4{0.f, 0.f, 0.f, 0.f};
         cqr[u] = p.nbins - 1 - cq[u];          // reversed-table index of key 0's bin offset
       }
-      const float isc2 = 1.f / sc2;
       for (int kc = 0; kc < Lp; kc += 32) {
         bf16x8 kf[2][KK];
 #pragma unroll
@@ -496,36 +497,36 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
             for (int kk = 0; kk < KK; ++kk)
               sa[u][bi] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[bi][kk], qf[u][kk], sa[u][bi], 0, 0, 0);
           }
-        // chunk maxima (the raw MFMA outputs are not known canonical, so fmaxf would add a
-        // canonicalising v_max per value: v_max3 directly) and ONE wave-uniform test for all QB
-        // blocks -- after the first chunks no block moves its max by more than p.lazy
-        float cmax[QB];      // raw-score units (q.k + bias / scale)
-        bool need = p.lazy <= 0.f;
+        float cmax[QB];      // chunk max of x, relative to the running max
+        bool need = p.lazy <= 0.f || kc == 0;
 #pragma unroll
         for (int u = 0; u < QB; ++u) {
-          float t1, t2, t3, c;
-          asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(t1) : "v"(sa[u][0][0]), "v"(sa[u][0][1]), "v"(sa[u][0][2]));
-          asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(t2) : "v"(sa[u][0][3]), "v"(sa[u][1][0]), "v"(sa[u][1][1]));
-          asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(t3) : "v"(sa[u][1][2]), "v"(sa[u][1][3]), "v"(t1));
-          asm volatile("v_max_f32 %0, %1, %2" : "=v"(c) : "v"(t2), "v"(t3));
-          cmax[u] = c;
-          need = need || c > mlz[u];
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sa[u][bi][r] = fmaf(sa[u][bi][r], sc2, nm[u]);
+          cmax[u] = fmaxf(fmaxf(fmaxf(sa[u][0][0], sa[u][0][1]), fmaxf(sa[u][0][2], sa[u][0][3])),
+                          fmaxf(fmaxf(sa[u][1][0], sa[u][1][1]), fmaxf(sa[u][1][2], sa[u][1][3])));
+          need = need || cmax[u] > p.lazy;
         }
-        const bool resc = __builtin_amdgcn_readfirstlane((int)__any(need)) != 0;
-        if (resc) {
+        if (__builtin_amdgcn_readfirstlane((int)__any(need)) != 0) {
 #pragma unroll
           for (int u = 0; u < QB; ++u) {
-            float c = cmax[u] * sc2;                               // log2 units, as m
-            c = fmaxf(c, __shfl_xor(c, 16, 64));
+            float c = fmaxf(cmax[u], __shfl_xor(cmax[u], 16, 64));
             c = fmaxf(c, __shfl_xor(c, 32, 64));
-            const float mnew = fmaxf(m[u], c);
-            const float ms = mnew == -INFINITY ? 0.f : mnew;
-            const float alpha = fexp2(m[u] - ms);
-            m[u] = mnew;
-            nm[u] = -ms;
-            mlz[u] = (mnew + p.lazy) * isc2;
+            // the shift d moves the running max to the query's full max (first chunk: the chunk max
+            // itself; later: only upwards)
+            const bool first = m[u] == -INFINITY;
+            const float d = first ? c : fmaxf(c, 0.f);
+            const float alpha = first ? 1.f : fexp2(-d);     // (o, osum are still zero on the first)
+            nm[u] -= d;
+            m[u] = -nm[u];
 #pragma unroll
-            for (int d = 0; d < DB; ++d) o[u][d] *= alpha;
+            for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) sa[u][bi][r] -= d;
+#pragma unroll
+            for (int dd = 0; dd < DB; ++dd) o[u][dd] *= alpha;
             osum[u] *= alpha;
           }
         }
@@ -535,7 +536,7 @@ __global__ __launch_bounds__(W * 64) void attn_fwd_kernel(AP p) {
 #pragma unroll
           for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) sa[u][bi][r] = fexp2(fmaf(sa[u][bi][r], sc2, nm[u]));
+            for (int r = 0; r < 4; ++r) sa[u][bi][r] = fexp2(sa[u][bi][r]);
           pb[u] = pack_perm(sa[u][0], sa[u][1]);
         }
 #pragma unroll

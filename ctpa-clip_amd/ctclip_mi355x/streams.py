@@ -62,6 +62,21 @@ def join_aux(dev):
         torch.cuda.current_stream(dev).wait_stream(s)
 
 
+_STATUS = {}
+
+
+def status_stream(dev):
+    """A stream for the trainer's per-step status-word copy to pinned host memory (None when the
+    auxiliary streams are disabled): the copy is a blit kernel, and on the main stream it waited
+    for CUs behind the text-bucket Adam, holding the next step's first launch back."""
+    if not AUX_ENABLED or dev.type != 'cuda':
+        return None
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx not in _STATUS:
+        _STATUS[idx] = torch.cuda.Stream(idx)
+    return _STATUS[idx]
+
+
 # ------------------------------------------------------------------ deferred text-stream work
 # The text bucket's Adam (trainer.optimizer_step) is HBM-bound, and queued at the end of a step it
 # runs beside the next step's first image-tower kernels -- the HBM-bound patch LayerNorm -- and

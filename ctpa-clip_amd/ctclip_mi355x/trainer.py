@@ -20,6 +20,8 @@ from . import kernels as K
 
 # diagnostic A/B only (CTCLIP_DIAG_TEXT_ADAM=skip | main): NOT the reference's work when 'skip'
 _DIAG_TEXT_ADAM = os.environ.get('CTCLIP_DIAG_TEXT_ADAM', '')
+# the per-step status-word copy on its own stream (streams.status_stream); 0 = on the current stream
+STATUS_COPY_STREAM = os.environ.get('CTCLIP_STATUS_COPY_STREAM', '1') != '0'
 
 
 class FlatParams:
@@ -338,10 +340,19 @@ class CTClipTrainer:
         if not self._guard:
             return
         host = self._ln_host[self.steps % len(self._ln_host)]
-        # the step's skip word (the ranks' summed status): every rank raises for the same step
-        host.copy_(self.skip_ring[self.steps % 4:self.steps % 4 + 1], non_blocking=True)
+        # the step's skip word (the ranks' summed status): every rank raises for the same step.  The
+        # copy goes on its own stream (STATUS_COPY_STREAM), ordered after the current stream's work so
+        # far: the next step's first launches do not queue behind its blit kernel
+        cs = streams.status_stream(self.device) if STATUS_COPY_STREAM else None
         ev = torch.cuda.Event()
-        ev.record()
+        if cs is not None:
+            cs.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(cs):
+                host.copy_(self.skip_ring[self.steps % 4:self.steps % 4 + 1], non_blocking=True)
+                ev.record()
+        else:
+            host.copy_(self.skip_ring[self.steps % 4:self.steps % 4 + 1], non_blocking=True)
+            ev.record()
         self._ln_pending.append((self.steps, ev, host))
 
     def _check_ln(self, block_upto):

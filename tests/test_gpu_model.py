@@ -441,9 +441,9 @@ def test_train_step_bit_reproducible():
                      cbk.cluster_size.clone()])
         del model, tr
     names = ['losses', 'parameters', 'adam m', 'adam v', 'codebook', 'cluster size']
-    for r in runs[1:]:
+    for i, r in enumerate(runs[1:], 1):
         for n, a, b in zip(names, runs[0], r):
-            assert torch.equal(a, b), f'{n} differ: max {(a.double() - b.double()).abs().max().item():.3e}'
+            assert torch.equal(a, b), f'run {i}: {n} differ: max {(a.double() - b.double()).abs().max().item():.3e}'
     assert torch.isfinite(runs[0][0]).all()
 
 
