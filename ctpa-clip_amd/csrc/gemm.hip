@@ -225,20 +225,26 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
       const u16* hr = (const u16*)p.R + bidx * p.sR + gm * p.ldr + tg * 64 + cw;
       u16* dr = (u16*)p.C + bidx * p.sC + gm * p.ldc + tg * 64 + cw;
       float x[8], gt[8], ox[8], og[8];
-      if (p.r_f16) {
+      if (p.r_f16) {   // fp16 h: the derivative form [gelu(gate) | x gelu'(gate)] (gemm256.hip EP 2)
         unpack8h(*(const u32x4*)hr, x);
         unpack8h(*(const u32x4*)(hr + 32), gt);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = bf2f(f2bf(cs[row * CS_LD + cc + j] * p.alpha));
+          ox[j] = d * x[j];
+          og[j] = d * gt[j];
+        }
       } else {
         unpack8(*(const u32x4*)hr, x);
         unpack8(*(const u32x4*)(hr + 32), gt);
-      }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float d = bf2f(f2bf(cs[row * CS_LD + cc + j] * p.alpha));
-        float ge, dge;
-        gelu_erf_and_grad(gt[j], ge, dge);
-        ox[j] = d * ge;
-        og[j] = d * x[j] * dge;
+        for (int j = 0; j < 8; ++j) {
+          const float d = bf2f(f2bf(cs[row * CS_LD + cc + j] * p.alpha));
+          float ge, dge;
+          gelu_erf_and_grad(gt[j], ge, dge);
+          ox[j] = d * ge;
+          og[j] = d * x[j] * dge;
+        }
       }
       *(u32x4*)dr = pack8(ox);
       *(u32x4*)(dr + 32) = pack8(og);
@@ -308,8 +314,8 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[j] += rr[j];
       }
-      // the fp16 GEGLU GEMM (act 2) keeps h in fp16
-      *(u32x4*)Cb = (H16 && p.act == 2) ? pack8h(v) : pack8(v);
+      // the fp16 GEGLU GEMM (act 2) writes h (fp16, derivative form) in the GEGLU pass below
+      if (!(H16 && p.act == 2)) *(u32x4*)Cb = pack8(v);
     }
     if (p.C2 && p.act == 0) *(u32x4*)(p.C2 + bidx * p.sC2 + gm * p.ldc2 + gn) = pack8(v);
   }
@@ -322,14 +328,33 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
       const int64_t gm = m0 + row, gn = n0 / 2 + oc;
       if (gm >= p.M || n0 + grp * 64 >= p.N) continue;
       float v[8];
+      if (H16) {
+        // fp16 h in the derivative form [gelu(gate) | x gelu'(gate)] (the GEGLU backward's two
+        // factors; gemm256.hip EP 2), g from the f32 values
+        float av[8], bv[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x = cs[row * CS_LD + cc + j] * p.alpha;
-        const float gt = cs[row * CS_LD + 32 + cc + j] * p.alpha;
-        // round h as stored (bf16, or fp16 in the fp16 GEMM) first so forward g == geglu(stored h)
-        // bit-for-bit in backward
-        const float xb = H16 ? rh(x) : bf2f(f2bf(x)), gb = H16 ? rh(gt) : bf2f(f2bf(gt));
-        v[j] = gelu_erf(gb) * xb;
+        for (int j = 0; j < 8; ++j) {
+          const float x = cs[row * CS_LD + cc + j] * p.alpha;
+          const float gt = cs[row * CS_LD + 32 + cc + j] * p.alpha;
+          float ge, dge;
+          gelu_erf_and_grad(gt, ge, dge);
+          av[j] = ge;
+          bv[j] = x * dge;
+          v[j] = ge * x;
+        }
+        if (p.C) {
+          u16* hr = (u16*)p.C + bidx * p.sC + gm * p.ldc + n0 + cc;
+          *(u32x4*)hr = pack8h(av);
+          *(u32x4*)(hr + 32) = pack8h(bv);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = cs[row * CS_LD + cc + j] * p.alpha;
+          const float gt = cs[row * CS_LD + 32 + cc + j] * p.alpha;
+          // round h as stored (bf16) first so forward g == geglu(stored h) bit-for-bit in backward
+          v[j] = gelu_erf(bf2f(f2bf(gt))) * bf2f(f2bf(x));
+        }
       }
       *(u32x4*)(p.C2 + bidx * p.sC2 + gm * p.ldc2 + gn) = pack8(v);
     }

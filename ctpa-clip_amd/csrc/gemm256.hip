@@ -903,16 +903,21 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
         // split-fp16 kernel: h stored as fp16 (the GEGLU backward's operand), g from the unrounded
         // f32 h (the x3 forward carries ~22-bit values end to end), stored as its fp16 pair
         // (hi, lo = fp16(g - hi): FF2's A operand) and as bf16 (FF2's weight-gradient operand)
-        store_row_f16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N);
-        float gg[2][4], gh[2][4], gl[2][4];
+        // (h in the derivative form of the fp16 kernel below)
+        float gg[2][4], gh[2][4], gl[2][4], hv[4][4];
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            gg[j][r] = gelu_erf(v[j + 2][r]) * v[j][r];
+            float ge, dge;
+            gelu_erf_and_grad(v[j + 2][r], ge, dge);
+            hv[j][r] = ge;
+            hv[j + 2][r] = v[j][r] * dge;
+            gg[j][r] = ge * v[j][r];
             gh[j][r] = rh(gg[j][r]);
             gl[j][r] = gg[j][r] - gh[j][r];
           }
+        store_row_f16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, hv, g, rok, wcol0, p.N);
         // (cross-lane swaps outside the store guard: every lane takes part)
         const u32x4 dh = pair_swap_h(gh[0], gh[1]), dl = pair_swap_h(gl[0], gl[1]), db = pair_swap(gg[0], gg[1]);
         if (rok && wcol0 < p.N) {
@@ -923,20 +928,33 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
         }
         continue;
       }
-      // fp16 kernel: h stored as fp16, g from the fp16-rounded h (the backward recomputes g' from
-      // the stored h); bf16 kernel: both in bf16
+      // fp16 kernel (round 6): h is stored in its DERIVATIVE form, the two factors the GEGLU backward
+      // multiplies dg by -- [gelu(gate) | x gelu'(gate)] in place of [x | gate] (same bytes), so the
+      // backward epilogue is two multiplies per element instead of an erf + exp per element; g from
+      // the f32 values.  bf16 kernel: h = [x | gate] in bf16, g from the bf16-rounded h (the
+      // backward recomputes gelu from the stored h).
       // (h may be discarded, C = NULL: the eval forward needs only g, round 6)
-      if constexpr (H16) store_row_f16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok && p.C, wcol0, p.N);
-      else store_row_bf16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N, p.epi_lds == 3);
       float gg[2][4];
+      if constexpr (H16) {
+        float hv[4][4];
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float xb = H16 ? rh(v[j][r]) : bf2f(f2bf(v[j][r]));
-          const float gb = H16 ? rh(v[j + 2][r]) : bf2f(f2bf(v[j + 2][r]));
-          gg[j][r] = gelu_erf(gb) * xb;
-        }
+          for (int r = 0; r < 4; ++r) {
+            float ge, dge;
+            gelu_erf_and_grad(v[j + 2][r], ge, dge);
+            hv[j][r] = ge;
+            hv[j + 2][r] = v[j][r] * dge;
+            gg[j][r] = ge * v[j][r];
+          }
+        store_row_f16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, hv, g, rok && p.C, wcol0, p.N);
+      } else {
+        store_row_bf16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, v, g, rok, wcol0, p.N, p.epi_lds == 3);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) gg[j][r] = gelu_erf(bf2f(f2bf(v[j + 2][r]))) * bf2f(f2bf(v[j][r]));
+      }
       const u32x4 d = pair_swap(gg[0], gg[1]);
       if (rok && wcol0 < p.N) {
         if (p.epi_lds == 3) st16_sc1(p.C2 + bidx * p.sC2 + gm * p.ldc2 + (wcol0 >> 1) + pair_coff(g), d);
@@ -1068,19 +1086,24 @@ __device__ __forceinline__ void epilogue_geglu_bwd(const P& p, f32x4 (&acc)[8][4
       for (int r = 0; r < 4; ++r) { v0[r] = acc[i][2 * jp][r] * p.alpha; v1[r] = acc[i][2 * jp + 1][r] * p.alpha; }
       float d[8], x[8], gt[8], ox[8], og[8];
       unpack8(pair_swap(v0, v1), d);
-      if (p.h16) {   // h from the fp16 forward (wave-uniform)
-        unpack8h(hx[b][jp], x);
-        unpack8h(hg[b][jp], gt);
+      if (p.h16) {   // h from the fp16 forward (wave-uniform): the derivative form, two multiplies
+        unpack8h(hx[b][jp], x);    // gelu(gate)
+        unpack8h(hg[b][jp], gt);   // x gelu'(gate)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          ox[k] = d[k] * x[k];
+          og[k] = d[k] * gt[k];
+        }
       } else {
         unpack8(hx[b][jp], x);
         unpack8(hg[b][jp], gt);
-      }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float ge, dge;
-        gelu_erf_and_grad(gt[k], ge, dge);
-        ox[k] = d[k] * ge;
-        og[k] = d[k] * x[k] * dge;
+        for (int k = 0; k < 8; ++k) {
+          float ge, dge;
+          gelu_erf_and_grad(gt[k], ge, dge);
+          ox[k] = d[k] * ge;
+          og[k] = d[k] * x[k] * dge;
+        }
       }
       const int64_t t = t0 + jp;
       if (gm < p.M && t * 32 < p.N) {

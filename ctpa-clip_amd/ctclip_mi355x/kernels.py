@@ -652,7 +652,9 @@ def l2norm_scale_bwd(x, dy, H, D, scale, out, ds_out=None):
 # ----------------------------------------------------------------------------- elementwise
 def matmul_nn_geglu_bwd(dy, w2p, h, out=None):
     """dh = geglu_bwd(dy @ w2p, h) in one GEMM (act 4): dy [M, D] bf16, w2p [D, G] (the padded
-    FeedForward W2), h [M, 2G] the GEGLU pre-activation; returns dh [M, 2G] bf16."""
+    FeedForward W2), h [M, 2G] bf16 the GEGLU pre-activation [x | gate] per 64-column group, or fp16
+    in the derivative form [gelu(gate) | x gelu'(gate)] the fp16 FF1 writes (round 6); returns dh
+    [M, 2G] bf16."""
     M, D = dy.shape
     G = w2p.shape[1]
     assert w2p.shape[0] == D and h.shape == (M, 2 * G)
@@ -664,6 +666,9 @@ def matmul_nn_geglu_bwd(dy, w2p, h, out=None):
 
 
 def geglu_bwd(dg, h, out=None):
+    """Stand-alone GEGLU backward from the bf16 pre-activation h (an fp16 h is in the derivative form
+    and goes through matmul_nn_geglu_bwd)."""
+    assert h.dtype == BF16, h.dtype
     rows, gcols = dg.shape
     if out is None:
         out = torch.empty(rows, 2 * gcols, device=dg.device, dtype=BF16)

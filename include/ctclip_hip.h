@@ -87,8 +87,12 @@ typedef struct {
   int32_t ab_f16;                   /* A and B are IEEE fp16 (both K-contiguous; no B2, split-K,
                                      * act 3-6): the 3D-ViT forward GEMMs (3 more mantissa bits
                                      * than bf16 at the same MFMA rate).  With act 2 the h output
-                                     * C is fp16 too and g is computed from the fp16-rounded h */
-  int32_t r_f16;                    /* act 4: R (h) is fp16 (written by an ab_f16 act-2 GEMM) */
+                                     * C is fp16 in the DERIVATIVE form (round 6): per 64-column
+                                     * group [gelu(gate) | x gelu'(gate)] instead of [x | gate], the
+                                     * two factors act 4 multiplies dg by; g from the f32 values */
+  int32_t r_f16;                    /* act 4: R (h) is fp16 in that derivative form (written by an
+                                     * ab_f16 act-2 GEMM): dh = [dg gelu(gate) | dg x gelu'(gate)]
+                                     * by two multiplies */
   /* split-fp16 "x3" operands (round 6, ab_f16 required; K % 64 == 0, both K-contiguous, no bias-free
    * restrictions beyond act 0 / 2): A_lo / B_lo are the fp16 residual images of A / B (same ld), e.g.
    * A = fp16(x), A_lo = fp16(x - A), so the GEMM reads x to ~22 mantissa bits; every K-step runs

@@ -104,8 +104,9 @@ def test_x3_gemm_f32_rows(K, M, N, Kd):
 
 
 def test_x3_gemm_geglu(K):
-    """FF1 + GEGLU on the x3 GEMM: h (fp16) is the rounded x3 product; g = gelu(gate) x from the
-    UNROUNDED f32 h, stored as an fp16 pair (hi + lo = g to 2^-22) and as bf16; padded columns 0."""
+    """FF1 + GEGLU on the x3 GEMM: h (fp16) in the derivative form [gelu(gate) | x gelu'(gate)] of
+    the x3 product (round 6: the GEGLU backward's two factors); g = gelu(gate) x from the UNROUNDED
+    f32 product, stored as an fp16 pair (hi + lo = g to 2^-22) and as bf16; padded columns 0."""
     from ctclip_mi355x import functional as Fn
     torch.manual_seed(14)
     M, D, inner = 4096, 512, 1365
@@ -116,8 +117,12 @@ def test_x3_gemm_geglu(K):
     h, (gh, gl), gb = K.linear_x3_geglu(K.split_f16(x), K.pack_rows_x3(W1, 2 * P, D, rowmap=rm))
     W1p = K.pack_rows_f32(W1, 2 * P, D, rowmap=rm).double()
     hf = x.double() @ W1p.t()
-    assert rel(h, hf) < 5e-4                         # fp16 storage of h
     hp = hf.view(M, P // 32, 2, 32)
+    xp, gp = hp[:, :, 0], hp[:, :, 1]
+    cdf = 0.5 * (1 + torch.erf(gp / 2 ** 0.5))
+    pdf = torch.exp(-0.5 * gp * gp) / (2 * torch.pi) ** 0.5
+    hd = torch.stack([F.gelu(gp), xp * (cdf + gp * pdf)], 2).reshape(M, 2 * P)
+    assert rel(h, hd) < 5e-4                         # fp16 storage of the derivative form
     ref = (F.gelu(hp[:, :, 1]) * hp[:, :, 0]).reshape(M, P)
     g = _pair(gh, gl)
     e = rel(g, ref)
