@@ -33,7 +33,10 @@ TEXT_GATE = os.environ.get('CTCLIP_TEXT_GATE', '1') != '0'
 # optimizer_step calls flush_ema; any codebook reader, the next VQ or state_dict, queues a pending
 # update first); a plain model(...) call in train mode gets site '1', so the codebook read after it
 # is the updated one, as the reference updates it inside forward.  Measured (r05m_ema_site_ab.log):
-# '2' 204.30 vs '1' 203.70 pairs/s; '1' vs '0' within noise (r05g_ema_ab_env.log)
+# '2' 204.30 vs '1' 203.70 pairs/s; '1' vs '0' within noise (r05g_ema_ab_env.log).  '3' (round 6): as
+# '2', but the trainer leaves the update pending and the NEXT step's image tower queues it once its
+# patch embedding is queued (ctvit.encode_tokens), so it runs beside the GEMM-bound first layer
+# instead of beside the HBM-bound patch LayerNorm (any codebook reader still queues it first)
 DEFER_EMA = os.environ.get('CTCLIP_DEFER_EMA', '2')
 
 
@@ -196,7 +199,7 @@ class CTCLIP(nn.Module):
             t_raw = leaf
         W = self.to_visual_latent.weight
         i_raw = self._project(W, self._visual_weight_bf16(W), pooled, pooled_b)
-        if DEFER_EMA == '1' or (DEFER_EMA == '2' and not self.ema_after_step):
+        if DEFER_EMA == '1' or (DEFER_EMA in ('2', '3') and not self.ema_after_step):
             self.flush_ema()               # the codebook EMA, after the projection
         if self.defer_text_backward and torch.is_grad_enabled() and i_raw.requires_grad:
             # the image tower's backward is deferred too (CTClipTrainer.forward_backward): BERT's

@@ -180,6 +180,10 @@ class CTViT(nn.Module):
                                        self._offsets(video.shape, video.device))
         dist_sync.mark_ready(xf, 'vit_rest')   # with the CPB node below: the rest of the image tower
         streams.mark_image_head(video.device)   # deferred text-stream work may start (streams.py)
+        if self.training:
+            from . import ct_clip
+            if ct_clip.DEFER_EMA == '3':
+                self.vq.state.flush_ema()      # the previous step's codebook EMA (ct_clip.DEFER_EMA '3')
         # CTCLIP.encode may start BERT's forward only once the HBM-bound patch LayerNorm is done
         self._patch_done = torch.cuda.current_stream(dev).record_event() if dev.type == 'cuda' else None
         if trace is not None:

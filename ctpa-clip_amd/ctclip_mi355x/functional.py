@@ -1027,7 +1027,11 @@ class VQPoolFn(torch.autograd.Function):
                 bins_g, esum = state.ema_buffers(C, D, zf.device)
                 bins = bins_g[:C]
                 if zf.is_cuda:
-                    bins_g[C:].copy_(K.status_word(zf.device))
+                    # the guard: the trainer's summed skip word of this update's step when it owns the
+                    # step (DEFER_EMA '2' / '3': the update may run beside the NEXT step, whose
+                    # kernels may flag the live word for their own step), else the live word
+                    g_src, state.ema_guard = state.ema_guard, None
+                    bins_g[C:].copy_(g_src if g_src is not None else K.status_word(zf.device))
                 work = state.ema_work(C, xn.shape[0], zf.device) if _EMA_SORTED else None
                 K.vq_ema_accum(idx, xn, bins, esum, work=work)
                 dist_sync.sum_codebook_stats(bins_g, esum)
@@ -1095,6 +1099,7 @@ class VQState:
         self.last_indices = None
         self.defer_ema = False      # VQPoolFn leaves its EMA launch in pending_ema (CTCLIP.encode)
         self.pending_ema = None
+        self.ema_guard = None       # int32[1] guard word for the pending update (CTClipTrainer)
 
     def ema_buffers(self, C, D, device):
         """(bins f32 [C + 1], esum int64 [C, D]) of the EMA update, zero between updates (created on the

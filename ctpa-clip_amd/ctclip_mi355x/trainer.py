@@ -20,6 +20,11 @@ from . import kernels as K
 
 # diagnostic A/B only (CTCLIP_DIAG_TEXT_ADAM=skip | main): NOT the reference's work when 'skip'
 _DIAG_TEXT_ADAM = os.environ.get('CTCLIP_DIAG_TEXT_ADAM', '')
+def _ema_site():
+    from . import ct_clip
+    return ct_clip.DEFER_EMA
+
+
 # the per-step status-word copy on its own stream (streams.status_stream); 0 = on the current stream
 STATUS_COPY_STREAM = os.environ.get('CTCLIP_STATUS_COPY_STREAM', '1') != '0'
 
@@ -253,9 +258,15 @@ class CTClipTrainer:
         try:
             self._optimizer_step()
         finally:
+            vqs = getattr(self.model, '_vq_state', lambda: None)()
+            if vqs is not None and vqs.pending_ema is not None and self._guard:
+                # the pending update is guarded by this step's summed skip word (forward flags of
+                # every rank + a non-finite gradient norm), whenever it runs
+                vqs.ema_guard = self.skip_ring[self.steps % 4:self.steps % 4 + 1]
             fe = getattr(self.model, 'flush_ema', None)
-            if fe is not None:
-                fe()      # a codebook EMA train_step deferred past the optimizer (ct_clip.DEFER_EMA '2')
+            if fe is not None and _ema_site() != '3':
+                fe()      # a codebook EMA train_step deferred past the optimizer (ct_clip.DEFER_EMA '2';
+                #           '3': the next step's image tower queues it after its patch embedding)
 
     def _optimizer_step(self):
         if streams.pending_text(self.device):
