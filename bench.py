@@ -279,7 +279,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    K.TIMER.start(['ff1', 'dw'])
+    K.TIMER.start(['ff1', 'dw', 'patch_ln'])
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = trainer.train_step(text, hu)
@@ -364,6 +364,7 @@ def main():
         in_sync = bool(lo.item() == hi.item())
     ff1 = K.TIMER.summary('ff1')
     dw = K.TIMER.summary('dw')
+    pln = K.TIMER.summary('patch_ln')
     vit_ms = sum(s.elapsed_time(e) for s, e in vit_events) / max(1, len(vit_events))
 
     pairs = world * args.batch * args.steps
@@ -490,6 +491,10 @@ def main():
         result['vit_forward'] = {'ms': round(vit_ms, 3), 'achieved_tflops': round(vit_tf, 1),
                                  'frac_of_bf16_peak': round(vit_tf / PEAK_BF16_TFLOPS, 4),
                                  'gflop_per_volume': VIT_FWD_GFLOP_PER_VOL}
+    if pln:
+        result['patch_ln_in_step'] = {'avg_ms': round(pln['avg_ms'], 4), 'launches': pln['launches'],
+                                      'timing': 'HIP events around the patch LayerNorm on the main stream, '
+                                                'timed steps (beside whatever the other streams run)'}
     if vit_eval_ms:
         ev_tf = VIT_FWD_GFLOP_PER_VOL * args.batch / (vit_eval_ms * 1e-3) / 1e3
         result['vit_forward_eval'] = {'ms': round(vit_eval_ms, 3), 'achieved_tflops': round(ev_tf, 1),

@@ -754,8 +754,11 @@ def patch_ln(video, is_hu, PT, P, offs, eps=1e-5, ld=None, want_f16=False, want_
     out = torch.empty(B * T * Hg * Wg, ld, device=video.device, dtype=BF16) if want_bf16 else None
     out16 = torch.empty(B * T * Hg * Wg, ld, device=video.device, dtype=F16) if want_f16 or want_x3 else None
     out16lo = torch.empty(B * T * Hg * Wg, ld, device=video.device, dtype=F16) if want_x3 else None
+    end = TIMER('patch_ln', 0.0)      # (bench.py: the patch LayerNorm's in-step duration)
     call('ctclip_patch_ln_x3', ptr(video), int(video.dtype == F32), int(is_hu), B, C, Fr, H, W, PT, P, ptr(offs), eps,
          ptr(out), ptr(out16), ptr(out16lo), ld, stream_ptr())
+    if end is not None:
+        end.record()
     if want_x3:
         return out, (out16, out16lo)
     return (out, out16) if want_f16 else out
