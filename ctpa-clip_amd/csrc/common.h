@@ -162,7 +162,9 @@ __device__ __forceinline__ void gelu_erf_and_grad(float x, float& gelu, float& d
   const float e = __expf(-a * a);
   const float erf = copysignf(fmaf(-y, e, 1.0f), x);
   gelu = 0.5f * x * (1.0f + erf);
-  dgelu = 0.5f * (1.0f + erf) + x * (0.39894228040143268f * e);
+  // (the fma spelled out: left to -ffp-contract, its two possible fusions differ in the last bit
+  // between inlining contexts, and the fused / two-kernel GEGLU backward must agree bit for bit)
+  dgelu = fmaf(x, 0.39894228040143268f * e, 0.5f * (1.0f + erf));
 }
 __device__ __forceinline__ float gelu_erf_grad(float x) {   // one exp (gelu_erf_and_grad)
   float ge, dge;

@@ -330,17 +330,17 @@ __global__ __launch_bounds__(NTH, 2) void gemm_kernel(P p) {
       float v[8];
       if (H16) {
         // fp16 h in the derivative form [gelu(gate) | x gelu'(gate)] (the GEGLU backward's two
-        // factors; gemm256.hip EP 2), g from the f32 values
+        // factors; gemm256.hip EP 2), g and the factors from the fp16-rounded x / gate
         float av[8], bv[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float x = cs[row * CS_LD + cc + j] * p.alpha;
-          const float gt = cs[row * CS_LD + 32 + cc + j] * p.alpha;
+          const float xb = rh(cs[row * CS_LD + cc + j] * p.alpha);
+          const float gb = rh(cs[row * CS_LD + 32 + cc + j] * p.alpha);
           float ge, dge;
-          gelu_erf_and_grad(gt, ge, dge);
+          gelu_erf_and_grad(gb, ge, dge);
           av[j] = ge;
-          bv[j] = x * dge;
-          v[j] = ge * x;
+          bv[j] = xb * dge;
+          v[j] = ge * xb;
         }
         if (p.C) {
           u16* hr = (u16*)p.C + bidx * p.sC + gm * p.ldc + n0 + cc;

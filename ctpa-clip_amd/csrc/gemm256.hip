@@ -930,9 +930,10 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
       }
       // fp16 kernel (round 6): h is stored in its DERIVATIVE form, the two factors the GEGLU backward
       // multiplies dg by -- [gelu(gate) | x gelu'(gate)] in place of [x | gate] (same bytes), so the
-      // backward epilogue is two multiplies per element instead of an erf + exp per element; g from
-      // the f32 values.  bf16 kernel: h = [x | gate] in bf16, g from the bf16-rounded h (the
-      // backward recomputes gelu from the stored h).
+      // backward epilogue is two multiplies per element instead of an erf + exp per element; g and
+      // the factors from the fp16-rounded x / gate (the round-5 forward arithmetic: g bit for bit as
+      // before, the factors its exact derivative).  bf16 kernel: h = [x | gate] in bf16, g from the
+      // bf16-rounded h (the backward recomputes gelu from the stored h).
       // (h may be discarded, C = NULL: the eval forward needs only g, round 6)
       float gg[2][4];
       if constexpr (H16) {
@@ -941,11 +942,12 @@ __device__ __forceinline__ void epilogue_t(const P& p, f32x4 (&acc)[8][4], int w
         for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
+            const float xb = rh(v[j][r]);
             float ge, dge;
-            gelu_erf_and_grad(v[j + 2][r], ge, dge);
+            gelu_erf_and_grad(rh(v[j + 2][r]), ge, dge);
             hv[j][r] = ge;
-            hv[j + 2][r] = v[j][r] * dge;
-            gg[j][r] = ge * v[j][r];
+            hv[j + 2][r] = xb * dge;
+            gg[j][r] = ge * xb;
           }
         store_row_f16((u16*)p.C + bidx * p.sC + gm * p.ldc + wcol0, hv, g, rok && p.C, wcol0, p.N);
       } else {

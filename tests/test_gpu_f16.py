@@ -53,7 +53,7 @@ def test_f16_linear_epilogues(K, M, N, Kd):
 @pytest.mark.parametrize('M', [8192, 300])
 def test_f16_geglu_h_and_backward(K, M):
     """act 2 on fp16 operands: h stored in fp16 in the derivative form [gelu(gate) | x gelu'(gate)]
-    (round 6), g = gelu(gate) x from the f32 product (bf16); act 4 reads that fp16 h (r_f16) and
+    (round 6), g = gelu(gate) x from the fp16-rounded x / gate (bf16); act 4 reads that fp16 h (r_f16) and
     multiplies dg by its two factors -- against the stored factors and against the f64 truth (the
     GEGLU derivative at the exact pre-activation).  M = 300 takes the 128-tile kernel."""
     g_ = torch.Generator(device='cuda').manual_seed(2)
