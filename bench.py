@@ -175,7 +175,7 @@ def rocprof_avg_ms(key):
     return None, None, None
 
 
-PMC_TAG = 'r05ae'   # tools/pmc_gemm.sh <shape> <tag> on the current tree -> profiles/pmc_<tag>_<shape>.json
+PMC_TAG = 'r06v'   # tools/pmc_gemm.sh <shape> <tag> on the current tree -> profiles/pmc_<tag>_<shape>.json
 
 
 def pmc_record(shape, kernel_key):
