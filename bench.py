@@ -412,9 +412,10 @@ def main():
     # argument is its fp16-operand flag (the default 3D-ViT forward, functional.vit_f16, round 5)
     from ctclip_mi355x import functional as Fn
     h16 = (Fn.vit_f16() and Fn._LN1_FOLD and Fn._PEG_X32 and not args.fp8 and not args.f32_tower)
-    ff1_key = f'gemm8p_kernel<true, true, 2, {"true" if h16 else "false"}>'
+    # (the fifth template argument: the split-fp16 x3 kernels, round 6; the default step runs X3 = false)
+    ff1_key = f'gemm8p_kernel<true, true, 2, {"true" if h16 else "false"}, false>'
     ff1_shape = 'ff1h16' if h16 else 'ff1'
-    dw_key = 'gemm8p_kernel<false, false, -5, false>'
+    dw_key = 'gemm8p_kernel<false, false, -5, false, false>'
     if ff1:
         tflops = ff1['flops'] / (ff1['avg_ms'] * 1e-3) / 1e12
         M = args.batch * 24 * 24 * 24

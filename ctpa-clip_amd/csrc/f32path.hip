@@ -449,7 +449,10 @@ __global__ __launch_bounds__(256) void attn_f32_mfma_kernel(ctclip_attn_args a) 
 // the k-slots of lane group g in key pair P are keys 32 P + 16 (i >> 2) + 4 g + (i & 3), i = 0..7,
 // exactly the probabilities the lane holds, so V^T is staged in that key order.  Outputs: O as the
 // fp16 pair of the x3 to_out GEMM (oh, ol), O in bf16 and the natural-log LSE (the bf16 backward's
-// operands: it recomputes P from its bf16 q / k against this LSE).
+// operands: it recomputes P from its bf16 q / k against this LSE).  The probabilities go through
+// v_exp_f32 on log2-unit scores (scale log2 e folded into the score multiply, the bias table scaled
+// at staging), not libm expf: ~1 ulp, and the kernel's VALU work per score roughly halves (round 6).
+constexpr float X3_LOG2E = 1.4426950408889634f, X3_LN2 = 0.6931471805599453f;
 constexpr int X3_KLD = 40;            // K image row: 32 d + 8 pad (fp16)
 constexpr int X3_VLD = 72;            // V^T image row: 64 keys + 8 pad (fp16)
 
@@ -477,7 +480,8 @@ __global__ __launch_bounds__(256) void attn_x3_fwd_kernel(ctclip_attn_args a, u1
   const int Wg = bias ? a.grid_w : 1;
   const int nb = bias ? (2 * a.grid_h - 1) * (2 * Wg - 1) : 0;
   if (bias) {
-    for (int i = tid; i < nb; i += 256) Bs[i] = a.bias_u[(int64_t)h * nb + i];
+    // (log2 units: the scores go through v_exp_f32 directly, round 6)
+    for (int i = tid; i < nb; i += 256) Bs[i] = a.bias_u[(int64_t)h * nb + i] * X3_LOG2E;
     for (int i = tid; i < L + 64; i += 256) Kx[i] = i < L ? (i / Wg) * (2 * Wg - 1) + i % Wg : 0;
   }
   const int qi = blockIdx.x * 64 + w * 16 + r16;
@@ -498,6 +502,7 @@ __global__ __launch_bounds__(256) void attn_x3_fwd_kernel(ctclip_attn_args a, u1
   }
   int qbase = 0;
   if (bias) qbase = (qi / Wg + a.grid_h - 1) * (2 * Wg - 1) + qi % Wg + Wg - 1;
+  const float sc2 = a.scale * X3_LOG2E;
   float m = -INFINITY, l = 0.f;
   f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   const int kk = tid >> 2, c = tid & 3;   // staging: key kk of the chunk, head dims 8 c .. 8 c + 7
@@ -545,7 +550,7 @@ __global__ __launch_bounds__(256) void attn_x3_fwd_kernel(ctclip_attn_args a, u1
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v = acc[r] * a.scale;
+        float v = acc[r] * sc2;
         if (bias) v += qv ? Bs[qbase - kx[r]] : 0.f;
         x[j][r] = key0 + r < L ? v : -INFINITY;
         cm = fmaxf(cm, x[j][r]);
@@ -554,7 +559,7 @@ __global__ __launch_bounds__(256) void attn_x3_fwd_kernel(ctclip_attn_args a, u1
     cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
     cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
     const float mn = fmaxf(m, cm);
-    const float corr = expf(m - mn);   // m = -inf on the first chunk -> 0
+    const float corr = __builtin_amdgcn_exp2f(m - mn);   // m = -inf on the first chunk -> 0
     l *= corr;
 #pragma unroll
     for (int r = 0; r < 4; ++r) { o[0][r] *= corr; o[1][r] *= corr; }
@@ -564,7 +569,7 @@ __global__ __launch_bounds__(256) void attn_x3_fwd_kernel(ctclip_attn_args a, u1
       f16x8 ph, pl;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        const float pv = expf(x[2 * P + (i >> 2)][i & 3] - mn);
+        const float pv = __builtin_amdgcn_exp2f(x[2 * P + (i >> 2)][i & 3] - mn);
         l += pv;
         _Float16 hh, ll;
         split2h(pv, hh, ll);
@@ -599,7 +604,7 @@ __global__ __launch_bounds__(256) void attn_x3_fwd_kernel(ctclip_attn_args a, u1
     *(uint2*)(ol + ro + 16 * db) = pack4h(lv);
     if (ob) *(uint2*)(ob + ro + 16 * db) = pack4(ov);
   }
-  if (g == 0 && lse) lse[(int64_t)h * a.M + qrow] = m + logf(l);
+  if (g == 0 && lse) lse[(int64_t)h * a.M + qrow] = (m + log2f(l)) * X3_LN2;   // natural log
 }
 
 inline unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }
