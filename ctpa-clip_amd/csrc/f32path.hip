@@ -509,14 +509,20 @@ __global__ __launch_bounds__(256) void attn_x3_fwd_kernel(ctclip_attn_args a, u1
   // the key's position in the V^T image: pair P = kk >> 5, lane group gk = (kk >> 2) & 3, slot
   // i = 4 ((kk >> 4) & 1) + (kk & 3) (see above)
   const int vpos = (kk >> 5) * 32 + ((kk >> 2) & 3) * 8 + 4 * ((kk >> 4) & 1) + (kk & 3);
+  // this thread's K / V slice of a chunk, loaded one chunk ahead (registers) so the global load
+  // latency hides behind the previous chunk's MFMAs
+  f32x4 k_lo, k_hi, v_lo, v_hi;
+  auto fetch = [&](int c0) {
+    const int64_t krow = rbase + (int64_t)min(c0 + kk, L - 1) * a.s_pos;
+    k_lo = *(const f32x4*)(Kp + krow * a.ldk + h * 32 + 8 * c);
+    k_hi = *(const f32x4*)(Kp + krow * a.ldk + h * 32 + 8 * c + 4);
+    v_lo = *(const f32x4*)(Vp + krow * a.ldv + h * 32 + 8 * c);
+    v_hi = *(const f32x4*)(Vp + krow * a.ldv + h * 32 + 8 * c + 4);
+  };
+  fetch(0);
   for (int k0 = 0; k0 < L; k0 += 64) {
     __syncthreads();
     {
-      const int64_t krow = rbase + (int64_t)min(k0 + kk, L - 1) * a.s_pos;
-      const f32x4 k_lo = *(const f32x4*)(Kp + krow * a.ldk + h * 32 + 8 * c);
-      const f32x4 k_hi = *(const f32x4*)(Kp + krow * a.ldk + h * 32 + 8 * c + 4);
-      const f32x4 v_lo = *(const f32x4*)(Vp + krow * a.ldv + h * 32 + 8 * c);
-      const f32x4 v_hi = *(const f32x4*)(Vp + krow * a.ldv + h * 32 + 8 * c + 4);
       f16x8 kh8, kl8;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -531,6 +537,7 @@ __global__ __launch_bounds__(256) void attn_x3_fwd_kernel(ctclip_attn_args a, u1
       *(f16x8*)(Kh + kk * X3_KLD + 8 * c) = kh8;
       *(f16x8*)(Kl + kk * X3_KLD + 8 * c) = kl8;
     }
+    if (k0 + 64 < L) fetch(k0 + 64);
     __syncthreads();
     float x[4][4];
     float cm = -INFINITY;
