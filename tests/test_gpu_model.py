@@ -474,3 +474,27 @@ def test_defer_text_ordering():
     main.wait_stream(ts)
     torch.cuda.synchronize()
     assert y.item() == 2.0 and z.item() == 7.0
+
+
+def test_eval_lean_forward_matches_full_forward():
+    """The eval-mode lean 3D-ViT forward (round 6: under no_grad ViTLayerFn writes none of the
+    backward-only tensors -- bf16 shadows, the LSE, FF1's h, the bf16 O) computes the same tokens as
+    the full forward: encode_pooled under no_grad and with autograd recording, eval mode both,
+    bit-identical pooled latents and VQ indices (grid 8 x 8 x 4 with the LN1 fold and fp16 operands,
+    as the base config takes them)."""
+    cfg = cfg_small()
+    torch.manual_seed(0)
+    model = build(cfg)
+    model.eval()
+    vt = model.visual_transformer
+    hu = W.make_hu(2, cfg.vit).cuda()
+    with torch.no_grad():
+        p0, pb0 = vt.encode_pooled(hu)
+        i0 = vt.vq.state.last_indices.clone()
+    with torch.enable_grad():
+        p1, pb1 = vt.encode_pooled(hu)
+        i1 = vt.vq.state.last_indices.clone()
+    assert p1.requires_grad                     # the full path (tensors saved for a backward)
+    torch.cuda.synchronize()
+    assert torch.equal(i0, i1)
+    assert torch.equal(p0, p1.detach()) and torch.equal(pb0, pb1)
