@@ -565,8 +565,9 @@ extern "C" int ctclip_gemm(const ctclip_gemm_args* a, void* stream) {
       CT_REQUIRE(a->act == 0 && a->c_f32 && (!a->R || a->r_f32), CT_EINVAL);
     return ctclip_gemm256(a, 1, 1, stream);
   }
-  if (a->ab_f16)   // fp16 operands: the 3D-ViT forward GEMMs (K-contiguous A and B, no split-K / B2)
-    CT_REQUIRE(a->a_kcontig && a->b_kcontig && !a->B2 && split == 1 && (a->act == 0 || a->act == 2) &&
+  if (a->ab_f16)   // fp16 operands: the 3D-ViT forward GEMMs and the VQ distance GEMM (act 3, round 6;
+                   // K-contiguous A and B, no split-K / B2)
+    CT_REQUIRE(a->a_kcontig && a->b_kcontig && !a->B2 && split == 1 && (a->act == 0 || a->act == 2 || a->act == 3) &&
                    !a->accumulate && (a->batch <= 1),
                CT_EINVAL);
   if (!a->B2 && a->act != 6) {   // act 6 (GELU backward): the 128-tile kernel only (text tower)

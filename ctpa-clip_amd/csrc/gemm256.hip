@@ -1806,7 +1806,9 @@ int launch8_ep(const P& p, int batch, hipStream_t st) {
 // fp16 operands (the 3D-ViT forward: K-contiguous A and B only): the forward epilogues -- GEGLU (h in
 // fp16), plain 16-bit / l2norm-free outputs, the LDS-staged f32 / bias / residual rows
 int launch8_h16(const P& p, int batch, hipStream_t st) {
-  if (p.split_k > 1 || p.act == 3 || p.act == 4 || p.act == 5 || p.act == 6) return CT_EINVAL;
+  if (p.split_k > 1 || p.act == 4 || p.act == 5 || p.act == 6) return CT_EINVAL;
+  // the VQ distance GEMM on fp16 operands (round 6): the argmax epilogue works on the f32 sums
+  if (p.act == 3) return p.x3 ? CT_EINVAL : launch8<true, true, 3, true>(p, batch, st);
   if (p.x3) {
     // split-fp16 operands: the GEGLU pair epilogue, f32 rows (bias / f32 residual / bf16 copy)
     if (p.act == 2) return launch8<true, true, 2, true, true>(p, batch, st);

@@ -9,7 +9,11 @@
 // bf16 score is within 2^-7 of the f32 cosine (bf16 x, its l2norm and the codebook each round
 // at 2^-9 relative; Cauchy-Schwarz on unit vectors), so the true f32 winner's bf16 score is
 // >= best - 2^-6 and margin 2e-2 > 2^-6 makes the result the exact f32 argmax (first index on
-// f32 ties), independent of the bf16 rounding.
+// f32 ties), independent of the bf16 rounding.  The default path (round 6) feeds the GEMM fp16
+// operands instead (vq_l2norm_h16 + the codebook's fp16 high half): 2^-11 roundings, every
+// score within 2^-9 of the f32 cosine, margin 4e-3 > 2^-8, fewer full groups to re-score.
+// Every candidate is re-scored with one summation order (score_seq), so the candidate set --
+// which depends on the GEMM's operand rounding -- cannot change the f32 winner.
 #include "common.h"
 #include "../../include/ctclip_hip.h"
 
@@ -20,7 +24,31 @@
 
 namespace {
 
-constexpr int VQ_SB = 4;   // single-code candidates re-scored together
+// x_n . cb_row in f32, k = 0 .. D-1 in order, one fused multiply-add per term: the one summation
+// order every candidate is scored with
+__device__ __forceinline__ float score_seq(const float* xs, const float* __restrict__ cr, int D) {
+  float d = 0.f;
+  for (int k = 0; k < D; k += 4) {
+    const f32x4 w = *(const f32x4*)(cr + k);
+    const f32x4 xv = *(const f32x4*)(xs + k);
+    d = fmaf(xv[0], w[0], d);
+    d = fmaf(xv[1], w[1], d);
+    d = fmaf(xv[2], w[2], d);
+    d = fmaf(xv[3], w[3], d);
+  }
+  return d;
+}
+
+// fold the wave's (d, i) into (bv, bi): max score, ties to the lowest index (order independent)
+__device__ __forceinline__ void wave_argmax(float dv, int di, float& bv, int& bi) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float ov = __shfl_xor(dv, o, 64);
+    const int oi = __shfl_xor(di, o, 64);
+    if (ov > dv || (ov == dv && oi < di)) { dv = ov; di = oi; }
+  }
+  if (dv > bv || (dv == bv && di < bi)) { bv = dv; bi = di; }
+}
 
 // one wave per row; the row's f32 l2norm lives in a wave-private LDS strip (D floats) so the
 // full-group re-score can run one code per lane
@@ -62,67 +90,26 @@ __global__ __launch_bounds__(256) void vq_select_kernel(const float2* __restrict
       take = c.x >= thr;
       full = !CTCLIP_VQ_DIAG_NOFULL && take && cand2 && cand2[row * ntiles + t] >= thr;
     }
-    const unsigned long long mask = __ballot(take);
-    const unsigned long long fmask = __ballot(full);
-    // (bv, bi) = the max score, ties to the lowest code: independent of the order codes are scored
-    // in, so full groups go first and single codes after, VQ_SB at a time with their loads
-    // interleaved (one code per pass was a dependent load -> warp-sum chain per candidate)
-    unsigned long long gmask = mask & fmask, smask = mask & ~fmask;
+    // (bv, bi) = the max score, ties to the lowest code.  EVERY candidate is scored by one lane
+    // with the same sequential f32 sum (score_seq), so a code's score does not depend on how it
+    // became a candidate: which groups are 'full' depends on the low-precision GEMM's rounding
+    // (bf16 or fp16 operands, the margin), and with two summation orders an f32 near-tie
+    // (< 1 ulp apart) could resolve differently between the two.
+    unsigned long long gmask = __ballot(full);
     while (gmask) {
       const int src = __ffsll((long long)gmask) - 1;
       gmask &= gmask - 1;
       // several codes of this group are within the margin: score all of them, one per lane
       const int ci = (t0 + src) * 64 + lane;
-      float d = -INFINITY;
-      if (ci < C) {
-        const float* cr = cb + (int64_t)ci * D;
-        d = 0.f;
-        for (int k = 0; k < D; k += 4) {
-          const f32x4 w = *(const f32x4*)(cr + k);
-          const f32x4 xv = *(const f32x4*)(xs + k);
-          d += xv[0] * w[0];
-          d += xv[1] * w[1];
-          d += xv[2] * w[2];
-          d += xv[3] * w[3];
-        }
-      }
-      float dv = d;
-      int di = ci < C ? ci : 0x7fffffff;
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) {
-        const float ov = __shfl_xor(dv, o, 64);
-        const int oi = __shfl_xor(di, o, 64);
-        if (ov > dv || (ov == dv && oi < di)) { dv = ov; di = oi; }
-      }
-      if (dv > bv || (dv == bv && di < bi)) { bv = dv; bi = di; }
+      const float d = ci < C ? score_seq(xs, cb + (int64_t)ci * D, D) : -INFINITY;
+      wave_argmax(d, ci < C ? ci : 0x7fffffff, bv, bi);
     }
-    while (smask) {
-      int ci[VQ_SB];
-#pragma unroll
-      for (int q = 0; q < VQ_SB; ++q) {
-        ci[q] = -1;
-        if (smask) {   // wave-uniform
-          const int src = __ffsll((long long)smask) - 1;
-          smask &= smask - 1;
-          ci[q] = __float_as_int(__shfl(c.y, src, 64));
-        }
-      }
-      // per code the same sum as one at a time: lane k-slice in order, then the wave sum
-      float d[VQ_SB];
-#pragma unroll
-      for (int q = 0; q < VQ_SB; ++q) d[q] = 0.f;
-      for (int k = lane; k < D; k += 64) {
-        const float xk = xs[k];
-#pragma unroll
-        for (int q = 0; q < VQ_SB; ++q)
-          if (ci[q] >= 0) d[q] += xk * cb[(int64_t)ci[q] * D + k];
-      }
-#pragma unroll
-      for (int q = 0; q < VQ_SB; ++q) {
-        if (ci[q] < 0) continue;
-        const float dq = warp_sum(d[q]);
-        if (dq > bv || (dq == bv && ci[q] < bi)) { bv = dq; bi = ci[q]; }
-      }
+    // single-code candidates: each candidate lane scores its own code, all of them at once
+    if (__ballot(take && !full)) {
+      const int ci = __float_as_int(c.y);
+      const bool mine = take && !full;
+      const float d = mine ? score_seq(xs, cb + (int64_t)ci * D, D) : -INFINITY;
+      wave_argmax(d, mine ? ci : 0x7fffffff, bv, bi);
     }
   }
   // a row without any finite score (NaN / inf tokens) keeps bi = INT_MAX: clamp it into the
@@ -392,7 +379,42 @@ __global__ __launch_bounds__(256) void vq_pool_bwd_kernel(const float* __restric
 
 inline int gridn(int64_t n) { return (int)std::min<int64_t>(8192, std::max<int64_t>(1, (n + 255) / 256)); }
 
+// fp16 l2norm of the f32 tokens (round 6): the A operand of the fp16 VQ distance GEMM, one wave per
+// row, 16-B loads; y = fp16(x / max(||x||, 1e-12)) (F.normalize).  With the fp16 codebook image
+// every score is within ~2^-10 of the f32 cosine (one 2^-11 rounding per unit-norm operand), so
+// vq_select's re-score margin drops from 2e-2 (bf16: three 2^-9 roundings) to 4e-3
+__global__ __launch_bounds__(256) void vq_l2norm_h16_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows,
+                                                            int D, u16* __restrict__ y, int64_t ldy) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;   // (wave-uniform)
+  const float* xr = x + row * ldx;
+  float s = 0.f;
+  for (int c = lane * 4; c < D; c += 256) {
+    const f32x4 v = *(const f32x4*)(xr + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s = fmaf(v[e], v[e], s);
+  }
+  s = warp_sum(s);
+  const float n = fmaxf(sqrtf(s), 1e-12f);
+  for (int c = lane * 4; c < D; c += 256) {
+    const f32x4 v = *(const f32x4*)(xr + c);
+    const float o[4] = {v[0] / n, v[1] / n, v[2] / n, v[3] / n};
+    *(uint2*)(y + row * ldy + c) = pack4h(o);
+  }
+}
+
 }  // namespace
+
+extern "C" int ctclip_vq_l2norm_h16(const float* x, int64_t ldx, int64_t rows, int32_t D, void* y, int64_t ldy,
+                                    void* stream) {
+  if (rows == 0) return 0;
+  CT_REQUIRE(D % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && aligned16(x) && ((uintptr_t)y & 7) == 0, CT_EALIGN);
+  hipLaunchKernelGGL(vq_l2norm_h16_kernel, dim3((unsigned)cdiv(rows, 4)), dim3(256), 0, (hipStream_t)stream, x, ldx,
+                     rows, D, (u16*)y, ldy);
+  CT_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int ctclip_vq_select(const float* cand, const float* cand2, int32_t ntiles, const float* x, int64_t rows,
                                 int32_t D, const float* codebook, int32_t C, float margin, int32_t* idx,

@@ -169,6 +169,7 @@ _SIGS = {
     'ctclip_pack_qkv_fold_h16': [c_vp, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_i64, c_vp, c_vp],
     'ctclip_skinny_gemm_slices': [c_i64, c_i64, c_i64],
     'ctclip_skinny_gemm': [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp],
+    'ctclip_vq_l2norm_h16': [c_vp, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp],
     'ctclip_skinny_sgemm_slices': [c_i64, c_i64, c_i64],
     'ctclip_skinny_sgemm': [c_vp, c_i64, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i32, c_vp],
     'ctclip_reduce_slabs': [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_i64, c_i32, c_i32, c_vp],

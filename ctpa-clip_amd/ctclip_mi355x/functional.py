@@ -1073,20 +1073,33 @@ class VQPoolFn(torch.autograd.Function):
         return dz, None, None, None, None, None, None, None, None
 
 
+# the VQ distance GEMM on fp16 operands (round 6; CTCLIP_VQ_F16=0: bf16): l2norm(zf) and the codebook
+# each rounded once at 2^-11, so the f32 re-score margin is 4e-3 instead of 2e-2 and vq_select
+# re-scores ~3x fewer codes; same exact f32 argmax
+_VQ_F16 = os.environ.get('CTCLIP_VQ_F16', '1') != '0'
+
+
 def vq_assign(zf, zb, cb, state, want_xn=False):
     """Cosine-codebook assignment (vector_quantize_pytorch cosine sim + argmax, ct_clip/ctvit.py:427):
-    bf16 MFMA distance GEMM over l2norm(zb) with a per-64-code-group (best, index, second-best)
-    epilogue, then the f32 re-score of every code within the bf16 error margin (vq.hip) -> the
-    exact f32 argmax of l2norm(zf) . cb^T.  Returns (idx int32 [M], l2norm(zf) f32 or None)."""
+    16-bit MFMA distance GEMM with a per-64-code-group (best, index, second-best) epilogue -- fp16
+    l2norm(zf) against the fp16 codebook image (bf16 l2norm(zb) and codebook with CTCLIP_VQ_F16=0)
+    -- then the f32 re-score of every code within that GEMM's error margin (vq.hip) -> the exact
+    f32 argmax of l2norm(zf) . cb^T.  Returns (idx int32 [M], l2norm(zf) f32 or None)."""
     D = zf.shape[1]
     C = cb.shape[0]
-    cb_b = state.codebook_bf16(cb)
-    xn_b = K.l2norm_scale_fwd(zb, 1, D, state.ones(D, zf.device))
+    if _VQ_F16 and D % 64 == 0:
+        xn_s = K.vq_l2norm_h16(zf)
+        cb_s = K.split_f16(cb)[0]       # (the EMA updates cb in place: cast per call, 4 M elements)
+        margin = 4e-3
+    else:
+        xn_s = K.l2norm_scale_fwd(zb, 1, D, state.ones(D, zf.device))
+        cb_s = state.codebook_bf16(cb)
+        margin = 2e-2
     nt = (C + 63) // 64
     cand = torch.empty(zf.shape[0], nt, 2, device=zf.device, dtype=F32)
     cand2 = torch.empty(zf.shape[0], nt, device=zf.device, dtype=F32)
-    K.gemm_raw(zf.shape[0], C, D, xn_b, D, True, cb_b, D, True, cand, nt, C2=cand2, ldc2=nt, act=K.ACT_ARGMAX)
-    return K.vq_select(cand, zf, cb, want_xn=want_xn, cand2=cand2)
+    K.gemm_raw(zf.shape[0], C, D, xn_s, D, True, cb_s, D, True, cand, nt, C2=cand2, ldc2=nt, act=K.ACT_ARGMAX)
+    return K.vq_select(cand, zf, cb, margin=margin, want_xn=want_xn, cand2=cand2)
 
 
 class VQState:

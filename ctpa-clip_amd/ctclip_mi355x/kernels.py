@@ -1124,6 +1124,15 @@ def vq_select(cand, x, codebook_f32, margin=2e-2, want_xn=True, cand2=None):
     return idx, xn
 
 
+def vq_l2norm_h16(x):
+    """fp16 l2norm of the f32 tokens [rows, D] (ctclip_vq_l2norm_h16): the fp16 VQ distance GEMM's A."""
+    rows, D = x.shape
+    assert x.dtype == F32 and x.stride(1) == 1
+    y = torch.empty(rows, D, device=x.device, dtype=F16)
+    call('ctclip_vq_l2norm_h16', ptr(x), x.stride(0), rows, D, ptr(y), D, stream_ptr())
+    return y
+
+
 def vq_pool(idx, codebook_f32, B, T, HW, want_bf16=True):
     D = codebook_f32.shape[1]
     out = torch.empty(B, HW * D, device=idx.device, dtype=F32)

@@ -580,6 +580,11 @@ int ctclip_vq_select(const float* cand, const float* cand2, int32_t ntiles, cons
 int ctclip_vq_select_s(const float* cand, const float* cand2, int32_t ntiles, const float* x, int64_t rows, int32_t D,
                        const float* codebook, int32_t C, float margin, int32_t* idx, float* xn_out, int32_t* status,
                        void* stream);
+/* Round 6: the fp16 scoring operand of the VQ distance GEMM: y = fp16(x / max(||x||, 1e-12)) per row
+ * (x f32 [rows][ldx], D % 4 == 0).  With an fp16 image of the (unit-norm) codebook and
+ * ctclip_gemm_args.ab_f16 on the act-3 GEMM, every score is within ~2^-10 of the f32 cosine, and
+ * ctclip_vq_select's margin can be 4e-3 instead of 2e-2 (exact f32 argmax either way). */
+int ctclip_vq_l2norm_h16(const float* x, int64_t ldx, int64_t rows, int32_t D, void* y, int64_t ldy, void* stream);
 /* pooled[b][hw][:] = mean_t codebook[idx[b][t*HW+hw]]   (ct_clip/ct_clip.py:724,740) */
 int ctclip_vq_pool(const int32_t* idx, const float* codebook, int64_t B, int32_t T, int32_t HW, int32_t D,
                    float* out, void* out_bf16, void* stream);

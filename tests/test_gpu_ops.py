@@ -322,6 +322,16 @@ def test_vq_select_and_pool(K):
     ref = s64.argmax(1)
     tie = (top2[:, 0] - top2[:, 1]) < 1e-6        # only f32-level ties may differ
     assert (idx.long() != ref)[~tie].sum().item() == 0
+    # the fp16 scoring path (round 6, functional.vq_assign's default): fp16 l2norm(x) against the
+    # fp16 codebook image, re-score margin 4e-3 -- the same exact f32 argmax, on the 8-phase kernel
+    # (M = 3000) and the 128-tile one (M = 200)
+    for Mh in (M, 200):
+        candh = torch.empty(Mh, nt, 2, device=dev)
+        cand2h = torch.empty(Mh, nt, device=dev)
+        K.gemm_raw(Mh, C, D, K.vq_l2norm_h16(x[:Mh]), D, True, K.split_f16(cb)[0], D, True, candh, nt, C2=cand2h,
+                   ldc2=nt, act=K.ACT_ARGMAX)
+        idx_h, _ = K.vq_select(candh, x[:Mh], cb, margin=4e-3, cand2=cand2h)
+        assert (idx_h.long() != ref[:Mh])[~tie[:Mh]].sum().item() == 0
     # group winners only (cand2 = None) miss some of the in-group near-ties: the case the full-group
     # re-score exists for
     idx_w, _ = K.vq_select(cand, x, cb)
@@ -385,6 +395,10 @@ def test_vq_select_and_pool(K):
     assert idb[3].item() == 0 and idb[7].item() == 0
     assert torch.isfinite(xnb).all() and xnb[3].abs().sum().item() == 0 and xnb[7].abs().sum().item() == 0
     assert torch.equal(idb[:3], idx[:3])
+    # ... and flags the sticky step status word (CT_STATUS_VQ_NONFINITE = 8), cleared here so the
+    # trainer tests that follow in the same process start from a clean word
+    assert int(K.status_word(dev).item()) & 8
+    K.reset_ln_status(dev)
     bins_b = torch.zeros(C, device=dev)
     esum_b = torch.zeros(C, D, device=dev, dtype=torch.int64)
     K.vq_ema_accum(idb, xnb, bins_b, esum_b)
