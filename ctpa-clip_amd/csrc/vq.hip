@@ -12,7 +12,7 @@
 // f32 ties), independent of the bf16 rounding.  The default path (round 6) feeds the GEMM fp16
 // operands instead (vq_l2norm_h16 + the codebook's fp16 high half): 2^-11 roundings, every
 // score within 2^-9 of the f32 cosine, margin 4e-3 > 2^-8, fewer full groups to re-score.
-// Every candidate is re-scored with one summation order (score_seq), so the candidate set --
+// Every candidate is re-scored with one summation order (slice_partial + butterfly), so the candidate set --
 // which depends on the GEMM's operand rounding -- cannot change the f32 winner.
 #include "common.h"
 #include "../../include/ctclip_hip.h"
@@ -24,8 +24,63 @@
 
 namespace {
 
-// x_n . cb_row in f32, k = 0 .. D-1 in order, one fused multiply-add per term: the one summation
-// order every candidate is scored with
+constexpr int VQ_SB = 4;   // single-code candidates re-scored together
+
+// Scoring a candidate code (x_n . cb_row in f32).  The fast sum: lane l sums its slice
+// k in {4l .. 4l+3} + 256 j (j ascending, one fused multiply-add per term), then the 64 slice
+// partials are added as the xor butterfly of warp_sum (lane l + lane l^32, then ^16, ...) -- the
+// same bits whether a code is scored alone or in a full group (score_group).  The deciding sum
+// (score_seq): k = 0 .. D-1 in order, one lane.  vq_select returns the argmax under score_seq
+// (lowest index on ties); score_seq runs only for the codes whose fast score is within `win` of
+// the fast best, win = twice the two sums' worst-case difference, so the rows that need it
+// (a near-tie, ~1 %) are the only ones that pay for a D-long dependent chain.  Either way the
+// answer cannot depend on which codes became candidates (the low-precision GEMM's rounding).
+__device__ __forceinline__ float slice_partial(const float* xs, const float* __restrict__ cr, int D, int lane) {
+  float d = 0.f;
+  for (int k = lane * 4; k < D; k += 256) {
+    const f32x4 w = *(const f32x4*)(cr + k);
+    const f32x4 xv = *(const f32x4*)(xs + k);
+    d = fmaf(xv[0], w[0], d);
+    d = fmaf(xv[1], w[1], d);
+    d = fmaf(xv[2], w[2], d);
+    d = fmaf(xv[3], w[3], d);
+  }
+  return d;
+}
+
+// all 64 codes of group g at once: every lane forms its slice partial of each code, then a
+// reduce-scatter butterfly (63 shuffles instead of 64 warp sums) leaves code g*64 + lane's score --
+// the same additions, operand for operand, as warp_sum(slice_partial(code)) -- in lane `lane`
+__device__ __forceinline__ float score_group(const float* xs, const float* __restrict__ cb, int g, int C, int D,
+                                             int lane) {
+  float v[64];
+#pragma unroll
+  for (int c = 0; c < 64; ++c) v[c] = 0.f;
+  for (int k = lane * 4; k < D; k += 256) {
+    const f32x4 xv = *(const f32x4*)(xs + k);
+#pragma unroll
+    for (int c = 0; c < 64; ++c) {
+      const int ci = min(g * 64 + c, C - 1);   // past the codebook: a valid row, result discarded
+      const f32x4 w = *(const f32x4*)(cb + (int64_t)ci * D + k);
+      v[c] = fmaf(xv[0], w[0], v[c]);
+      v[c] = fmaf(xv[1], w[1], v[c]);
+      v[c] = fmaf(xv[2], w[2], v[c]);
+      v[c] = fmaf(xv[3], w[3], v[c]);
+    }
+  }
+#pragma unroll
+  for (int h = 32; h >= 1; h >>= 1) {   // lane bit h <-> code bit h
+    const bool up = lane & h;
+#pragma unroll
+    for (int i = 0; i < h; ++i) {
+      const float send = up ? v[i] : v[i + h];
+      const float keep = up ? v[i + h] : v[i];
+      v[i] = keep + __shfl_xor(send, h, 64);
+    }
+  }
+  return v[0];
+}
+
 __device__ __forceinline__ float score_seq(const float* xs, const float* __restrict__ cr, int D) {
   float d = 0.f;
   for (int k = 0; k < D; k += 4) {
@@ -79,38 +134,87 @@ __global__ __launch_bounds__(256) void vq_select_kernel(const float2* __restrict
   for (int t = lane; t < ntiles; t += 64) best = fmaxf(best, cand[row * ntiles + t].x);
   best = warp_max(best);
   const float thr = best - margin;
+  // every candidate code: onfull(score, code) per lane for the 64 codes of a full group (code >= C
+  // past the codebook's end: skip), onsingle(score, code) wave-uniform for a single code
+  auto walk = [&](auto&& onfull, auto&& onsingle) {
+    for (int t0 = 0; t0 < ntiles; t0 += 64) {
+      const int t = t0 + lane;
+      bool take = false, full = false;
+      float2 c = make_float2(-INFINITY, 0.f);
+      if (t < ntiles) {
+        c = cand[row * ntiles + t];
+        take = c.x >= thr;
+        full = !CTCLIP_VQ_DIAG_NOFULL && take && cand2 && cand2[row * ntiles + t] >= thr;
+      }
+      unsigned long long gmask = __ballot(full);
+      unsigned long long smask = __ballot(take) & ~gmask;
+      while (gmask) {
+        const int src = __ffsll((long long)gmask) - 1;
+        gmask &= gmask - 1;
+        // several codes of this group are within the margin: score all of them, one per lane
+        onfull(score_group(xs, cb, t0 + src, C, D, lane), (t0 + src) * 64 + lane);
+      }
+      while (smask) {   // single-code candidates, VQ_SB at a time (their loads interleaved)
+        int ci[VQ_SB];
+#pragma unroll
+        for (int q = 0; q < VQ_SB; ++q) {
+          ci[q] = -1;
+          if (smask) {   // wave-uniform
+            const int src = __ffsll((long long)smask) - 1;
+            smask &= smask - 1;
+            ci[q] = __float_as_int(__shfl(c.y, src, 64));
+          }
+        }
+        float d[VQ_SB];
+#pragma unroll
+        for (int q = 0; q < VQ_SB; ++q)
+          d[q] = ci[q] >= 0 ? slice_partial(xs, cb + (int64_t)ci[q] * D, D, lane) : 0.f;
+#pragma unroll
+        for (int q = 0; q < VQ_SB; ++q)
+          if (ci[q] >= 0) onsingle(warp_sum(d[q]), ci[q]);
+      }
+    }
+  };
+  // pass 1: the fast scores' best (ties to the lowest code) and runner-up, per lane then per wave
+  float b1v = -INFINITY, b2v = -INFINITY;
+  int b1i = 0x7fffffff;
+  auto top2 = [&](float v, int i) {
+    if (v > b1v || (v == b1v && i < b1i)) {
+      b2v = b1v;
+      b1v = v;
+      b1i = i;
+    } else if (v > b2v) {
+      b2v = v;
+    }
+  };
+  walk([&](float v, int i) { if (i < C) top2(v, i); }, top2);
   float bv = -INFINITY;
   int bi = 0x7fffffff;
-  for (int t0 = 0; t0 < ntiles; t0 += 64) {
-    const int t = t0 + lane;
-    bool take = false, full = false;
-    float2 c = make_float2(-INFINITY, 0.f);
-    if (t < ntiles) {
-      c = cand[row * ntiles + t];
-      take = c.x >= thr;
-      full = !CTCLIP_VQ_DIAG_NOFULL && take && cand2 && cand2[row * ntiles + t] >= thr;
-    }
-    // (bv, bi) = the max score, ties to the lowest code.  EVERY candidate is scored by one lane
-    // with the same sequential f32 sum (score_seq), so a code's score does not depend on how it
-    // became a candidate: which groups are 'full' depends on the low-precision GEMM's rounding
-    // (bf16 or fp16 operands, the margin), and with two summation orders an f32 near-tie
-    // (< 1 ulp apart) could resolve differently between the two.
-    unsigned long long gmask = __ballot(full);
-    while (gmask) {
-      const int src = __ffsll((long long)gmask) - 1;
-      gmask &= gmask - 1;
-      // several codes of this group are within the margin: score all of them, one per lane
-      const int ci = (t0 + src) * 64 + lane;
-      const float d = ci < C ? score_seq(xs, cb + (int64_t)ci * D, D) : -INFINITY;
-      wave_argmax(d, ci < C ? ci : 0x7fffffff, bv, bi);
-    }
-    // single-code candidates: each candidate lane scores its own code, all of them at once
-    if (__ballot(take && !full)) {
-      const int ci = __float_as_int(c.y);
-      const bool mine = take && !full;
-      const float d = mine ? score_seq(xs, cb + (int64_t)ci * D, D) : -INFINITY;
-      wave_argmax(d, mine ? ci : 0x7fffffff, bv, bi);
-    }
+  wave_argmax(b1v, b1i, bv, bi);
+  const float sec = warp_max(b1v == bv && b1i == bi ? b2v : b1v);
+  // |fast - seq| <= (D + D/64 + 6) 2^-24 ||cb row|| per code (unit x); win: twice that, for rows of
+  // norm <= 4 (the cosine codebook's are unit)
+  const float win = 8.f * (float)(D + D / 64 + 8) * 5.9604645e-8f;
+  if (sec >= bv - win) {   // wave-uniform: a near-tie -> pass 2, the deciding sum
+    const float lo = bv - win;
+    float sv = -INFINITY;
+    int si = 0x7fffffff;
+    walk(
+        [&](float v, int i) {
+          if (i < C && v >= lo) {
+            const float q = score_seq(xs, cb + (int64_t)i * D, D);
+            if (q > sv || (q == sv && i < si)) { sv = q; si = i; }
+          }
+        },
+        [&](float v, int i) {
+          if (v >= lo) {
+            const float q = score_seq(xs, cb + (int64_t)i * D, D);
+            if (q > sv || (q == sv && i < si)) { sv = q; si = i; }
+          }
+        });
+    bv = -INFINITY;
+    bi = 0x7fffffff;
+    wave_argmax(sv, si, bv, bi);
   }
   // a row without any finite score (NaN / inf tokens) keeps bi = INT_MAX: clamp it into the
   // codebook so no consumer (pool, gather, EMA statistics) reads outside it, and zero its
