@@ -85,7 +85,8 @@ typedef struct {
                                      * (the text tower's hi / lo split weights); 128-tile kernel only,
                                      * not with act 3 */
   int32_t ab_f16;                   /* A and B are IEEE fp16 (both K-contiguous; no B2, split-K,
-                                     * act 3-6): the 3D-ViT forward GEMMs (3 more mantissa bits
+                                     * act 4-6): the 3D-ViT forward GEMMs and (round 6) the act-3
+                                     * VQ distance GEMM (3 more mantissa bits
                                      * than bf16 at the same MFMA rate).  With act 2 the h output
                                      * C is fp16 in the DERIVATIVE form (round 6): per 64-column
                                      * group [gelu(gate) | x gelu'(gate)] instead of [x | gate], the
@@ -572,7 +573,11 @@ int ctclip_pack_rows_f32(const float* src, int64_t ld_src, const int32_t* map, i
  * ntiles = ceil(C / 64).  select re-scores in f32 (f32 x, f32 codebook [C][D]) every code whose bf16
  * score can lie within `margin` of the best -- group winners, and whole groups whose second-best is
  * within it -> the exact f32 argmax (first index on ties) for margin >= 2^-6 (bf16 scoring error
- * bound, see vq.hip).  cand2 = NULL re-scores group winners only.  D % 4 == 0, D <= 4096. */
+ * bound, see vq.hip).  cand2 = NULL re-scores group winners only.  D % 4 == 0, D <= 4096.
+ * Round 6: "the f32 argmax" is the argmax of the SEQUENTIAL f32 dot product (k = 0 .. D-1, one fma
+ * per term): fast slice / butterfly sums decide every row whose best two are further apart than
+ * their worst-case difference, the sequential sum decides the near-ties -- so the index does not
+ * depend on which codes the low-precision GEMM made candidates (codebook rows of norm <= 4). */
 int ctclip_vq_select(const float* cand, const float* cand2, int32_t ntiles, const float* x, int64_t rows, int32_t D,
                      const float* codebook, int32_t C, float margin, int32_t* idx, float* xn_out, void* stream);
 /* ... with the step status word: a row without any finite score (NaN / inf token) gets idx 0 and a
