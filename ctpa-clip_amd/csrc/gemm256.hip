@@ -45,6 +45,7 @@ struct P {
   int64_t kper;
   int debug;     // diagnostic knob (CTCLIP_G256_DEBUG): 1 = skip the epilogue, 2 = skip the main loop
   int group_gx;  // grouped (8-row) tile walk when the N tile count >= this (CTCLIP_GEMM_GROUP_GX, default 8)
+  int group_gm;  // rows per group of that walk (CTCLIP_GEMM_GROUP_GM; 0 = 8)
   int stagger;   // start delay (s_sleep units of 64 cycles) for the second co-resident workgroup
   int gz;        // batch * split_k (8-phase tile count = ceil(N/256) * ceil(M/256) * gz)
   int persist;   // 8-phase: persistent workgroups (one per CU) walking the tile sequence
@@ -1450,7 +1451,7 @@ __device__ __forceinline__ Tile tile_at(const P& p, int lin, int gx, int gy, int
     // wide N (the VQ distance GEMM: 32 codebook tiles = 8 MB): groups of 8 tile rows walked
     // column by column, so an XCD's ~32 concurrent tiles touch 8 A panels + 4 B panels (3 MB,
     // L2-resident) instead of 1 A panel + the whole codebook streamed through its 4 MB L2
-    constexpr int GM = 8;
+    const int GM = p.group_gm > 0 ? p.group_gm : 8;
     const int grp = rem / (GM * gx), y0 = grp * GM, gsz = min(gy - y0, GM), r = rem - grp * GM * gx;
     ty = y0 + r % gsz;
     tx = r / gsz;
@@ -1834,7 +1835,7 @@ int launch8_any(const P& p, bool bk, int batch, hipStream_t st) {
 // called from ctclip_gemm (gemm.hip) after argument validation
 int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream) {
   using namespace g256;
-  P p;
+  P p{};
   memset(&p, 0, sizeof(p));
   p.M = a->M; p.N = a->N; p.K = a->K;
   p.A = (const u16*)a->A; p.lda = a->lda;
@@ -1882,6 +1883,9 @@ int ctclip_gemm256(const ctclip_gemm_args* a, int split, int batch, void* stream
   static int ggx = -1;
   if (ggx < 0) { const char* e = getenv("CTCLIP_GEMM_GROUP_GX"); ggx = e ? atoi(e) : 8; }   // r02: FF1 (11 tiles) -2%, VQ (32) -17%; N <= 6 tiles: neutral to +4% (not grouped)
   p.group_gx = ggx;
+  static int ggm = -1;
+  if (ggm < 0) { const char* e = getenv("CTCLIP_GEMM_GROUP_GM"); ggm = e ? atoi(e) : 8; }
+  p.group_gm = ggm;
   // (round 4 sweep, profiles/r04a_stagger.log, interleaved rounds: no start stagger is best for the
   // GEGLU GEMM now -- 0.4229 vs 0.4289 ms at the old default 4; the GEGLU backward gains ~1.5 % at 8)
   p.stagger = variant() == 8 ? (g_stagger8 >= 0 ? g_stagger8 : (a->act == 4 ? 8 : 0)) : (tile_rows() == 1 ? stag : 0);
@@ -1927,7 +1931,7 @@ extern "C" int ctclip_gemm_ln(const ctclip_gemm_args* a, const ctclip_ln_epilogu
     CT_REQUIRE(ln->X && aligned16(ln->X) && ln->ldx % 8 == 0 && ln->part_gamma && !ln->beta && a->C2 && a->R,
                CT_EINVAL);
   }
-  P p;
+  P p{};
   memset(&p, 0, sizeof(p));
   p.M = a->M; p.N = a->N; p.K = a->K;
   p.A = (const u16*)a->A; p.lda = a->lda;
@@ -1990,7 +1994,7 @@ extern "C" int ctclip_gemm_qkv_lnfold2(const ctclip_gemm_args* a, const float* m
   CT_REQUIRE(aligned16(a->A) && aligned16(a->B) && aligned16(a->C) && aligned16(a->C2) && aligned16(a->bias) &&
                  aligned16(fold_cs) && a->lda % 8 == 0 && a->ldb % 8 == 0 && a->ldc % 8 == 0 && a->ldc2 % 8 == 0,
              CT_EALIGN);
-  P p;
+  P p{};
   memset(&p, 0, sizeof(p));
   p.M = a->M; p.N = a->N; p.K = a->K;
   p.A = (const u16*)a->A; p.lda = a->lda;
@@ -2036,7 +2040,7 @@ extern "C" int ctclip_gemm_lnfold_bwd(const ctclip_gemm_args* a, const void* X, 
                  a->lda % 8 == 0 && a->ldb % 8 == 0 && a->ldc % 8 == 0 && a->ldr % 8 == 0 && ldx % 8 == 0,
              CT_EALIGN);
   if (a->C2) CT_REQUIRE(aligned16(a->C2) && a->ldc2 % 8 == 0, CT_EALIGN);
-  P p;
+  P p{};
   memset(&p, 0, sizeof(p));
   p.M = a->M; p.N = a->N; p.K = a->K;
   p.A = (const u16*)a->A; p.lda = a->lda;
