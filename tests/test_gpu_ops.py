@@ -409,6 +409,64 @@ def test_vq_select_and_pool(K):
 
 # ----------------------------------------------------------------------------- loss
 @pytest.mark.parametrize('Bg', [2, 8, 64])
+
+def _seq_f32_scores(xn, rows_cb):
+    """x_n . w in f32 as vq.hip's score_seq sums it: k = 0 .. D-1, one fused multiply-add per term
+    (each fma emulated in f64: the product is exact there, the sum rounds twice only at an f32
+    midpoint, ~2^-29 per term)."""
+    d = torch.zeros(rows_cb.shape[0], dtype=torch.float64, device=xn.device)
+    xd, wd = xn.double(), rows_cb.double()
+    for k in range(xn.shape[-1]):
+        d = (xd[..., k] * wd[:, k] + d).float().double()
+    return d
+
+
+def test_vq_select_order_independent(K):
+    """Round 6: vq_select's index is the argmax of the SEQUENTIAL f32 dot product (ties to the lowest
+    code) whatever the GEMM that proposed the candidates -- bf16 operands with margin 2e-2 or fp16
+    with 4e-3 give the same index on every row, sub-ulp near-ties and exact duplicate codes included."""
+    torch.manual_seed(5)
+    M, D, C = 2048, 512, 8192
+    x = torch.randn(M, D, device=dev)
+    cb = F.normalize(torch.randn(C, D, device=dev), dim=-1)
+    xn = F.normalize(x, dim=-1)
+    g = torch.Generator(device=dev).manual_seed(12)
+    # rows 0..127: two codes (one group or two) within ~1e-7 of each other in f64 -- about one f32
+    # ulp at 0.9998; rows 128..191: an exact duplicate of the winning code at a higher index
+    for i in range(128):
+        base = F.normalize(xn[i] + 0.02 * F.normalize(torch.randn(D, device=dev, generator=g), dim=0), dim=0)
+        tweak = base + 1e-7 * torch.randn(D, device=dev, generator=g)
+        cb[64 * i + 3] = base
+        cb[64 * ((i + i % 2) % 128) + 7] = F.normalize(tweak, dim=0)   # same group (even i) or the next
+    for i in range(128, 192):
+        w = F.normalize(xn[i] + 0.02 * F.normalize(torch.randn(D, device=dev, generator=g), dim=0), dim=0)
+        cb[64 * (i - 128) + 11] = w
+        cb[64 * (i - 128 + 64) + 11] = w
+    nt = C // 64
+    cand = torch.empty(M, nt, 2, device=dev)
+    cand2 = torch.empty(M, nt, device=dev)
+    K.gemm_raw(M, C, D, xn.bfloat16(), D, True, cb.bfloat16(), D, True, cand, nt, C2=cand2, ldc2=nt,
+               act=K.ACT_ARGMAX)
+    idx_b, xno = K.vq_select(cand, x, cb, cand2=cand2)
+    candh = torch.empty(M, nt, 2, device=dev)
+    cand2h = torch.empty(M, nt, device=dev)
+    K.gemm_raw(M, C, D, K.vq_l2norm_h16(x), D, True, K.split_f16(cb)[0], D, True, candh, nt, C2=cand2h,
+               ldc2=nt, act=K.ACT_ARGMAX)
+    idx_h, _ = K.vq_select(candh, x, cb, margin=4e-3, cand2=cand2h)
+    assert torch.equal(idx_b, idx_h)
+    # the near-tie and duplicate rows against the sequential f32 sum of the kernel's own x_n: the
+    # winner among the 8 best f64 codes (every code within the select's window is among them)
+    s64 = xno.double() @ cb.double().t()
+    top = s64[:192].topk(8, dim=1).indices
+    seq = torch.stack([_seq_f32_scores(xno[r], cb[top[r]]) for r in range(192)])
+    best = seq.max(1, keepdim=True).values
+    win = torch.where(seq == best, top, torch.full_like(top, C)).min(1).values   # ties: lowest code
+    assert torch.equal(idx_b[:192].long(), win)
+    assert (idx_b[128:192].long() == 64 * torch.arange(64, device=dev) + 11).all()   # the lower duplicate
+    ties = (seq.topk(2, dim=1).values[:, 0] - seq.topk(2, dim=1).values[:, 1] == 0).sum().item()
+    print(f'order-independent select: {M} rows, bf16 vs fp16 candidates identical; {ties} of 192 '
+          'constructed rows tie exactly in f32 (lowest code wins)')
+
 def test_clip_loss(K, Bg):
     torch.manual_seed(5)
     t = torch.randn(Bg, 512, device=dev)
