@@ -25,6 +25,9 @@
 namespace {
 
 constexpr int VQ_SB = 4;   // single-code candidates re-scored together
+constexpr int VQ_CT = 2;   // candidate words of up to 2 x 64 groups (C <= 8192) held in registers
+static_assert(VQ_CT == 2, "vq_select picks the preloaded word with a select");
+constexpr int VQ_XR = 8;   // the token in registers for D <= 512
 
 // Scoring a candidate code (x_n . cb_row in f32).  The fast sum: lane l sums its slice
 // k in {4l .. 4l+3} + 256 j (j ascending, one fused multiply-add per term), then the 64 slice
@@ -119,33 +122,69 @@ __global__ __launch_bounds__(256) void vq_select_kernel(const float2* __restrict
   if (row >= rows) return;
   float* xs = xs_all + (threadIdx.x >> 6) * D;
   const float* xr = x + row * D;
-  // f32 l2norm of x (F.normalize, eps 1e-12)
+  // the row's candidate words first (up to VQ_CT x 64 groups, held in registers), so their loads are
+  // in flight beside the token's
+  const bool pre = ntiles <= 64 * VQ_CT;   // wave-uniform
+  float2 cpre[VQ_CT];
+  float c2pre[VQ_CT];
+#pragma unroll
+  for (int j = 0; j < VQ_CT; ++j) {
+    const int t = j * 64 + lane;
+    const bool in = pre && t < ntiles;
+    cpre[j] = in ? cand[row * ntiles + t] : make_float2(-INFINITY, 0.f);
+    c2pre[j] = in && cand2 ? cand2[row * ntiles + t] : -INFINITY;
+  }
+  // f32 l2norm of x (F.normalize, eps 1e-12); D <= 64 VQ_XR: the token held in registers
   float ss = 0.f;
-  for (int c = lane; c < D; c += 64) ss += xr[c] * xr[c];
+  float xreg[VQ_XR];
+  const bool xin = D <= 64 * VQ_XR;   // wave-uniform
+  if (xin) {
+#pragma unroll
+    for (int j = 0; j < VQ_XR; ++j) {
+      const int c = lane + 64 * j;
+      xreg[j] = c < D ? xr[c] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < VQ_XR; ++j) ss += xreg[j] * xreg[j];   // (past D: + 0, exactly)
+  } else {
+    for (int c = lane; c < D; c += 64) ss += xr[c] * xr[c];
+  }
   ss = warp_sum(ss);
   const float inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
-  for (int c = lane; c < D; c += 64) {
-    const float v = xr[c] * inv;
-    xs[c] = v;
-    if (xn_out) xn_out[row * D + c] = v;
+  if (xin) {
+#pragma unroll
+    for (int j = 0; j < VQ_XR; ++j) {
+      const int c = lane + 64 * j;
+      if (c < D) {
+        const float v = xreg[j] * inv;
+        xs[c] = v;
+        if (xn_out) xn_out[row * D + c] = v;
+      }
+    }
+  } else {
+    for (int c = lane; c < D; c += 64) {
+      const float v = xr[c] * inv;
+      xs[c] = v;
+      if (xn_out) xn_out[row * D + c] = v;
+    }
   }
-  // best bf16 score over groups
+  // best 16-bit score over groups
   float best = -INFINITY;
-  for (int t = lane; t < ntiles; t += 64) best = fmaxf(best, cand[row * ntiles + t].x);
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < VQ_CT; ++j) best = fmaxf(best, cpre[j].x);
+  } else {
+    for (int t = lane; t < ntiles; t += 64) best = fmaxf(best, cand[row * ntiles + t].x);
+  }
   best = warp_max(best);
   const float thr = best - margin;
   // every candidate code: onfull(score, code) per lane for the 64 codes of a full group (code >= C
   // past the codebook's end: skip), onsingle(score, code) wave-uniform for a single code
   auto walk = [&](auto&& onfull, auto&& onsingle) {
-    for (int t0 = 0; t0 < ntiles; t0 += 64) {
+    auto chunk = [&](int t0, float2 c, float c2) {
       const int t = t0 + lane;
-      bool take = false, full = false;
-      float2 c = make_float2(-INFINITY, 0.f);
-      if (t < ntiles) {
-        c = cand[row * ntiles + t];
-        take = c.x >= thr;
-        full = !CTCLIP_VQ_DIAG_NOFULL && take && cand2 && cand2[row * ntiles + t] >= thr;
-      }
+      const bool take = t < ntiles && c.x >= thr;
+      const bool full = !CTCLIP_VQ_DIAG_NOFULL && take && cand2 && c2 >= thr;
       unsigned long long gmask = __ballot(full);
       unsigned long long smask = __ballot(take) & ~gmask;
       while (gmask) {
@@ -173,6 +212,20 @@ __global__ __launch_bounds__(256) void vq_select_kernel(const float2* __restrict
         for (int q = 0; q < VQ_SB; ++q)
           if (ci[q] >= 0) onsingle(warp_sum(d[q]), ci[q]);
       }
+    };
+#pragma unroll 1
+    for (int t0 = 0; t0 < ntiles; t0 += 64) {
+      const int t = t0 + lane;
+      float2 c;
+      float c2;
+      if (pre) {   // (VQ_CT == 2: a select, not a dynamically indexed register array)
+        c = t0 == 0 ? cpre[0] : cpre[1];
+        c2 = t0 == 0 ? c2pre[0] : c2pre[1];
+      } else {
+        c = t < ntiles ? cand[row * ntiles + t] : make_float2(-INFINITY, 0.f);
+        c2 = t < ntiles && cand2 ? cand2[row * ntiles + t] : -INFINITY;
+      }
+      chunk(t0, c, c2);
     }
   };
   // pass 1: the fast scores' best (ties to the lowest code) and runner-up, per lane then per wave
