@@ -407,9 +407,6 @@ def test_vq_select_and_pool(K):
     assert torch.isfinite(emb_b).all()
 
 
-# ----------------------------------------------------------------------------- loss
-@pytest.mark.parametrize('Bg', [2, 8, 64])
-
 def _seq_f32_scores(xn, rows_cb):
     """x_n . w in f32 as vq.hip's score_seq sums it: k = 0 .. D-1, one fused multiply-add per term
     (each fma emulated in f64: the product is exact there, the sum rounds twice only at an f32
@@ -467,6 +464,9 @@ def test_vq_select_order_independent(K):
     print(f'order-independent select: {M} rows, bf16 vs fp16 candidates identical; {ties} of 192 '
           'constructed rows tie exactly in f32 (lowest code wins)')
 
+
+# ----------------------------------------------------------------------------- loss
+@pytest.mark.parametrize('Bg', [2, 8, 64])
 def test_clip_loss(K, Bg):
     torch.manual_seed(5)
     t = torch.randn(Bg, 512, device=dev)
