@@ -438,16 +438,18 @@ def main():
             'hbm_frac': round(algo_bytes / (ff1['avg_ms'] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
             'avg_launch_ms': round(ff1['avg_ms'], 4), 'flops_per_launch': ff1['flops'],
             'launches': ff1['launches'], 'timing': 'HIP events around each launch on its stream, timed region'}
-        # headline = the committed rocprofv3 summary's average for the same kernel (the judge's
-        # reference clock); the live HIP-event figures stay beside it as live_*
+        # headline = this run's HIP-event average (the contract's clock); the committed rocprofv3
+        # summary's average for the same kernel is the cross-check beside it (rocprof_*, and the
+        # ratio of the two: the profiled run's slower host shifts the text stream's overlap)
+        result['roofline']['frac_source'] = 'live'
         rp_ms, rp_calls, rp_src = rocprof_avg_ms(ff1_key)
         if rp_ms and args.batch == 8:
             rtf = ff1['flops'] / (rp_ms * 1e-3) / 1e12
             result['roofline'].update({
-                'achieved': round(rtf, 1), 'frac': round(rtf / PEAK_BF16_TFLOPS, 4), 'frac_source': 'rocprof',
                 'live_achieved': round(tflops, 1), 'live_frac': round(tflops / PEAK_BF16_TFLOPS, 4),
                 'rocprof_avg_launch_ms': round(rp_ms, 4), 'rocprof_achieved': round(rtf, 1),
                 'rocprof_frac': round(rtf / PEAK_BF16_TFLOPS, 4),
+                'rocprof_over_live': round(rp_ms / ff1['avg_ms'], 3),
                 'rocprof_source': f'{rp_src} ({rp_calls} launches)'})
     if dw:
         # the kernel with the largest share of the step's time (rocprof): the split-K weight-gradient
@@ -481,11 +483,12 @@ def main():
         if rp_ms and args.batch == 8:
             avg_flops = dw['total_flops'] / dw['launches']
             rtf = avg_flops / (rp_ms * 1e-3) / 1e12
-            result['roofline_dominant'].update({'achieved': round(rtf, 1), 'frac': round(rtf / PEAK_BF16_TFLOPS, 4),
-                                                'frac_source': 'rocprof', 'live_achieved': round(tf, 1),
+            result['roofline_dominant'].update({'frac_source': 'live', 'live_achieved': round(tf, 1),
                                                 'live_frac': round(tf / PEAK_BF16_TFLOPS, 4),
                                                 'rocprof_avg_launch_ms': round(rp_ms, 4),
+                                                'rocprof_achieved': round(rtf, 1),
                                                 'rocprof_frac': round(rtf / PEAK_BF16_TFLOPS, 4),
+                                                'rocprof_over_live': round(rp_ms / (dw['total_ms'] / dw['launches']), 3),
                                                 'rocprof_source': f'{rp_src} ({rp_calls} launches)'})
     if vit_ms > 0:
         vit_tf = VIT_FWD_GFLOP_PER_VOL * args.batch / (vit_ms * 1e-3) / 1e3
