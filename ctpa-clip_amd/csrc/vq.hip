@@ -546,6 +546,28 @@ __global__ __launch_bounds__(256) void vq_l2norm_h16_kernel(const float* __restr
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;   // (wave-uniform)
   const float* xr = x + row * ldx;
+  if (D <= 512) {   // wave-uniform: the row in registers (two 16-B words per lane), read once
+    const int c0 = lane * 4, c1 = c0 + 256;
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 a = c0 < D ? *(const f32x4*)(xr + c0) : z, b = c1 < D ? *(const f32x4*)(xr + c1) : z;
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s = fmaf(a[e], a[e], s);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s = fmaf(b[e], b[e], s);
+    s = warp_sum(s);
+    const float r = 1.f / fmaxf(sqrtf(s), 1e-12f);   // (the GEMM operand: x r rounds to the same fp16 as
+                                                      // x / n but at the last f32 ulp; vq_select re-scores)
+    if (c0 < D) {
+      const float o[4] = {a[0] * r, a[1] * r, a[2] * r, a[3] * r};
+      *(uint2*)(y + row * ldy + c0) = pack4h(o);
+    }
+    if (c1 < D) {
+      const float o[4] = {b[0] * r, b[1] * r, b[2] * r, b[3] * r};
+      *(uint2*)(y + row * ldy + c1) = pack4h(o);
+    }
+    return;
+  }
   float s = 0.f;
   for (int c = lane * 4; c < D; c += 256) {
     const f32x4 v = *(const f32x4*)(xr + c);
