@@ -62,6 +62,23 @@ def join_aux(dev):
         torch.cuda.current_stream(dev).wait_stream(s)
 
 
+_MAIN = {}
+# round 6 experiment: run the trainer's step on a high-priority stream (the text / aux streams keep
+# the default priority), so the dispatcher prefers the critical path's workgroups when both wait
+MAIN_PRIORITY = ENABLED and os.environ.get('CTCLIP_MAIN_PRIORITY', '1') != '0'
+
+
+def main_stream(dev):
+    """The high-priority stream the trainer's step runs on (None with CTCLIP_MAIN_PRIORITY=0)."""
+    if not MAIN_PRIORITY or dev.type != 'cuda':
+        return None
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    if idx not in _MAIN:
+        lo, hi = torch.cuda.Stream.priority_range()
+        _MAIN[idx] = torch.cuda.Stream(idx, priority=min(lo, hi))
+    return _MAIN[idx]
+
+
 _STATUS = {}
 
 

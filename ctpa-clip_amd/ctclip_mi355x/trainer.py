@@ -396,6 +396,20 @@ class CTClipTrainer:
         """One contrastive step; returns the loss tensor (no host sync).  Raises
         LayerNormExchangeError once the status copy of an earlier step shows a timed-out LayerNorm
         exchange (at the latest two steps later; ``check()`` / ``flush()`` wait for all)."""
+        hp = streams.main_stream(self.device)
+        if hp is None:
+            return self._train_step(text, video)
+        # CTCLIP_MAIN_PRIORITY=1: the step on the high-priority stream, ordered after the caller's
+        # work so far, and the caller's stream after it
+        caller = torch.cuda.current_stream(self.device)
+        hp.wait_stream(caller)
+        with torch.cuda.stream(hp):
+            loss = self._train_step(text, video)
+        caller.wait_stream(hp)
+        loss.record_stream(caller)
+        return loss
+
+    def _train_step(self, text, video):
         self._check_ln(block_upto=self.steps - 2)
         self.model.train()
         own = hasattr(self.model, 'ema_after_step')
